@@ -1,0 +1,213 @@
+// PyTorch-ROCm binding of the native kd-tree core (module parallel_kd_tree_amd._C).
+// Device work runs on the caller's current HIP stream; workspaces come from the torch
+// caching allocator, so repeated builds allocate nothing from HIP.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pkdtree/common.hpp"
+#include "pkdtree/cpu_tree.hpp"
+#include "pkdtree/generator.hpp"
+#include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_query.hpp"
+
+namespace pk = pkdtree;
+
+namespace pkdtree {
+void bind_dist_ops(pybind11::module& m);  // dist_bindings.cpp
+}
+
+namespace {
+
+hipStream_t cur_stream(const torch::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_points(const torch::Tensor& pts, bool cuda) {
+  TORCH_CHECK(pts.dim() == 2, "points must be [n, dim]");
+  TORCH_CHECK(pts.scalar_type() == torch::kFloat32, "points must be float32");
+  TORCH_CHECK(pts.is_contiguous(), "points must be contiguous");
+  TORCH_CHECK(pts.is_cuda() == cuda, cuda ? "points must be on a GPU" : "points must be on the CPU");
+}
+
+const pk::u32* opt_ids(const c10::optional<torch::Tensor>& ids, int64_t n, bool cuda) {
+  if (!ids.has_value() || !ids->defined()) return nullptr;
+  TORCH_CHECK(ids->scalar_type() == torch::kInt32, "ids must be int32 (bits are used as uint32)");
+  TORCH_CHECK(ids->is_contiguous() && ids->numel() == n, "ids must be contiguous [n]");
+  TORCH_CHECK(ids->is_cuda() == cuda, "ids on the wrong device");
+  return reinterpret_cast<const pk::u32*>(ids->data_ptr<int32_t>());
+}
+
+// Reusable builder bound to (n, dim, options) with a torch-allocated workspace.
+struct Builder {
+  pk::GpuBuilder b;
+  torch::Tensor ws;
+  Builder(int64_t n, int64_t dim, int64_t depth0, int64_t subtree_max)
+      : b(n, int(dim), pk::BuildOptions{int(subtree_max), int(depth0)}) {}
+
+  void ensure_ws(const torch::Device& dev) {
+    if (!ws.defined() || ws.device() != dev)
+      ws = torch::empty({int64_t(b.workspace_bytes())}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
+  }
+
+  std::vector<torch::Tensor> build(const torch::Tensor& pts, const c10::optional<torch::Tensor>& ids,
+                                   int64_t id_base, c10::optional<torch::Tensor> out_pts,
+                                   c10::optional<torch::Tensor> out_ids) {
+    check_points(pts, true);
+    TORCH_CHECK(pts.size(0) == b.n() && pts.size(1) == b.dim(), "points shape does not match the builder");
+    const c10::hip::HIPGuard guard(pts.device());
+    ensure_ws(pts.device());
+    torch::Tensor op = out_pts.has_value() ? *out_pts : torch::empty_like(pts);
+    torch::Tensor oi = out_ids.has_value() ? *out_ids
+                                           : torch::empty({b.n()}, pts.options().dtype(torch::kInt32));
+    TORCH_CHECK(op.sizes() == pts.sizes() && op.is_contiguous(), "out_pts must match points");
+    TORCH_CHECK(oi.numel() == b.n() && oi.scalar_type() == torch::kInt32, "out_ids must be int32 [n]");
+    b.build(pts.data_ptr<float>(), opt_ids(ids, b.n(), true), pk::u32(id_base), op.data_ptr<float>(),
+            reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(), cur_stream(pts));
+    return {op, oi};
+  }
+
+  // SoA input view inside the workspace: [(dim+1), n] float32 (row dim holds id bits).
+  torch::Tensor soa_input(const torch::Device& dev) {
+    ensure_ws(dev);
+    return torch::from_blob(b.soa_input(ws.data_ptr()), {b.dim() + 1, b.n()},
+                            torch::TensorOptions().dtype(torch::kFloat32).device(dev));
+  }
+
+  std::vector<torch::Tensor> build_from_soa(const torch::Device& dev) {
+    const c10::hip::HIPGuard guard(dev);
+    ensure_ws(dev);
+    auto opts = torch::TensorOptions().device(dev);
+    torch::Tensor op = torch::empty({b.n(), b.dim()}, opts.dtype(torch::kFloat32));
+    torch::Tensor oi = torch::empty({b.n()}, opts.dtype(torch::kInt32));
+    b.build_from_soa(op.data_ptr<float>(), reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(),
+                     c10::hip::getCurrentHIPStream(dev.index()).stream());
+    return {op, oi};
+  }
+};
+
+torch::Tensor generate(int64_t seed, int64_t dim, int64_t rows, int64_t first, int64_t threads) {
+  TORCH_CHECK(dim > 0 && rows >= 0 && first >= 0, "bad generator arguments");
+  torch::Tensor x = torch::empty({rows, dim}, torch::kFloat32);
+  pk::generate_rows(int(seed), int(dim), first, rows, x.data_ptr<float>(), int(threads));
+  return x;
+}
+
+std::vector<torch::Tensor> build_cpu(const torch::Tensor& pts, const c10::optional<torch::Tensor>& ids,
+                                     const std::string& mode, int64_t depth0, int64_t threads) {
+  check_points(pts, false);
+  const int64_t n = pts.size(0);
+  const int dim = int(pts.size(1));
+  std::vector<pk::u32> perm(size_t(std::max<int64_t>(n, 1)));
+  const pk::u32* idp = opt_ids(ids, n, false);
+  if (mode == "exact") {
+    pk::build_exact_cpu(pts.data_ptr<float>(), idp, n, dim, int(depth0), perm.data(), int(threads));
+  } else if (mode == "reference") {
+    TORCH_CHECK(depth0 == 0, "reference mode builds whole trees only");
+    pk::build_reference_cpu(pts.data_ptr<float>(), n, dim, perm.data());
+  } else {
+    TORCH_CHECK(false, "mode must be 'exact' or 'reference'");
+  }
+  torch::Tensor tp = torch::empty_like(pts);
+  torch::Tensor ti = torch::empty({n}, torch::kInt32);
+  pk::gather_rows(pts.data_ptr<float>(), idp, perm.data(), n, dim, tp.data_ptr<float>(),
+                  reinterpret_cast<pk::u32*>(ti.data_ptr<int32_t>()));
+  return {tp, ti};
+}
+
+// CPU search with the reference's procedure: returns (slot, d2) per query.
+std::vector<torch::Tensor> search_cpu(const torch::Tensor& tree_pts, const torch::Tensor& queries, int64_t depth0,
+                                      bool brute) {
+  check_points(tree_pts, false);
+  check_points(queries, false);
+  TORCH_CHECK(queries.size(1) == tree_pts.size(1), "dimension mismatch");
+  const int64_t nq = queries.size(0);
+  const int dim = int(tree_pts.size(1));
+  torch::Tensor slots = torch::empty({nq}, torch::kInt64);
+  torch::Tensor d2 = torch::empty({nq}, torch::kFloat32);
+  for (int64_t i = 0; i < nq; ++i) {
+    const float* q = queries.data_ptr<float>() + i * dim;
+    const pk::NNResult r = brute ? pk::nn_brute_cpu(tree_pts.data_ptr<float>(), tree_pts.size(0), dim, q)
+                                 : pk::nn_search_cpu(tree_pts.data_ptr<float>(), tree_pts.size(0), dim, int(depth0), q);
+    slots.data_ptr<int64_t>()[i] = r.slot;
+    d2.data_ptr<float>()[i] = r.d2;
+  }
+  return {slots, d2};
+}
+
+int64_t invariant_violations(const torch::Tensor& tree_pts, const torch::Tensor& tree_ids, int64_t depth0) {
+  check_points(tree_pts, false);
+  TORCH_CHECK(tree_ids.scalar_type() == torch::kInt32 && !tree_ids.is_cuda(), "tree_ids must be CPU int32");
+  return pk::count_invariant_violations(tree_pts.data_ptr<float>(),
+                                        reinterpret_cast<const pk::u32*>(tree_ids.data_ptr<int32_t>()),
+                                        tree_pts.size(0), int(tree_pts.size(1)), int(depth0));
+}
+
+// Packed (d2, id) results as int64 (bit pattern of the u64 packing).
+torch::Tensor nn_gpu(const torch::Tensor& pts, const c10::optional<torch::Tensor>& ids, int64_t id_base,
+                     const torch::Tensor& queries, const std::string& method, int64_t depth0,
+                     c10::optional<torch::Tensor> into) {
+  check_points(pts, true);
+  check_points(queries, true);
+  TORCH_CHECK(queries.size(1) == pts.size(1), "dimension mismatch");
+  const c10::hip::HIPGuard guard(pts.device());
+  const int64_t nq = queries.size(0);
+  hipStream_t s = cur_stream(pts);
+  torch::Tensor out;
+  if (into.has_value()) {
+    out = *into;
+    TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == nq && out.is_cuda(), "bad `into` tensor");
+  } else {
+    out = torch::empty({nq}, queries.options().dtype(torch::kInt64));
+    pk::nn_init(reinterpret_cast<pk::u64*>(out.data_ptr<int64_t>()), nq, s);
+  }
+  auto* o = reinterpret_cast<pk::u64*>(out.data_ptr<int64_t>());
+  const pk::u32* idp = opt_ids(ids, pts.size(0), true);
+  if (method == "brute") {
+    pk::nn_brute(pts.data_ptr<float>(), idp, pk::u32(id_base), pts.size(0), int(pts.size(1)),
+                 queries.data_ptr<float>(), nq, o, s);
+  } else if (method == "traverse") {
+    TORCH_CHECK(idp != nullptr, "traverse needs the tree ids");
+    pk::nn_traverse(pts.data_ptr<float>(), idp, pts.size(0), int(pts.size(1)), int(depth0), queries.data_ptr<float>(),
+                    nq, o, s);
+  } else {
+    TORCH_CHECK(false, "method must be 'brute' or 'traverse'");
+  }
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native kd-tree core (HIP/CDNA4 kernels + C++ runtime)";
+  py::class_<Builder>(m, "GpuBuilder")
+      .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0,
+           py::arg("subtree_max") = 0)
+      .def("build", &Builder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0,
+           py::arg("out_pts") = c10::nullopt, py::arg("out_ids") = c10::nullopt)
+      .def("soa_input", &Builder::soa_input)
+      .def("build_from_soa", &Builder::build_from_soa)
+      .def_property_readonly("workspace_bytes", [](const Builder& b) { return int64_t(b.b.workspace_bytes()); })
+      .def_property_readonly("global_levels", [](const Builder& b) { return b.b.global_levels(); })
+      .def_property_readonly("subtree_max", [](const Builder& b) { return b.b.subtree_max(); })
+      .def("describe", [](const Builder& b) { return b.b.describe(); })
+      .def("read_error", [](Builder& b) {
+        return int64_t(b.b.read_error(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream()));
+      });
+  m.def("generate", &generate, py::arg("seed"), py::arg("dim"), py::arg("rows"), py::arg("first") = 0,
+        py::arg("threads") = 0);
+  m.def("build_cpu", &build_cpu, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("mode") = "exact",
+        py::arg("depth0") = 0, py::arg("threads") = 1);
+  m.def("search_cpu", &search_cpu, py::arg("tree_pts"), py::arg("queries"), py::arg("depth0") = 0,
+        py::arg("brute") = false);
+  m.def("invariant_violations", &invariant_violations, py::arg("tree_pts"), py::arg("tree_ids"),
+        py::arg("depth0") = 0);
+  m.def("nn", &nn_gpu, py::arg("points"), py::arg("ids"), py::arg("id_base"), py::arg("queries"),
+        py::arg("method") = "brute", py::arg("depth0") = 0, py::arg("into") = c10::nullopt);
+  m.def("subtree_capacity", &pk::default_subtree_max);
+  pkdtree::bind_dist_ops(m);
+}

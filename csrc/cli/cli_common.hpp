@@ -1,0 +1,70 @@
+// Shared CLI front-end for the kdtree_* executables.
+//
+// Reference behaviour (Utility.cpp:92-120, kdtree_sequential.cpp:140-193): with DEBUG 0 the
+// program prints READY, reads the seed from stdin and uses dim=128, N=500000; with DEBUG 1
+// it takes SEED DIM_POINTS NUM_POINTS from argv and prints "elapsed time". Here the mode is
+// chosen at run time: three positional arguments (or --debug / KDTREE_DEBUG=1) select the
+// debug protocol, none selects the eval protocol. Options start with "--" and never reach
+// the positional parser, so `prog 42 3 1024` behaves exactly like the reference's DEBUG
+// build.
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "pkdtree/protocol.hpp"
+
+namespace pkdtree {
+namespace cli {
+
+struct Options {
+  bool debug = false;
+  std::string mode = "exact";      // exact | reference
+  std::string query = "auto";      // auto | brute | traverse
+  int threads = 0;
+  int num_queries = 10;            // kdtree_sequential.cpp:144
+  bool metrics = false;            // per-phase timings as one JSON line on stderr
+  int device = 0;
+  std::vector<char*> positional;   // argv[0] + positionals
+};
+
+inline Options parse(int argc, char** argv) {
+  Options o;
+  o.positional.push_back(argv[0]);
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&](const char* name) -> std::string {
+      const std::string pre = std::string(name) + "=";
+      if (a.rfind(pre, 0) == 0) return a.substr(pre.size());
+      if (a == name && i + 1 < argc) return argv[++i];
+      std::cerr << "missing value for " << name << std::endl;
+      std::exit(1);
+    };
+    if (a == "--debug") o.debug = true;
+    else if (a == "--metrics-json") o.metrics = true;
+    else if (a.rfind("--mode", 0) == 0) o.mode = val("--mode");
+    else if (a.rfind("--query", 0) == 0) o.query = val("--query");
+    else if (a.rfind("--threads", 0) == 0) o.threads = std::atoi(val("--threads").c_str());
+    else if (a.rfind("--queries", 0) == 0) o.num_queries = std::atoi(val("--queries").c_str());
+    else if (a.rfind("--device", 0) == 0) o.device = std::atoi(val("--device").c_str());
+    else o.positional.push_back(argv[i]);
+  }
+  const char* env = std::getenv("KDTREE_DEBUG");
+  if (env && std::strcmp(env, "0") != 0) o.debug = true;
+  if (o.positional.size() > 1) o.debug = true;
+  if (o.mode != "exact" && o.mode != "reference") {
+    std::cerr << "--mode must be exact or reference" << std::endl;
+    std::exit(1);
+  }
+  return o;
+}
+
+inline Problem specify(Options& o) {
+  if (o.debug) return specify_problem_argv(int(o.positional.size()), o.positional.data());
+  return specify_problem_stdin();
+}
+
+}  // namespace cli
+}  // namespace pkdtree

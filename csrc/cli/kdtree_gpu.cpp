@@ -1,0 +1,88 @@
+// kdtree_gpu — single-MI355X executable with the reference's protocol
+// (kdtree_sequential.cpp:140-208): host generation of the reference data, level-synchronous
+// HIP build, exact GPU queries. --metrics-json prints per-phase times (hipEvents) on stderr.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <iostream>
+#include <vector>
+
+#include "cli_common.hpp"
+#include "pkdtree/generator.hpp"
+#include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_query.hpp"
+#include "pkdtree/hip_check.hpp"
+
+using namespace pkdtree;
+
+int main(int argc, char** argv) {
+  cli::Options o = cli::parse(argc, argv);
+  if (o.mode != "exact") {
+    std::cerr << "kdtree_gpu builds exact trees only; use kdtree_sequential --mode reference" << std::endl;
+    return 1;
+  }
+  const auto tick = std::chrono::high_resolution_clock::now();
+  const Problem p = cli::specify(o);
+  const int Q = o.num_queries;
+  const i64 N = p.num_points;
+  const int dim = p.dim;
+  try {
+    PKD_HIP_CHECK(hipSetDevice(o.device));
+    const auto g0 = std::chrono::high_resolution_clock::now();
+    std::vector<float> x = generate_problem(p.seed, dim, N + Q);
+    const auto g1 = std::chrono::high_resolution_clock::now();
+    hipStream_t s;
+    PKD_HIP_CHECK(hipStreamCreate(&s));
+    GpuBuilder b(N, dim);
+    float *d_x = nullptr, *d_tree = nullptr;
+    u32* d_ids = nullptr;
+    u64* d_res = nullptr;
+    void* ws = nullptr;
+    PKD_HIP_CHECK(hipMalloc(&d_x, x.size() * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(N) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(N) * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_res, size_t(Q) * 8));
+    PKD_HIP_CHECK(hipMalloc(&ws, b.workspace_bytes()));
+    hipEvent_t e0, e1, e2, e3;
+    for (hipEvent_t* e : {&e0, &e1, &e2, &e3}) PKD_HIP_CHECK(hipEventCreate(e));
+    PKD_HIP_CHECK(hipEventRecord(e0, s));
+    PKD_HIP_CHECK(hipMemcpyAsync(d_x, x.data(), x.size() * 4, hipMemcpyHostToDevice, s));
+    PKD_HIP_CHECK(hipEventRecord(e1, s));
+    b.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);  // reference point IDs are 1..N
+    PKD_HIP_CHECK(hipEventRecord(e2, s));
+    const float* d_q = d_x + size_t(N) * dim;
+    nn_init(d_res, Q, s);
+    const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
+    if (traverse) nn_traverse(d_tree, d_ids, N, dim, 0, d_q, Q, d_res, s);
+    else nn_brute(d_tree, d_ids, 0, N, dim, d_q, Q, d_res, s);
+    PKD_HIP_CHECK(hipEventRecord(e3, s));
+    std::vector<u64> res(static_cast<size_t>(Q));
+    PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    for (int q = 0; q < Q; ++q) print_result_line(N + q, std::sqrt(packed_dist(res[size_t(q)])));
+    if (o.debug) {
+      const auto tock = std::chrono::high_resolution_clock::now();
+      print_elapsed(std::chrono::duration<double>(tock - tick).count());
+    }
+    print_done();
+    if (o.metrics) {
+      float h2d = 0, bld = 0, qry = 0;
+      PKD_HIP_CHECK(hipEventElapsedTime(&h2d, e0, e1));
+      PKD_HIP_CHECK(hipEventElapsedTime(&bld, e1, e2));
+      PKD_HIP_CHECK(hipEventElapsedTime(&qry, e2, e3));
+      const double gen = std::chrono::duration<double, std::milli>(g1 - g0).count();
+      std::fprintf(stderr,
+                   "{\"gen_ms\": %.3f, \"h2d_ms\": %.3f, \"build_ms\": %.3f, \"query_ms\": %.3f, "
+                   "\"build_mpts_per_s\": %.2f, \"global_levels\": %d, \"subtree_max\": %d}\n",
+                   gen, h2d, bld, qry, double(N) / 1e3 / bld, b.global_levels(), b.subtree_max());
+    }
+    (void)hipFree(d_x); (void)hipFree(d_tree); (void)hipFree(d_ids); (void)hipFree(d_res); (void)hipFree(ws);
+    (void)hipStreamDestroy(s);
+  } catch (const std::exception& ex) {
+    std::cerr << "kdtree_gpu: " << ex.what() << std::endl;
+    return 2;
+  }
+  return 0;
+}

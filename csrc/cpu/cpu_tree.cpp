@@ -1,0 +1,179 @@
+// CPU kd-tree builders and searches on the implicit in-order layout (see cpu_tree.hpp).
+#include "pkdtree/cpu_tree.hpp"
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace pkdtree {
+
+namespace {
+
+struct ExactCtx {
+  const float* pts;
+  const u32* ids;
+  int dim;
+  int depth0;
+  u32* perm;
+};
+
+inline u64 ckey(const ExactCtx& c, u32 row, int axis) {
+  const u32 id = c.ids ? c.ids[row] : row;
+  return composite_key(c.pts[size_t(row) * size_t(c.dim) + size_t(axis)], id);
+}
+
+void exact_rec(const ExactCtx& c, i64 lo, i64 n, int depth, int spawn_levels) {
+  while (n > 1) {
+    const int axis = (c.depth0 + depth) % c.dim;
+    u32* b = c.perm + lo;
+    std::nth_element(b, b + n / 2, b + n, [&](u32 x, u32 y) { return ckey(c, x, axis) < ckey(c, y, axis); });
+    const i64 nl = left_n(n), nr = right_n(n);
+    if (spawn_levels > 0) {
+      std::thread t([&c, lo, nl, depth, spawn_levels] { exact_rec(c, lo, nl, depth + 1, spawn_levels - 1); });
+      exact_rec(c, lo + nl + 1, nr, depth + 1, spawn_levels - 1);
+      t.join();
+      return;
+    }
+    exact_rec(c, lo, nl, depth + 1, 0);
+    lo = lo + nl + 1;
+    n = nr;
+    ++depth;
+  }
+}
+
+void reference_rec(const float* pts, int dim, u32* perm, i64 lo, i64 n, int depth) {
+  // Mirrors build_tree_rec (kdtree_sequential.cpp:30-66) on an index array: the sort
+  // range deliberately excludes the last element of the segment.
+  while (n > 1) {
+    const int axis = depth % dim;
+    std::sort(perm + lo, perm + lo + (n - 1), [&](u32 a, u32 b) {
+      return pts[size_t(a) * size_t(dim) + size_t(axis)] < pts[size_t(b) * size_t(dim) + size_t(axis)];
+    });
+    const i64 nl = left_n(n), nr = right_n(n);
+    reference_rec(pts, dim, perm, lo, nl, depth + 1);
+    lo = lo + nl + 1;
+    n = nr;
+    ++depth;
+  }
+}
+
+struct SearchCtx {
+  const float* P;
+  int dim;
+  int depth0;
+  const float* q;
+};
+
+inline float d2_at(const SearchCtx& s, i64 slot) { return sq_dist(s.P + size_t(slot) * size_t(s.dim), s.q, s.dim); }
+
+// Returns the best slot of this subtree given the incoming best (never -1 unless n <= 0).
+i64 nearest_rec(const SearchCtx& s, i64 lo, i64 n, int depth, i64 best, float best_dist) {
+  if (n <= 0) return -1;
+  const int axis = (s.depth0 + depth) % s.dim;
+  const i64 m = median_pos(lo, n);
+  const float* p = s.P + size_t(m) * size_t(s.dim);
+  i64 best_local = best;
+  float bdl = best_dist;
+  const float d_e = sq_dist(p, s.q, s.dim);
+  const float d_axis = s.q[axis] - p[axis];
+  const float d_axis2 = d_axis * d_axis;
+  if (d_e < bdl) { best_local = m; bdl = d_e; }
+  const i64 l_lo = lo, l_n = left_n(n), r_lo = m + 1, r_n = right_n(n);
+  const bool go_left = d_axis < 0;
+  i64 further = go_left ? nearest_rec(s, l_lo, l_n, depth + 1, best_local, bdl)
+                        : nearest_rec(s, r_lo, r_n, depth + 1, best_local, bdl);
+  if (further >= 0) {
+    const float df = d2_at(s, further);
+    if (df < bdl) { bdl = df; best_local = further; }
+  }
+  if (d_axis2 < bdl) {
+    further = go_left ? nearest_rec(s, r_lo, r_n, depth + 1, best_local, bdl)
+                      : nearest_rec(s, l_lo, l_n, depth + 1, best_local, bdl);
+    if (further >= 0) {
+      const float df = d2_at(s, further);
+      if (df < bdl) best_local = further;
+    }
+  }
+  return best_local;
+}
+
+struct MinMax {
+  u64 mn, mx;
+};
+
+// Returns per-axis (min, max) composite keys of the subtree; counts violations.
+void check_rec(const float* P, const u32* ids, int dim, int depth0, i64 lo, i64 n, int depth,
+               MinMax* out, std::vector<std::vector<MinMax>>& scratch, i64& bad) {
+  for (int a = 0; a < dim; ++a) out[a] = {~u64(0), 0};
+  if (n <= 0) return;
+  if (scratch.size() < size_t(2 * (depth + 1))) scratch.resize(size_t(2 * (depth + 1)));
+  auto& L = scratch[size_t(2 * depth)];
+  auto& R = scratch[size_t(2 * depth + 1)];
+  L.assign(size_t(dim), {~u64(0), 0});
+  R.assign(size_t(dim), {~u64(0), 0});
+  const i64 m = median_pos(lo, n);
+  check_rec(P, ids, dim, depth0, lo, left_n(n), depth + 1, L.data(), scratch, bad);
+  check_rec(P, ids, dim, depth0, m + 1, right_n(n), depth + 1, R.data(), scratch, bad);
+  // scratch may have been resized by the recursion: re-fetch
+  auto& L2 = scratch[size_t(2 * depth)];
+  auto& R2 = scratch[size_t(2 * depth + 1)];
+  const int axis = (depth0 + depth) % dim;
+  const u64 km = composite_key(P[size_t(m) * size_t(dim) + size_t(axis)], ids[m]);
+  if (left_n(n) > 0 && !(L2[size_t(axis)].mx < km)) ++bad;
+  if (right_n(n) > 0 && !(R2[size_t(axis)].mn > km)) ++bad;
+  for (int a = 0; a < dim; ++a) {
+    const u64 k = composite_key(P[size_t(m) * size_t(dim) + size_t(a)], ids[m]);
+    out[a].mn = std::min({L2[size_t(a)].mn, R2[size_t(a)].mn, k});
+    out[a].mx = std::max({L2[size_t(a)].mx, R2[size_t(a)].mx, k});
+  }
+}
+
+}  // namespace
+
+void build_exact_cpu(const float* pts, const u32* ids, i64 n, int dim, int depth0, u32* perm, int threads) {
+  for (i64 i = 0; i < n; ++i) perm[i] = u32(i);
+  int spawn = 0;
+  while ((1 << spawn) < threads && spawn < 6) ++spawn;
+  ExactCtx c{pts, ids, dim, depth0, perm};
+  exact_rec(c, 0, n, 0, spawn);
+}
+
+void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm) {
+  for (i64 i = 0; i < n; ++i) perm[i] = u32(i);
+  reference_rec(pts, dim, perm, 0, n, 0);
+}
+
+void gather_rows(const float* pts, const u32* ids, const u32* perm, i64 n, int dim, float* tree_pts, u32* tree_ids) {
+  for (i64 k = 0; k < n; ++k) {
+    const u32 r = perm[k];
+    std::copy(pts + size_t(r) * size_t(dim), pts + size_t(r + 1) * size_t(dim), tree_pts + size_t(k) * size_t(dim));
+    if (tree_ids) tree_ids[k] = ids ? ids[r] : r;
+  }
+}
+
+NNResult nn_search_cpu(const float* tree_pts, i64 n, int dim, int depth0, const float* q) {
+  if (n <= 0) return {-1, 0.0f};
+  SearchCtx s{tree_pts, dim, depth0, q};
+  const i64 root = median_pos(0, n);
+  const i64 best = nearest_rec(s, 0, n, 0, root, d2_at(s, root));
+  return {best, d2_at(s, best)};
+}
+
+NNResult nn_brute_cpu(const float* pts, i64 n, int dim, const float* q) {
+  NNResult r{-1, 0.0f};
+  for (i64 i = 0; i < n; ++i) {
+    const float d = sq_dist(pts + size_t(i) * size_t(dim), q, dim);
+    if (r.slot < 0 || d < r.d2) r = {i, d};
+  }
+  return r;
+}
+
+i64 count_invariant_violations(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0) {
+  std::vector<MinMax> root(static_cast<size_t>(dim));
+  std::vector<std::vector<MinMax>> scratch(size_t(2 * (tree_height(n) + 2)));
+  i64 bad = 0;
+  check_rec(tree_pts, tree_ids, dim, depth0, 0, n, 0, root.data(), scratch, bad);
+  return bad;
+}
+
+}  // namespace pkdtree

@@ -1,0 +1,734 @@
+// Global (HBM-streaming) levels of the level-synchronous kd-tree build + the host plan.
+//
+// Per global level l (segments = contiguous slot ranges of the implicit tree):
+//   k_select    one workgroup per segment: prefix-scan the segment's bucket histogram and
+//               pick the bucket b* that holds rank n/2 (exact counts: below / inside b*).
+//   k_partition grid over all points: bucket -> zone (left / middle / right of b*), each
+//               wave ranks its points per zone with ballots, one atomic per zone reserves a
+//               run in the destination, rows are moved SoA (coalesced runs), and the next
+//               level's histogram (next axis, child segment) is accumulated in LDS on the
+//               fly and flushed once per block.
+//   k_refine    one workgroup per segment: ranks the middle zone (typically a handful of
+//               points; radix passes on the 64-bit (key,id) composite when it is large)
+//               so the exact median lands on slot lo+n/2 and is written to the output.
+// Replaces build_tree_rec's per-node std::sort (kdtree_sequential.cpp:30-66).
+#include <algorithm>
+#include <cstdio>
+#include <sstream>
+
+#include "device_utils.hpp"
+#include "pkdtree/gpu_build.hpp"
+#include "pkdtree/hip_check.hpp"
+#include "subtree.hpp"
+
+namespace pkdtree {
+
+using dev::BucketParams;
+using dev::bucket_of;
+using dev::make_params;
+using dev::mbcnt;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kItems = 16;                  // kItems * 4 waves = 64 (i,wave) groups per chunk
+constexpr int kChunk = kBlock * kItems;     // 4096 points per partition chunk
+constexpr int kMaxBins = 4096;              // per-segment histogram bins (global levels)
+constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one workgroup
+constexpr int kRadixBits = 11;
+constexpr int kRadixBins = 1 << kRadixBits;
+
+struct SegState {
+  u32 bstar;
+  u32 cnt_less;
+  u32 cnt_mid;
+  u32 pad;
+  u32 cur[4];                 // zone cursors (relative to segment start)
+  unsigned long long mid_min;  // composite (key,id) range of the middle zone
+  unsigned long long mid_max;
+};
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------------------
+// Geometry: heap-ordered (lo, n) of every segment of levels 0..L (node h: children 2h+1,
+// 2h+2). Deterministic from n, so it is computed on the device once per build.
+__global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i64 heap_nodes, i64 n) {
+  const i64 h = i64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (h >= heap_nodes) return;
+  const int l = 63 - __builtin_clzll(u64(h + 1));
+  const i64 j = h + 1 - (i64(1) << l);
+  i64 lo = 0, m = n;
+  for (int b = l - 1; b >= 0; --b) {
+    if ((j >> b) & 1) {
+      lo = lo + m / 2 + 1;
+      m = m - m / 2 - 1;
+    } else {
+      m = m / 2;
+    }
+    if (m < 0) m = 0;
+  }
+  seg_lo[h] = lo;
+  seg_n[h] = m;
+}
+
+// ---------------------------------------------------------------------------------------
+// AoS input -> SoA working columns (+ ids column) and the bounding box (orderable u32).
+__global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                 u32 id_base, float* __restrict__ cols, i64 n, int dim,
+                                                 u32* __restrict__ bbox) {
+  extern __shared__ __align__(16) u32 sbox[];  // [2*dim]
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sbox[c] = (c < dim) ? 0xffffffffu : 0u;
+  __syncthreads();
+  const i64 total = n * i64(dim);
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 f = i64(blockIdx.x) * kBlock + threadIdx.x; f < total; f += stride) {
+    const float v = pts[f];
+    const i64 r = f / dim;
+    const int c = int(f - r * dim);
+    cols[i64(c) * n + r] = v;
+    const u32 k = orderable(v);
+    atomicMin(&sbox[c], k);
+    atomicMax(&sbox[dim + c], k);
+  }
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * n);
+  for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride)
+    idcol[r] = ids ? ids[r] : id_base + u32(r);
+  __syncthreads();
+  for (int c = threadIdx.x; c < dim; c += kBlock) {
+    atomicMin(&bbox[c], sbox[c]);
+    atomicMax(&bbox[dim + c], sbox[dim + c]);
+  }
+}
+
+// bbox over SoA columns (distributed path: points arrive already in SoA).
+__global__ __launch_bounds__(kBlock) void k_bbox_soa(const float* __restrict__ cols, i64 n, int dim,
+                                                     u32* __restrict__ bbox) {
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (int c = 0; c < dim; ++c) {
+    u32 mn = 0xffffffffu, mx = 0u;
+    for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
+      const u32 k = orderable(cols[i64(c) * n + r]);
+      mn = min(mn, k);
+      mx = max(mx, k);
+    }
+    mn = dev::wave_min_u32(mn);
+    mx = dev::wave_max_u32(mx);
+    if (dev::lane() == 0) {
+      atomicMin(&bbox[c], mn);
+      atomicMax(&bbox[dim + c], mx);
+    }
+  }
+}
+
+__global__ void k_bbox_init(u32* bbox, int dim) {
+  for (int c = threadIdx.x; c < 2 * dim; c += blockDim.x) bbox[c] = (c < dim) ? 0xffffffffu : 0u;
+}
+
+// Root cell = bounding box; root bucketing parameters for the level-0 axis.
+__global__ void k_root(const u32* __restrict__ bbox, int dim, float* __restrict__ cells,
+                       BucketParams* __restrict__ params, int axis0, int bins0) {
+  for (int c = threadIdx.x; c < dim; c += blockDim.x) {
+    cells[2 * c] = from_orderable(bbox[c]);
+    cells[2 * c + 1] = from_orderable(bbox[dim + c]);
+  }
+  if (threadIdx.x == 0)
+    params[0] = make_params(from_orderable(bbox[axis0]), from_orderable(bbox[dim + axis0]), bins0);
+}
+
+// ---------------------------------------------------------------------------------------
+struct LevelArgs {
+  const float* src;      // SoA columns of this level's input (dim coords + ids)
+  float* dst;            // SoA columns of this level's output
+  i64 ncol;              // column stride (= n)
+  int dim;
+  const i64* seg_lo;
+  const i64* seg_n;
+  SegState* state;       // heap-indexed
+  BucketParams* params;  // heap-indexed (this level's axis)
+  float* cells;          // heap-indexed [h][dim][2]
+  i64 heap0;             // heap index of segment 0 of this level
+  int bps;               // partition blocks per segment
+  int axis;
+  int next_axis;
+  int bins;
+  int next_bins;         // 0 => next level is not a global level (no fused histogram)
+  const u32* hist;       // this level's histograms [segs][bins]
+  u32* hist_next;        // next level's histograms [2*segs][next_bins]
+  float* out_pts;
+  u32* out_ids;
+  u32* err;              // sticky error word (bit 0: partition overflow, bit 1: refine)
+};
+
+// Histogram of a level's keys (used for the first global level only; later levels get
+// theirs from the fused partition pass).
+__global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ hist) {
+  extern __shared__ __align__(16) u32 sh[];
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  for (int b = threadIdx.x; b < a.bins; b += kBlock) sh[b] = 0;
+  __syncthreads();
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const BucketParams p = a.params[h];
+  const float* key = a.src + i64(a.axis) * a.ncol + lo;
+  for (i64 e = b0 + threadIdx.x; e < b1; e += kBlock) atomicAdd(&sh[bucket_of(key[e], p, a.bins)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < a.bins; b += kBlock) {
+    const u32 v = sh[b];
+    if (v) atomicAdd(&hist[s * a.bins + b], v);
+  }
+}
+
+// Block-wide exclusive scan of one value per thread (256 threads).
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* sh4, u32* total) {
+  const int w = threadIdx.x / 64;
+  const u32 incl = dev::wave_incl_scan(v);
+  if (dev::lane() == 63) sh4[w] = incl;
+  __syncthreads();
+  u32 off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; ++k) {
+    const u32 t = sh4[k];
+    if (k < w) off += t;
+    tot += t;
+  }
+  *total = tot;
+  return off + incl - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
+  __shared__ u32 sh4[4];
+  __shared__ u32 found[3];
+  const i64 s = blockIdx.x;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  // Children's histograms are zeroed even for empty segments (their select reads them).
+  if (a.next_bins > 0) {
+    u32* hn = a.hist_next + (2 * s) * a.next_bins;
+    for (int b = threadIdx.x; b < 2 * a.next_bins; b += kBlock) hn[b] = 0;
+  }
+  if (n <= 0) return;
+  const u32 r = u32(n / 2);
+  const u32* hs = a.hist + s * a.bins;
+  const int per = (a.bins + kBlock - 1) / kBlock;
+  const int b0 = min(a.bins, int(threadIdx.x) * per), b1 = min(a.bins, b0 + per);
+  u32 sum = 0;
+  for (int b = b0; b < b1; ++b) sum += hs[b];
+  u32 total;
+  const u32 excl = block_excl_scan(sum, sh4, &total);
+  if (r >= excl && r < excl + sum) {
+    u32 c = excl;
+    for (int b = b0; b < b1; ++b) {
+      const u32 v = hs[b];
+      if (r < c + v) {
+        found[0] = u32(b);
+        found[1] = c;
+        found[2] = v;
+        break;
+      }
+      c += v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    SegState st;
+    st.bstar = found[0];
+    st.cnt_less = found[1];
+    st.cnt_mid = found[2];
+    st.pad = 0;
+    st.cur[0] = 0;
+    st.cur[1] = found[1];
+    st.cur[2] = found[1] + found[2];
+    st.cur[3] = 0;
+    st.mid_min = ~0ull;
+    st.mid_max = 0ull;
+    a.state[h] = st;
+    if (a.next_bins > 0) {
+      // Children's bucketing on the next axis. For dim > 1 the child cell on that axis is
+      // the parent's; for dim == 1 it is approximated from the bucket edges (any monotone
+      // bucketing is correct, this only sets the resolution).
+      const float* cell = a.cells + h * 2 * a.dim;
+      const float clo = cell[2 * a.next_axis], chi = cell[2 * a.next_axis + 1];
+      BucketParams pl = make_params(clo, chi, a.next_bins), pr = pl;
+      if (a.next_axis == a.axis) {
+        const BucketParams p = a.params[h];
+        if (p.scale > 0.0f) {
+          const float e_hi = p.lo + float(st.bstar + 1) / p.scale;
+          const float e_lo = p.lo + float(st.bstar) / p.scale;
+          pl = make_params(clo, fminf(chi, e_hi), a.next_bins);
+          pr = make_params(fmaxf(clo, e_lo), chi, a.next_bins);
+        }
+      }
+      a.params[2 * h + 1] = pl;
+      a.params[2 * h + 2] = pr;
+    }
+  }
+}
+
+template <int DIMC>  // DIMC > 0: compile-time dim; 0: runtime
+__global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
+  extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
+  __shared__ u32 gcnt[3][64];
+  const int dim = DIMC > 0 ? DIMC : a.dim;
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const bool fuse = a.next_bins > 0;
+  if (fuse) {
+    for (int b = threadIdx.x; b < 2 * a.next_bins; b += kBlock) nh[b] = 0;
+  }
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  SegState* st = a.state + h;
+  const u32 bstar = st->bstar;
+  const BucketParams prm = a.params[h];
+  BucketParams cprm[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  if (fuse) {
+    cprm[0] = a.params[2 * h + 1];
+    cprm[1] = a.params[2 * h + 2];
+  }
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  const i64 nc = a.ncol;
+  const int w = threadIdx.x / 64;
+  const int ln = dev::lane();
+  __syncthreads();
+
+  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+    u32 zone_pre[kItems];  // (zone << 16) | rank-in-wave
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const i64 e = c0 + i * kBlock + threadIdx.x;
+      const bool valid = e < b1;
+      u32 z = 3;
+      if (valid) {
+        const float key = src[i64(a.axis) * nc + lo + e];
+        const u32 b = bucket_of(key, prm, a.bins);
+        z = b < bstar ? 0u : (b == bstar ? 1u : 2u);
+      }
+      const u64 m0 = __ballot(z == 0), m1 = __ballot(z == 1), m2 = __ballot(z == 2);
+      if (ln == 0) {
+        gcnt[0][i * 4 + w] = __popcll(m0);
+        gcnt[1][i * 4 + w] = __popcll(m1);
+        gcnt[2][i * 4 + w] = __popcll(m2);
+      }
+      const u64 mz = z == 0 ? m0 : (z == 1 ? m1 : m2);
+      zone_pre[i] = (z << 16) | mbcnt(mz);
+      if (m1 != 0 && z == 1) {  // rare: track the middle zone's composite key range
+        const u32 id = reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e];
+        const u64 k = composite_key(src[i64(a.axis) * nc + lo + e], id);
+        atomicMin(&st->mid_min, (unsigned long long)k);
+        atomicMax(&st->mid_max, (unsigned long long)k);
+      }
+    }
+    __syncthreads();
+    if (w < 3) {  // wave w scans zone w over the 64 (item, wave) groups in slot order
+      const u32 v = gcnt[w][ln];
+      const u32 incl = dev::wave_incl_scan(v);
+      const u32 tot = __shfl(incl, 63, 64);
+      u32 base = 0;
+      if (ln == 0 && tot) base = atomicAdd(&st->cur[w], tot);
+      base = __shfl(base, 0, 64);
+      gcnt[w][ln] = base + incl - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const i64 e = c0 + i * kBlock + threadIdx.x;
+      const u32 z = zone_pre[i] >> 16;
+      if (z < 3) {
+        const i64 p = lo + e;
+        const i64 q = lo + i64(gcnt[z][i * 4 + w] + (zone_pre[i] & 0xffffu));
+        if (q >= lo + n) {  // impossible unless the histogram and the keys disagree
+          atomicOr(a.err, 1u);
+          continue;
+        }
+        for (int c = 0; c <= dim; ++c) dst[i64(c) * nc + q] = src[i64(c) * nc + p];
+        if (fuse && z != 1) {
+          const int child = z == 0 ? 0 : 1;
+          const u32 nb = bucket_of(src[i64(a.next_axis) * nc + p], cprm[child], a.next_bins);
+          atomicAdd(&nh[child * a.next_bins + nb], 1u);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (fuse) {
+    u32* hn = a.hist_next + (2 * s) * a.next_bins;
+    for (int b = threadIdx.x; b < 2 * a.next_bins; b += kBlock) {
+      const u32 v = nh[b];
+      if (v) atomicAdd(&hn[b], v);
+    }
+  }
+}
+
+// Bitonic sort of (key, idx) pairs in LDS, cnt <= cap (cap a power of two).
+__device__ void block_bitonic(u64* keys, u32* idx, int cnt, int cap) {
+  int np = 1;
+  while (np < cnt) np <<= 1;
+  for (int i = cnt + threadIdx.x; i < np; i += kBlock) {
+    keys[i] = ~0ull;
+    idx[i] = 0xffffffffu;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np; i += kBlock) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const u64 ki = keys[i], kl = keys[l];
+          if ((ki > kl) == up) {
+            keys[i] = kl;
+            keys[l] = ki;
+            const u32 t = idx[i];
+            idx[i] = idx[l];
+            idx[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  (void)cap;
+}
+
+// Adds the next-level histogram contribution of a middle point that ended on `side`.
+__device__ __forceinline__ void add_next_hist(const LevelArgs& a, i64 s, i64 h, int side, float nkey) {
+  const BucketParams p = a.params[2 * h + 1 + side];
+  const u32 nb = bucket_of(nkey, p, a.next_bins);
+  atomicAdd(&a.hist_next[(2 * s + side) * a.next_bins + nb], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
+  __shared__ u64 keys[kRefineCap];
+  __shared__ u32 idx[kRefineCap];
+  __shared__ u32 rh[kRadixBins];
+  __shared__ u32 sh4[4];
+  __shared__ u32 info[4];
+  const int dim = a.dim;
+  const i64 s = blockIdx.x;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  if (n <= 0) return;
+  const i64 lo = a.seg_lo[h];
+  const SegState st = a.state[h];
+  const i64 nc = a.ncol;
+  float* __restrict__ dst = a.dst;           // the middle zone lives here
+  float* __restrict__ alt = const_cast<float*>(a.src);  // dead input buffer: staging area
+  const bool fuse = a.next_bins > 0;
+  i64 zlo = lo + st.cnt_less;
+  i64 zc = st.cnt_mid;
+  i64 t = n / 2 - i64(st.cnt_less);
+  auto ckey = [&](i64 p) -> u64 {
+    const u32 id = reinterpret_cast<const u32*>(dst)[i64(dim) * nc + p];
+    return composite_key(dst[i64(a.axis) * nc + p], id);
+  };
+  auto copy_row = [&](float* to, i64 q, const float* from, i64 p) {
+    for (int c = 0; c <= dim; ++c) to[i64(c) * nc + q] = from[i64(c) * nc + p];
+  };
+
+  // Large middle zone (heavy duplicates, or a huge segment): radix passes over the
+  // composite key, 11 bits at a time starting at the highest differing bit.
+  if (zc > kRefineCap) {
+    const u64 diff = u64(st.mid_min) ^ u64(st.mid_max);
+    int hb = diff ? 63 - __builtin_clzll(diff) : 0;
+    while (zc > kRefineCap) {
+      const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
+      for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
+      __syncthreads();
+      for (i64 e = threadIdx.x; e < zc; e += kBlock)
+        atomicAdd(&rh[u32(ckey(zlo + e) >> shift) & (kRadixBins - 1)], 1u);
+      __syncthreads();
+      {
+        const int per = kRadixBins / kBlock;
+        u32 sum = 0;
+        for (int b = 0; b < per; ++b) sum += rh[threadIdx.x * per + b];
+        u32 total;
+        const u32 excl = block_excl_scan(sum, sh4, &total);
+        if (u64(t) >= excl && u64(t) < u64(excl) + sum) {
+          u32 c = excl;
+          for (int b = 0; b < per; ++b) {
+            const u32 v = rh[threadIdx.x * per + b];
+            if (u64(t) < u64(c) + v) {
+              info[0] = u32(threadIdx.x * per + b);
+              info[1] = c;
+              info[2] = v;
+              break;
+            }
+            c += v;
+          }
+        }
+        __syncthreads();
+      }
+      const u32 bsel = info[0], cl = info[1], ce = info[2];
+      if (threadIdx.x == 0) {
+        rh[0] = 0;       // reuse as cursors
+        rh[1] = cl;
+        rh[2] = cl + ce;
+      }
+      __syncthreads();
+      for (i64 e0 = 0; e0 < zc; e0 += kBlock) {
+        const i64 e = e0 + threadIdx.x;
+        u32 z = 3;
+        if (e < zc) {
+          const u32 d = u32(ckey(zlo + e) >> shift) & (kRadixBins - 1);
+          z = d < bsel ? 0u : (d == bsel ? 1u : 2u);
+        }
+        u32 dest = 0;
+#pragma unroll
+        for (u32 zz = 0; zz < 3; ++zz) {
+          const u64 m = __ballot(z == zz);
+          if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            u32 base = 0;
+            if (dev::lane() == leader) base = atomicAdd(&rh[zz], u32(__popcll(m)));
+            base = __shfl(base, leader, 64);
+            if (z == zz) dest = base + mbcnt(m);
+          }
+        }
+        if (z < 3 && dest >= zc) {
+          atomicOr(a.err, 2u);
+          z = 3;
+        }
+        if (z < 3) {
+          copy_row(alt, zlo + dest, dst, zlo + e);
+          if (fuse && z != 1) add_next_hist(a, s, h, z == 0 ? 0 : 1, dst[i64(a.next_axis) * nc + zlo + e]);
+        }
+      }
+      __syncthreads();
+      for (i64 e = threadIdx.x; e < zc; e += kBlock) copy_row(dst, zlo + e, alt, zlo + e);
+      __syncthreads();
+      zlo += cl;
+      zc = ce;
+      t -= cl;
+      if (shift == 0) break;
+      hb = shift - 1;
+    }
+  }
+
+  // Final ranking of the (small) middle zone.
+  const i64 mpos = lo + n / 2;
+  if (zc <= 64) {
+    if (threadIdx.x < 64) {
+      const int l = dev::lane();
+      const bool valid = l < zc;
+      const u64 k = valid ? ckey(zlo + l) : ~0ull;
+      u32 rank = 0;
+      for (int j = 0; j < zc; ++j) rank += dev::shfl_u64(k, j) < k ? 1u : 0u;
+      if (valid && rank < zc) copy_row(alt, zlo + rank, dst, zlo + l);
+    }
+  } else {
+    for (i64 e = threadIdx.x; e < zc; e += kBlock) {
+      keys[e] = ckey(zlo + e);
+      idx[e] = u32(e);
+    }
+    __syncthreads();
+    block_bitonic(keys, idx, int(zc), kRefineCap);
+    for (i64 k = threadIdx.x; k < zc; k += kBlock) copy_row(alt, zlo + k, dst, zlo + idx[k]);
+  }
+  __syncthreads();
+  for (i64 e = threadIdx.x; e < zc; e += kBlock) {
+    const i64 q = zlo + e;
+    copy_row(dst, q, alt, q);
+    if (e == t) {
+      for (int c = 0; c < dim; ++c) a.out_pts[mpos * dim + c] = alt[i64(c) * nc + q];
+      a.out_ids[mpos] = reinterpret_cast<const u32*>(alt)[i64(dim) * nc + q];
+    } else if (fuse) {
+      add_next_hist(a, s, h, e < t ? 0 : 1, alt[i64(a.next_axis) * nc + q]);
+    }
+  }
+  // Children cells: the split value bounds the split axis.
+  const float split = alt[i64(a.axis) * nc + zlo + t];
+  const float* cell = a.cells + h * 2 * dim;
+  float* cl_ = a.cells + (2 * h + 1) * 2 * dim;
+  float* cr_ = a.cells + (2 * h + 2) * 2 * dim;
+  for (int c = threadIdx.x; c < dim; c += kBlock) {
+    const float clo = cell[2 * c], chi = cell[2 * c + 1];
+    cl_[2 * c] = clo;
+    cl_[2 * c + 1] = c == a.axis ? split : chi;
+    cr_[2 * c] = c == a.axis ? split : clo;
+    cr_[2 * c + 1] = chi;
+  }
+}
+
+int pow2_floor(i64 v) {
+  int p = 1;
+  while (i64(p) * 2 <= v) p *= 2;
+  return p;
+}
+
+int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 8)))); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+int default_subtree_max(int dim) { return subtree_capacity(dim); }
+
+GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
+  if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
+  if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
+  nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity(dim)) : subtree_capacity(dim);
+  lg_ = 0;
+  while ((n_ >> lg_) > nsub_) ++lg_;
+  heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
+  max_bins_ = 0;
+  max_hist_ = 1;
+  for (int l = 0; l < lg_; ++l) {
+    LevelPlan lp;
+    lp.level = l;
+    lp.segs = i64(1) << l;
+    lp.nmax = n_ >> l;
+    lp.bins = global_bins(lp.nmax);
+    lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
+    const i64 range = std::max<i64>(kChunk * 16, i64(kChunk));
+    lp.bps = int(std::max<i64>(1, (lp.nmax + range - 1) / range));
+    lp.axis = (opt.depth0 + l) % dim;
+    levels_.push_back(lp);
+    max_bins_ = std::max(max_bins_, lp.bins);
+    max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
+  }
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + std::max<size_t>(bytes, 1));
+    return o;
+  };
+  const size_t colbytes = size_t(dim + 1) * size_t(std::max<i64>(n, 1)) * 4;
+  off_cols_a_ = take(colbytes);
+  off_cols_b_ = take(colbytes);
+  off_seg_lo_ = take(size_t(heap_nodes_) * 8);
+  off_seg_n_ = take(size_t(heap_nodes_) * 8);
+  off_state_ = take(size_t(heap_nodes_) * sizeof(SegState));
+  off_params_ = take(size_t(heap_nodes_) * sizeof(BucketParams));
+  off_cells_ = take(size_t(heap_nodes_) * size_t(2 * dim) * 4);
+  off_hist0_ = take(size_t(max_hist_) * 4);
+  off_hist1_ = take(size_t(max_hist_) * 4);
+  off_bbox_ = take(size_t(2 * dim) * 4);
+  off_err_ = take(16);
+  ws_bytes_ = off;
+}
+
+std::string GpuBuilder::describe() const {
+  std::ostringstream os;
+  os << "GpuBuilder(n=" << n_ << ", dim=" << dim_ << ", global_levels=" << lg_ << ", subtree_max=" << nsub_
+     << ", workspace=" << ws_bytes_ << "B)";
+  for (const auto& lp : levels_)
+    os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
+       << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis;
+  return os.str();
+}
+
+u32 GpuBuilder::read_error(const void* workspace, hipStream_t stream) const {
+  u32 e = 0;
+  PKD_HIP_CHECK(hipMemcpyAsync(&e, static_cast<const char*>(workspace) + off_err_, 4, hipMemcpyDeviceToHost, stream));
+  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  return e;
+}
+
+float* GpuBuilder::soa_input(void* workspace) const {
+  return reinterpret_cast<float*>(static_cast<char*>(workspace) + off_cols_a_);
+}
+
+void GpuBuilder::build(const float* pts, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
+                       void* workspace, hipStream_t stream) const {
+  if (n_ == 0) return;
+  char* ws = static_cast<char*>(workspace);
+  float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
+  u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
+  k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
+  const i64 total = n_ * dim_;
+  const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
+  k_prep<<<grid, kBlock, size_t(2 * dim_) * 4, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox);
+  PKD_LAUNCH_CHECK();
+  run_levels(out_pts, out_ids, ws, stream);
+}
+
+void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
+  if (n_ == 0) return;
+  char* ws = static_cast<char*>(workspace);
+  float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
+  u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
+  k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
+  const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
+  k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, bbox);
+  PKD_LAUNCH_CHECK();
+  run_levels(out_pts, out_ids, ws, stream);
+}
+
+void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const {
+  float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
+  float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
+  i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
+  i64* seg_n = reinterpret_cast<i64*>(ws + off_seg_n_);
+  SegState* state = reinterpret_cast<SegState*>(ws + off_state_);
+  BucketParams* params = reinterpret_cast<BucketParams*>(ws + off_params_);
+  float* cells = reinterpret_cast<float*>(ws + off_cells_);
+  u32* hist[2] = {reinterpret_cast<u32*>(ws + off_hist0_), reinterpret_cast<u32*>(ws + off_hist1_)};
+  u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
+  u32* err = reinterpret_cast<u32*>(ws + off_err_);
+  PKD_HIP_CHECK(hipMemsetAsync(err, 0, 16, stream));
+
+  k_geometry<<<int((heap_nodes_ + kBlock - 1) / kBlock), kBlock, 0, stream>>>(seg_lo, seg_n, heap_nodes_, n_);
+  PKD_LAUNCH_CHECK();
+  const int axis0 = opt_.depth0 % dim_;
+  k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
+  PKD_LAUNCH_CHECK();
+
+  float* src = colsA;
+  float* dst = colsB;
+  for (int l = 0; l < lg_; ++l) {
+    const LevelPlan& lp = levels_[size_t(l)];
+    LevelArgs a;
+    a.src = src;
+    a.dst = dst;
+    a.ncol = n_;
+    a.dim = dim_;
+    a.seg_lo = seg_lo;
+    a.seg_n = seg_n;
+    a.state = state;
+    a.params = params;
+    a.cells = cells;
+    a.heap0 = lp.segs - 1;
+    a.bps = lp.bps;
+    a.axis = lp.axis;
+    a.next_axis = (opt_.depth0 + l + 1) % dim_;
+    a.bins = lp.bins;
+    a.next_bins = lp.next_bins;
+    a.hist = hist[l & 1];
+    a.hist_next = hist[(l + 1) & 1];
+    a.out_pts = out_pts;
+    a.out_ids = out_ids;
+    a.err = err;
+    if (l == 0) {
+      PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
+      k_hist<<<int(lp.segs * lp.bps), kBlock, size_t(lp.bins) * 4, stream>>>(a, hist[0]);
+      PKD_LAUNCH_CHECK();
+    }
+    k_select<<<int(lp.segs), kBlock, 0, stream>>>(a);
+    PKD_LAUNCH_CHECK();
+    const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
+    const int grid = int(lp.segs * lp.bps);
+    switch (dim_) {
+      case 1: k_partition<1><<<grid, kBlock, lds, stream>>>(a); break;
+      case 2: k_partition<2><<<grid, kBlock, lds, stream>>>(a); break;
+      case 3: k_partition<3><<<grid, kBlock, lds, stream>>>(a); break;
+      case 4: k_partition<4><<<grid, kBlock, lds, stream>>>(a); break;
+      case 8: k_partition<8><<<grid, kBlock, lds, stream>>>(a); break;
+      default: k_partition<0><<<grid, kBlock, lds, stream>>>(a); break;
+    }
+    PKD_LAUNCH_CHECK();
+    k_refine<<<int(lp.segs), kBlock, 0, stream>>>(a);
+    PKD_LAUNCH_CHECK();
+    std::swap(src, dst);
+  }
+  const i64 heap0 = (i64(1) << lg_) - 1;
+  launch_subtree(src, n_, dim_, seg_lo, seg_n, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts, out_ids,
+                 stream);
+}
+
+}  // namespace pkdtree

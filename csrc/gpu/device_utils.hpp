@@ -1,0 +1,97 @@
+// Wave64 / workgroup helpers for gfx950 (CDNA4). Wave width is 64 everywhere: ballots are
+// 64-bit, lane ranks come from v_mbcnt, scans use 64-lane shuffles.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pkdtree/common.hpp"
+
+namespace pkdtree {
+namespace dev {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane() { return int(__lane_id()); }
+
+// Number of set bits of `mask` in lanes below this one.
+__device__ __forceinline__ u32 mbcnt(u64 mask) {
+  return __builtin_amdgcn_mbcnt_hi(u32(mask >> 32), __builtin_amdgcn_mbcnt_lo(u32(mask), 0u));
+}
+
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  const int l = lane();
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const u32 t = __shfl_up(v, o, kWave);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+// Inclusive scan inside aligned groups of G lanes (G power of two <= 64).
+template <int G>
+__device__ __forceinline__ u32 group_incl_scan(u32 v) {
+  const int l = lane() & (G - 1);
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const u32 t = __shfl_up(v, o, G);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ u32 wave_min_u32(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (u32)__shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ u32 wave_max_u32(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (u32)__shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+  const u32 lo = __shfl(u32(v), src, kWave);
+  const u32 hi = __shfl(u32(v >> 32), src, kWave);
+  return (u64(hi) << 32) | lo;
+}
+__device__ __forceinline__ u64 wave_min_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 t = shfl_u64(v, lane() ^ o);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 t = shfl_u64(v, lane() ^ o);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
+// Bucketing used by every histogram/partition pair. Monotone non-decreasing in x, so the
+// bucket order never contradicts the key order; identical inputs give identical buckets
+// in every kernel (-ffp-contract=off, no FMA possible in this expression).
+struct BucketParams {
+  float lo;
+  float scale;
+};
+
+__device__ __forceinline__ u32 bucket_of(float x, BucketParams p, int nb) {
+  float t = (x - p.lo) * p.scale;
+  t = fminf(fmaxf(t, 0.0f), float(nb - 1));
+  return u32(t);
+}
+
+PKD_HD BucketParams make_params(float lo, float hi, int nb) {
+  BucketParams p;
+  p.lo = lo;
+  const float span = hi - lo;
+  p.scale = (span > 0.0f) ? float(nb) / span : 0.0f;
+  return p;
+}
+
+}  // namespace dev
+}  // namespace pkdtree

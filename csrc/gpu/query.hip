@@ -1,0 +1,148 @@
+// Exact 1-NN kernels (see gpu_query.hpp).
+#include <algorithm>
+
+#include "device_utils.hpp"
+#include "pkdtree/gpu_query.hpp"
+#include "pkdtree/hip_check.hpp"
+
+namespace pkdtree {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kQTile = 16;     // queries per brute-force tile (registers per thread)
+constexpr int kStack = 64;     // traversal stack (tree height <= 33 for n < 2^32)
+
+__global__ void k_init(u64* out, i64 nq) {
+  const i64 i = i64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < nq) out[i] = kPackedInf;
+}
+
+// grid.x: point blocks, grid.y: query tiles. Queries of the tile are staged in LDS.
+__global__ __launch_bounds__(kBlock) void k_brute(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                  u32 id_base, i64 n, int dim, const float* __restrict__ queries,
+                                                  i64 nq, u64* __restrict__ out) {
+  extern __shared__ __align__(16) float qs[];  // [kQTile][dim]
+  const i64 q0 = i64(blockIdx.y) * kQTile;
+  const int qt = int(std::min<i64>(kQTile, nq - q0));
+  for (int f = threadIdx.x; f < qt * dim; f += kBlock) qs[f] = queries[q0 * dim + f];
+  __syncthreads();
+  u64 best[kQTile];
+#pragma unroll
+  for (int k = 0; k < kQTile; ++k) best[k] = kPackedInf;
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
+    const float* p = pts + r * dim;
+    const u32 id = ids ? ids[r] : id_base + u32(r);
+#pragma unroll
+    for (int k = 0; k < kQTile; ++k) {
+      if (k < qt) {
+        const float d2 = sq_dist(p, qs + k * dim, dim);
+        const u64 v = pack_dist_idx(d2, id);
+        best[k] = v < best[k] ? v : best[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kQTile; ++k) {
+    if (k < qt) {
+      const u64 v = dev::wave_min_u64(best[k]);
+      if (dev::lane() == 0 && v != kPackedInf) atomicMin((unsigned long long*)&out[q0 + k], (unsigned long long)v);
+    }
+  }
+}
+
+// One thread per query; explicit stack of far children with their lower bound.
+__global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P, const u32* __restrict__ ids, i64 n,
+                                                     int dim, int depth0, const float* __restrict__ queries, i64 nq,
+                                                     u64* __restrict__ out) {
+  const i64 qi = i64(blockIdx.x) * kBlock + threadIdx.x;
+  if (qi >= nq || n <= 0) return;
+  const float* q = queries + qi * dim;
+  u32 st_lo[kStack], st_n[kStack];
+  unsigned char st_d[kStack];
+  float st_b[kStack];
+  int sp = 0;
+  u64 best = out[qi];
+  float bd = packed_dist(best);
+  u32 lo = 0, cnt = u32(n);
+  int depth = 0;
+  for (;;) {
+    while (cnt > 0) {
+      const u32 m = lo + cnt / 2;
+      const float* p = P + i64(m) * dim;
+      const float d2 = sq_dist(p, q, dim);
+      const u64 v = pack_dist_idx(d2, ids[m]);
+      if (v < best) {
+        best = v;
+        bd = d2;
+      }
+      const int axis = (depth0 + depth) % dim;
+      const float dax = q[axis] - p[axis];
+      const float dax2 = dax * dax;
+      const u32 ln_ = cnt / 2, rn = cnt - cnt / 2 - 1;
+      u32 near_lo, near_n, far_lo, far_n;
+      if (dax < 0) {
+        near_lo = lo; near_n = ln_; far_lo = m + 1; far_n = rn;
+      } else {
+        near_lo = m + 1; near_n = rn; far_lo = lo; far_n = ln_;
+      }
+      if (far_n > 0 && dax2 <= bd && sp < kStack) {
+        st_lo[sp] = far_lo;
+        st_n[sp] = far_n;
+        st_d[sp] = (unsigned char)(depth + 1);
+        st_b[sp] = dax2;
+        ++sp;
+      }
+      lo = near_lo;
+      cnt = near_n;
+      ++depth;
+    }
+    bool found = false;
+    while (sp > 0) {
+      --sp;
+      if (st_b[sp] <= bd) {
+        lo = st_lo[sp];
+        cnt = st_n[sp];
+        depth = st_d[sp];
+        found = true;
+        break;
+      }
+    }
+    if (!found) break;
+  }
+  out[qi] = best;
+}
+
+}  // namespace
+
+void nn_init(u64* out, i64 nq, hipStream_t stream) {
+  if (nq <= 0) return;
+  k_init<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(out, nq);
+  PKD_LAUNCH_CHECK();
+}
+
+void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq, u64* out,
+              hipStream_t stream) {
+  if (nq <= 0 || n <= 0) return;
+  const i64 tiles = (nq + kQTile - 1) / kQTile;
+  // enough point blocks to fill 256 CUs several times over across all query tiles
+  const i64 want = std::max<i64>(1, 2048 / tiles);
+  const int gx = int(std::min<i64>(want, (n + kBlock - 1) / kBlock));
+  for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
+    const i64 ty = std::min<i64>(65535, tiles - t0);
+    k_brute<<<dim3(unsigned(gx), unsigned(ty)), kBlock, size_t(kQTile) * dim * 4, stream>>>(
+        pts, ids, id_base, n, dim, queries + t0 * kQTile * dim, nq - t0 * kQTile, out + t0 * kQTile);
+    PKD_LAUNCH_CHECK();
+  }
+}
+
+void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries, i64 nq,
+                 u64* out, hipStream_t stream) {
+  if (nq <= 0 || n <= 0) return;
+  k_traverse<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries, nq,
+                                                                    out);
+  PKD_LAUNCH_CHECK();
+}
+
+}  // namespace pkdtree

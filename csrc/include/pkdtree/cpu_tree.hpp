@@ -1,0 +1,44 @@
+// CPU kd-tree on the implicit in-order layout.
+//
+// * build_exact_cpu      — exact median under the (orderable(key), id) total order; the test
+//                          oracle for every GPU path, and the threaded "omp" variant named
+//                          in the reference Makefile (Makefile:23-27; source absent there).
+// * build_reference_cpu  — reproduces the reference tree exactly, including its
+//                          off-by-one sort of the first n-1 points (kdtree_sequential.cpp:46-48,
+//                          SURVEY.md F1/Q1).
+// * nn_search_cpu        — the reference's recursive NN procedure (kdtree_sequential.cpp:75-136)
+//                          on the implicit layout: same visit order, same strict pruning.
+// * nn_brute_cpu         — exact brute force with the reference's distance summation order.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "pkdtree/common.hpp"
+
+namespace pkdtree {
+
+// perm[k] = input row placed at in-order slot k. ids may be null (id = row index).
+void build_exact_cpu(const float* pts, const u32* ids, i64 n, int dim, int depth0, u32* perm,
+                     int threads = 1);
+void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm);
+
+// Gather rows/ids through a permutation (tree_pts[k] = pts[perm[k]]).
+void gather_rows(const float* pts, const u32* ids, const u32* perm, i64 n, int dim, float* tree_pts,
+                 u32* tree_ids);
+
+struct NNResult {
+  i64 slot;   // in-order slot of the nearest point (-1 if the tree is empty)
+  float d2;   // squared distance computed as distance_squared(point, query)
+};
+
+// Reference-semantics traversal (strict '<' everywhere, ties go right).
+NNResult nn_search_cpu(const float* tree_pts, i64 n, int dim, int depth0, const float* q);
+// Exact brute force: lexicographic (d2, slot) minimum.
+NNResult nn_brute_cpu(const float* pts, i64 n, int dim, const float* q);
+
+// Number of violations of the exact-mode invariant: for every node, every element of the
+// left subtree is < the node and every element of the right subtree is > the node under
+// the (key, id) order on the node's axis. O(n log n).
+i64 count_invariant_violations(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0);
+
+}  // namespace pkdtree

@@ -1,0 +1,88 @@
+// Level-synchronous kd-tree builder for MI355X (gfx950).
+//
+// Replaces the reference's recursive std::sort build (build_tree_rec,
+// kdtree_sequential.cpp:30-66; O(N log^2 N) pointer chasing) with:
+//   * global levels — while segments are larger than the LDS subtree capacity, every level
+//     is one streaming pass over HBM: a per-segment linear-bucket histogram (computed in
+//     the previous pass) picks the bucket holding the median, a 3-way partition moves each
+//     point to its left / middle / right zone and histograms the next level's axis in
+//     the same pass, and a tiny refine kernel ranks the few middle-bucket points exactly
+//     under the (key, id) order to place the median;
+//   * an LDS subtree kernel — one workgroup per remaining segment builds all of its
+//     remaining levels in the 160 KiB LDS and writes the final in-order rows.
+// Output is the implicit in-order tree: slot k holds the point of the node
+// whose segment median sits at k; no pointers, no per-node allocation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pkdtree/common.hpp"
+
+namespace pkdtree {
+
+struct BuildOptions {
+  int subtree_max = 0;   // max segment handled by the LDS kernel (0 = auto from dim)
+  int depth0 = 0;        // depth of the root (subtrees of a distributed tree start deeper)
+};
+
+struct LevelPlan {
+  int level;        // 0-based global level
+  i64 segs;         // 2^level
+  i64 nmax;         // largest segment at this level
+  int bins;         // histogram bins per segment at this level
+  int next_bins;    // bins per segment at level+1 (0 if level+1 is the subtree level)
+  int bps;          // partition blocks per segment
+  int axis;         // split axis at this level
+};
+
+class GpuBuilder {
+ public:
+  GpuBuilder(i64 n, int dim, BuildOptions opt = {});
+
+  i64 n() const { return n_; }
+  int dim() const { return dim_; }
+  int global_levels() const { return lg_; }
+  int subtree_max() const { return nsub_; }
+  const std::vector<LevelPlan>& levels() const { return levels_; }
+  size_t workspace_bytes() const { return ws_bytes_; }
+  std::string describe() const;
+
+  // pts: [n, dim] AoS fp32 on the device; ids: [n] u32 or nullptr (id = id_base + row).
+  // Writes the in-order tree to out_pts [n, dim] and out_ids [n]. The input is not
+  // modified. Enqueued on `stream`; no host synchronisation, no allocation (graph-safe).
+  void build(const float* pts, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
+             void* workspace, hipStream_t stream) const;
+
+  // Same, but the input already sits in SoA columns inside the workspace (column c of
+  // row r at cols[c*n + r], column dim = ids); used by the distributed path which
+  // receives points straight into that layout.
+  float* soa_input(void* workspace) const;
+  // Sticky error word of the last build (0 = ok); synchronises the stream. Debug aid.
+  u32 read_error(const void* workspace, hipStream_t stream) const;
+  void build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
+
+ private:
+  void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const;
+
+  i64 n_;
+  int dim_;
+  BuildOptions opt_;
+  int lg_ = 0;      // number of global levels
+  int nsub_ = 0;    // LDS subtree capacity
+  std::vector<LevelPlan> levels_;
+  i64 heap_nodes_ = 0;  // nodes of levels 0..lg_
+  int max_bins_ = 0;
+  i64 max_hist_ = 0;
+  // workspace offsets
+  size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
+         off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0,
+         ws_bytes_ = 0;
+};
+
+// Subtree kernel capacity for a dimension (largest power of two whose LDS image fits).
+int default_subtree_max(int dim);
+
+}  // namespace pkdtree

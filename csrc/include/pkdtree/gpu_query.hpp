@@ -1,0 +1,31 @@
+// Exact 1-NN queries on the GPU.
+//
+// The reference answers queries with a recursive DFS on heap nodes (nearest,
+// kdtree_sequential.cpp:75-136). At d=128 that DFS visits every node, so
+// two exact kernels are provided and give identical answers:
+//   * brute force: every point against a tile of queries, for high dimension / few queries;
+//   * traversal: one thread per query walks the implicit in-order tree with an explicit
+//     stack, for low dimension / many queries.
+// Results are packed (float_bits(d2) << 32 | id); unsigned MIN is the lexicographic
+// (distance, id) minimum, so results from different ranks/trees combine with one MIN
+// reduction (the reference's MPI_Reduce(MIN), kdtree_mpi.cpp:253, but carrying the id).
+// Distances use the reference's summation order (see common.hpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pkdtree/common.hpp"
+
+namespace pkdtree {
+
+// Initialise `out[q]` to kPackedInf for q < nq (queries then MIN into it).
+void nn_init(u64* out, i64 nq, hipStream_t stream);
+
+// pts [n, dim] AoS; ids [n] or nullptr (id = id_base + row). out[q] = min over points.
+void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq,
+              u64* out, hipStream_t stream);
+
+// tree_pts/tree_ids: in-order implicit tree of n points whose root is at depth `depth0`.
+void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
+                 i64 nq, u64* out, hipStream_t stream);
+
+}  // namespace pkdtree

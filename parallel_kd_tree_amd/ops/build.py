@@ -1,0 +1,84 @@
+"""Tree-build ops.
+
+GPU: the level-synchronous HIP builder (csrc/gpu/build_global.hip + build_subtree.hip);
+CPU: the native exact / reference-mode builders (csrc/cpu/cpu_tree.cpp).
+Both return the implicit in-order tree ``(tree_pts [n, d] float32, tree_ids [n] int32)``:
+slot k holds the node whose segment median is k (root at n // 2).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import native
+
+
+class GpuTreeBuilder:
+    """Reusable builder for a fixed (n, dim) on one device.
+
+    Holds the plan and a workspace from the torch caching allocator, so repeated builds
+    (benchmarks, rebuilds of a streaming index) allocate nothing.
+    """
+
+    def __init__(self, n: int, dim: int, depth0: int = 0, subtree_max: int = 0):
+        self._b = native().GpuBuilder(int(n), int(dim), int(depth0), int(subtree_max))
+        self.n, self.dim, self.depth0 = int(n), int(dim), int(depth0)
+
+    @property
+    def workspace_bytes(self) -> int:
+        return self._b.workspace_bytes
+
+    @property
+    def global_levels(self) -> int:
+        return self._b.global_levels
+
+    @property
+    def subtree_max(self) -> int:
+        return self._b.subtree_max
+
+    def describe(self) -> str:
+        return self._b.describe()
+
+    def read_error(self) -> int:
+        """Sticky device error word of the last build (0 = ok). Synchronises."""
+        return int(self._b.read_error())
+
+    def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
+              out_pts: Optional[torch.Tensor] = None, out_ids: Optional[torch.Tensor] = None):
+        return tuple(self._b.build(points, ids, int(id_base), out_pts, out_ids))
+
+    def soa_input(self, device) -> torch.Tensor:
+        """[(dim + 1), n] float32 view of the builder's input columns (row ``dim`` = id bits)."""
+        return self._b.soa_input(torch.device(device))
+
+    def build_from_soa(self, device):
+        return tuple(self._b.build_from_soa(torch.device(device)))
+
+
+_builders: dict = {}
+
+
+def build_gpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0, depth0: int = 0,
+              subtree_max: int = 0):
+    """Build the exact tree of ``points`` ([n, d] float32 on a GPU)."""
+    if not points.is_cuda:
+        raise ValueError("build_gpu needs a GPU tensor")
+    points = points.contiguous()
+    key = (points.shape[0], points.shape[1], depth0, subtree_max, points.device)
+    b = _builders.get(key)
+    if b is None:
+        if len(_builders) > 8:
+            _builders.clear()
+        b = _builders[key] = GpuTreeBuilder(points.shape[0], points.shape[1], depth0, subtree_max)
+    return b.build(points, ids, id_base)
+
+
+def build_cpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, mode: str = "exact", depth0: int = 0,
+              threads: int = 1):
+    """Native CPU build. ``mode='reference'`` reproduces the reference tree exactly
+    (first n-1 points sorted per node, kdtree_sequential.cpp:46-48)."""
+    points = points.detach().to("cpu", torch.float32).contiguous()
+    if ids is not None:
+        ids = ids.to("cpu", torch.int32).contiguous()
+    return tuple(native().build_cpu(points, ids, mode, int(depth0), int(threads)))

@@ -1,0 +1,100 @@
+"""Communication layer over torch.distributed.
+
+On MI355X the backend is "nccl", which is RCCL over xGMI; CPU tests use "gloo" with the same
+code. Rendezvous comes from the torchrun environment (RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT), replacing the reference's MPI_Init / Comm_rank / Comm_size
+(kdtree_mpi.cpp:177-183). Every collective here is tiny (config broadcast, MIN reductions,
+histograms) except the all-to-all redistribution of the global decomposition.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+_device: Optional[torch.device] = None
+
+
+def init(backend: Optional[str] = None, device: Optional[torch.device] = None, timeout_s: int = 600) -> None:
+    """Initialise the default process group from the environment (idempotent)."""
+    global _device
+    if dist.is_initialized():
+        return
+    if backend is None:
+        backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29512")
+    kw = {}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _device = device if device is not None else torch.device("cpu")
+
+
+def is_initialized() -> bool:
+    return dist.is_initialized()
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def device() -> torch.device:
+    return _device if _device is not None else torch.device("cpu")
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[device().index])
+        else:
+            dist.barrier()
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def forest_slice(n: int, p: int, r: int) -> Tuple[int, int]:
+    """Rank r's generation-order slice: local = n // p, remainder to the last rank
+    (kdtree_mpi.cpp:208-216). Returns (first_row, rows)."""
+    local = n // p
+    first = local * r
+    if r == p - 1:
+        local += n % p
+    return first, local
+
+
+def broadcast_ints(vals: List[int], src: int = 0) -> List[int]:
+    """MPI_Bcast of the {seed, dim, N} config (kdtree_mpi.cpp:199)."""
+    t = torch.tensor(vals, dtype=torch.int64, device=device())
+    if dist.is_initialized():
+        dist.broadcast(t, src)
+    return [int(v) for v in t.tolist()]
+
+
+def allreduce_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    if dist.is_initialized() and world() > 1:
+        dist.all_reduce(t, op=op)
+    return t
+
+
+def max_float(v: float) -> float:
+    t = torch.tensor([v], dtype=torch.float64, device=device())
+    allreduce_(t, dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def min_packed_(packed: torch.Tensor) -> torch.Tensor:
+    """MIN-reduce packed (d2 << 32 | id) results. The packing never sets bit 63, so the
+    signed int64 MIN equals the unsigned one (reference: MPI_Reduce MIN, kdtree_mpi.cpp:253,
+    which drops the id; here the id rides along)."""
+    return allreduce_(packed, dist.ReduceOp.MIN)

@@ -1,0 +1,96 @@
+"""CPU tree: exact builder invariants, NN vs brute force, reference-mode parity, save/load,
+Point/Node facade (Node.hpp:9-45)."""
+import numpy as np
+import pytest
+import torch
+
+import parallel_kd_tree_amd as pk
+from parallel_kd_tree_amd import ops
+
+
+def brute_d2(x, q):
+    d = ((x[None, :, :].double() - q[:, None, :].double()) ** 2).sum(-1)
+    return d.min(1)
+
+
+@pytest.mark.parametrize("n,dim", [(1, 3), (2, 3), (3, 1), (7, 2), (100, 3), (1024, 3), (5000, 1), (3000, 8),
+                                   (500, 128)])
+def test_exact_invariant_and_nn(n, dim):
+    x = pk.generate_problem(n + dim, dim, n + 20)
+    t = pk.KDTree.build(x[:n])
+    assert t.invariant_violations() == 0
+    assert sorted(t.tree_ids.tolist()) == list(range(n))
+    d, ids = t.query(x[n:])
+    ref, _ = brute_d2(x[:n], x[n:])
+    # exact: the NN distance equals brute force (same fp32 point, recomputed in fp64 here)
+    got = ((x[ids] .double() - x[n:].double()) ** 2).sum(-1)
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)
+
+
+def test_exact_ties_total_order():
+    # heavy duplicates: integer grid, 3 distinct values per axis
+    g = torch.randint(0, 3, (4000, 3)).float()
+    t = pk.KDTree.build(g)
+    assert t.invariant_violations() == 0
+    same = torch.zeros(2000, 2)
+    t2 = pk.KDTree.build(same)
+    assert t2.invariant_violations() == 0
+    # unique tree: permuting the input rows (with ids attached) gives the same tree
+    perm = torch.randperm(4000)
+    t3 = pk.KDTree.build(g[perm], ids=perm.to(torch.int32))
+    assert torch.equal(t3.tree_ids, t.tree_ids)
+
+
+def test_threaded_build_equals_serial():
+    x = pk.generate_problem(3, 3, 200000)
+    a = ops.build_cpu(x, None, "exact", 0, 1)
+    b = ops.build_cpu(x, None, "exact", 0, 8)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+
+
+def test_reference_mode_quirk_differs_from_exact():
+    # the off-by-one sort makes the reference search miss some NNs at low dim
+    x = pk.generate_problem(2, 2, 2100)
+    tr = pk.KDTree.build(x[:2000], mode="reference")
+    te = pk.KDTree.build(x[:2000])
+    dr, _ = tr.query(x[2000:])
+    de, _ = te.query(x[2000:])
+    assert (dr >= de).all()
+    assert te.invariant_violations() == 0
+
+
+def test_depth0_axis_offset():
+    x = pk.generate_problem(5, 3, 3000)
+    t = pk.KDTree.build(x, depth0=2)
+    assert t.invariant_violations() == 0
+    assert t.root.axis == 2
+
+
+def test_save_load_roundtrip(tmp_path):
+    x = pk.generate_problem(1, 3, 1000)
+    t = pk.KDTree.build(x, id_base=1)
+    p = tmp_path / "t.pkd"
+    t.save(p)
+    u = pk.KDTree.load(p)
+    assert torch.equal(u.tree_pts, t.tree_pts) and torch.equal(u.tree_ids, t.tree_ids)
+    assert u.mode == "exact" and u.depth0 == 0
+
+
+def test_point_node_facade():
+    x = pk.generate_problem(42, 8, 100)
+    t = pk.KDTree.build(x, id_base=1)
+    r = t.root
+    assert r.slot == 50 and r.left.n == 50 and r.right.n == 49
+    p = r.point
+    # Node.cpp:16-28 prints at most 5 coordinates then ", , ..., last"
+    s = repr(p)
+    assert s.startswith(f"Point(ID={p.ID}, dimension=8, coordinates=[") and ", , ..., " in s
+    q = pk.Point(8, 101, x[0].numpy())
+    nn = pk.nearest_neighbor(r, q)
+    assert nn.point.ID == 1 and q.distance(nn.point) == 0.0
+    assert pk.Point.compare(pk.Point(2, 0, [1, 2]), pk.Point(2, 1, [2, 0]), 0)
+
+
+def test_tree_height():
+    for n, h in [(0, 0), (1, 1), (2, 2), (3, 2), (4, 3), (1023, 10), (1024, 11), (500000, 19)]:
+        assert pk.tree_height(n) == h

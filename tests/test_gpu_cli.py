@@ -1,0 +1,23 @@
+"""kdtree_gpu (single MI355X) prints byte-identical results to the exact CPU executable."""
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def out(exe, args, stdin=None):
+    r = subprocess.run([str(exe), *map(str, args)], input=stdin, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    return [l for l in r.stdout.splitlines() if not l.startswith("elapsed time")]
+
+
+@pytest.mark.parametrize("cfg", [(42, 3, 1024), (7, 2, 50000), (3, 8, 200000), (5, 128, 20000), (1, 3, 1)])
+def test_gpu_cli_matches_cpu(bin_dir, cfg):
+    assert out(bin_dir / "kdtree_gpu", cfg) == out(bin_dir / "kdtree_sequential", cfg)
+
+
+def test_gpu_cli_eval_mode(bin_dir):
+    a = out(bin_dir / "kdtree_gpu", [], stdin="3\n")
+    b = out(bin_dir / "kdtree_sequential", ["--threads", "16"], stdin="3\n")
+    assert a == b and a[0] == "READY" and a[-1] == "DONE"
