@@ -3,7 +3,7 @@
 // caching allocator, so repeated builds allocate nothing from HIP.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include <memory>
 #include <string>
@@ -59,7 +59,7 @@ struct Builder {
                                    c10::optional<torch::Tensor> out_ids) {
     check_points(pts, true);
     TORCH_CHECK(pts.size(0) == b.n() && pts.size(1) == b.dim(), "points shape does not match the builder");
-    const c10::hip::HIPGuard guard(pts.device());
+    const c10::DeviceGuard guard(pts.device());
     ensure_ws(pts.device());
     torch::Tensor op = out_pts.has_value() ? *out_pts : torch::empty_like(pts);
     torch::Tensor oi = out_ids.has_value() ? *out_ids
@@ -79,7 +79,7 @@ struct Builder {
   }
 
   std::vector<torch::Tensor> build_from_soa(const torch::Device& dev) {
-    const c10::hip::HIPGuard guard(dev);
+    const c10::DeviceGuard guard(dev);
     ensure_ws(dev);
     auto opts = torch::TensorOptions().device(dev);
     torch::Tensor op = torch::empty({b.n(), b.dim()}, opts.dtype(torch::kFloat32));
@@ -154,7 +154,7 @@ torch::Tensor nn_gpu(const torch::Tensor& pts, const c10::optional<torch::Tensor
   check_points(pts, true);
   check_points(queries, true);
   TORCH_CHECK(queries.size(1) == pts.size(1), "dimension mismatch");
-  const c10::hip::HIPGuard guard(pts.device());
+  const c10::DeviceGuard guard(pts.device());
   const int64_t nq = queries.size(0);
   hipStream_t s = cur_stream(pts);
   torch::Tensor out;
