@@ -180,6 +180,16 @@ torch::Tensor nn_gpu(const torch::Tensor& pts, const c10::optional<torch::Tensor
   return out;
 }
 
+std::vector<torch::Tensor> nn_finalize(const torch::Tensor& packed) {
+  TORCH_CHECK(packed.is_cuda() && packed.scalar_type() == torch::kInt64 && packed.is_contiguous(), "bad packed");
+  const c10::DeviceGuard guard(packed.device());
+  torch::Tensor d = torch::empty({packed.numel()}, packed.options().dtype(torch::kFloat32));
+  torch::Tensor i = torch::empty({packed.numel()}, packed.options().dtype(torch::kInt64));
+  pk::nn_finalize(reinterpret_cast<const pk::u64*>(packed.data_ptr<int64_t>()), packed.numel(), d.data_ptr<float>(),
+                  i.data_ptr<int64_t>(), cur_stream(packed));
+  return {d, i};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -208,6 +218,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("depth0") = 0);
   m.def("nn", &nn_gpu, py::arg("points"), py::arg("ids"), py::arg("id_base"), py::arg("queries"),
         py::arg("method") = "brute", py::arg("depth0") = 0, py::arg("into") = c10::nullopt);
+  m.def("nn_finalize", &nn_finalize, py::arg("packed"));
   m.def("subtree_capacity", &pk::default_subtree_max);
   pkdtree::bind_dist_ops(m);
 }

@@ -114,7 +114,23 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P
   out[qi] = best;
 }
 
+// Correctly rounded sqrtf (gfx950 ocml with correctly-rounded sqrt), matching the
+// reference's sqrt(distance_squared) (Node.cpp:36-38) bit for bit.
+__global__ void k_finalize(const u64* __restrict__ packed, i64 nq, float* __restrict__ dist, i64* __restrict__ ids) {
+  const i64 i = i64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const u64 p = packed[i];
+  dist[i] = sqrtf(packed_dist(p));
+  ids[i] = i64(packed_idx(p));
+}
+
 }  // namespace
+
+void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t stream) {
+  if (nq <= 0) return;
+  k_finalize<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(packed, nq, dist, ids);
+  PKD_LAUNCH_CHECK();
+}
 
 void nn_init(u64* out, i64 nq, hipStream_t stream) {
   if (nq <= 0) return;

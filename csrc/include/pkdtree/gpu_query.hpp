@@ -28,4 +28,7 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
                  i64 nq, u64* out, hipStream_t stream);
 
+// packed -> (sqrt(d2) correctly rounded, id)
+void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t stream);
+
 }  // namespace pkdtree

@@ -104,8 +104,7 @@ class KDTree:
         on the CPU reproduce the reference search (which can miss the NN).
         """
         if self.tree_pts.is_cuda and self.mode == "exact":
-            d2, ids = ops.unpack(self.query_packed(queries, method))
-            return torch.sqrt(d2), ids
+            return ops.finalize(self.query_packed(queries, method))
         q = queries.detach().cpu().to(torch.float32).contiguous()
         slots, d2 = ops.nn_cpu(self.tree_pts.cpu().contiguous(), q, self.depth0, brute=(method == "brute"))
         ids = self.tree_ids.cpu().to(torch.int64)[slots] & 0xFFFFFFFF

@@ -28,6 +28,6 @@ def native_path() -> str:
 
 
 from .build import GpuTreeBuilder, build_gpu, build_cpu  # noqa: E402
-from .query import nn_gpu, unpack, nn_cpu  # noqa: E402
+from .query import nn_gpu, unpack, finalize, nn_cpu  # noqa: E402
 
-__all__ = ["native", "native_path", "GpuTreeBuilder", "build_gpu", "build_cpu", "nn_gpu", "unpack", "nn_cpu"]
+__all__ = ["native", "native_path", "GpuTreeBuilder", "build_gpu", "build_cpu", "nn_gpu", "unpack", "finalize", "nn_cpu"]

@@ -33,6 +33,16 @@ def unpack(packed: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return d2, ids
 
 
+def finalize(packed: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Packed -> (distance = correctly rounded sqrtf(d2), id). On the GPU this runs a HIP
+    kernel: torch's device sqrt is not correctly rounded, the reference's is."""
+    if packed.is_cuda:
+        d, i = native().nn_finalize(packed.contiguous())
+        return d, i
+    d2, ids = unpack(packed)
+    return torch.sqrt(d2), ids
+
+
 def nn_cpu(tree_pts: torch.Tensor, queries: torch.Tensor, depth0: int = 0, brute: bool = False):
     """Reference-procedure search on a CPU tree: returns (slot int64, d2 float32)."""
     return tuple(native().search_cpu(tree_pts.contiguous(), queries.to(torch.float32).contiguous(), int(depth0),
