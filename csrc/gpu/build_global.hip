@@ -268,11 +268,16 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
   }
 }
 
-template <int DIMC>  // DIMC > 0: compile-time dim; 0: runtime
+// NCOL > 0: rows of NCOL columns (dim + id) are loaded whole into registers before any
+// store, so every chunk pays one HBM latency; NCOL == 0: runtime dim, columns are moved one
+// at a time (loads of a column batched before its stores). Loads and stores never
+// interleave per item: the compiler cannot prove src/dst disjoint and would otherwise
+// serialise each load behind the previous store.
+template <int NCOL>
 __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
   __shared__ u32 gcnt[3][64];
-  const int dim = DIMC > 0 ? DIMC : a.dim;
+  const int dim = NCOL > 0 ? NCOL - 1 : a.dim;
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
   const i64 h = a.heap0 + s;
@@ -294,19 +299,43 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   const float* __restrict__ src = a.src;
   float* __restrict__ dst = a.dst;
   const i64 nc = a.ncol;
+  const int axis = a.axis, naxis = a.next_axis;
   const int w = threadIdx.x / 64;
   const int ln = dev::lane();
   __syncthreads();
 
   for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+    constexpr int NR = NCOL > 0 ? NCOL : 1;
+    float row[kItems][NR];
+    float kk[NCOL > 0 ? 1 : kItems], nkk[NCOL > 0 ? 1 : kItems];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const i64 e = c0 + i * kBlock + threadIdx.x;
+      const i64 p = lo + (e < b1 ? e : b0);
+      if (NCOL > 0) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c) row[i][c] = src[i64(c) * nc + p];
+      } else {
+        kk[i] = src[i64(axis) * nc + p];
+        nkk[i] = src[i64(naxis) * nc + p];
+      }
+    }
     u32 zone_pre[kItems];  // (zone << 16) | rank-in-wave
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
       const i64 e = c0 + i * kBlock + threadIdx.x;
       const bool valid = e < b1;
+      // split-axis and next-axis keys: select chains over the compile-time row (no indexing)
+      float key = NCOL > 0 ? row[i][0] : kk[i], nkey = NCOL > 0 ? row[i][0] : nkk[i];
+      if (NCOL > 0) {
+#pragma unroll
+        for (int c = 1; c < NR - 1; ++c) {
+          key = (c == axis) ? row[i][c] : key;
+          nkey = (c == naxis) ? row[i][c] : nkey;
+        }
+      }
       u32 z = 3;
       if (valid) {
-        const float key = src[i64(a.axis) * nc + lo + e];
         const u32 b = bucket_of(key, prm, a.bins);
         z = b < bstar ? 0u : (b == bstar ? 1u : 2u);
       }
@@ -320,9 +349,13 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       zone_pre[i] = (z << 16) | mbcnt(mz);
       if (m1 != 0 && z == 1) {  // rare: track the middle zone's composite key range
         const u32 id = reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e];
-        const u64 k = composite_key(src[i64(a.axis) * nc + lo + e], id);
+        const u64 k = composite_key(key, id);
         atomicMin(&st->mid_min, (unsigned long long)k);
         atomicMax(&st->mid_max, (unsigned long long)k);
+      }
+      if (fuse && z < 3 && z != 1) {
+        const int child = z == 0 ? 0 : 1;
+        atomicAdd(&nh[child * a.next_bins + bucket_of(nkey, cprm[child], a.next_bins)], 1u);
       }
     }
     __syncthreads();
@@ -337,22 +370,38 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      const i64 e = c0 + i * kBlock + threadIdx.x;
+    for (int i = 0; i < kItems; ++i) {  // zone_pre becomes the destination offset in the segment
       const u32 z = zone_pre[i] >> 16;
+      u32 off = 0xffffffffu;
       if (z < 3) {
-        const i64 p = lo + e;
-        const i64 q = lo + i64(gcnt[z][i * 4 + w] + (zone_pre[i] & 0xffffu));
-        if (q >= lo + n) {  // impossible unless the histogram and the keys disagree
+        off = gcnt[z][i * 4 + w] + (zone_pre[i] & 0xffffu);
+        if (i64(off) >= n) {  // impossible unless histogram and keys disagree
           atomicOr(a.err, 1u);
-          continue;
+          off = 0xffffffffu;
         }
-        for (int c = 0; c <= dim; ++c) dst[i64(c) * nc + q] = src[i64(c) * nc + p];
-        if (fuse && z != 1) {
-          const int child = z == 0 ? 0 : 1;
-          const u32 nb = bucket_of(src[i64(a.next_axis) * nc + p], cprm[child], a.next_bins);
-          atomicAdd(&nh[child * a.next_bins + nb], 1u);
+      }
+      zone_pre[i] = off;
+    }
+    if (NCOL > 0) {
+#pragma unroll
+      for (int i = 0; i < kItems; ++i) {
+        if (zone_pre[i] != 0xffffffffu) {
+          const i64 q = lo + zone_pre[i];
+#pragma unroll
+          for (int c = 0; c < NR; ++c) dst[i64(c) * nc + q] = row[i][c];
         }
+      }
+    } else {
+      for (int c = 0; c <= dim; ++c) {
+        float v[kItems];
+#pragma unroll
+        for (int i = 0; i < kItems; ++i) {
+          const i64 e = c0 + i * kBlock + threadIdx.x;
+          v[i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
+        }
+#pragma unroll
+        for (int i = 0; i < kItems; ++i)
+          if (zone_pre[i] != 0xffffffffu) dst[i64(c) * nc + lo + zone_pre[i]] = v[i];
       }
     }
     __syncthreads();
@@ -572,7 +621,7 @@ int default_subtree_max(int dim) { return subtree_capacity(dim); }
 GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
-  nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity(dim)) : subtree_capacity(dim);
+  nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity_max(dim)) : subtree_capacity(dim);
   lg_ = 0;
   while ((n_ >> lg_) > nsub_) ++lg_;
   heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
@@ -714,11 +763,10 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
     const int grid = int(lp.segs * lp.bps);
     switch (dim_) {
-      case 1: k_partition<1><<<grid, kBlock, lds, stream>>>(a); break;
-      case 2: k_partition<2><<<grid, kBlock, lds, stream>>>(a); break;
-      case 3: k_partition<3><<<grid, kBlock, lds, stream>>>(a); break;
-      case 4: k_partition<4><<<grid, kBlock, lds, stream>>>(a); break;
-      case 8: k_partition<8><<<grid, kBlock, lds, stream>>>(a); break;
+      case 1: k_partition<2><<<grid, kBlock, lds, stream>>>(a); break;
+      case 2: k_partition<3><<<grid, kBlock, lds, stream>>>(a); break;
+      case 3: k_partition<4><<<grid, kBlock, lds, stream>>>(a); break;
+      case 4: k_partition<5><<<grid, kBlock, lds, stream>>>(a); break;
       default: k_partition<0><<<grid, kBlock, lds, stream>>>(a); break;
     }
     PKD_LAUNCH_CHECK();
@@ -727,8 +775,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     std::swap(src, dst);
   }
   const i64 heap0 = (i64(1) << lg_) - 1;
-  launch_subtree(src, n_, dim_, seg_lo, seg_n, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts, out_ids,
-                 stream);
+  launch_subtree(src, n_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
+                 out_ids, err, stream);
 }
 
 }  // namespace pkdtree

@@ -28,16 +28,17 @@ using dev::mbcnt;
 
 namespace {
 
-constexpr int kBlock = 256;
 constexpr int kSmall = 16;
 constexpr u32 kDone = 0xffffu;
 constexpr u32 kMid = 0x8000u;
-constexpr size_t kLdsBudget = 160 * 1024 - 2048;  // leave room for static LDS
+constexpr size_t kLdsMax = 160 * 1024 - 1024;  // minus static LDS
 
-size_t subtree_lds_bytes(int dim, int nmax) {
-  // rows (dim+1) + slot + keyv + sub + hist (nmax/2) + stats (nmax/2), all 32-bit words
-  return size_t(dim + 1) * size_t(nmax) * 4 + size_t(nmax) * 4 * 3 + size_t(nmax) * 4;
+// 32-bit words of dynamic LDS for capacity nm:
+//   rows (dim+1)*nm | slot nm | keyv nm | sub nm | hist nm/2 | st 8*(nm/16) | cells 2*(nm/8)*dim*2
+size_t subtree_lds_words(int dim, int nm) {
+  return size_t(dim + 1) * nm + 3 * size_t(nm) + nm / 2 + 8 * size_t(nm / 16) + 2 * size_t(nm / 8) * dim * 2;
 }
+size_t subtree_lds_bytes(int dim, int nm) { return 4 * subtree_lds_words(dim, nm); }
 
 struct SubArgs {
   const float* cols;
@@ -45,43 +46,84 @@ struct SubArgs {
   int dim;
   const i64* seg_lo;
   const i64* seg_n;
+  const float* cells;  // heap-indexed [h][dim][2] cell of every segment root
   i64 heap0;
   int depth_base;
-  int nmax;
   float* out_pts;
   u32* out_ids;
+  u32* err;
 };
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
 
-template <int ITEMS>
-__global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
+// Wave-aggregated LDS reservation: lanes with equal `key` get consecutive slots from
+// cursor[key]; returns this lane's slot. One LDS atomic per distinct key per wave.
+__device__ __forceinline__ u32 reserve(u32 key, bool active, u32* cursor) {
+  u64 pending = __ballot(active);
+  u32 mine = 0;
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const u32 lk = __shfl(key, leader, 64);
+    const u64 m = __ballot(active && key == lk) & pending;
+    u32 base = 0;
+    if (dev::lane() == leader) base = atomicAdd(&cursor[lk], u32(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    if (active && key == lk) mine = base + mbcnt(m);
+    pending &= ~m;
+  }
+  return mine;
+}
+
+template <int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
   extern __shared__ __align__(16) u32 smem[];
-  __shared__ u32 gcnt[3][64];
+  constexpr int NM = ITEMS * THREADS;
   const int dim = a.dim;
-  const int NM = a.nmax;
   const i64 h = a.heap0 + blockIdx.x;
   const int n = int(a.seg_n[h]);
   if (n <= 0) return;
   const i64 glo = a.seg_lo[h];
-  float* rows = reinterpret_cast<float*>(smem);          // [(dim+1) * NM]
-  u32* slot = smem + size_t(dim + 1) * NM;               // [NM]
-  u32* keyv = slot + NM;                                 // [NM]
-  u32* sub = keyv + NM;                                  // [NM]   (lo << 16) | n
-  u32* hist = sub + NM;                                  // [NM/2]
-  u32* stats = hist + NM / 2;                            // [NM/2]
+  float* rows = reinterpret_cast<float*>(smem);  // [(dim+1)][NM]
+  u32* slot = smem + size_t(dim + 1) * NM;       // idx | sid << 16
+  u32* keyv = slot + NM;                         // orderable key by slot (counting levels)
+  u32* sub = keyv + NM;                          // (lo << 16) | n per sub-segment
+  u32* hist = sub + NM;                          // [NM/2]
+  u32* st = hist + NM / 2;                       // [8][NM/16]: bstar, cless, cmid, -, cursors[4]
+  float* cellA = reinterpret_cast<float*>(st + 8 * (NM / 16));  // [NM/8][dim][2]
+  float* cellB = cellA + (NM / 8) * dim * 2;
+  constexpr int SB = NM / 16;
+  u32* bst = st;
+  u32* cle = st + SB;
+  u32* cmi = st + 2 * SB;
+  u32* cur = st + 4 * SB;  // [SB][4]
   const int tid = threadIdx.x;
-  const int w = tid / 64;
-  const int ln = dev::lane();
+  const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
 
   for (int c = 0; c <= dim; ++c) {
     const float* col = a.cols + i64(c) * a.ncol + glo;
-    for (int k = tid; k < n; k += kBlock) rows[c * NM + k] = col[k];
+    float v[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int k = tid + i * THREADS;
+      v[i] = k < n ? col[k] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int k = tid + i * THREADS;
+      if (k < n) rows[c * NM + k] = v[i];
+    }
   }
-  for (int k = tid; k < n; k += kBlock) slot[k] = u32(k);
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int k = tid + i * THREADS;
+    if (k < n) slot[k] = u32(k);
+  }
+  for (int b = tid; b < NM / 2; b += THREADS) hist[b] = 0;
   if (tid == 0) sub[0] = u32(n);
-  const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
+  for (int c = tid; c < 2 * dim; c += THREADS) cellA[c] = a.cells[h * 2 * dim + c];
   __syncthreads();
+  float* cc = cellA;  // cells of the current level
+  float* nc = cellB;  // cells of the next level
 
   for (int l = 0;; ++l) {
     const int ml = n >> l;
@@ -89,68 +131,39 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
     const int S = 1 << l;
     const int axis = (a.depth_base + l) % dim;
     const float* kcol = rows + axis * NM;
-    u32 sl[ITEMS], ok[ITEMS];
+    const bool more = (n >> (l + 1)) > 0;
+    u32 sl[ITEMS];
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      const int p = tid + i * kBlock;
+      const int p = tid + i * THREADS;
       sl[i] = p < n ? slot[p] : (kDone << 16);
-      ok[i] = 0;
-      if ((sl[i] >> 16) != kDone) {
-        ok[i] = orderable(kcol[sl[i] & 0xffffu]);
-        keyv[p] = ok[i];
-      }
     }
+    float kf[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) kf[i] = ((sl[i] >> 16) != kDone) ? kcol[sl[i] & 0xffffu] : 0.0f;
+    u32 ev[ITEMS];  // sub-segment table entries this thread rewrites for the next level
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int j = tid + i * THREADS;
+      ev[i] = (more && j < S) ? sub[j] : 0u;
+    }
+    u32 np[ITEMS], ns[ITEMS];
     if (ml > kSmall) {
       // ---------------- bucket path ----------------
-      const int B = min(1024, max(8, pow2_floor_dev(ml / 4)));
-      u32* mn = stats;
-      u32* mx = stats + S;
-      u32* bst = stats + 2 * S;
-      u32* cle = stats + 3 * S;
-      u32* cmi = stats + 4 * S;
-      u32* bas = stats + 5 * S;  // [3][S]
-      for (int j = tid; j < S; j += kBlock) {
-        mn[j] = 0xffffffffu;
-        mx[j] = 0u;
-      }
-      for (int b = tid; b < S * B; b += kBlock) hist[b] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const u32 sid = sl[i] >> 16;
-        const bool act = sid != kDone;
-        // waves mostly sit inside one sub-segment: reduce first when they do
-        const u32 s0 = __builtin_amdgcn_readfirstlane(act ? sid : 0xffffffffu);
-        if (__all(!act || sid == s0)) {
-          const u32 vmin = dev::wave_min_u32(act ? ok[i] : 0xffffffffu);
-          const u32 vmax = dev::wave_max_u32(act ? ok[i] : 0u);
-          if (ln == 0 && s0 != 0xffffffffu) {
-            atomicMin(&mn[s0], vmin);
-            atomicMax(&mx[s0], vmax);
-          }
-        } else if (act) {
-          atomicMin(&mn[sid], ok[i]);
-          atomicMax(&mx[sid], ok[i]);
-        }
-      }
-      __syncthreads();
-      // The bucket goes through LDS (keyv) rather than a register array: carrying it in
-      // registers across the select phase crashes ROCm 7.2's gfx950 instruction selector.
+      const int B = min(1024, max(8, pow2_floor_dev(ml / 2)));
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 sid = sl[i] >> 16;
         if (sid != kDone) {
-          const BucketParams prm = make_params(from_orderable(mn[sid]), from_orderable(mx[sid]), B);
-          const u32 b = bucket_of(from_orderable(ok[i]), prm, B);
-          keyv[tid + i * kBlock] = b;
-          atomicAdd(&hist[sid * B + b], 1u);
+          const float* cl = cc + (sid * dim + axis) * 2;
+          const BucketParams prm = make_params(cl[0], cl[1], B);
+          atomicAdd(&hist[sid * B + bucket_of(kf[i], prm, B)], 1u);
         }
       }
       __syncthreads();
-      // select: G lanes per sub-segment
-      {
-        const int G = min(64, max(1, kBlock / S));
-        const int groups = kBlock / G;
+      {  // select: G lanes per sub-segment
+        const int G = min(64, max(1, THREADS / S));
+        const int groups = THREADS / G;
         const int gl = tid & (G - 1);
         const int per = (B + G - 1) / G;
         for (int j = tid / G; j < S; j += groups) {
@@ -166,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
             if (gl >= o) incl += t;
           }
           const u32 excl = incl - sum;
-          if ((e & 0xffffu) > 0 && r >= excl && r < incl) {
+          if (r >= excl && r < incl) {
             u32 c = excl;
             for (int b = b0; b < b1; ++b) {
               const u32 v = hs[b];
@@ -174,6 +187,9 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
                 bst[j] = u32(b);
                 cle[j] = c;
                 cmi[j] = v;
+                cur[4 * j + 0] = 0;
+                cur[4 * j + 1] = c;
+                cur[4 * j + 2] = c + v;
                 break;
               }
               c += v;
@@ -182,111 +198,84 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
         }
       }
       __syncthreads();
-      u32 zz[ITEMS];
+      // zones -> reserved slots (LDS cursors), in place: all reads of `slot` are done
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 sid = sl[i] >> 16;
-        u32 z = 3;
-        if (sid != kDone) {
+        const bool act = sid != kDone;
+        u32 z = 0;
+        if (act) {
+          const float* cl = cc + (sid * dim + axis) * 2;
+          const BucketParams prm = make_params(cl[0], cl[1], B);
+          const u32 b = bucket_of(kf[i], prm, B);
           const u32 bs = bst[sid];
-          const u32 b = keyv[tid + i * kBlock];
           z = b < bs ? 0u : (b == bs ? 1u : 2u);
         }
-        zz[i] = z;
-        const u64 m0 = __ballot(z == 0), m1 = __ballot(z == 1), m2 = __ballot(z == 2);
-        if (ln == 0) {
-          gcnt[0][i * 4 + w] = __popcll(m0);
-          gcnt[1][i * 4 + w] = __popcll(m1);
-          gcnt[2][i * 4 + w] = __popcll(m2);
-        }
-      }
-      for (int i = ITEMS; i < 16; ++i) {
-        if (ln == 0) gcnt[0][i * 4 + w] = gcnt[1][i * 4 + w] = gcnt[2][i * 4 + w] = 0;
-      }
-      __syncthreads();
-      if (w < 3) {
-        const u32 v = gcnt[w][ln];
-        gcnt[w][ln] = dev::wave_incl_scan(v) - v;
-      }
-      __syncthreads();
-      // zone prefix of every point; first point of each sub-segment publishes the bases
-      u32 pz[ITEMS];
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const int p = tid + i * kBlock;
-        const u32 z = zz[i];
-        const u64 m0 = __ballot(z == 0), m1 = __ballot(z == 1), m2 = __ballot(z == 2);
-        const u32 p0 = gcnt[0][i * 4 + w] + mbcnt(m0);
-        const u32 p1 = gcnt[1][i * 4 + w] + mbcnt(m1);
-        const u32 p2 = gcnt[2][i * 4 + w] + mbcnt(m2);
-        pz[i] = z == 0 ? p0 : (z == 1 ? p1 : p2);
-        if (z < 3) {
-          const u32 sid = sl[i] >> 16;
-          if (u32(p) == (sub[sid] >> 16)) {
-            bas[sid] = p0;
-            bas[S + sid] = p1;
-            bas[2 * S + sid] = p2;
-          }
-        }
-      }
-      __syncthreads();
-      u32 np[ITEMS], ns[ITEMS];
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const u32 z = zz[i];
+        const u32 d = reserve(sid * 4 + z, act, cur);
         np[i] = 0xffffffffu;
-        if (z < 3) {
-          const u32 sid = sl[i] >> 16;
-          const u32 jlo = sub[sid] >> 16;
-          const u32 start = z == 0 ? 0u : (z == 1 ? cle[sid] : cle[sid] + cmi[sid]);
-          np[i] = jlo + start + pz[i] - bas[z * S + sid];
+        if (act) {
+          np[i] = (sub[sid] >> 16) + d;
           const u32 nsid = z == 0 ? 2 * sid : (z == 2 ? 2 * sid + 1 : (kMid | sid));
           ns[i] = (sl[i] & 0xffffu) | (nsid << 16);
         }
       }
-      __syncthreads();
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i)
         if (np[i] != 0xffffffffu) slot[np[i]] = ns[i];
+      for (int b = tid; b < NM / 2; b += THREADS) hist[b] = 0;  // for the next level
       __syncthreads();
-      // exact ranking inside the median bucket
+      // exact (key, id) ranking inside each median bucket; the median fixes the cells
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        const int p = tid + i * kBlock;
+        const int p = tid + i * THREADS;
         np[i] = 0xffffffffu;
-        if (p < n) {
-          const u32 s = slot[p];
-          const u32 tag = s >> 16;
-          if (tag != kDone && (tag & kMid)) {
-            const u32 sid = tag & 0x7fffu;
-            const u32 idx = s & 0xffffu;
-            const u32 e = sub[sid];
-            const u32 jlo = e >> 16, jn = e & 0xffffu;
-            const u32 zlo = jlo + cle[sid], zc = cmi[sid];
-            const u32 mk = orderable(kcol[idx]);
-            const u32 mid = idrow[idx];
-            u32 rank = 0;
-            for (u32 q = zlo; q < zlo + zc; ++q) {
-              const u32 oi = slot[q] & 0xffffu;
-              const u32 qk = orderable(kcol[oi]);
-              rank += (qk < mk || (qk == mk && idrow[oi] < mid)) ? 1u : 0u;
+        const u32 s = p < n ? slot[p] : (kDone << 16);
+        const u32 tag = s >> 16;
+        if (tag != kDone && (tag & kMid)) {
+          const u32 sid = tag & 0x7fffu;
+          const u32 idx = s & 0xffffu;
+          const u32 e = sub[sid];
+          const u32 jn = e & 0xffffu;
+          const u32 zlo = (e >> 16) + cle[sid], zc = cmi[sid];
+          const float mkf = kcol[idx];
+          const u32 mk = orderable(mkf);
+          const u32 mid = idrow[idx];
+          u32 rank = 0;
+          for (u32 q = zlo; q < zlo + zc; ++q) {
+            const u32 oi = slot[q] & 0xffffu;
+            const u32 qk = orderable(kcol[oi]);
+            rank += (qk < mk || (qk == mk && idrow[oi] < mid)) ? 1u : 0u;
+          }
+          const u32 t = jn / 2 - cle[sid];
+          const u32 nsid = rank < t ? 2 * sid : (rank > t ? 2 * sid + 1 : kDone);
+          np[i] = zlo + rank;
+          ns[i] = idx | (nsid << 16);
+          if (rank == t && more) {
+            const float* pc = cc + sid * dim * 2;
+            float* lc = nc + (2 * sid) * dim * 2;
+            float* rc = nc + (2 * sid + 1) * dim * 2;
+            for (int c = 0; c < dim; ++c) {
+              const float clo = pc[2 * c], chi = pc[2 * c + 1];
+              lc[2 * c] = clo;
+              lc[2 * c + 1] = c == axis ? mkf : chi;
+              rc[2 * c] = c == axis ? mkf : clo;
+              rc[2 * c + 1] = chi;
             }
-            const u32 t = jn / 2 - cle[sid];
-            const u32 nsid = rank < t ? 2 * sid : (rank > t ? 2 * sid + 1 : kDone);
-            np[i] = zlo + rank;
-            ns[i] = idx | (nsid << 16);
           }
         }
       }
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i)
-        if (np[i] != 0xffffffffu) slot[np[i]] = ns[i];
-      __syncthreads();
+      float* t = cc;
+      cc = nc;
+      nc = t;
     } else {
       // ---------------- counting path (sub-segments of <= kSmall points) ----------------
-      __syncthreads();  // keyv complete
-      u32 np[ITEMS], ns[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid + i * THREADS;
+        if ((sl[i] >> 16) != kDone) keyv[p] = orderable(kf[i]);
+      }
+      __syncthreads();
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         np[i] = 0xffffffffu;
@@ -295,12 +284,20 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
           const u32 idx = sl[i] & 0xffffu;
           const u32 e = sub[sid];
           const u32 jlo = e >> 16, jn = e & 0xffffu;
-          const u32 mk = ok[i];
-          const u32 mid = idrow[idx];
-          u32 rank = 0;
-          for (u32 q = jlo; q < jlo + jn; ++q) {
-            const u32 qk = keyv[q];
-            rank += (qk < mk || (qk == mk && idrow[slot[q] & 0xffffu] < mid)) ? 1u : 0u;
+          const u32 mk = orderable(kf[i]);
+          u32 qk[kSmall];
+#pragma unroll
+          for (int k = 0; k < kSmall; ++k) qk[k] = k < int(jn) ? keyv[jlo + k] : 0xffffffffu;
+          u32 rank = 0, ties = 0;
+#pragma unroll
+          for (int k = 0; k < kSmall; ++k) {
+            rank += qk[k] < mk ? 1u : 0u;
+            ties |= (k < int(jn) && qk[k] == mk && jlo + k != u32(tid + i * THREADS)) ? (1u << k) : 0u;
+          }
+          if (ties) {  // equal coordinates: order by id
+            const u32 mid = idrow[idx];
+            for (int k = 0; k < kSmall; ++k)
+              if ((ties >> k) & 1u) rank += idrow[slot[jlo + k] & 0xffffu] < mid ? 1u : 0u;
           }
           const u32 half = jn / 2;
           const u32 nsid = rank < half ? 2 * sid : (rank > half ? 2 * sid + 1 : kDone);
@@ -309,23 +306,14 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
         }
       }
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i)
-        if (np[i] != 0xffffffffu) slot[np[i]] = ns[i];
-      __syncthreads();
     }
-    // sub-segment table of the next level
-    if ((n >> (l + 1)) > 0) {
-      u32 ev[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+      if (np[i] != 0xffffffffu) slot[np[i]] = ns[i];
+    if (more) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        const int j = tid + i * kBlock;
-        ev[i] = j < S ? sub[j] : 0u;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const int j = tid + i * kBlock;
+        const int j = tid + i * THREADS;
         if (j < S) {
           const u32 lo = ev[i] >> 16, m = ev[i] & 0xffffu;
           const u32 mr = m >= 1 ? m - m / 2 - 1 : 0u;
@@ -333,50 +321,63 @@ __global__ __launch_bounds__(kBlock) void k_subtree(SubArgs a) {
           sub[2 * j + 1] = ((lo + m / 2 + 1) << 16) | mr;
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
   }
   // in-order rows out, AoS, coalesced
   const i64 total = i64(n) * dim;
   float* outp = a.out_pts + glo * dim;
-  for (i64 f = tid; f < total; f += kBlock) {
+  for (i64 f = tid; f < total; f += THREADS) {
     const int k = int(f / dim);
     const int c = int(f - i64(k) * dim);
     outp[f] = rows[c * NM + (slot[k] & 0xffffu)];
   }
-  for (int k = tid; k < n; k += kBlock) a.out_ids[glo + k] = idrow[slot[k] & 0xffffu];
+  for (int k = tid; k < n; k += THREADS) a.out_ids[glo + k] = idrow[slot[k] & 0xffffu];
 }
 
-template <int ITEMS>
-void launch_items(const SubArgs& a, i64 segs, size_t lds, hipStream_t stream) {
+template <int ITEMS, int THREADS>
+void launch_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
   static bool attr_set = false;
+  const size_t lds = subtree_lds_bytes(a.dim, ITEMS * THREADS);
   if (!attr_set) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree<ITEMS>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBudget)));
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree<ITEMS, THREADS>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
     attr_set = true;
   }
-  k_subtree<ITEMS><<<dim3(unsigned(segs)), kBlock, lds, stream>>>(a);
+  k_subtree<ITEMS, THREADS><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
   PKD_LAUNCH_CHECK();
 }
 
 }  // namespace
 
 int subtree_capacity(int dim) {
-  for (int nm = 4096; nm >= 32; nm /= 2)
-    if (subtree_lds_bytes(dim, nm) <= kLdsBudget) return nm;
+  // Prefer two workgroups per CU (LDS <= ~78 KiB) so one block's barriers hide behind the
+  // other's work; fall back to smaller capacities for high dimensions.
+  for (int nm = 2048; nm >= 64; nm /= 2)
+    if (subtree_lds_bytes(dim, nm) <= kLdsMax / 2) return nm;
+  for (int nm = 64; nm >= 32; nm /= 2)
+    if (subtree_lds_bytes(dim, nm) <= kLdsMax) return nm;
   throw std::invalid_argument("pkdtree: dimension too large for the LDS subtree kernel");
 }
 
-void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, const i64* seg_n, i64 heap0, i64 segs,
-                    int depth_base, int nmax, float* out_pts, u32* out_ids, hipStream_t stream) {
+int subtree_capacity_max(int dim) {
+  for (int nm = 4096; nm >= 32; nm /= 2)
+    if (subtree_lds_bytes(dim, nm) <= kLdsMax) return nm;
+  throw std::invalid_argument("pkdtree: dimension too large for the LDS subtree kernel");
+}
+
+void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, const i64* seg_n, const float* cells,
+                    i64 heap0, i64 segs, int depth_base, int nmax, float* out_pts, u32* out_ids, u32* err,
+                    hipStream_t stream) {
   if (segs <= 0) return;
-  SubArgs a{cols, ncol, dim, seg_lo, seg_n, heap0, depth_base, nmax, out_pts, out_ids};
-  const size_t lds = subtree_lds_bytes(dim, nmax);
-  if (nmax > 2048) launch_items<16>(a, segs, lds, stream);
-  else if (nmax > 1024) launch_items<8>(a, segs, lds, stream);
-  else if (nmax > 512) launch_items<4>(a, segs, lds, stream);
-  else if (nmax > 256) launch_items<2>(a, segs, lds, stream);
-  else launch_items<1>(a, segs, lds, stream);
+  SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err};
+  if (nmax > 2048) launch_cfg<4, 1024>(a, segs, stream);
+  else if (nmax > 1024) launch_cfg<4, 512>(a, segs, stream);
+  else if (nmax > 512) launch_cfg<4, 256>(a, segs, stream);
+  else if (nmax > 256) launch_cfg<2, 256>(a, segs, stream);
+  else if (nmax > 128) launch_cfg<1, 256>(a, segs, stream);
+  else if (nmax > 64) launch_cfg<1, 128>(a, segs, stream);
+  else launch_cfg<1, 64>(a, segs, stream);
 }
 
 }  // namespace pkdtree

@@ -109,7 +109,7 @@ class KDTree:
         slots, d2 = ops.nn_cpu(self.tree_pts.cpu().contiguous(), q, self.depth0, brute=(method == "brute"))
         ids = self.tree_ids.cpu().to(torch.int64)[slots] & 0xFFFFFFFF
         # distance printed by the reference: sqrt(distance_squared(query, nn)), computed in fp32
-        return torch.sqrt(d2), ids
+        return ops.query.sqrt_exact(d2), ids
 
     def nearest_neighbor(self, query: Point) -> Optional[Node]:
         """Reference API (kdtree_sequential.cpp:133-136): the Node of the nearest point."""

@@ -40,7 +40,14 @@ def finalize(packed: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         d, i = native().nn_finalize(packed.contiguous())
         return d, i
     d2, ids = unpack(packed)
-    return torch.sqrt(d2), ids
+    return sqrt_exact(d2), ids
+
+
+def sqrt_exact(d2: torch.Tensor) -> torch.Tensor:
+    """Correctly rounded fp32 sqrt on the host. torch's CPU sqrt may use a 0.5001-ulp SIMD
+    polynomial on some CPUs; numpy uses the hardware sqrt instruction (IEEE exact)."""
+    import numpy as np
+    return torch.from_numpy(np.sqrt(d2.detach().cpu().to(torch.float32).numpy()))
 
 
 def nn_cpu(tree_pts: torch.Tensor, queries: torch.Tensor, depth0: int = 0, brute: bool = False):
