@@ -74,14 +74,50 @@ __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i6
 
 // ---------------------------------------------------------------------------------------
 // AoS input -> SoA working columns (+ ids column) and the bounding box (orderable u32).
+// D > 0: one thread per row, the row's D loads issued before its D column stores (each
+// column store is fully coalesced) and the box reduced in registers; D == 0: runtime dim.
+template <int D>
 __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                  u32 id_base, float* __restrict__ cols, i64 n, int dim,
                                                  u32* __restrict__ bbox) {
   extern __shared__ __align__(16) u32 sbox[];  // [2*dim]
+  const i64 stride = i64(gridDim.x) * kBlock;
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * n);
+  if (D > 0) {
+    constexpr int DD = D > 0 ? D : 1;
+    u32 mn[DD], mx[DD];
+#pragma unroll
+    for (int c = 0; c < DD; ++c) {
+      mn[c] = 0xffffffffu;
+      mx[c] = 0u;
+    }
+    for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
+      float v[DD];
+#pragma unroll
+      for (int c = 0; c < DD; ++c) v[c] = pts[r * DD + c];
+      const u32 id = ids ? ids[r] : id_base + u32(r);
+#pragma unroll
+      for (int c = 0; c < DD; ++c) {
+        cols[i64(c) * n + r] = v[c];
+        const u32 k = orderable(v[c]);
+        mn[c] = min(mn[c], k);
+        mx[c] = max(mx[c], k);
+      }
+      idcol[r] = id;
+    }
+#pragma unroll
+    for (int c = 0; c < DD; ++c) {
+      const u32 a = dev::wave_min_u32(mn[c]), b = dev::wave_max_u32(mx[c]);
+      if (dev::lane() == 0) {
+        atomicMin(&bbox[c], a);
+        atomicMax(&bbox[DD + c], b);
+      }
+    }
+    return;
+  }
   for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sbox[c] = (c < dim) ? 0xffffffffu : 0u;
   __syncthreads();
   const i64 total = n * i64(dim);
-  const i64 stride = i64(gridDim.x) * kBlock;
   for (i64 f = i64(blockIdx.x) * kBlock + threadIdx.x; f < total; f += stride) {
     const float v = pts[f];
     const i64 r = f / dim;
@@ -91,7 +127,6 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
     atomicMin(&sbox[c], k);
     atomicMax(&sbox[dim + c], k);
   }
-  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * n);
   for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride)
     idcol[r] = ids ? ids[r] : id_base + u32(r);
   __syncthreads();
@@ -158,6 +193,8 @@ struct LevelArgs {
   float* out_pts;
   u32* out_ids;
   u32* err;              // sticky error word (bit 0: partition overflow, bit 1: refine)
+  int block_reserve;     // 1: count the block's zones first and reserve once per block
+  int small_done;        // 1: k_refine_small already resolved middle zones of <= 64 points
 };
 
 // Histogram of a level's keys (used for the first global level only; later levels get
@@ -302,6 +339,38 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   const int axis = a.axis, naxis = a.next_axis;
   const int w = threadIdx.x / 64;
   const int ln = dev::lane();
+  __shared__ u32 bcur[4];
+  if (a.block_reserve) {
+    // Few segments and many blocks per segment: per-chunk cursor atomics would all hit the
+    // same three words. Count this block's zones from the key column first (an extra 4 B
+    // read per point, served from the Infinity Cache on the second pass) and reserve once.
+    u32 cnt0 = 0, cnt1 = 0;
+    const float* kc = src + i64(axis) * nc + lo;
+    for (i64 e = b0 + threadIdx.x; e < b1; e += kBlock) {
+      const u32 b = bucket_of(kc[e], prm, a.bins);
+      cnt0 += b < bstar ? 1u : 0u;
+      cnt1 += b == bstar ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cnt0 += __shfl_xor(cnt0, o, 64);
+      cnt1 += __shfl_xor(cnt1, o, 64);
+    }
+    if (ln == 0) {
+      gcnt[0][w] = cnt0;
+      gcnt[1][w] = cnt1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      u32 t0 = 0, t1 = 0;
+      for (int k = 0; k < kBlock / 64; ++k) {
+        t0 += gcnt[0][k];
+        t1 += gcnt[1][k];
+      }
+      const u32 tz = threadIdx.x == 0 ? t0 : (threadIdx.x == 1 ? t1 : u32(b1 - b0) - t0 - t1);
+      bcur[threadIdx.x] = tz ? atomicAdd(&st->cur[threadIdx.x], tz) : 0u;
+    }
+  }
   __syncthreads();
 
   for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
@@ -364,8 +433,13 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       const u32 incl = dev::wave_incl_scan(v);
       const u32 tot = __shfl(incl, 63, 64);
       u32 base = 0;
-      if (ln == 0 && tot) base = atomicAdd(&st->cur[w], tot);
-      base = __shfl(base, 0, 64);
+      if (a.block_reserve) {
+        base = bcur[w];
+        if (ln == 0) bcur[w] = base + tot;
+      } else {
+        if (ln == 0 && tot) base = atomicAdd(&st->cur[w], tot);
+        base = __shfl(base, 0, 64);
+      }
       gcnt[w][ln] = base + incl - v;
     }
     __syncthreads();
@@ -470,6 +544,7 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   float* __restrict__ dst = a.dst;           // the middle zone lives here
   float* __restrict__ alt = const_cast<float*>(a.src);  // dead input buffer: staging area
   const bool fuse = a.next_bins > 0;
+  if (a.small_done && st.cnt_mid <= 64) return;
   i64 zlo = lo + st.cnt_less;
   i64 zc = st.cnt_mid;
   i64 t = n / 2 - i64(st.cnt_less);
@@ -605,6 +680,64 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   }
 }
 
+// One wave per segment for the common case of a middle zone of <= 64 points: each lane
+// holds one whole row (NCOL = dim + 1 <= 9 registers), ranks its composite key against the
+// other lanes with shuffles and writes the row back in place (a wave's stores issue only
+// after all of its loads returned, so in-place is safe inside the wave).
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_refine_small(LevelArgs a, i64 segs) {
+  constexpr int D = NCOL - 1;
+  const i64 s = i64(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  if (s >= segs) return;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  if (n <= 0) return;
+  const SegState st = a.state[h];
+  if (st.cnt_mid > 64) return;
+  const i64 lo = a.seg_lo[h];
+  const int zc = int(st.cnt_mid);
+  const int t = int(n / 2 - i64(st.cnt_less));
+  const i64 zlo = lo + st.cnt_less;
+  const i64 nc = a.ncol;
+  const int l = dev::lane();
+  const bool valid = l < zc;
+  float row[NCOL];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) row[c] = valid ? a.dst[i64(c) * nc + zlo + l] : 0.0f;
+  float key = row[0], nkey = row[0];
+#pragma unroll
+  for (int c = 1; c < D; ++c) {
+    key = c == a.axis ? row[c] : key;
+    nkey = c == a.next_axis ? row[c] : nkey;
+  }
+  const u32 id = __float_as_uint(row[D]);
+  const u64 k = valid ? composite_key(key, id) : ~0ull;
+  u32 rank = 0;
+  for (int j = 0; j < zc; ++j) rank += dev::shfl_u64(k, j) < k ? 1u : 0u;
+  if (!valid) return;
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) a.dst[i64(c) * nc + zlo + rank] = row[c];
+  if (int(rank) == t) {
+    const i64 mpos = lo + n / 2;
+#pragma unroll
+    for (int c = 0; c < D; ++c) a.out_pts[mpos * D + c] = row[c];
+    a.out_ids[mpos] = id;
+    const float* cell = a.cells + h * 2 * D;
+    float* cl_ = a.cells + (2 * h + 1) * 2 * D;
+    float* cr_ = a.cells + (2 * h + 2) * 2 * D;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const float clo = cell[2 * c], chi = cell[2 * c + 1];
+      cl_[2 * c] = clo;
+      cl_[2 * c + 1] = c == a.axis ? key : chi;
+      cr_[2 * c] = c == a.axis ? key : clo;
+      cr_[2 * c + 1] = chi;
+    }
+  } else if (a.next_bins > 0) {
+    add_next_hist(a, s, h, int(rank) < t ? 0 : 1, nkey);
+  }
+}
+
 int pow2_floor(i64 v) {
   int p = 1;
   while (i64(p) * 2 <= v) p *= 2;
@@ -690,9 +823,20 @@ void GpuBuilder::build(const float* pts, const u32* ids, u32 id_base, float* out
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
-  const i64 total = n_ * dim_;
+  const i64 total = dim_ <= 8 ? n_ : n_ * dim_;
   const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
-  k_prep<<<grid, kBlock, size_t(2 * dim_) * 4, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox);
+  const size_t lds = size_t(2 * dim_) * 4;
+  switch (dim_) {
+    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+  }
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }
@@ -753,6 +897,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.out_pts = out_pts;
     a.out_ids = out_ids;
     a.err = err;
+    a.block_reserve = lp.bps > 4 ? 1 : 0;
     if (l == 0) {
       PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
       k_hist<<<int(lp.segs * lp.bps), kBlock, size_t(lp.bins) * 4, stream>>>(a, hist[0]);
@@ -770,6 +915,21 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       default: k_partition<0><<<grid, kBlock, lds, stream>>>(a); break;
     }
     PKD_LAUNCH_CHECK();
+    a.small_done = dim_ <= 8 ? 1 : 0;
+    if (a.small_done) {
+      const int g = int((lp.segs + 3) / 4);
+      switch (dim_) {
+        case 1: k_refine_small<2><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 2: k_refine_small<3><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 3: k_refine_small<4><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 4: k_refine_small<5><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 5: k_refine_small<6><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 6: k_refine_small<7><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        case 7: k_refine_small<8><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+        default: k_refine_small<9><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
+      }
+      PKD_LAUNCH_CHECK();
+    }
     k_refine<<<int(lp.segs), kBlock, 0, stream>>>(a);
     PKD_LAUNCH_CHECK();
     std::swap(src, dst);

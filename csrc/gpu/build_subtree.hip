@@ -57,21 +57,25 @@ struct SubArgs {
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
 
 // Wave-aggregated LDS reservation: lanes with equal `key` get consecutive slots from
-// cursor[key]; returns this lane's slot. One LDS atomic per distinct key per wave.
+// cursor[key]; returns this lane's slot. One LDS atomic per distinct key per wave; the
+// atomics are issued back to back (group leaders are found with scalar readlanes) and
+// their results are gathered with a single permute at the end.
 __device__ __forceinline__ u32 reserve(u32 key, bool active, u32* cursor) {
   u64 pending = __ballot(active);
-  u32 mine = 0;
+  u32 lead_res = 0, my_leader = 0, my_rank = 0;
+  const int ln = dev::lane();
   while (pending) {
     const int leader = __ffsll((long long)pending) - 1;
-    const u32 lk = __shfl(key, leader, 64);
+    const u32 lk = __builtin_amdgcn_readlane(key, leader);
     const u64 m = __ballot(active && key == lk) & pending;
-    u32 base = 0;
-    if (dev::lane() == leader) base = atomicAdd(&cursor[lk], u32(__popcll(m)));
-    base = __shfl(base, leader, 64);
-    if (active && key == lk) mine = base + mbcnt(m);
+    if (ln == leader) lead_res = atomicAdd(&cursor[lk], u32(__popcll(m)));
+    if (active && key == lk) {
+      my_leader = u32(leader);
+      my_rank = mbcnt(m);
+    }
     pending &= ~m;
   }
-  return mine;
+  return __shfl(lead_res, int(my_leader), 64) + my_rank;
 }
 
 template <int ITEMS, int THREADS>
@@ -240,11 +244,22 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
           const float mkf = kcol[idx];
           const u32 mk = orderable(mkf);
           const u32 mid = idrow[idx];
+          // the zone holds ~2 points on average: gather up to 8 with independent loads
+          constexpr int kZ = 8;
+          u32 oi[kZ];
+#pragma unroll
+          for (int k = 0; k < kZ; ++k) oi[k] = u32(k) < zc ? (slot[zlo + k] & 0xffffu) : idx;
           u32 rank = 0;
-          for (u32 q = zlo; q < zlo + zc; ++q) {
-            const u32 oi = slot[q] & 0xffffu;
-            const u32 qk = orderable(kcol[oi]);
-            rank += (qk < mk || (qk == mk && idrow[oi] < mid)) ? 1u : 0u;
+#pragma unroll
+          for (int k = 0; k < kZ; ++k) {
+            const u32 qk = orderable(kcol[oi[k]]);
+            const u32 qi = idrow[oi[k]];
+            rank += (qk < mk || (qk == mk && qi < mid)) ? 1u : 0u;
+          }
+          for (u32 q = zlo + kZ; q < zlo + zc; ++q) {
+            const u32 o = slot[q] & 0xffffu;
+            const u32 qk = orderable(kcol[o]);
+            rank += (qk < mk || (qk == mk && idrow[o] < mid)) ? 1u : 0u;
           }
           const u32 t = jn / 2 - cle[sid];
           const u32 nsid = rank < t ? 2 * sid : (rank > t ? 2 * sid + 1 : kDone);
