@@ -897,7 +897,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.out_pts = out_pts;
     a.out_ids = out_ids;
     a.err = err;
-    a.block_reserve = lp.bps > 4 ? 1 : 0;
+    a.block_reserve = (lp.segs <= 8 && lp.bps > 4) ? 1 : 0;  // only where cursor contention is high
     if (l == 0) {
       PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
       k_hist<<<int(lp.segs * lp.bps), kBlock, size_t(lp.bins) * 4, stream>>>(a, hist[0]);
