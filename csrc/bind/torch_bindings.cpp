@@ -16,6 +16,7 @@
 #include "pkdtree/gpu_query.hpp"
 
 namespace pk = pkdtree;
+using pk::u32;
 
 namespace pkdtree {
 void bind_dist_ops(pybind11::module& m);  // dist_bindings.cpp
@@ -206,7 +207,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("subtree_max", [](const Builder& b) { return b.b.subtree_max(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
       .def("read_error", [](Builder& b) {
-        return int64_t(b.b.read_error(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream()));
+        u32 d[3];
+        const u32 e = b.b.read_error(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream(), d);
+        return std::vector<int64_t>{int64_t(e), int64_t(d[0]), int64_t(d[1]), int64_t(d[2])};
       });
   m.def("generate", &generate, py::arg("seed"), py::arg("dim"), py::arg("rows"), py::arg("first") = 0,
         py::arg("threads") = 0);

@@ -805,11 +805,16 @@ std::string GpuBuilder::describe() const {
   return os.str();
 }
 
-u32 GpuBuilder::read_error(const void* workspace, hipStream_t stream) const {
-  u32 e = 0;
-  PKD_HIP_CHECK(hipMemcpyAsync(&e, static_cast<const char*>(workspace) + off_err_, 4, hipMemcpyDeviceToHost, stream));
+u32 GpuBuilder::read_error(const void* workspace, hipStream_t stream, u32* detail) const {
+  u32 e[4] = {0, 0, 0, 0};
+  PKD_HIP_CHECK(hipMemcpyAsync(e, static_cast<const char*>(workspace) + off_err_, 16, hipMemcpyDeviceToHost, stream));
   PKD_HIP_CHECK(hipStreamSynchronize(stream));
-  return e;
+  if (detail) {
+    detail[0] = e[1];
+    detail[1] = e[2];
+    detail[2] = e[3];
+  }
+  return e[0];
 }
 
 float* GpuBuilder::soa_input(void* workspace) const {

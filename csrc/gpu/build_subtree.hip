@@ -98,8 +98,25 @@ struct Lds {
 // touches is private to the wave and LDS operations of one wave execute in order.
 //   wsub  : local sub-segment table (rel_lo << 16 | n), n0 entries (aliases sub + lo0)
 //   whist : 128 bins; wst: 128 words of per-sub-segment state; wcA/wcB: 2 x [16][dim][2]
+// Orders this wave's LDS writes before its later LDS reads (different lanes): waits for the
+// wave's outstanding LDS operations and fences the compiler.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
+  atomicOr(err, 4u);
+  if (atomicCAS(err + 1, 0u, code) == 0u) {
+    err[2] = t;
+    err[3] = v;
+  }
+}
+
 __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int depth0, u32* wsub, u32* whist,
-                           u32* wst, float* wcA, float* wcB) {
+                           u32* wst, float* wcA, float* wcB, u32* err) {
   const int ln = dev::lane();
   const u32* idrow = reinterpret_cast<const u32*>(L.rows + dim * NM);
   u32* bst = wst;
@@ -109,6 +126,12 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
   float* plo = reinterpret_cast<float*>(wst + 96);
   float* psc = reinterpret_cast<float*>(wst + 112);
   if (ln == 0) wsub[0] = u32(n0);
+  // the block phase left its own sub-segment ids in the slots: restart at local id 0
+  for (int q = ln; q < n0; q += 64) {
+    const u32 sv = L.slot[lo0 + q];
+    if ((sv >> 16) != kDone) L.slot[lo0 + q] = sv & 0xffffu;
+  }
+  wave_sync();
   for (int t = 0;; ++t) {
     const int m = n0 >> t;
     if (m == 0) break;
@@ -135,12 +158,15 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
     if (m > kSmall) {
       const int B = min(64, max(2, pow2_floor_dev(m / 2)));  // S * B <= n0 / 2 <= 128
       if (ln < S) {
+        cmi[ln] = 0;
+        cle[ln] = 0xffffffffu;
         const float* c = wcA + (ln * dim + axis) * 2;
         const BucketParams pr = make_params(c[0], c[1], B);
         plo[ln] = pr.lo;
         psc[ln] = pr.scale;
       }
       for (int b = ln; b < S * B; b += 64) whist[b] = 0;
+      wave_sync();
       u32 bk[kWI];
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -154,6 +180,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           atomicAdd(&whist[sid * B + bk[k]], 1u);
         }
       }
+      wave_sync();
       {  // select: lane l owns bins [2l, 2l+2); sub-segment j owns lanes [j*B/2, (j+1)*B/2)
         const int nb = S * B;
         const int b0 = 2 * ln;
@@ -168,11 +195,16 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           if (r >= rel && r < rel + sum) {
             const u32 v0 = whist[b0];
             const bool first = r < rel + v0;
-            bst[js] = first ? u32(b0) : u32(b0 + 1);
+            bst[js] = (first ? u32(b0) : u32(b0 + 1)) - u32(js * B);  // bucket index within js
             cle[js] = first ? rel : rel + v0;
             cmi[js] = first ? v0 : whist[b0 + 1];
           }
         }
+      }
+      wave_sync();
+      if (ln < S) {  // every sub-segment must have found its median bucket
+        const u32 r = (wsub[ln] & 0xffffu) / 2;
+        if (cle[ln] == 0xffffffffu || r < cle[ln] || r >= cle[ln] + cmi[ln]) report(err, 0x100u | u32(ln), u32(t), wsub[ln]);
       }
       // zone prefixes over the wave's slots (rows of 64 in slot order) with ballots
       u32 zk[kWI], pz[kWI];
@@ -198,6 +230,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
         run1 += __popcll(m1);
         run2 += __popcll(m2);
       }
+      wave_sync();
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
         np[k] = 0xffffffffu;
@@ -206,6 +239,10 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           const u32 sid = sl[k] >> 16;
           const u32 start = z == 0 ? 0u : (z == 1 ? cle[sid] : cle[sid] + cmi[sid]);
           np[k] = (wsub[sid] >> 16) + start + pz[k] - bas[16 * z + sid];
+          if (np[k] - (wsub[sid] >> 16) >= (wsub[sid] & 0xffffu)) {
+            report(err, 0x200u | z, u32(t), np[k]);
+            np[k] = 0xffffffffu;
+          }
           const u32 nsid = z == 0 ? 2 * sid : (z == 2 ? 2 * sid + 1 : (kMid | sid));
           ns[k] = (sl[k] & 0xffffu) | (nsid << 16);
         }
@@ -213,6 +250,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
       for (int k = 0; k < kWI; ++k)
         if (np[k] != 0xffffffffu) L.slot[lo0 + np[k]] = ns[k];
+      wave_sync();
       // exact ranking inside each median bucket
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -239,7 +277,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
             const u32 qk = orderable(kcol[oi[r]]);
             rank += (qk < mk || (qk == mk && idrow[oi[r]] < mid)) ? 1u : 0u;
           }
-          for (u32 r = kZ; r < zc; ++r) {
+          for (u32 r = kZ; r < zc && r < 4096u; ++r) {
             const u32 o = L.slot[lo0 + zlo + r] & 0xffffu;
             const u32 qk = orderable(kcol[o]);
             rank += (qk < mk || (qk == mk && idrow[o] < mid)) ? 1u : 0u;
@@ -262,6 +300,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           }
         }
       }
+      wave_sync();
       float* tmp = wcA;
       wcA = wcB;
       wcB = tmp;
@@ -270,6 +309,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
       for (int k = 0; k < kWI; ++k)
         if ((sl[k] >> 16) != kDone) L.keyv[lo0 + ln + 64 * k] = orderable(kf[k]);
+      wave_sync();
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
         np[k] = 0xffffffffu;
@@ -304,6 +344,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
     for (int k = 0; k < kWI; ++k)
       if (np[k] != 0xffffffffu) L.slot[lo0 + np[k]] = ns[k];
+    wave_sync();
     if (more) {
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -316,6 +357,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
         }
       }
     }
+    wave_sync();
   }
 }
 
@@ -499,7 +541,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
           const u32 qk = orderable(kcol[oi[k]]);
           rank += (qk < mk || (qk == mk && idrow[oi[k]] < mid)) ? 1u : 0u;
         }
-        for (u32 q = zlo + kZ; q < zlo + zc; ++q) {
+        for (u32 q = zlo + kZ; q < zlo + zc && q < zlo + 4096u; ++q) {
           const u32 o = slot[q] & 0xffffu;
           const u32 qk = orderable(kcol[o]);
           rank += (qk < mk || (qk == mk && idrow[o] < mid)) ? 1u : 0u;
@@ -552,7 +594,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
       float* wcA = nc + w * 64 * dim;  // the non-current cell buffer is free now
       float* wcB = wcA + 32 * dim;
       for (int c = dev::lane(); c < 2 * dim; c += 64) wcA[c] = cc[w * 2 * dim + c];
-      wave_build(L, NM, dim, lo0, n0, a.depth_base + l, sub + lo0, hist + w * 128, L.st + w * 128, wcA, wcB);
+      wave_build(L, NM, dim, lo0, n0, a.depth_base + l, sub + lo0, hist + w * 128, L.st + w * 128, wcA, wcB, a.err);
     }
   }
   __syncthreads();

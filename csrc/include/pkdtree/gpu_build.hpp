@@ -61,7 +61,8 @@ class GpuBuilder {
   // receives points straight into that layout.
   float* soa_input(void* workspace) const;
   // Sticky error word of the last build (0 = ok); synchronises the stream. Debug aid.
-  u32 read_error(const void* workspace, hipStream_t stream) const;
+  // detail (optional, 3 words): first failure code, level, value.
+  u32 read_error(const void* workspace, hipStream_t stream, u32* detail = nullptr) const;
   void build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
 
  private:

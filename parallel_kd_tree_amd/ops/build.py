@@ -42,7 +42,11 @@ class GpuTreeBuilder:
 
     def read_error(self) -> int:
         """Sticky device error word of the last build (0 = ok). Synchronises."""
-        return int(self._b.read_error())
+        return int(self._b.read_error()[0])
+
+    def read_error_detail(self):
+        """(error word, first failure code, level, value). Synchronises."""
+        return tuple(int(v) for v in self._b.read_error())
 
     def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
               out_pts: Optional[torch.Tensor] = None, out_ids: Optional[torch.Tensor] = None):
