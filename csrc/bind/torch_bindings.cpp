@@ -15,6 +15,10 @@
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_query.hpp"
 
+namespace pkdtree {
+std::string subtree_stamp_report();
+}
+
 namespace pk = pkdtree;
 using pk::u32;
 
@@ -69,6 +73,19 @@ struct Builder {
     TORCH_CHECK(oi.numel() == b.n() && oi.scalar_type() == torch::kInt32, "out_ids must be int32 [n]");
     b.build(pts.data_ptr<float>(), opt_ids(ids, b.n(), true), pk::u32(id_base), op.data_ptr<float>(),
             reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(), cur_stream(pts));
+    return {op, oi};
+  }
+
+  // Rows [n, dim+1] (coordinates, id bits): the all-to-all exchange format.
+  std::vector<torch::Tensor> build_rows(const torch::Tensor& rows) {
+    TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == torch::kFloat32 && rows.is_contiguous(), "rows: cuda f32");
+    TORCH_CHECK(rows.dim() == 2 && rows.size(0) == b.n() && rows.size(1) == b.dim() + 1, "rows must be [n, dim+1]");
+    const c10::DeviceGuard guard(rows.device());
+    ensure_ws(rows.device());
+    torch::Tensor op = torch::empty({b.n(), b.dim()}, rows.options());
+    torch::Tensor oi = torch::empty({b.n()}, rows.options().dtype(torch::kInt32));
+    b.build_rows(rows.data_ptr<float>(), op.data_ptr<float>(), reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()),
+                 ws.data_ptr(), cur_stream(rows));
     return {op, oi};
   }
 
@@ -200,6 +217,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("subtree_max") = 0)
       .def("build", &Builder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0,
            py::arg("out_pts") = c10::nullopt, py::arg("out_ids") = c10::nullopt)
+      .def("build_rows", &Builder::build_rows, py::arg("rows"))
       .def("soa_input", &Builder::soa_input)
       .def("build_from_soa", &Builder::build_from_soa)
       .def_property_readonly("workspace_bytes", [](const Builder& b) { return int64_t(b.b.workspace_bytes()); })
@@ -223,5 +241,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("method") = "brute", py::arg("depth0") = 0, py::arg("into") = c10::nullopt);
   m.def("nn_finalize", &nn_finalize, py::arg("packed"));
   m.def("subtree_capacity", &pk::default_subtree_max);
+  m.def("subtree_stamp_report", &pk::subtree_stamp_report);
   pkdtree::bind_dist_ops(m);
 }

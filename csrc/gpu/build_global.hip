@@ -79,7 +79,7 @@ __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i6
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                  u32 id_base, float* __restrict__ cols, i64 n, int dim,
-                                                 u32* __restrict__ bbox) {
+                                                 u32* __restrict__ bbox, int rs, int ids_in_row) {
   extern __shared__ __align__(16) u32 sbox[];  // [2*dim]
   const i64 stride = i64(gridDim.x) * kBlock;
   u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * n);
@@ -94,8 +94,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
     for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
       float v[DD];
 #pragma unroll
-      for (int c = 0; c < DD; ++c) v[c] = pts[r * DD + c];
-      const u32 id = ids ? ids[r] : id_base + u32(r);
+      for (int c = 0; c < DD; ++c) v[c] = pts[r * rs + c];
+      const u32 id = ids_in_row ? __float_as_uint(pts[r * rs + DD]) : (ids ? ids[r] : id_base + u32(r));
 #pragma unroll
       for (int c = 0; c < DD; ++c) {
         cols[i64(c) * n + r] = v[c];
@@ -119,16 +119,16 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
   __syncthreads();
   const i64 total = n * i64(dim);
   for (i64 f = i64(blockIdx.x) * kBlock + threadIdx.x; f < total; f += stride) {
-    const float v = pts[f];
     const i64 r = f / dim;
     const int c = int(f - r * dim);
+    const float v = pts[r * rs + c];
     cols[i64(c) * n + r] = v;
     const u32 k = orderable(v);
     atomicMin(&sbox[c], k);
     atomicMax(&sbox[dim + c], k);
   }
   for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride)
-    idcol[r] = ids ? ids[r] : id_base + u32(r);
+    idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
   __syncthreads();
   for (int c = threadIdx.x; c < dim; c += kBlock) {
     atomicMin(&bbox[c], sbox[c]);
@@ -823,6 +823,16 @@ float* GpuBuilder::soa_input(void* workspace) const {
 
 void GpuBuilder::build(const float* pts, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
                        void* workspace, hipStream_t stream) const {
+  prep_and_run(pts, dim_, false, ids, id_base, out_pts, out_ids, workspace, stream);
+}
+
+void GpuBuilder::build_rows(const float* rows, float* out_pts, u32* out_ids, void* workspace,
+                            hipStream_t stream) const {
+  prep_and_run(rows, dim_ + 1, true, nullptr, 0, out_pts, out_ids, workspace, stream);
+}
+
+void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base,
+                              float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
@@ -832,15 +842,15 @@ void GpuBuilder::build(const float* pts, const u32* ids, u32 id_base, float* out
   const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
   const size_t lds = size_t(2 * dim_) * 4;
   switch (dim_) {
-    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
-    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox); break;
+    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
   }
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);

@@ -13,7 +13,11 @@
 // This collapses the bottom ~12 levels of build_tree_rec (kdtree_sequential.cpp:30-66),
 // where the reference spends millions of tiny sorts and `new Node`s.
 #include <algorithm>
+#include <cstdlib>
+#include <sstream>
 #include <stdexcept>
+#include <string>
+#include <vector>
 
 #include "device_utils.hpp"
 #include "pkdtree/hip_check.hpp"
@@ -52,6 +56,7 @@ struct SubArgs {
   float* out_pts;
   u32* out_ids;
   u32* err;
+  unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][8] s_memtime
 };
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
@@ -107,6 +112,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ void stamp(const SubArgs& a, int i) {
+  if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memtime();
+}
+
 __device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
   atomicOr(err, 4u);
   if (atomicCAS(err + 1, 0u, code) == 0u) {
@@ -131,7 +140,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
     const u32 sv = L.slot[lo0 + q];
     if ((sv >> 16) != kDone) L.slot[lo0 + q] = sv & 0xffffu;
   }
-  wave_sync();
+  const int rows_used = (n0 + 63) / 64;  // wave-uniform: rows of 64 slots that exist
   for (int t = 0;; ++t) {
     const int m = n0 >> t;
     if (m == 0) break;
@@ -144,7 +153,7 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
     for (int k = 0; k < kWI; ++k) {
       const int q = ln + 64 * k;
-      sl[k] = q < n0 ? L.slot[lo0 + q] : (kDone << 16);
+      sl[k] = (k < rows_used && q < n0) ? L.slot[lo0 + q] : (kDone << 16);
     }
 #pragma unroll
     for (int k = 0; k < kWI; ++k) kf[k] = ((sl[k] >> 16) != kDone) ? kcol[sl[k] & 0xffffu] : 0.0f;
@@ -166,7 +175,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
         psc[ln] = pr.scale;
       }
       for (int b = ln; b < S * B; b += 64) whist[b] = 0;
-      wave_sync();
       u32 bk[kWI];
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -180,7 +188,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           atomicAdd(&whist[sid * B + bk[k]], 1u);
         }
       }
-      wave_sync();
       {  // select: lane l owns bins [2l, 2l+2); sub-segment j owns lanes [j*B/2, (j+1)*B/2)
         const int nb = S * B;
         const int b0 = 2 * ln;
@@ -201,7 +208,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           }
         }
       }
-      wave_sync();
       if (ln < S) {  // every sub-segment must have found its median bucket
         const u32 r = (wsub[ln] & 0xffffu) / 2;
         if (cle[ln] == 0xffffffffu || r < cle[ln] || r >= cle[ln] + cmi[ln]) report(err, 0x100u | u32(ln), u32(t), wsub[ln]);
@@ -230,7 +236,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
         run1 += __popcll(m1);
         run2 += __popcll(m2);
       }
-      wave_sync();
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
         np[k] = 0xffffffffu;
@@ -250,7 +255,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
       for (int k = 0; k < kWI; ++k)
         if (np[k] != 0xffffffffu) L.slot[lo0 + np[k]] = ns[k];
-      wave_sync();
       // exact ranking inside each median bucket
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -267,17 +271,9 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           const float mkf = kcol[idx];
           const u32 mk = orderable(mkf);
           const u32 mid = idrow[idx];
-          constexpr int kZ = 8;
-          u32 oi[kZ];
-#pragma unroll
-          for (int r = 0; r < kZ; ++r) oi[r] = u32(r) < zc ? (L.slot[lo0 + zlo + r] & 0xffffu) : idx;
           u32 rank = 0;
-#pragma unroll
-          for (int r = 0; r < kZ; ++r) {
-            const u32 qk = orderable(kcol[oi[r]]);
-            rank += (qk < mk || (qk == mk && idrow[oi[r]] < mid)) ? 1u : 0u;
-          }
-          for (u32 r = kZ; r < zc && r < 4096u; ++r) {
+#pragma unroll 4
+          for (u32 r = 0; r < zc && r < 4096u; ++r) {
             const u32 o = L.slot[lo0 + zlo + r] & 0xffffu;
             const u32 qk = orderable(kcol[o]);
             rank += (qk < mk || (qk == mk && idrow[o] < mid)) ? 1u : 0u;
@@ -300,7 +296,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           }
         }
       }
-      wave_sync();
       float* tmp = wcA;
       wcA = wcB;
       wcB = tmp;
@@ -309,7 +304,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
       for (int k = 0; k < kWI; ++k)
         if ((sl[k] >> 16) != kDone) L.keyv[lo0 + ln + 64 * k] = orderable(kf[k]);
-      wave_sync();
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
         np[k] = 0xffffffffu;
@@ -319,20 +313,12 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
           const u32 e = wsub[sid];
           const u32 jlo = e >> 16, jn = e & 0xffffu;
           const u32 mk = orderable(kf[k]);
-          u32 qk[kSmall];
-#pragma unroll
-          for (int r = 0; r < kSmall; ++r) qk[r] = r < int(jn) ? L.keyv[lo0 + jlo + r] : 0xffffffffu;
-          u32 rank = 0, ties = 0;
+          u32 rank = 0;
           const u32 self = u32(ln + 64 * k) - jlo;
-#pragma unroll
-          for (int r = 0; r < kSmall; ++r) {
-            rank += qk[r] < mk ? 1u : 0u;
-            ties |= (r < int(jn) && qk[r] == mk && u32(r) != self) ? (1u << r) : 0u;
-          }
-          if (ties) {
-            const u32 mid = idrow[idx];
-            for (int r = 0; r < kSmall; ++r)
-              if ((ties >> r) & 1u) rank += idrow[L.slot[lo0 + jlo + r] & 0xffffu] < mid ? 1u : 0u;
+#pragma unroll 8
+          for (u32 r = 0; r < jn; ++r) {
+            const u32 qk = L.keyv[lo0 + jlo + r];
+            rank += (qk < mk || (qk == mk && r != self && idrow[L.slot[lo0 + jlo + r] & 0xffffu] < idrow[idx])) ? 1u : 0u;
           }
           const u32 half = jn / 2;
           const u32 nsid = rank < half ? 2 * sid : (rank > half ? 2 * sid + 1 : kDone);
@@ -344,7 +330,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
 #pragma unroll
     for (int k = 0; k < kWI; ++k)
       if (np[k] != 0xffffffffu) L.slot[lo0 + np[k]] = ns[k];
-    wave_sync();
     if (more) {
 #pragma unroll
       for (int k = 0; k < kWI; ++k) {
@@ -357,7 +342,6 @@ __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int d
         }
       }
     }
-    wave_sync();
   }
 }
 
@@ -392,6 +376,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
   const int tid = threadIdx.x;
   const int w = tid / 64;
   const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
+  stamp(a, 0);
 
   for (int c = 0; c <= dim; ++c) {
     const float* col = a.cols + i64(c) * a.ncol + glo;
@@ -416,6 +401,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
   if (tid == 0) sub[0] = u32(n);
   for (int c = tid; c < 2 * dim; c += THREADS) L.cellA[c] = a.cells[h * 2 * dim + c];
   __syncthreads();
+  stamp(a, 1);
   float* cc = L.cellA;  // cells of the current level
   float* nc = L.cellB;  // cells of the next level
 
@@ -584,6 +570,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
     __syncthreads();
   }
 
+  stamp(a, 2);
   // ---------------- wave phase: every sub-segment (<= kWaveMax) to one wave ----------------
   {
     const int S0 = 1 << l;  // <= W by construction (NM <= W * kWaveMax)
@@ -598,6 +585,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
     }
   }
   __syncthreads();
+  stamp(a, 3);
   // in-order rows out, AoS, coalesced
   const i64 total = i64(n) * dim;
   float* outp = a.out_pts + glo * dim;
@@ -607,6 +595,8 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
     outp[f] = rows[c * NM + (slot[k] & 0xffffu)];
   }
   for (int k = tid; k < n; k += THREADS) a.out_ids[glo + k] = idrow[slot[k] & 0xffffu];
+  __syncthreads();
+  stamp(a, 4);
   (void)W;
 }
 
@@ -624,6 +614,31 @@ void launch_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
 }
 
 }  // namespace
+
+unsigned long long*& subtree_stamp_buffer() {
+  static unsigned long long* p = nullptr;
+  return p;
+}
+
+std::string subtree_stamp_report() {
+  unsigned long long* d = subtree_stamp_buffer();
+  if (!d) return "stamps disabled (set PKD_SUBTREE_STAMPS=1)";
+  std::vector<unsigned long long> h(4096 * 8);
+  PKD_HIP_CHECK(hipDeviceSynchronize());
+  PKD_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+  double acc[4] = {0, 0, 0, 0};
+  int cnt = 0;
+  for (int b = 0; b < 4096; ++b) {
+    const unsigned long long* s = &h[size_t(b) * 8];
+    if (!s[0] || !s[4]) continue;
+    for (int i = 0; i < 4; ++i) acc[i] += double(s[i + 1] - s[i]);
+    ++cnt;
+  }
+  std::ostringstream os;
+  os << "subtree stamps over " << cnt << " blocks (mean cycles): load " << acc[0] / cnt << ", block-phase "
+     << acc[1] / cnt << ", wave-phase " << acc[2] / cnt << ", store " << acc[3] / cnt;
+  return os.str();
+}
 
 int subtree_capacity(int dim) {
   // Prefer two workgroups per CU (LDS <= ~78 KiB) so one block's barriers hide behind the
@@ -645,7 +660,13 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
                     i64 heap0, i64 segs, int depth_base, int nmax, float* out_pts, u32* out_ids, u32* err,
                     hipStream_t stream) {
   if (segs <= 0) return;
-  SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err};
+  static unsigned long long* stamps = nullptr;
+  if (std::getenv("PKD_SUBTREE_STAMPS") && !stamps) {
+    PKD_HIP_CHECK(hipMalloc(&stamps, 4096 * 8 * sizeof(unsigned long long)));
+    PKD_HIP_CHECK(hipMemset(stamps, 0, 4096 * 8 * sizeof(unsigned long long)));
+  }
+  subtree_stamp_buffer() = stamps;
+  SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps};
   if (nmax > 2048) launch_cfg<4, 1024>(a, segs, stream);
   else if (nmax > 1024) launch_cfg<4, 512>(a, segs, stream);
   else if (nmax > 512) launch_cfg<4, 256>(a, segs, stream);

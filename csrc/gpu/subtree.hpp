@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "pkdtree/common.hpp"
 
 namespace pkdtree {
@@ -18,5 +20,8 @@ int subtree_capacity_max(int dim);
 void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, const i64* seg_n, const float* cells,
                     i64 heap0, i64 segs, int depth_base, int nmax, float* out_pts, u32* out_ids, u32* err,
                     hipStream_t stream);
+
+// Diagnostic: per-phase s_memtime report of the last subtree launch (PKD_SUBTREE_STAMPS=1).
+std::string subtree_stamp_report();
 
 }  // namespace pkdtree

@@ -56,6 +56,9 @@ class GpuBuilder {
   void build(const float* pts, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
              void* workspace, hipStream_t stream) const;
 
+  // Rows of dim+1 floats: coordinates then the id bits (the distributed exchange format).
+  void build_rows(const float* rows, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
+
   // Same, but the input already sits in SoA columns inside the workspace (column c of
   // row r at cols[c*n + r], column dim = ids); used by the distributed path which
   // receives points straight into that layout.
@@ -66,6 +69,8 @@ class GpuBuilder {
   void build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
 
  private:
+  void prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base, float* out_pts,
+                    u32* out_ids, void* workspace, hipStream_t stream) const;
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const;
 
   i64 n_;

@@ -1,0 +1,108 @@
+"""Python CLI with the reference protocol, single process or one rank per GPU (torchrun).
+
+    python -m parallel_kd_tree_amd.cli [--decomp single|forest|global] [--mode exact|reference]
+                                       [--device cuda|cpu] [SEED DIM_POINTS NUM_POINTS]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m parallel_kd_tree_amd.cli --decomp global 42 3 100000000
+
+With no positional arguments rank 0 prints READY, reads the seed from stdin and uses dim=128,
+N=500000 (Utility.cpp:92-102); the config is broadcast to every rank (kdtree_mpi.cpp:199).
+forest reproduces kdtree_mpi.cpp (independent per-rank trees + MIN reduction), global builds
+one distributed tree (parallel/global_tree.py). Only rank 0 prints.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="parallel_kd_tree_amd.cli", add_help=True)
+    ap.add_argument("--decomp", choices=["single", "forest", "global"], default=None)
+    ap.add_argument("--mode", choices=["exact", "reference"], default="exact")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default=None)
+    ap.add_argument("--query", choices=["auto", "brute", "traverse"], default="auto")
+    ap.add_argument("--queries", type=int, default=10)
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--metrics-json", action="store_true")
+    ap.add_argument("positional", nargs="*")
+    a = ap.parse_args(argv)
+    tick = time.perf_counter()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_type = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    device = torch.device("cuda", local_rank) if dev_type == "cuda" else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    decomp = a.decomp or ("forest" if world > 1 else "single")
+
+    from .parallel import comm
+    if world > 1:
+        comm.init(backend="nccl" if device.type == "cuda" else "gloo", device=device)
+    from .utils import protocol
+    debug = a.debug or bool(a.positional) or os.environ.get("KDTREE_DEBUG", "0") not in ("", "0")
+    cfg = [0, 0, 0]
+    if rank == 0:
+        if debug:
+            cfg = list(protocol.specify_problem_argv(sys.argv[0], a.positional))
+        else:
+            cfg = list(protocol.specify_problem_stdin())
+    if world > 1:
+        cfg = comm.broadcast_ints(cfg)
+    seed, dim, n = cfg
+    Q = a.queries
+
+    import parallel_kd_tree_amd as pk
+    from . import ops
+    t_gen = time.perf_counter()
+    if decomp == "single":
+        first, cnt = 0, n
+    else:
+        first, cnt = comm.forest_slice(n, world, rank)
+    x = pk.generate_slice(seed, dim, first, cnt).to(device)
+    q = pk.generate_slice(seed, dim, n, Q).to(device)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t_build = time.perf_counter()
+    if decomp == "single":
+        tree = pk.KDTree.build(x, id_base=1, mode=a.mode)
+        from .parallel.global_tree import _local_packed
+        packed = _local_packed(tree, q, a.query)
+    elif decomp == "forest":
+        from .parallel.forest import ForestTree
+        f = ForestTree.build(x, first, n, id_base=1, mode=a.mode)
+        packed = f.query_packed(q, a.query)
+    else:
+        if a.mode != "exact":
+            raise SystemExit("--decomp global builds exact trees only")
+        from .parallel.global_tree import GlobalTreeBuilder
+        t = GlobalTreeBuilder(n, dim, device=device).build(x, id_base=first + 1)
+        packed = t.query_packed(q, a.query)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t_done = time.perf_counter()
+    dist_sq = ops.unpack(packed.cpu())[0]
+    d = ops.query.sqrt_exact(dist_sq).numpy()
+    if rank == 0:
+        lines = [protocol.result_line(n + i, float(np.float32(d[i]))) for i in range(Q)]
+        print("\n".join(lines), flush=True)
+        if debug:
+            print(f"elapsed time {time.perf_counter() - tick:g} second", flush=True)
+        print("DONE", flush=True)
+        if a.metrics_json:
+            print(json.dumps({"decomp": decomp, "ranks": world, "gen_ms": (t_build - t_gen) * 1e3,
+                              "build_query_ms": (t_done - t_build) * 1e3}), file=sys.stderr, flush=True)
+    if world > 1:
+        comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

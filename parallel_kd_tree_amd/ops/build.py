@@ -52,6 +52,10 @@ class GpuTreeBuilder:
               out_pts: Optional[torch.Tensor] = None, out_ids: Optional[torch.Tensor] = None):
         return tuple(self._b.build(points, ids, int(id_base), out_pts, out_ids))
 
+    def build_rows(self, rows: torch.Tensor):
+        """Build from rows [n, dim+1]: coordinates followed by the id bits (int32 viewed as f32)."""
+        return tuple(self._b.build_rows(rows.contiguous()))
+
     def soa_input(self, device) -> torch.Tensor:
         """[(dim + 1), n] float32 view of the builder's input columns (row ``dim`` = id bits)."""
         return self._b.soa_input(torch.device(device))

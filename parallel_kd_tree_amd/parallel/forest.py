@@ -1,0 +1,36 @@
+"""Forest decomposition — the reference's MPI design (kdtree_mpi.cpp:170-291), one rank per GPU.
+
+Each rank owns the generation-order slice [local*rank, local*rank+local) (remainder on the
+last rank, kdtree_mpi.cpp:208-216), builds an independent tree on it, answers every query
+locally, and one MIN reduction combines the answers (kdtree_mpi.cpp:253). The reduction
+carries the packed (distance, id), so the result also names the neighbour; ranks with no
+points contribute +inf instead of crashing.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..models.kdtree import KDTree
+from . import comm
+from .global_tree import _local_packed
+
+
+class ForestTree:
+    def __init__(self, local: KDTree, first_row: int, n_total: int):
+        self.local = local
+        self.first_row = int(first_row)
+        self.n_total = int(n_total)
+
+    @classmethod
+    def build(cls, points: torch.Tensor, first_row: int, n_total: int, id_base: int = 1, mode: str = "exact",
+              threads: int = 1) -> "ForestTree":
+        """points: this rank's slice; ids are the global ids first_row + i + id_base."""
+        t = KDTree.build(points, id_base=first_row + id_base, mode=mode, threads=threads)
+        return cls(t, first_row, n_total)
+
+    def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
+        """Packed (d2, global id) of the nearest point over all ranks. Reference-mode forests
+        use the reference search on each rank (so results match kdtree_mpi exactly)."""
+        return comm.min_packed_(_local_packed(self.local, queries, method).to(comm.device()))

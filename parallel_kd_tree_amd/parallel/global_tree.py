@@ -1,0 +1,354 @@
+"""Global decomposition: ONE exact kd-tree over P ranks (P a power of two).
+
+North-star design (BASELINE.json): the reference's forest of independent per-rank trees
+(kdtree_mpi.cpp:204-253) becomes a single distributed tree:
+
+1. bounding box: allreduce MIN / MAX of the per-rank boxes;
+2. top log2(P) levels, level by level: every rank histograms its points (routed below the
+   pivots decided so far) into linear buckets of its node's cell, the histograms are
+   allreduced (SUM), the bucket holding each node's median is found, the few points of that
+   bucket are all-gathered and ranked under the (key, id) order -> the exact pivot point of
+   every node at that level, identical on every rank;
+3. one all-to-all: every point goes to the rank owning its top-level leaf (rank r owns heap
+   node P-1+r), pivots stay replicated;
+4. each rank builds its subtree (depth log2 P) with the single-GPU builder.
+
+The result is slot-for-slot the tree a single GPU builds on the concatenated points.
+Communication uses torch.distributed: backend "nccl" (= RCCL over xGMI) on MI355X, "gloo" in
+CPU tests, where the per-rank device ops run as torch code with identical arithmetic.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from . import comm
+from .geometry import composite_u64, make_params, median_slot, segment
+
+TOP_BINS = 8192  # nodes * bins per top level (LDS histogram in the kernel)
+DONE = 0xFFFFFFFF
+
+
+def _to_rows(points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) -> torch.Tensor:
+    n, dim = points.shape
+    if ids is None:
+        ids = (torch.arange(n, dtype=torch.int64, device=points.device) + int(id_base)).to(torch.int32)
+    rows = torch.empty((n, dim + 1), dtype=torch.float32, device=points.device)
+    rows[:, :dim] = points
+    rows[:, dim] = ids.to(torch.int32).view(torch.float32)
+    return rows
+
+
+def _signed_keys(rows: torch.Tensor, dim: int, axis: int) -> torch.Tensor:
+    """Composite keys as int64 with the top bit flipped, so signed order == unsigned order."""
+    kb = rows[:, axis].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    ok = torch.where((kb & 0x80000000) != 0, (~kb) & 0xFFFFFFFF, kb | 0x80000000)
+    ib = rows[:, dim].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return ((ok ^ 0x80000000) << 32) | ib
+
+
+def _u64_to_signed(v: int) -> int:
+    v ^= 1 << 63
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+# --------------------------------------------------------------------------- CPU reference ops
+# Same arithmetic as csrc/gpu/dist_ops.hip; used when the points live on the CPU (gloo tests).
+def _bucket_cpu(x: torch.Tensor, lo: torch.Tensor, scale: torch.Tensor, nb: int) -> torch.Tensor:
+    t = (x - lo) * scale
+    t = torch.nan_to_num(t, nan=0.0, posinf=float(nb - 1), neginf=0.0)
+    return t.clamp(0, nb - 1).to(torch.int64)
+
+
+def _route_cpu(rows, dim, node, pivots_signed, axis):
+    live = node != DONE
+    h = node[live]
+    k = _signed_keys(rows[live], dim, axis)
+    pv = pivots_signed[h]
+    nh = torch.where(k < pv, 2 * h + 1, torch.where(k > pv, 2 * h + 2, torch.full_like(h, DONE)))
+    node[live] = nh
+    return node
+
+
+class _Backend:
+    """Per-rank device ops: HIP kernels on GPU tensors, torch reference code on CPU tensors."""
+
+    def __init__(self, device: torch.device):
+        self.gpu = device.type == "cuda"
+        self.device = device
+
+    def route_hist(self, rows, dim, node, level, pivots_u64, prev_axis, axis, params, bins):
+        nodes = 1 << level
+        if self.gpu:
+            hist = torch.zeros(nodes * bins, dtype=torch.int32, device=self.device)
+            piv = torch.from_numpy(pivots_u64.view(np.int64)).to(self.device)
+            prm = torch.from_numpy(params.reshape(-1)).to(self.device)
+            ops.native().top_route_hist(rows, dim, node, level, piv, prev_axis, axis, prm, bins, hist)
+            return hist
+        if level > 0:
+            piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
+            _route_cpu(rows, dim, node, piv, prev_axis)
+        live = node != DONE
+        j = node[live] - (nodes - 1)
+        prm = torch.from_numpy(params)
+        b = _bucket_cpu(rows[live, axis], prm[j, 0], prm[j, 1], bins)
+        return torch.bincount(j * bins + b, minlength=nodes * bins).to(torch.int32)
+
+    def collect_middle(self, rows, dim, node, level, axis, params, bins, bstar):
+        nodes = 1 << level
+        if self.gpu:
+            prm = torch.from_numpy(params.reshape(-1)).to(self.device)
+            bs = torch.from_numpy(bstar.astype(np.int32)).to(self.device)
+            cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
+            cap = 4096
+            while True:
+                out = torch.empty((cap, dim + 2), dtype=torch.float32, device=self.device)
+                ops.native().top_collect_middle(rows, dim, node, level, axis, prm, bins, bs, out, cnt)
+                c = int(cnt.item())
+                if c <= cap:
+                    return out[:c]
+                cap = c
+        live = (node != DONE).nonzero().flatten()
+        j = node[live] - (nodes - 1)
+        prm = torch.from_numpy(params)
+        b = _bucket_cpu(rows[live, axis], prm[j, 0], prm[j, 1], bins)
+        sel = live[b == torch.from_numpy(bstar.astype(np.int64))[j]]
+        out = torch.empty((sel.numel(), dim + 2), dtype=torch.float32)
+        out[:, :dim + 1] = rows[sel]
+        out[:, dim + 1] = node[sel].to(torch.int32).view(torch.float32)
+        return out
+
+    def pack(self, rows, dim, node, levels, pivots_u64, last_axis, P):
+        if self.gpu:
+            n = rows.shape[0]
+            out = torch.empty_like(rows)
+            counts = torch.empty(P, dtype=torch.int32, device=self.device)
+            scratch = torch.empty(ops.native().top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=self.device)
+            piv = torch.from_numpy(pivots_u64.view(np.int64)).to(self.device)
+            ops.native().top_pack(rows, dim, node, levels, piv, last_axis, P, out, counts, scratch)
+            c = counts.to(torch.int64)
+            return out[: int(c.sum().item())], c
+        piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
+        _route_cpu(rows, dim, node, piv, last_axis)
+        live = (node != DONE).nonzero().flatten()
+        dest = node[live] - (P - 1)
+        order = torch.sort(dest, stable=True).indices
+        return rows[live[order]].contiguous(), torch.bincount(dest, minlength=P).to(torch.int64)
+
+
+@dataclass
+class DistTree:
+    """A rank's share of the global tree plus the replicated top tree."""
+    n_total: int
+    dim: int
+    depth0: int
+    P: int
+    rank: int
+    tree_pts: torch.Tensor           # this rank's subtree (in-order), slots [slot_lo, slot_lo + n)
+    tree_ids: torch.Tensor
+    slot_lo: int
+    top_slots: List[int] = field(default_factory=list)
+    top_rows: Optional[torch.Tensor] = None   # [P-1, dim+1] pivot rows, heap order
+    timings: Dict[str, float] = field(default_factory=dict)
+
+    def gather_full(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Assemble the whole in-order tree on every rank (for checks and small N)."""
+        dev = self.tree_pts.device
+        rows = torch.empty((self.tree_pts.shape[0], self.dim + 1), dtype=torch.float32, device=dev)
+        rows[:, :self.dim] = self.tree_pts
+        rows[:, self.dim] = self.tree_ids.view(torch.float32)
+        parts = _all_gather_var(rows)
+        full = torch.empty((self.n_total, self.dim + 1), dtype=torch.float32, device=dev)
+        for r, part in enumerate(parts):
+            lo, _ = segment(self.n_total, self.P - 1 + r)
+            full[lo:lo + part.shape[0]] = part
+        if self.top_rows is not None:
+            for i, s in enumerate(self.top_slots):
+                if s >= 0:
+                    full[s] = self.top_rows[i].to(dev)
+        return full[:, :self.dim].contiguous(), full[:, self.dim].contiguous().view(torch.int32)
+
+    def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
+        """Exact NN over the whole distributed tree: local subtree + top pivots, MIN-reduced."""
+        from ..models.kdtree import KDTree
+        local = KDTree(self.tree_pts, self.tree_ids, self.depth0 + int(math.log2(self.P)))
+        packed = _local_packed(local, queries, method)
+        if self.top_rows is not None and self.rank == 0:
+            valid = [i for i, s in enumerate(self.top_slots) if s >= 0]
+            if valid:
+                tr = self.top_rows[valid].to(packed.device)
+                pk = _brute_packed(tr[:, :self.dim].contiguous(), tr[:, self.dim].contiguous().view(torch.int32),
+                                   queries.to(packed.device))
+                packed = torch.minimum(packed, pk)
+        return comm.min_packed_(packed)
+
+
+def _local_packed(tree, queries, method):
+    """Packed (d2, id) per query on one rank's tree: GPU kernels for exact GPU trees, the
+    reference search procedure (csrc/cpu/cpu_tree.cpp) for CPU or reference-mode trees."""
+    if tree.tree_pts.is_cuda and tree.mode == "exact":
+        if tree.n == 0:
+            return torch.full((queries.shape[0],), ops.query.INF_PACKED, dtype=torch.int64, device=tree.device)
+        return tree.query_packed(queries, method)
+    if tree.n == 0:
+        return torch.full((queries.shape[0],), ops.query.INF_PACKED, dtype=torch.int64)
+    slots, d2 = ops.nn_cpu(tree.tree_pts.cpu(), queries.cpu().to(torch.float32), tree.depth0)
+    ids = tree.tree_ids.cpu().to(torch.int64)[slots] & 0xFFFFFFFF
+    return ((d2.view(torch.int32).to(torch.int64) << 32) | ids).to(tree.tree_pts.device)
+
+
+def _brute_packed(pts, ids, queries):
+    """Packed (d2, id) minimum over a small point set (the replicated top pivots)."""
+    if pts.is_cuda:
+        return ops.nn_gpu(pts, ids, queries.to(pts.device, torch.float32), "brute")
+    q = queries.cpu().to(torch.float32)
+    best = torch.full((q.shape[0],), ops.query.INF_PACKED, dtype=torch.int64)
+    for i in range(pts.shape[0]):
+        acc = torch.zeros(q.shape[0], dtype=torch.float32)
+        for c in range(pts.shape[1]):  # reference summation order, separately rounded
+            t = pts[i, c].cpu() - q[:, c]
+            acc = acc + t * t
+        v = (acc.view(torch.int32).to(torch.int64) << 32) | (int(ids[i]) & 0xFFFFFFFF)
+        best = torch.minimum(best, v)
+    return best
+
+
+def _all_gather_var(t: torch.Tensor) -> List[torch.Tensor]:
+    """all_gather of tensors whose first dimension differs per rank."""
+    P = comm.world()
+    if P == 1:
+        return [t]
+    cnt = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(P)]
+    dist.all_gather(cnts, cnt)
+    sizes = [int(c.item()) for c in cnts]
+    mx = max(sizes)
+    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    outs = [torch.empty_like(pad) for _ in range(P)]
+    dist.all_gather(outs, pad)
+    return [o[:s] for o, s in zip(outs, sizes)]
+
+
+class GlobalTreeBuilder:
+    """Builds the global tree; reusable across builds of the same (n_total, dim)."""
+
+    def __init__(self, n_total: int, dim: int, device: Optional[torch.device] = None, depth0: int = 0):
+        self.P = comm.world()
+        self.rank = comm.rank()
+        if self.P & (self.P - 1):
+            raise ValueError(f"global decomposition needs a power-of-two world size, got {self.P}")
+        self.L = int(math.log2(self.P))
+        self.n_total, self.dim, self.depth0 = int(n_total), int(dim), int(depth0)
+        self.device = device if device is not None else comm.device()
+        self.backend = _Backend(self.device)
+        leaf = self.P - 1 + self.rank
+        self.slot_lo, self.n_leaf = segment(self.n_total, leaf)
+        self._builder = None
+        if self.device.type == "cuda" and self.n_leaf > 0:
+            self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
+
+    # ------------------------------------------------------------------------------------
+    def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
+        dim, P, L = self.dim, self.P, self.L
+        timings: Dict[str, float] = {}
+        rows = _to_rows(points.to(torch.float32), ids, id_base)
+        n_local = rows.shape[0]
+        # 1. bounding box
+        if n_local > 0:
+            lo = points.amin(0).to(torch.float32)
+            hi = points.amax(0).to(torch.float32)
+        else:
+            lo = torch.full((dim,), float("inf"), device=points.device)
+            hi = torch.full((dim,), float("-inf"), device=points.device)
+        comm.allreduce_(lo, dist.ReduceOp.MIN)
+        comm.allreduce_(hi, dist.ReduceOp.MAX)
+        root_cell = np.stack([lo.cpu().numpy(), hi.cpu().numpy()], 1).astype(np.float32)  # [dim][2]
+        cells = {0: root_cell}
+        node = torch.zeros(n_local, dtype=torch.int64 if not self.backend.gpu else torch.int32, device=rows.device)
+        pivots = np.zeros(max(P - 1, 1), dtype=np.uint64)
+        top_rows = torch.zeros((max(P - 1, 1), dim + 1), dtype=torch.float32)
+        top_slots = [-1] * max(P - 1, 1)
+        # 2. top levels
+        for level in range(L):
+            nodes = 1 << level
+            first = nodes - 1
+            axis = (self.depth0 + level) % dim
+            prev_axis = (self.depth0 + level - 1) % dim
+            bins = TOP_BINS // nodes
+            params = np.zeros((nodes, 2), dtype=np.float32)
+            for j in range(nodes):
+                c = cells.get(first + j, root_cell)
+                params[j] = make_params(c[axis, 0], c[axis, 1], bins)
+            hist = self.backend.route_hist(rows, dim, node, level, pivots, prev_axis, axis, params, bins)
+            comm.allreduce_(hist, dist.ReduceOp.SUM)
+            hh = hist.cpu().numpy().astype(np.int64).reshape(nodes, bins)
+            bstar = np.zeros(nodes, dtype=np.int64)
+            cless = np.zeros(nodes, dtype=np.int64)
+            sizes = [segment(self.n_total, first + j)[1] for j in range(nodes)]
+            for j in range(nodes):
+                if sizes[j] <= 0:
+                    bstar[j] = -1
+                    continue
+                r = sizes[j] // 2
+                cum = np.cumsum(hh[j])
+                if cum[-1] != sizes[j]:
+                    raise RuntimeError(f"top level {level} node {first + j}: {cum[-1]} points, expected {sizes[j]}")
+                b = int(np.searchsorted(cum, r, side="right"))
+                bstar[j] = b
+                cless[j] = int(cum[b - 1]) if b > 0 else 0
+            mid_local = self.backend.collect_middle(rows, dim, node, level, axis, params, bins,
+                                                    np.where(bstar < 0, bins + 1, bstar))
+            mids = torch.cat(_all_gather_var(mid_local), 0).cpu()
+            mnode = mids[:, dim + 1].contiguous().view(torch.int32).numpy().astype(np.int64) & 0xFFFFFFFF
+            mid_np = mids.numpy()
+            for j in range(nodes):
+                h = first + j
+                if bstar[j] < 0:
+                    pivots[h] = np.uint64(0xFFFFFFFFFFFFFFFF)
+                    continue
+                sel = mid_np[mnode == h]
+                keys = composite_u64(sel[:, axis], sel[:, dim].view(np.uint32))
+                order = np.argsort(keys, kind="stable")
+                t = sizes[j] // 2 - int(cless[j])
+                if not (0 <= t < len(order)):
+                    raise RuntimeError(f"top level {level} node {h}: middle bucket has {len(order)} points, "
+                                       f"rank {t} requested")
+                pr = sel[order[t]]
+                pivots[h] = keys[order[t]]
+                top_rows[h] = torch.from_numpy(pr[:dim + 1].copy())
+                top_slots[h] = median_slot(self.n_total, h)
+                cl = cells.get(h, root_cell).copy()
+                cr = cl.copy()
+                cl[axis, 1] = pr[axis]
+                cr[axis, 0] = pr[axis]
+                cells[2 * h + 1] = cl
+                cells[2 * h + 2] = cr
+        # 3. exchange
+        last_axis = (self.depth0 + L - 1) % dim
+        send, counts = self.backend.pack(rows, dim, node, L, pivots, last_axis, P)
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts)
+        in_splits = counts.cpu().tolist()
+        out_splits = recv_counts.cpu().tolist()
+        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=rows.device)
+        dist.all_to_all_single(recv, send, out_splits, in_splits)
+        if recv.shape[0] != self.n_leaf:
+            raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
+        # 4. local subtree
+        if self.n_leaf == 0:
+            tp = torch.empty((0, dim), dtype=torch.float32, device=rows.device)
+            ti = torch.empty((0,), dtype=torch.int32, device=rows.device)
+        elif self._builder is not None:
+            tp, ti = self._builder.build_rows(recv)
+        else:
+            tp, ti = ops.build_cpu(recv[:, :dim].contiguous(), recv[:, dim].contiguous().view(torch.int32), "exact",
+                                   self.depth0 + L, 1)
+        return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
+                        top_slots[: P - 1], top_rows[: P - 1], timings)

@@ -42,6 +42,9 @@ for dim in args.dim:
                 b.build(x, None, 0, tp, ti)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
+            if os.environ.get("PKD_SUBTREE_STAMPS"):
+                from parallel_kd_tree_amd.ops import native
+                print(native().subtree_stamp_report(), flush=True)
             print(json.dumps({"n": n, "dim": dim, "subtree_max": b.subtree_max, "global_levels": b.global_levels,
                               "ms": round(ms, 3), "mpts_s": round(n / ms / 1e3, 1), "err": err, "same_as_first": same}),
                   flush=True)
