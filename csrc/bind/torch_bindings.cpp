@@ -92,7 +92,7 @@ struct Builder {
   // SoA input view inside the workspace: [(dim+1), n] float32 (row dim holds id bits).
   torch::Tensor soa_input(const torch::Device& dev) {
     ensure_ws(dev);
-    return torch::from_blob(b.soa_input(ws.data_ptr()), {b.dim() + 1, b.n()},
+    return torch::from_blob(b.soa_input(ws.data_ptr()), {b.dim() + 1, b.n()}, {b.column_stride(), 1},
                             torch::TensorOptions().dtype(torch::kFloat32).device(dev));
   }
 

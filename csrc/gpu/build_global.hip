@@ -35,6 +35,7 @@ constexpr int kItems = 16;                  // kItems * 4 waves = 64 (i,wave) gr
 constexpr int kChunk = kBlock * kItems;     // 4096 points per partition chunk
 constexpr int kMaxBins = 4096;              // per-segment histogram bins (global levels)
 constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one workgroup
+constexpr int kRefineBigCap = 8192;         // same, top levels (96 KiB of LDS)
 constexpr int kRadixBits = 11;
 constexpr int kRadixBins = 1 << kRadixBits;
 
@@ -79,10 +80,10 @@ __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i6
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                  u32 id_base, float* __restrict__ cols, i64 n, int dim,
-                                                 u32* __restrict__ bbox, int rs, int ids_in_row) {
+                                                 u32* __restrict__ bbox, int rs, int ids_in_row, i64 ncol) {
   extern __shared__ __align__(16) u32 sbox[];  // [2*dim]
   const i64 stride = i64(gridDim.x) * kBlock;
-  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * n);
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * ncol);
   if (D > 0) {
     constexpr int DD = D > 0 ? D : 1;
     u32 mn[DD], mx[DD];
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
       const u32 id = ids_in_row ? __float_as_uint(pts[r * rs + DD]) : (ids ? ids[r] : id_base + u32(r));
 #pragma unroll
       for (int c = 0; c < DD; ++c) {
-        cols[i64(c) * n + r] = v[c];
+        cols[i64(c) * ncol + r] = v[c];
         const u32 k = orderable(v[c]);
         mn[c] = min(mn[c], k);
         mx[c] = max(mx[c], k);
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
     const i64 r = f / dim;
     const int c = int(f - r * dim);
     const float v = pts[r * rs + c];
-    cols[i64(c) * n + r] = v;
+    cols[i64(c) * ncol + r] = v;
     const u32 k = orderable(v);
     atomicMin(&sbox[c], k);
     atomicMax(&sbox[dim + c], k);
@@ -136,14 +137,71 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
   }
 }
 
+// d = 3, contiguous AoS input: a thread moves 4 rows with three 16-B loads and four 16-B
+// column stores (x, y, z, id), all fully coalesced; columns are 256-B aligned (ncol % 64 == 0).
+__global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                   u32 id_base, float* __restrict__ cols, i64 n, i64 ncol,
+                                                   u32* __restrict__ bbox) {
+  const i64 nq = n / 4;
+  const i64 stride = i64(gridDim.x) * kBlock;
+  u32 mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
+  const float4* in = reinterpret_cast<const float4*>(pts);
+  float4* cx = reinterpret_cast<float4*>(cols);
+  float4* cy = reinterpret_cast<float4*>(cols + ncol);
+  float4* cz = reinterpret_cast<float4*>(cols + 2 * ncol);
+  uint4* ci = reinterpret_cast<uint4*>(cols + 3 * ncol);
+  auto upd = [&](int c, float v) {
+    const u32 k = orderable(v);
+    mn[c] = min(mn[c], k);
+    mx[c] = max(mx[c], k);
+  };
+  for (i64 t = i64(blockIdx.x) * kBlock + threadIdx.x; t < nq; t += stride) {
+    const float4 a = in[3 * t], b = in[3 * t + 1], c = in[3 * t + 2];
+    // rows: (a.x a.y a.z) (a.w b.x b.y) (b.z b.w c.x) (c.y c.z c.w)
+    const float4 x = make_float4(a.x, a.w, b.z, c.y);
+    const float4 y = make_float4(a.y, b.x, b.w, c.z);
+    const float4 z = make_float4(a.z, b.y, c.x, c.w);
+    uint4 id;
+    if (ids) {
+      id = reinterpret_cast<const uint4*>(ids)[t];
+    } else {
+      const u32 b0 = id_base + u32(4 * t);
+      id = make_uint4(b0, b0 + 1, b0 + 2, b0 + 3);
+    }
+    cx[t] = x;
+    cy[t] = y;
+    cz[t] = z;
+    ci[t] = id;
+    upd(0, x.x); upd(0, x.y); upd(0, x.z); upd(0, x.w);
+    upd(1, y.x); upd(1, y.y); upd(1, y.z); upd(1, y.w);
+    upd(2, z.x); upd(2, z.y); upd(2, z.z); upd(2, z.w);
+  }
+  for (i64 r = 4 * nq + i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {  // tail rows
+    for (int c = 0; c < 3; ++c) {
+      const float v = pts[r * 3 + c];
+      cols[i64(c) * ncol + r] = v;
+      upd(c, v);
+    }
+    reinterpret_cast<u32*>(cols + 3 * ncol)[r] = ids ? ids[r] : id_base + u32(r);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const u32 lo = dev::wave_min_u32(mn[c]), hi = dev::wave_max_u32(mx[c]);
+    if (dev::lane() == 0) {
+      atomicMin(&bbox[c], lo);
+      atomicMax(&bbox[3 + c], hi);
+    }
+  }
+}
+
 // bbox over SoA columns (distributed path: points arrive already in SoA).
 __global__ __launch_bounds__(kBlock) void k_bbox_soa(const float* __restrict__ cols, i64 n, int dim,
-                                                     u32* __restrict__ bbox) {
+                                                     u32* __restrict__ bbox, i64 ncol) {
   const i64 stride = i64(gridDim.x) * kBlock;
   for (int c = 0; c < dim; ++c) {
     u32 mn = 0xffffffffu, mx = 0u;
     for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
-      const u32 k = orderable(cols[i64(c) * n + r]);
+      const u32 k = orderable(cols[i64(c) * ncol + r]);
       mn = min(mn, k);
       mx = max(mx, k);
     }
@@ -527,9 +585,13 @@ __device__ __forceinline__ void add_next_hist(const LevelArgs& a, i64 s, i64 h, 
   atomicAdd(&a.hist_next[(2 * s + side) * a.next_bins + nb], 1u);
 }
 
+// CAP: largest middle zone sorted in LDS (keys + indices in dynamic LDS); larger zones are
+// first narrowed by radix passes over the composite key.
+template <int CAP>
 __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
-  __shared__ u64 keys[kRefineCap];
-  __shared__ u32 idx[kRefineCap];
+  extern __shared__ __align__(16) u64 dynk[];
+  u64* keys = dynk;
+  u32* idx = reinterpret_cast<u32*>(dynk + CAP);
   __shared__ u32 rh[kRadixBins];
   __shared__ u32 sh4[4];
   __shared__ u32 info[4];
@@ -558,10 +620,10 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
 
   // Large middle zone (heavy duplicates, or a huge segment): radix passes over the
   // composite key, 11 bits at a time starting at the highest differing bit.
-  if (zc > kRefineCap) {
+  if (zc > CAP) {
     const u64 diff = u64(st.mid_min) ^ u64(st.mid_max);
     int hb = diff ? 63 - __builtin_clzll(diff) : 0;
-    while (zc > kRefineCap) {
+    while (zc > CAP) {
       const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
       for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
       __syncthreads();
@@ -652,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
       idx[e] = u32(e);
     }
     __syncthreads();
-    block_bitonic(keys, idx, int(zc), kRefineCap);
+    block_bitonic(keys, idx, int(zc), CAP);
     for (i64 k = threadIdx.x; k < zc; k += kBlock) copy_row(alt, zlo + k, dst, zlo + idx[k]);
   }
   __syncthreads();
@@ -752,6 +814,12 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 int default_subtree_max(int dim) { return subtree_capacity(dim); }
 
 GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_refine<kRefineBigCap>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kRefineBigCap * 12));
+    attr_done = true;
+  }
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity_max(dim)) : subtree_capacity(dim);
@@ -780,7 +848,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     off = align_up(off + std::max<size_t>(bytes, 1));
     return o;
   };
-  const size_t colbytes = size_t(dim + 1) * size_t(std::max<i64>(n, 1)) * 4;
+  ncol_ = std::max<i64>(64, (n + 63) / 64 * 64);  // 256-B aligned columns (vector stores)
+  const size_t colbytes = size_t(dim + 1) * size_t(ncol_) * 4;
   off_cols_a_ = take(colbytes);
   off_cols_b_ = take(colbytes);
   off_seg_lo_ = take(size_t(heap_nodes_) * 8);
@@ -841,16 +910,25 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   const i64 total = dim_ <= 8 ? n_ : n_ * dim_;
   const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
   const size_t lds = size_t(2 * dim_) * 4;
+  const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
+                    (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
+  if (vec3) {
+    const int g = int(std::min<i64>(4096, std::max<i64>(1, (n_ / 4 + kBlock - 1) / kBlock)));
+    k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, bbox);
+    PKD_LAUNCH_CHECK();
+    run_levels(out_pts, out_ids, ws, stream);
+    return;
+  }
   switch (dim_) {
-    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
-    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0); break;
+    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
   }
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
@@ -863,7 +941,7 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
   const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
-  k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, bbox);
+  k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, bbox, ncol_);
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }
@@ -894,7 +972,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     LevelArgs a;
     a.src = src;
     a.dst = dst;
-    a.ncol = n_;
+    a.ncol = ncol_;
     a.dim = dim_;
     a.seg_lo = seg_lo;
     a.seg_n = seg_n;
@@ -945,12 +1023,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       }
       PKD_LAUNCH_CHECK();
     }
-    k_refine<<<int(lp.segs), kBlock, 0, stream>>>(a);
+    if (lp.segs <= 16) {  // top levels: middle zones of thousands of points, one LDS sort
+      k_refine<kRefineBigCap><<<int(lp.segs), kBlock, size_t(kRefineBigCap) * 12, stream>>>(a);
+    } else {
+      k_refine<kRefineCap><<<int(lp.segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
+    }
     PKD_LAUNCH_CHECK();
     std::swap(src, dst);
   }
   const i64 heap0 = (i64(1) << lg_) - 1;
-  launch_subtree(src, n_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
+  launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
                  out_ids, err, stream);
 }
 

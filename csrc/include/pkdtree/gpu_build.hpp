@@ -43,6 +43,7 @@ class GpuBuilder {
   GpuBuilder(i64 n, int dim, BuildOptions opt = {});
 
   i64 n() const { return n_; }
+  i64 column_stride() const { return ncol_; }
   int dim() const { return dim_; }
   int global_levels() const { return lg_; }
   int subtree_max() const { return nsub_; }
@@ -74,6 +75,7 @@ class GpuBuilder {
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const;
 
   i64 n_;
+  i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)
   int dim_;
   BuildOptions opt_;
   int lg_ = 0;      // number of global levels
