@@ -35,7 +35,6 @@ constexpr int kItems = 16;                  // kItems * 4 waves = 64 (i,wave) gr
 constexpr int kChunk = kBlock * kItems;     // 4096 points per partition chunk
 constexpr int kMaxBins = 4096;              // per-segment histogram bins (global levels)
 constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one workgroup
-constexpr int kRefineBigCap = 8192;         // same, top levels (96 KiB of LDS)
 constexpr int kRadixBits = 11;
 constexpr int kRadixBins = 1 << kRadixBits;
 
@@ -43,11 +42,16 @@ struct SegState {
   u32 bstar;
   u32 cnt_less;
   u32 cnt_mid;
-  u32 pad;
+  u32 stage2;                 // 1: the median bucket is split again by a second histogram
   u32 cur[4];                 // zone cursors (relative to segment start)
   unsigned long long mid_min;  // composite (key,id) range of the middle zone
   unsigned long long mid_max;
+  u32 sbstar;                 // stage 2: sub-bucket holding the median
+  float p2lo, p2scale;        // stage 2: bucketing of the median bucket's value range
+  u32 pad2;
 };
+
+constexpr int kBins2 = 4096;  // stage-2 sub-buckets
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
@@ -155,26 +159,41 @@ __global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts
     mn[c] = min(mn[c], k);
     mx[c] = max(mx[c], k);
   };
-  for (i64 t = i64(blockIdx.x) * kBlock + threadIdx.x; t < nq; t += stride) {
-    const float4 a = in[3 * t], b = in[3 * t + 1], c = in[3 * t + 2];
-    // rows: (a.x a.y a.z) (a.w b.x b.y) (b.z b.w c.x) (c.y c.z c.w)
-    const float4 x = make_float4(a.x, a.w, b.z, c.y);
-    const float4 y = make_float4(a.y, b.x, b.w, c.z);
-    const float4 z = make_float4(a.z, b.y, c.x, c.w);
-    uint4 id;
-    if (ids) {
-      id = reinterpret_cast<const uint4*>(ids)[t];
-    } else {
-      const u32 b0 = id_base + u32(4 * t);
-      id = make_uint4(b0, b0 + 1, b0 + 2, b0 + 3);
+  // U quads per thread per iteration, all loads issued before any store (the compiler cannot
+  // prove the AoS input and the columns disjoint, so it would otherwise serialise them)
+  constexpr int U = 4;
+  for (i64 t0 = i64(blockIdx.x) * kBlock + threadIdx.x; t0 < nq; t0 += stride * U) {
+    float4 a[U], b[U], c[U];
+    uint4 id[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 t = t0 + i64(u) * stride;
+      const i64 tt = t < nq ? t : t0;
+      a[u] = in[3 * tt];
+      b[u] = in[3 * tt + 1];
+      c[u] = in[3 * tt + 2];
+      if (ids) id[u] = reinterpret_cast<const uint4*>(ids)[tt];
     }
-    cx[t] = x;
-    cy[t] = y;
-    cz[t] = z;
-    ci[t] = id;
-    upd(0, x.x); upd(0, x.y); upd(0, x.z); upd(0, x.w);
-    upd(1, y.x); upd(1, y.y); upd(1, y.z); upd(1, y.w);
-    upd(2, z.x); upd(2, z.y); upd(2, z.z); upd(2, z.w);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 t = t0 + i64(u) * stride;
+      if (t >= nq) break;
+      // rows: (a.x a.y a.z) (a.w b.x b.y) (b.z b.w c.x) (c.y c.z c.w)
+      const float4 x = make_float4(a[u].x, a[u].w, b[u].z, c[u].y);
+      const float4 y = make_float4(a[u].y, b[u].x, b[u].w, c[u].z);
+      const float4 z = make_float4(a[u].z, b[u].y, c[u].x, c[u].w);
+      if (!ids) {
+        const u32 b0 = id_base + u32(4 * t);
+        id[u] = make_uint4(b0, b0 + 1, b0 + 2, b0 + 3);
+      }
+      cx[t] = x;
+      cy[t] = y;
+      cz[t] = z;
+      ci[t] = id[u];
+      upd(0, x.x); upd(0, x.y); upd(0, x.z); upd(0, x.w);
+      upd(1, y.x); upd(1, y.y); upd(1, y.z); upd(1, y.w);
+      upd(2, z.x); upd(2, z.y); upd(2, z.z); upd(2, z.w);
+    }
   }
   for (i64 r = 4 * nq + i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {  // tail rows
     for (int c = 0; c < 3; ++c) {
@@ -253,7 +272,19 @@ struct LevelArgs {
   u32* err;              // sticky error word (bit 0: partition overflow, bit 1: refine)
   int block_reserve;     // 1: count the block's zones first and reserve once per block
   int small_done;        // 1: k_refine_small already resolved middle zones of <= 64 points
+  u32* hist2;            // stage-2 histograms [segs][kBins2] (levels with stage2)
 };
+
+// Zone of a point: 0 left of the median bucket, 1 inside (the middle zone), 2 right.
+// Stage 2 splits the median bucket once more with its own linear sub-buckets.
+__device__ __forceinline__ u32 zone_of(float key, const BucketParams& prm, int bins, u32 bstar, u32 stage2,
+                                       const BucketParams& p2, u32 sbstar) {
+  const u32 b = bucket_of(key, prm, bins);
+  if (b != bstar) return b < bstar ? 0u : 2u;
+  if (!stage2) return 1u;
+  const u32 sb = bucket_of(key, p2, kBins2);
+  return sb < sbstar ? 0u : (sb == sbstar ? 1u : 2u);
+}
 
 // Histogram of a level's keys (used for the first global level only; later levels get
 // theirs from the fused partition pass).
@@ -333,13 +364,27 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
     st.bstar = found[0];
     st.cnt_less = found[1];
     st.cnt_mid = found[2];
-    st.pad = 0;
     st.cur[0] = 0;
     st.cur[1] = found[1];
     st.cur[2] = found[1] + found[2];
     st.cur[3] = 0;
     st.mid_min = ~0ull;
     st.mid_max = 0ull;
+    st.stage2 = 0;
+    st.sbstar = 0;
+    st.pad2 = 0;
+    {  // stage-2 bucketing of the median bucket's value range
+      const BucketParams p = a.params[h];
+      const float* cl = a.cells + h * 2 * a.dim;
+      float lo2 = cl[2 * a.axis], hi2 = cl[2 * a.axis + 1];
+      if (p.scale > 0.0f) {
+        lo2 = p.lo + float(st.bstar) / p.scale;
+        hi2 = p.lo + float(st.bstar + 1) / p.scale;
+      }
+      const BucketParams p2 = make_params(lo2, hi2, kBins2);
+      st.p2lo = p2.lo;
+      st.p2scale = p2.scale;
+    }
     a.state[h] = st;
     if (a.next_bins > 0) {
       // Children's bucketing on the next axis. For dim > 1 the child cell on that axis is
@@ -360,6 +405,86 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
       a.params[2 * h + 1] = pl;
       a.params[2 * h + 2] = pr;
     }
+  }
+}
+
+// Stage 2 (top levels): histogram of the median bucket's points over kBins2 sub-buckets.
+__global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
+  __shared__ u32 sh[kBins2];
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  for (int b = threadIdx.x; b < kBins2; b += kBlock) sh[b] = 0;
+  __syncthreads();
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const BucketParams p = a.params[h];
+  const SegState* st = a.state + h;
+  const u32 bstar = st->bstar;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const float* key = a.src + i64(a.axis) * a.ncol + lo;
+  constexpr int U = 8;
+  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
+    float k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock;
+      k[u] = e < b1 ? key[e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock;
+      if (e < b1 && bucket_of(k[u], p, a.bins) == bstar) atomicAdd(&sh[bucket_of(k[u], p2, kBins2)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kBins2; b += kBlock) {
+    const u32 v = sh[b];
+    if (v) atomicAdd(&a.hist2[s * kBins2 + b], v);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
+  __shared__ u32 sh4[4];
+  __shared__ u32 found[3];
+  const i64 s = blockIdx.x;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  if (n <= 0) return;
+  SegState* st = a.state + h;
+  const u32 t = u32(n / 2) - st->cnt_less;  // rank inside the median bucket
+  const u32* hs = a.hist2 + s * kBins2;
+  constexpr int per = kBins2 / kBlock;
+  u32 sum = 0;
+  for (int b = 0; b < per; ++b) sum += hs[threadIdx.x * per + b];
+  u32 total;
+  const u32 excl = block_excl_scan(sum, sh4, &total);
+  if (t >= excl && t < excl + sum) {
+    u32 c = excl;
+    for (int b = 0; b < per; ++b) {
+      const u32 v = hs[threadIdx.x * per + b];
+      if (t < c + v) {
+        found[0] = u32(threadIdx.x * per + b);
+        found[1] = c;
+        found[2] = v;
+        break;
+      }
+      c += v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 cl = st->cnt_less + found[1];
+    st->stage2 = 1;
+    st->sbstar = found[0];
+    st->cnt_less = cl;
+    st->cnt_mid = found[2];
+    st->cur[0] = 0;
+    st->cur[1] = cl;
+    st->cur[2] = cl + found[2];
   }
 }
 
@@ -385,6 +510,10 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
   SegState* st = a.state + h;
   const u32 bstar = st->bstar;
+  const u32 stage2 = st->stage2, sbstar = st->sbstar;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
   const BucketParams prm = a.params[h];
   BucketParams cprm[2] = {{0.f, 0.f}, {0.f, 0.f}};
   if (fuse) {
@@ -405,9 +534,9 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     u32 cnt0 = 0, cnt1 = 0;
     const float* kc = src + i64(axis) * nc + lo;
     for (i64 e = b0 + threadIdx.x; e < b1; e += kBlock) {
-      const u32 b = bucket_of(kc[e], prm, a.bins);
-      cnt0 += b < bstar ? 1u : 0u;
-      cnt1 += b == bstar ? 1u : 0u;
+      const u32 z = zone_of(kc[e], prm, a.bins, bstar, stage2, p2, sbstar);
+      cnt0 += z == 0 ? 1u : 0u;
+      cnt1 += z == 1 ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -462,10 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
         }
       }
       u32 z = 3;
-      if (valid) {
-        const u32 b = bucket_of(key, prm, a.bins);
-        z = b < bstar ? 0u : (b == bstar ? 1u : 2u);
-      }
+      if (valid) z = zone_of(key, prm, a.bins, bstar, stage2, p2, sbstar);
       const u64 m0 = __ballot(z == 0), m1 = __ballot(z == 1), m2 = __ballot(z == 2);
       if (ln == 0) {
         gcnt[0][i * 4 + w] = __popcll(m0);
@@ -806,7 +932,7 @@ int pow2_floor(i64 v) {
   return p;
 }
 
-int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 8)))); }
+int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 24)))); }
 
 }  // namespace
 
@@ -814,12 +940,7 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 int default_subtree_max(int dim) { return subtree_capacity(dim); }
 
 GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_refine<kRefineBigCap>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kRefineBigCap * 12));
-    attr_done = true;
-  }
+
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity_max(dim)) : subtree_capacity(dim);
@@ -838,6 +959,9 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     const i64 range = std::max<i64>(kChunk * 16, i64(kChunk));
     lp.bps = int(std::max<i64>(1, (lp.nmax + range - 1) / range));
     lp.axis = (opt.depth0 + l) % dim;
+    // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
+    lp.stage2 = lp.nmax / lp.bins > kRefineCap;
+    if (lp.stage2) max_hist2_ = std::max<i64>(max_hist2_, lp.segs * kBins2);
     levels_.push_back(lp);
     max_bins_ = std::max(max_bins_, lp.bins);
     max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
@@ -859,6 +983,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   off_cells_ = take(size_t(heap_nodes_) * size_t(2 * dim) * 4);
   off_hist0_ = take(size_t(max_hist_) * 4);
   off_hist1_ = take(size_t(max_hist_) * 4);
+  off_hist2_ = take(size_t(std::max<i64>(max_hist2_, 1)) * 4);
   off_bbox_ = take(size_t(2 * dim) * 4);
   off_err_ = take(16);
   ws_bytes_ = off;
@@ -870,7 +995,7 @@ std::string GpuBuilder::describe() const {
      << ", workspace=" << ws_bytes_ << "B)";
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
-       << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis;
+       << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "");
   return os.str();
 }
 
@@ -913,7 +1038,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
-    const int g = int(std::min<i64>(4096, std::max<i64>(1, (n_ / 4 + kBlock - 1) / kBlock)));
+    const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
     k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, bbox);
     PKD_LAUNCH_CHECK();
     run_levels(out_pts, out_ids, ws, stream);
@@ -996,8 +1121,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       k_hist<<<int(lp.segs * lp.bps), kBlock, size_t(lp.bins) * 4, stream>>>(a, hist[0]);
       PKD_LAUNCH_CHECK();
     }
+    a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
     k_select<<<int(lp.segs), kBlock, 0, stream>>>(a);
     PKD_LAUNCH_CHECK();
+    if (lp.stage2) {
+      PKD_HIP_CHECK(hipMemsetAsync(a.hist2, 0, size_t(lp.segs) * kBins2 * 4, stream));
+      k_hist2<<<int(lp.segs * lp.bps), kBlock, 0, stream>>>(a);
+      PKD_LAUNCH_CHECK();
+      k_select2<<<int(lp.segs), kBlock, 0, stream>>>(a);
+      PKD_LAUNCH_CHECK();
+    }
     const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
     const int grid = int(lp.segs * lp.bps);
     switch (dim_) {
@@ -1023,11 +1156,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       }
       PKD_LAUNCH_CHECK();
     }
-    if (lp.segs <= 16) {  // top levels: middle zones of thousands of points, one LDS sort
-      k_refine<kRefineBigCap><<<int(lp.segs), kBlock, size_t(kRefineBigCap) * 12, stream>>>(a);
-    } else {
-      k_refine<kRefineCap><<<int(lp.segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
-    }
+    k_refine<kRefineCap><<<int(lp.segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
     PKD_LAUNCH_CHECK();
     std::swap(src, dst);
   }

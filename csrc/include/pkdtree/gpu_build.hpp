@@ -36,6 +36,7 @@ struct LevelPlan {
   int next_bins;    // bins per segment at level+1 (0 if level+1 is the subtree level)
   int bps;          // partition blocks per segment
   int axis;         // split axis at this level
+  bool stage2 = false;  // median bucket split by a second (key-only) histogram pass
 };
 
 class GpuBuilder {
@@ -84,9 +85,10 @@ class GpuBuilder {
   i64 heap_nodes_ = 0;  // nodes of levels 0..lg_
   int max_bins_ = 0;
   i64 max_hist_ = 0;
+  i64 max_hist2_ = 0;
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
-         off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0,
+         off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0,
          ws_bytes_ = 0;
 };
 
