@@ -3,6 +3,9 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <optional>
+#include <vector>
+
 #include "pkdtree/dist_ops.hpp"
 
 namespace pkdtree {
@@ -11,50 +14,117 @@ namespace {
 
 hipStream_t stream_of(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
-void check_rows(const torch::Tensor& rows, int64_t dim) {
-  TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == torch::kFloat32 && rows.is_contiguous(), "rows: cuda f32");
-  TORCH_CHECK(rows.dim() == 2 && rows.size(1) == dim + 1, "rows must be [n, dim+1]");
+void check_cuda(const torch::Tensor& t, torch::ScalarType st, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == st && t.is_contiguous(), what, ": contiguous cuda tensor of ",
+              c10::toString(st), " expected");
+}
+
+TopPoints points_of(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base) {
+  check_cuda(pts, torch::kFloat32, "points");
+  TORCH_CHECK(pts.dim() == 2, "points must be [n, dim]");
+  TopPoints p;
+  p.pts = pts.data_ptr<float>();
+  p.n = pts.size(0);
+  p.dim = int(pts.size(1));
+  p.id_base = u32(id_base);
+  p.ids = nullptr;
+  if (ids && ids->defined()) {
+    check_cuda(*ids, torch::kInt32, "ids");
+    TORCH_CHECK(ids->numel() == p.n, "ids must have one entry per point");
+    p.ids = reinterpret_cast<const u32*>(ids->data_ptr<int32_t>());
+  }
+  return p;
+}
+
+TopSizes sizes_of(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() <= size_t(kTopMaxNodes), "too many nodes per top level");
+  TopSizes s{};
+  for (size_t i = 0; i < v.size(); ++i) s.n[i] = v[i];
+  return s;
 }
 
 u32* u32p(torch::Tensor& t) { return reinterpret_cast<u32*>(t.data_ptr<int32_t>()); }
-const u64* u64p(const torch::Tensor& t) { return reinterpret_cast<const u64*>(t.data_ptr<int64_t>()); }
+const u32* cu32p(const torch::Tensor& t) { return reinterpret_cast<const u32*>(t.data_ptr<int32_t>()); }
+u64* u64p(torch::Tensor& t) { return reinterpret_cast<u64*>(t.data_ptr<int64_t>()); }
+const u64* cu64p(const torch::Tensor& t) { return reinterpret_cast<const u64*>(t.data_ptr<int64_t>()); }
 
-void route_hist(const torch::Tensor& rows, int64_t dim, torch::Tensor node, int64_t level, const torch::Tensor& pivots,
-                int64_t prev_axis, int64_t axis, const torch::Tensor& params, int64_t bins, torch::Tensor hist) {
-  check_rows(rows, dim);
-  const c10::DeviceGuard g(rows.device());
-  top_route_hist(rows.data_ptr<float>(), rows.size(0), int(dim), u32p(node), int(level), u64p(pivots),
-                 int(prev_axis), int(axis), params.data_ptr<float>(), int(bins), u32p(hist), stream_of(rows));
+void bbox(const torch::Tensor& pts, torch::Tensor box) {
+  const c10::DeviceGuard g(pts.device());
+  check_cuda(box, torch::kInt64, "box");
+  TopPoints p = points_of(pts, std::nullopt, 0);
+  TORCH_CHECK(box.numel() == 2 * p.dim, "box must have 2*dim entries");
+  top_bbox(p, box.data_ptr<int64_t>(), stream_of(pts));
 }
 
-int64_t collect_middle(const torch::Tensor& rows, int64_t dim, const torch::Tensor& node, int64_t level,
-                       int64_t axis, const torch::Tensor& params, int64_t bins, const torch::Tensor& bstar,
-                       torch::Tensor out, torch::Tensor count) {
-  check_rows(rows, dim);
-  const c10::DeviceGuard g(rows.device());
-  top_collect_middle(rows.data_ptr<float>(), rows.size(0), int(dim),
-                     reinterpret_cast<const u32*>(node.data_ptr<int32_t>()), int(level), int(axis),
-                     params.data_ptr<float>(), int(bins), reinterpret_cast<const u32*>(bstar.data_ptr<int32_t>()),
-                     out.data_ptr<float>(), out.size(0), reinterpret_cast<unsigned long long*>(count.data_ptr<int64_t>()),
-                     stream_of(rows));
-  return 0;
+void root_cell(const torch::Tensor& box, int64_t dim, torch::Tensor cells) {
+  const c10::DeviceGuard g(box.device());
+  check_cuda(cells, torch::kFloat32, "cells");
+  top_root_cell(box.data_ptr<int64_t>(), int(dim), cells.data_ptr<float>(), stream_of(box));
 }
 
-void pack(const torch::Tensor& rows, int64_t dim, torch::Tensor node, int64_t levels, const torch::Tensor& pivots,
-          int64_t last_axis, int64_t P, torch::Tensor out, torch::Tensor counts, torch::Tensor scratch) {
-  check_rows(rows, dim);
-  const c10::DeviceGuard g(rows.device());
-  TORCH_CHECK(size_t(scratch.numel()) >= top_pack_scratch_bytes(rows.size(0), int(P)), "scratch too small");
-  top_pack(rows.data_ptr<float>(), rows.size(0), int(dim), u32p(node), int(levels), u64p(pivots), int(last_axis),
-           int(P), out.data_ptr<float>(), u32p(counts), scratch.data_ptr(), stream_of(rows));
+void route_hist(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base,
+                torch::Tensor node, int64_t level, const torch::Tensor& pivots, int64_t prev_axis, int64_t axis,
+                const torch::Tensor& cells, int64_t bins, torch::Tensor hist) {
+  const c10::DeviceGuard g(pts.device());
+  TopPoints p = points_of(pts, ids, id_base);
+  TORCH_CHECK(node.numel() >= p.n, "node array too small");
+  TORCH_CHECK(hist.numel() >= (int64_t(1) << level) * bins, "hist too small");
+  top_route_hist(p, u32p(node), int(level), cu64p(pivots), int(prev_axis), int(axis), cells.data_ptr<float>(),
+                 int(bins), u32p(hist), stream_of(pts));
+}
+
+void select(const torch::Tensor& hist, int64_t level, int64_t bins, const std::vector<int64_t>& sizes,
+            torch::Tensor sel, torch::Tensor err) {
+  const c10::DeviceGuard g(hist.device());
+  TORCH_CHECK(int64_t(sizes.size()) == (int64_t(1) << level), "one size per node");
+  top_select(cu32p(hist), int(level), int(bins), sizes_of(sizes), u32p(sel), u32p(err), stream_of(hist));
+}
+
+void collect(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base,
+             const torch::Tensor& node, int64_t level, int64_t axis, const torch::Tensor& cells, int64_t bins,
+             const torch::Tensor& sel, torch::Tensor buf, int64_t cap) {
+  const c10::DeviceGuard g(pts.device());
+  TopPoints p = points_of(pts, ids, id_base);
+  TORCH_CHECK(size_t(buf.numel()) >= top_middle_words(p.dim, cap), "middle buffer too small");
+  top_collect(p, cu32p(node), int(level), int(axis), cells.data_ptr<float>(), int(bins), cu32p(sel),
+              buf.data_ptr<float>(), cap, stream_of(pts));
+}
+
+void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level, int64_t axis, int64_t dim,
+           const std::vector<int64_t>& sizes, const torch::Tensor& sel, torch::Tensor pivots, torch::Tensor top_rows,
+           torch::Tensor cells, torch::Tensor err) {
+  const c10::DeviceGuard g(gathered.device());
+  TORCH_CHECK(size_t(gathered.numel()) >= size_t(P) * top_middle_words(int(dim), cap), "gathered buffer too small");
+  TORCH_CHECK(int64_t(sizes.size()) == (int64_t(1) << level), "one size per node");
+  top_pivot(gathered.data_ptr<float>(), int(P), cap, int(level), int(axis), int(dim), sizes_of(sizes), cu32p(sel),
+            u64p(pivots), top_rows.data_ptr<float>(), cells.data_ptr<float>(), u32p(err), stream_of(gathered));
+}
+
+void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base, torch::Tensor node,
+          int64_t levels, const torch::Tensor& pivots, int64_t last_axis, int64_t P, torch::Tensor out,
+          torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
+  const c10::DeviceGuard g(pts.device());
+  TopPoints p = points_of(pts, ids, id_base);
+  check_cuda(out, torch::kFloat32, "out");
+  TORCH_CHECK(out.size(0) >= p.n && out.size(1) == p.dim + 1, "out must be [>= n, dim+1]");
+  check_cuda(counts, torch::kInt64, "counts");
+  TORCH_CHECK(counts.numel() == 2 * P, "counts must have 2*P entries");
+  TORCH_CHECK(size_t(scratch.numel()) >= top_pack_scratch_bytes(p.n, int(P)), "scratch too small");
+  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), out.data_ptr<float>(),
+           counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
 }
 
 }  // namespace
 
 void bind_dist_ops(pybind11::module& m) {
+  m.def("top_bbox", &bbox);
+  m.def("top_root_cell", &root_cell);
   m.def("top_route_hist", &route_hist);
-  m.def("top_collect_middle", &collect_middle);
+  m.def("top_select", &select);
+  m.def("top_collect", &collect);
+  m.def("top_pivot", &pivot);
   m.def("top_pack", &pack);
+  m.def("top_middle_words", [](int64_t dim, int64_t cap) { return int64_t(top_middle_words(int(dim), cap)); });
   m.def("top_pack_scratch_bytes", [](int64_t n, int64_t P) { return int64_t(top_pack_scratch_bytes(n, int(P))); });
 }
 

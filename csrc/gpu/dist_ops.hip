@@ -1,5 +1,6 @@
 // Device ops of the global (distributed) decomposition; see dist_ops.hpp.
 #include <algorithm>
+#include <stdexcept>
 
 #include "device_utils.hpp"
 #include "pkdtree/dist_ops.hpp"
@@ -9,50 +10,94 @@ namespace pkdtree {
 
 using dev::BucketParams;
 using dev::bucket_of;
+using dev::make_params;
 using dev::mbcnt;
 
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kMaxTopBins = 8192;  // nodes * bins per level (LDS histogram)
+constexpr int kPivotThreads = 1024;
+constexpr int kPivotLdsKeys = 12288;  // 96 KiB of keys per node in LDS; larger middles stream from L2
 
-__device__ __forceinline__ u64 row_key(const float* r, int dim, int axis) {
-  return composite_key(r[axis], __float_as_uint(r[dim]));
-}
+__device__ __forceinline__ u32 point_id(const TopPoints& p, i64 i) { return p.ids ? p.ids[i] : p.id_base + u32(i); }
 
-// Route one point one level down below the pivot of its node (heap order).
-__device__ __forceinline__ u32 route(u32 h, const float* r, int dim, int axis, const u64* pivots) {
+// Route one point one level down below the pivot of its node (heap order). The id is only
+// read when the keys tie.
+__device__ __forceinline__ u32 route(u32 h, const TopPoints& p, i64 i, int axis, const u64* pivots) {
   if (h == kTopDone) return h;
-  const u64 k = row_key(r, dim, axis);
+  const u32 k = orderable(p.pts[i * p.dim + axis]);
   const u64 pv = pivots[h];
-  return k < pv ? 2 * h + 1 : (k > pv ? 2 * h + 2 : kTopDone);
+  const u32 pk = u32(pv >> 32);
+  if (k != pk) return k < pk ? 2 * h + 1 : 2 * h + 2;
+  const u32 id = point_id(p, i), pid = u32(pv);
+  return id < pid ? 2 * h + 1 : (id > pid ? 2 * h + 2 : kTopDone);
 }
 
-__global__ __launch_bounds__(kBlock) void k_top_route_hist(const float* __restrict__ rows, i64 n, int dim,
-                                                           u32* __restrict__ node, int level,
+// ---- bounding box --------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_top_bbox(TopPoints p, i64 T, i64* __restrict__ box) {
+  extern __shared__ __align__(16) u32 sb[];  // [2 * dim]
+  const int dim = p.dim;
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sb[c] = 0xffffffffu;
+  __syncthreads();
+  const i64 t = i64(blockIdx.x) * kBlock + threadIdx.x;
+  if (t < T) {  // T is a multiple of dim, so this thread always sees axis t % dim
+    const int c = int(t % dim);
+    u32 lo = 0xffffffffu, nhi = 0xffffffffu;
+    const i64 total = p.n * dim;
+    for (i64 f = t; f < total; f += T) {
+      const u32 k = orderable(p.pts[f]);
+      lo = min(lo, k);
+      nhi = min(nhi, ~k);
+    }
+    atomicMin(&sb[c], lo);
+    atomicMin(&sb[dim + c], nhi);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) {
+    if (sb[c] != 0xffffffffu)
+      atomicMin(reinterpret_cast<unsigned long long*>(box + c), (unsigned long long)sb[c]);
+  }
+}
+
+__global__ void k_top_root_cell(const i64* __restrict__ box, int dim, float* __restrict__ cells) {
+  for (int c = threadIdx.x; c < dim; c += blockDim.x) {
+    cells[2 * c] = from_orderable(u32(box[c]));
+    cells[2 * c + 1] = from_orderable(~u32(box[dim + c]));
+  }
+}
+
+// ---- route + histogram ---------------------------------------------------------------
+__device__ __forceinline__ void load_params(BucketParams* prm, const float* cells, int first, int nodes, int dim,
+                                            int axis, int bins) {
+  for (int j = threadIdx.x; j < nodes; j += blockDim.x) {
+    const float* c = cells + (size_t(first + j) * dim + axis) * 2;
+    prm[j] = make_params(c[0], c[1], bins);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_top_route_hist(TopPoints p, u32* __restrict__ node, int level,
                                                            const u64* __restrict__ pivots, int prev_axis, int axis,
-                                                           const float* __restrict__ params, int bins,
+                                                           const float* __restrict__ cells, int bins,
                                                            u32* __restrict__ hist) {
   extern __shared__ __align__(16) u32 sh[];
-  const u32 first = (1u << level) - 1;
-  const int nb_total = (1 << level) * bins;
+  __shared__ BucketParams prm[kTopMaxNodes];
+  const int nodes = 1 << level;
+  const u32 first = u32(nodes - 1);
+  const int nb_total = nodes * bins;
   for (int b = threadIdx.x; b < nb_total; b += kBlock) sh[b] = 0;
+  load_params(prm, cells, int(first), nodes, p.dim, axis, bins);
   __syncthreads();
   const i64 stride = i64(gridDim.x) * kBlock;
-  const int rs = dim + 1;
-  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += stride) {
-    const float* r = rows + p * rs;
-    u32 h = node[p];
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += stride) {
+    u32 h = 0;
     if (level > 0) {
-      h = route(h, r, dim, prev_axis, pivots);
-      node[p] = h;
+      h = level > 1 ? node[i] : 0u;
+      h = route(h, p, i, prev_axis, pivots);
+      node[i] = h;
     }
     if (h == kTopDone) continue;
     const u32 j = h - first;
-    BucketParams pr;
-    pr.lo = params[2 * j];
-    pr.scale = params[2 * j + 1];
-    atomicAdd(&sh[j * bins + bucket_of(r[axis], pr, bins)], 1u);
+    atomicAdd(&sh[j * bins + bucket_of(p.pts[i * p.dim + axis], prm[j], bins)], 1u);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < nb_total; b += kBlock) {
@@ -61,61 +106,266 @@ __global__ __launch_bounds__(kBlock) void k_top_route_hist(const float* __restri
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_top_collect(const float* __restrict__ rows, i64 n, int dim,
-                                                        const u32* __restrict__ node, int level, int axis,
-                                                        const float* __restrict__ params, int bins,
-                                                        const u32* __restrict__ bstar, float* __restrict__ out,
-                                                        i64 cap, unsigned long long* __restrict__ count) {
-  const u32 first = (1u << level) - 1;
-  const i64 stride = i64(gridDim.x) * kBlock;
-  const int rs = dim + 1;
-  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += stride) {
-    const u32 h = node[p];
-    if (h == kTopDone) continue;
-    const float* r = rows + p * rs;
-    const u32 j = h - first;
-    BucketParams pr;
-    pr.lo = params[2 * j];
-    pr.scale = params[2 * j + 1];
-    if (bucket_of(r[axis], pr, bins) != bstar[j]) continue;
-    const unsigned long long slot = atomicAdd(count, 1ull);
-    if (i64(slot) < cap) {
-      float* o = out + i64(slot) * (rs + 1);
-      for (int c = 0; c < rs; ++c) o[c] = r[c];
-      o[rs] = __uint_as_float(h);  // node of the middle point rides along
+// ---- median bucket per node ----------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_top_select(const u32* __restrict__ hist, int level, int bins,
+                                                       TopSizes sizes, u32* __restrict__ sel, u32* __restrict__ err) {
+  __shared__ u32 part[kBlock];
+  const int j = blockIdx.x;
+  const u32* hs = hist + size_t(j) * bins;
+  const i64 size = sizes.n[j];
+  const int per = (bins + kBlock - 1) / kBlock;
+  const int b0 = min(bins, int(threadIdx.x) * per), b1 = min(bins, b0 + per);
+  u32 s = 0;
+  for (int b = b0; b < b1; ++b) s += hs[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 256 partial sums: a serial scan is cheaper than a barrier tree here
+    u32 acc = 0;
+    for (int t = 0; t < kBlock; ++t) {
+      const u32 v = part[t];
+      part[t] = acc;
+      acc += v;
+    }
+    if (i64(acc) != size) atomicOr(err, 2u);
+    if (size == 0) {
+      sel[4 * j + 0] = 0xffffffffu;
+      sel[4 * j + 1] = 0;
+      sel[4 * j + 2] = 0;
+    }
+  }
+  __syncthreads();
+  if (size == 0) return;
+  const u32 r = u32(size / 2);
+  const u32 ex = part[threadIdx.x];
+  if (r >= ex && r < ex + s) {
+    u32 c = ex;
+    for (int b = b0; b < b1; ++b) {
+      const u32 v = hs[b];
+      if (r < c + v) {
+        sel[4 * j + 0] = u32(b);
+        sel[4 * j + 1] = c;
+        sel[4 * j + 2] = v;
+        break;
+      }
+      c += v;
     }
   }
 }
 
-// --- counting sort by destination (P <= 64) -------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_pack_count(const float* __restrict__ rows, i64 n, int dim,
-                                                       u32* __restrict__ node, const u64* __restrict__ pivots,
-                                                       int last_axis, int P, i64 per_block,
-                                                       u32* __restrict__ bcount) {
+// ---- middle-bucket compaction --------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* __restrict__ node, int level,
+                                                        int axis, const float* __restrict__ cells, int bins,
+                                                        const u32* __restrict__ sel, float* __restrict__ buf,
+                                                        i64 cap) {
+  __shared__ BucketParams prm[kTopMaxNodes];
+  __shared__ u32 bs[kTopMaxNodes];
+  const int nodes = 1 << level;
+  const u32 first = u32(nodes - 1);
+  load_params(prm, cells, int(first), nodes, p.dim, axis, bins);
+  for (int j = threadIdx.x; j < nodes; j += kBlock) bs[j] = sel[4 * j];
+  __syncthreads();
+  u32* count = reinterpret_cast<u32*>(buf);
+  float* rows = buf + 4;
+  const int rs = p.dim + 2;
+  const i64 stride = i64(gridDim.x) * kBlock;
+  // the trip count is uniform across the wave (ballots below need every lane)
+  for (i64 base = i64(blockIdx.x) * kBlock; base < p.n; base += stride) {
+    const i64 i = base + threadIdx.x;
+    bool take = false;
+    u32 h = 0;
+    if (i < p.n) {
+      h = level > 0 ? node[i] : 0u;
+      if (h != kTopDone) {
+        const u32 j = h - first;
+        take = bucket_of(p.pts[i * p.dim + axis], prm[j], bins) == bs[j];
+      }
+    }
+    const u64 m = __ballot(take);
+    if (!m) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    u32 base_slot = 0;
+    if (dev::lane() == leader) base_slot = atomicAdd(count, u32(__popcll(m)));
+    base_slot = __shfl(base_slot, leader, 64);
+    if (take) {
+      const i64 slot = i64(base_slot) + mbcnt(m);
+      if (slot < cap) {
+        float* o = rows + slot * rs;
+        const float* r = p.pts + i * p.dim;
+        for (int c = 0; c < p.dim; ++c) o[c] = r[c];
+        o[p.dim] = __uint_as_float(point_id(p, i));
+        o[p.dim + 1] = __uint_as_float(h);
+      }
+    }
+  }
+}
+
+// ---- exact pivot per node (radix select over the gathered middles) ---------------------
+struct MidView {
+  const float* g;
+  i64 stride;  // words per rank buffer
+  i64 cap;
+  int P, dim, axis;
+  __device__ u32 count(int r) const { return min(u32(cap), reinterpret_cast<const u32*>(g + r * stride)[0]); }
+  __device__ const float* row(int r, u32 k) const { return g + r * stride + 4 + i64(k) * (dim + 2); }
+  __device__ u64 key(const float* row) const {
+    return composite_key(row[axis], __float_as_uint(row[dim]));
+  }
+  __device__ u32 node(const float* row) const { return __float_as_uint(row[dim + 1]); }
+};
+
+__global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int level, TopSizes sizes,
+                                                             const u32* __restrict__ sel, u64* __restrict__ pivots,
+                                                             float* __restrict__ top_rows, float* __restrict__ cells,
+                                                             u32* __restrict__ err) {
+  extern __shared__ __align__(16) u64 keys[];  // [kPivotLdsKeys]
+  __shared__ u32 hist[256];
+  __shared__ u32 s_cnt, s_digit, s_rem, s_found;
+  const int j = blockIdx.x;
+  const u32 h = u32((1 << level) - 1 + j);
+  const int dim = mv.dim, axis = mv.axis;
+  const int tid = threadIdx.x;
+  const i64 size = sizes.n[j];
+  float* cl = cells + size_t(2 * h + 1) * dim * 2;
+  float* cr = cells + size_t(2 * h + 2) * dim * 2;
+  const float* cp = cells + size_t(h) * dim * 2;
+  for (int c = tid; c < 2 * dim; c += kPivotThreads) {
+    cl[c] = cp[c];
+    cr[c] = cp[c];
+  }
+  if (size == 0) {
+    if (tid == 0) pivots[h] = ~0ull;
+    for (int c = tid; c <= dim; c += kPivotThreads) top_rows[size_t(h) * (dim + 1) + c] = 0.0f;
+    return;
+  }
+  if (tid == 0) {
+    s_cnt = 0;
+    s_found = 0;
+    for (int r = 0; r < mv.P; ++r)
+      if (reinterpret_cast<const u32*>(mv.g + r * mv.stride)[0] > u32(mv.cap)) atomicOr(err, 1u);
+  }
+  __syncthreads();
+  // 1. this node's keys into LDS
+  for (int r = 0; r < mv.P; ++r) {
+    const u32 c = mv.count(r);
+    for (u32 k = tid; k < c; k += kPivotThreads) {
+      const float* row = mv.row(r, k);
+      if (mv.node(row) == h) {
+        const u32 s = atomicAdd(&s_cnt, 1u);
+        if (s < u32(kPivotLdsKeys)) keys[s] = mv.key(row);
+      }
+    }
+  }
+  __syncthreads();
+  const u32 m = s_cnt;
+  const u32 cmid = sel[4 * j + 2];
+  const u32 target = u32(size / 2) - sel[4 * j + 1];
+  if (m != cmid || target >= m) {
+    if (tid == 0) {
+      atomicOr(err, 1u);
+      pivots[h] = ~0ull;
+    }
+    return;
+  }
+  const bool in_lds = m <= u32(kPivotLdsKeys);
+  // 2. radix select, 8 bits per pass from the top
+  u64 prefix = 0;
+  u32 rem = target;
+  for (int pass = 7; pass >= 0; --pass) {
+    const int shift = pass * 8;
+    const u64 hmask = pass == 7 ? 0ull : (~0ull << (shift + 8));
+    for (int b = tid; b < 256; b += kPivotThreads) hist[b] = 0;
+    __syncthreads();
+    if (in_lds) {
+      for (u32 k = tid; k < m; k += kPivotThreads) {
+        const u64 key = keys[k];
+        if ((key & hmask) == (prefix & hmask)) atomicAdd(&hist[u32(key >> shift) & 255u], 1u);
+      }
+    } else {
+      for (int r = 0; r < mv.P; ++r) {
+        const u32 c = mv.count(r);
+        for (u32 k = tid; k < c; k += kPivotThreads) {
+          const float* row = mv.row(r, k);
+          if (mv.node(row) != h) continue;
+          const u64 key = mv.key(row);
+          if ((key & hmask) == (prefix & hmask)) atomicAdd(&hist[u32(key >> shift) & 255u], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int l = tid;
+      u32 v[4], s = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = hist[4 * l + q];
+        s += v[q];
+      }
+      const u32 incl = dev::wave_incl_scan(s);
+      u32 c = incl - s;
+      if (rem >= c && rem < incl) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (rem >= c && rem < c + v[q]) {
+            s_digit = u32(4 * l + q);
+            s_rem = rem - c;
+          }
+          c += v[q];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= u64(s_digit) << shift;
+    rem = s_rem;
+    __syncthreads();
+  }
+  // 3. the pivot row (composite keys are unique)
+  for (int r = 0; r < mv.P; ++r) {
+    const u32 c = mv.count(r);
+    for (u32 k = tid; k < c; k += kPivotThreads) {
+      const float* row = mv.row(r, k);
+      if (mv.node(row) == h && mv.key(row) == prefix) {
+        s_found = 1;
+        pivots[h] = prefix;
+        float* tr = top_rows + size_t(h) * (dim + 1);
+        for (int q = 0; q <= dim; ++q) tr[q] = row[q];
+        cl[2 * axis + 1] = row[axis];
+        cr[2 * axis] = row[axis];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && !s_found) atomicOr(err, 1u);
+}
+
+// ---- counting sort by destination (P <= 64) -------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restrict__ node, int levels,
+                                                       const u64* __restrict__ pivots, int last_axis, int P,
+                                                       i64 per_block, u32* __restrict__ bcount) {
   __shared__ u32 cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(n, b0 + per_block);
+  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const u32 first = u32(P - 1);
-  for (i64 p = b0 + threadIdx.x; p < b1; p += kBlock) {
-    const u32 h = route(node[p], rows + p * (dim + 1), dim, last_axis, pivots);
-    node[p] = h;
+  for (i64 i = b0 + threadIdx.x; i < b1; i += kBlock) {
+    const u32 h = route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots);
+    node[i] = h;
     if (h != kTopDone) atomicAdd(&cnt[h - first], 1u);
   }
   __syncthreads();
   if (threadIdx.x < P) bcount[i64(blockIdx.x) * P + threadIdx.x] = cnt[threadIdx.x];
 }
 
-// offsets[block][d] = sum_{d' < d} total[d'] + sum_{b' < block} bcount[b'][d]; counts[d] = total[d]
+// offsets[block][d] = sum_{d' < d} total[d'] + sum_{b' < block} bcount[b'][d]
 __global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u32* __restrict__ offsets,
-                            u32* __restrict__ counts) {
+                            i64* __restrict__ counts, const u32* __restrict__ err) {
   __shared__ u32 tot[64];
   const int d = threadIdx.x;
   if (d < P) {
     u32 s = 0;
     for (int b = 0; b < blocks; ++b) s += bcount[i64(b) * P + d];
     tot[d] = s;
-    counts[d] = s;
+    counts[2 * d] = i64(s);
+    counts[2 * d + 1] = i64(*err);
   }
   __syncthreads();
   if (d < P) {
@@ -128,20 +378,20 @@ __global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_pack_scatter(const float* __restrict__ rows, i64 n, int dim,
-                                                         const u32* __restrict__ node, int P, i64 per_block,
-                                                         const u32* __restrict__ offsets, float* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int P,
+                                                         i64 per_block, const u32* __restrict__ offsets,
+                                                         float* __restrict__ out) {
   __shared__ u32 cur[64];
-  __shared__ u32 wcnt[4][64];
+  __shared__ u32 wcnt[kBlock / 64][64];
   const u32 first = u32(P - 1);
   if (threadIdx.x < P) cur[threadIdx.x] = offsets[i64(blockIdx.x) * P + threadIdx.x];
   __syncthreads();
-  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(n, b0 + per_block);
+  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const int w = threadIdx.x / 64, ln = dev::lane();
-  const int rs = dim + 1;
+  const int dim = p.dim, rs = dim + 1;
   for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
-    const i64 p = c0 + threadIdx.x;
-    const u32 h = p < b1 ? node[p] : kTopDone;
+    const i64 i = c0 + threadIdx.x;
+    const u32 h = i < b1 ? node[i] : kTopDone;
     const int d = h == kTopDone ? -1 : int(h - first);
     u32 my = 0;
     for (int e = 0; e < P; ++e) {  // stable rank among same-destination points of the chunk
@@ -154,8 +404,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const float* __restrict
       u32 off = cur[d];
       for (int v = 0; v < w; ++v) off += wcnt[v][d];
       float* o = out + i64(off + my) * rs;
-      const float* r = rows + p * rs;
-      for (int c = 0; c < rs; ++c) o[c] = r[c];
+      const float* r = p.pts + i * dim;
+      for (int c = 0; c < dim; ++c) o[c] = r[c];
+      o[dim] = __uint_as_float(point_id(p, i));
     }
     __syncthreads();
     if (threadIdx.x < P) {
@@ -168,45 +419,80 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const float* __restrict
 }
 
 int pack_blocks(i64 n) { return int(std::max<i64>(1, std::min<i64>(2048, (n + 8191) / 8192))); }
+int stream_grid(i64 n) { return int(std::max<i64>(1, std::min<i64>(512, (n + 16383) / 16384))); }
 
 }  // namespace
 
-void top_route_hist(const float* rows, i64 n, int dim, u32* node, int level, const u64* pivots, int prev_axis,
-                    int axis, const float* params, int bins, u32* hist, hipStream_t stream) {
-  if (n <= 0) return;
-  const int nb_total = (1 << level) * bins;
-  if (nb_total > kMaxTopBins) throw std::invalid_argument("top_route_hist: nodes * bins exceeds 8192");
-  const int grid = int(std::min<i64>(2048, (n + kBlock - 1) / kBlock));
-  k_top_route_hist<<<grid, kBlock, size_t(nb_total) * 4, stream>>>(rows, n, dim, node, level, pivots, prev_axis,
-                                                                    axis, params, bins, hist);
+void top_bbox(const TopPoints& p, i64* box, hipStream_t stream) {
+  if (p.n <= 0) return;
+  const int dim = p.dim;
+  const i64 want = std::min<i64>(p.n * dim, i64(1024) * kBlock);
+  const i64 T = std::max<i64>(dim, (want / dim) * dim);
+  const int grid = int((T + kBlock - 1) / kBlock);
+  k_top_bbox<<<grid, kBlock, size_t(2) * dim * 4, stream>>>(p, T, box);
   PKD_LAUNCH_CHECK();
 }
 
-void top_collect_middle(const float* rows, i64 n, int dim, const u32* node, int level, int axis, const float* params,
-                        int bins, const u32* bstar, float* out_rows, i64 cap, unsigned long long* out_count,
-                        hipStream_t stream) {
-  PKD_HIP_CHECK(hipMemsetAsync(out_count, 0, 8, stream));
-  if (n <= 0) return;
-  const int grid = int(std::min<i64>(2048, (n + kBlock - 1) / kBlock));
-  k_top_collect<<<grid, kBlock, 0, stream>>>(rows, n, dim, node, level, axis, params, bins, bstar, out_rows, cap,
-                                              out_count);
+void top_root_cell(const i64* box, int dim, float* cells, hipStream_t stream) {
+  k_top_root_cell<<<1, 256, 0, stream>>>(box, dim, cells);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_route_hist(const TopPoints& p, u32* node, int level, const u64* pivots, int prev_axis, int axis,
+                    const float* cells, int bins, u32* hist, hipStream_t stream) {
+  if ((1 << level) > kTopMaxNodes) throw std::invalid_argument("top_route_hist: too many nodes");
+  const int nb_total = (1 << level) * bins;
+  if (nb_total > kTopBins) throw std::invalid_argument("top_route_hist: nodes * bins exceeds 8192");
+  if (p.n <= 0) return;
+  k_top_route_hist<<<stream_grid(p.n), kBlock, size_t(nb_total) * 4, stream>>>(p, node, level, pivots, prev_axis,
+                                                                               axis, cells, bins, hist);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err,
+                hipStream_t stream) {
+  k_top_select<<<1 << level, kBlock, 0, stream>>>(hist, level, bins, sizes, sel, err);
+  PKD_LAUNCH_CHECK();
+}
+
+size_t top_middle_words(int dim, i64 cap) { return 4 + size_t(cap) * size_t(dim + 2); }
+
+void top_collect(const TopPoints& p, const u32* node, int level, int axis, const float* cells, int bins,
+                 const u32* sel, float* buf, i64 cap, hipStream_t stream) {
+  PKD_HIP_CHECK(hipMemsetAsync(buf, 0, 16, stream));
+  if (p.n <= 0) return;
+  k_top_collect<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, cells, bins, sel, buf, cap);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
+               const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream) {
+  static bool attr = false;
+  const size_t lds = size_t(kPivotLdsKeys) * 8;
+  if (!attr) {
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_top_pivot),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    attr = true;
+  }
+  MidView mv{gathered, i64(top_middle_words(dim, cap)), cap, P, dim, axis};
+  k_top_pivot<<<1 << level, kPivotThreads, lds, stream>>>(mv, level, sizes, sel, pivots, top_rows, cells, err);
   PKD_LAUNCH_CHECK();
 }
 
 size_t top_pack_scratch_bytes(i64 n, int P) { return size_t(2) * pack_blocks(n) * size_t(P) * 4; }
 
-void top_pack(const float* rows, i64 n, int dim, u32* node, int levels, const u64* pivots, int last_axis, int P,
-              float* out_rows, u32* counts, void* scratch, hipStream_t stream) {
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
+              i64* counts, const u32* err, void* scratch, hipStream_t stream) {
   if (P > 64 || P != (1 << levels)) throw std::invalid_argument("top_pack: P must be 2^levels <= 64");
-  const int blocks = pack_blocks(n);
-  const i64 per_block = (std::max<i64>(n, 1) + blocks - 1) / blocks;
+  const int blocks = pack_blocks(p.n);
+  const i64 per_block = (std::max<i64>(p.n, 1) + blocks - 1) / blocks;
   u32* bcount = static_cast<u32*>(scratch);
   u32* offsets = bcount + size_t(blocks) * P;
-  k_pack_count<<<blocks, kBlock, 0, stream>>>(rows, n, dim, node, pivots, last_axis, P, per_block, bcount);
+  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, P, per_block, bcount);
   PKD_LAUNCH_CHECK();
-  k_pack_scan<<<1, 64, 0, stream>>>(bcount, blocks, P, offsets, counts);
+  k_pack_scan<<<1, 64, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
   PKD_LAUNCH_CHECK();
-  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(rows, n, dim, node, P, per_block, offsets, out_rows);
+  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, per_block, offsets, out_rows);
   PKD_LAUNCH_CHECK();
 }
 

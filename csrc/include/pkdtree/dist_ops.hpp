@@ -6,9 +6,13 @@
 // order, found by gathering the few points of the median bucket), every point is then sent to
 // the rank that owns its top-level leaf with a single all-to-all, and each GPU builds its
 // subtree locally. These kernels are the per-rank pieces; communication is done by the caller
-// (torch.distributed over RCCL).
+// (torch.distributed over RCCL). Every per-level decision (median bucket, exact pivot,
+// children cells) is computed on the device from the collective outputs, so the top levels
+// run without a single host round trip; only the all-to-all split sizes are read back.
 //
-// Rows are (dim + 1) floats: the coordinates followed by the id bits.
+// Input points are the caller's [n][dim] f32 rows; ids are either an explicit u32 array or
+// implicit (id_base + row). Rows sent by the all-to-all are (dim + 1) floats: the coordinates
+// followed by the id bits.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -17,29 +21,60 @@
 namespace pkdtree {
 
 constexpr u32 kTopDone = 0xffffffffu;  // node index of a point that became a top-tree pivot
+constexpr int kTopMaxNodes = 32;       // nodes per top level (P <= 64)
+constexpr int kTopBins = 8192;         // nodes * bins per top level (LDS histogram)
+
+struct TopPoints {
+  const float* pts;  // [n][dim]
+  const u32* ids;    // [n] or nullptr: id = id_base + row
+  i64 n;
+  int dim;
+  u32 id_base;
+};
+
+// Global sizes of the nodes of one top level (heap nodes 2^l - 1 ...), known on the host
+// from the implicit-tree geometry.
+struct TopSizes {
+  i64 n[kTopMaxNodes];
+};
+
+// Per-rank bounding box, encoded for ONE allreduce(MIN) over int64: box[c] = orderable(lo_c),
+// box[dim + c] = ~orderable(hi_c) (both < 2^32). The caller fills box with 0xffffffff first.
+void top_bbox(const TopPoints& p, i64* box, hipStream_t stream);
+// cells[0] ([dim][2] lo/hi) from the reduced box.
+void top_root_cell(const i64* box, int dim, float* cells, hipStream_t stream);
 
 // One top level: (a) if level > 0, route each point below the pivot of its node from the
-// previous level (node = 2*node+1 / 2*node+2 in heap order; the pivot itself -> kTopDone);
-// (b) histogram the level's axis into hist[(node - first_node) * bins + b] using the node's
-// bucket params (lo, scale). hist must be zeroed by the caller.
-//   pivots: composite keys (orderable(key) << 32 | id) of every decided top node (heap order)
-//   prev_axis: split axis of the previous level (ignored at level 0)
-void top_route_hist(const float* rows, i64 n, int dim, u32* node, int level, const u64* pivots, int prev_axis,
-                    int axis, const float* params /* [nodes][2] lo, scale */, int bins, u32* hist,
-                    hipStream_t stream);
+// previous level (heap order: 2h+1 / 2h+2; the pivot itself -> kTopDone) and store the node;
+// at level 0 every point is at the root and `node` is not read; (b) histogram the level's
+// axis into hist[(node - first) * bins + b] with the node's cell (cells, heap-indexed
+// [h][dim][2]) as bucket range. hist must be zeroed by the caller.
+void top_route_hist(const TopPoints& p, u32* node, int level, const u64* pivots, int prev_axis, int axis,
+                    const float* cells, int bins, u32* hist, hipStream_t stream);
 
-// Compacts the rows of points whose bucket (same function as top_route_hist) equals
-// bstar[node]: out_rows [cap][dim+1], out_count[0] = number found (may exceed cap: caller
-// retries with a larger buffer).
-void top_collect_middle(const float* rows, i64 n, int dim, const u32* node, int level, int axis,
-                        const float* params, int bins, const u32* bstar, float* out_rows, i64 cap,
-                        unsigned long long* out_count, hipStream_t stream);
+// Per node of the level: the bucket b* holding the element of rank size/2 and the counts
+// below / inside it. sel[j] = {b*, count_less, count_mid, 0}. err |= 2 on inconsistent sums.
+void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err,
+                hipStream_t stream);
+
+// Middle-bucket compaction: buf = [4 header words: count, 0, 0, 0][cap][dim + 2] floats
+// (coordinates, id bits, node); count may exceed cap (the pivot kernel flags it).
+size_t top_middle_words(int dim, i64 cap);
+void top_collect(const TopPoints& p, const u32* node, int level, int axis, const float* cells, int bins,
+                 const u32* sel, float* buf, i64 cap, hipStream_t stream);
+
+// Exact pivots of one level from the all-gathered middle buffers (P consecutive buffers of
+// top_middle_words(dim, cap) words): per node, the element of rank size/2 - count_less among
+// the gathered middles (radix select over (orderable(key) << 32 | id)). Writes pivots[h],
+// top_rows[h] (dim + 1 floats) and the children cells. err |= 1 if a buffer overflowed.
+void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
+               const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream);
 
 // Final routing below the last top level + counting sort of rows by destination leaf
-// (dest = node - (P - 1)): out_rows [n_kept][dim+1] grouped by destination, counts [P].
-// Pivot points are dropped. `scratch` holds 2 * blocks * P u32 (see top_pack_scratch).
+// (dest = node - (P - 1)): out_rows [n_kept][dim+1] grouped by destination (stable),
+// counts [P][2] int64 = (rows for dest, err word). Pivot points are dropped.
 size_t top_pack_scratch_bytes(i64 n, int P);
-void top_pack(const float* rows, i64 n, int dim, u32* node, int levels, const u64* pivots, int last_axis, int P,
-              float* out_rows, u32* counts, void* scratch, hipStream_t stream);
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
+              i64* counts, const u32* err, void* scratch, hipStream_t stream);
 
 }  // namespace pkdtree

@@ -75,16 +75,16 @@ def forest_slice(n: int, p: int, r: int) -> Tuple[int, int]:
 
 def broadcast_ints(vals: List[int], src: int = 0) -> List[int]:
     """MPI_Bcast of the {seed, dim, N} config (kdtree_mpi.cpp:199)."""
-    t = torch.tensor(vals, dtype=torch.int64, device=device())
+    t = torch.tensor(vals, dtype=torch.int64)
     if dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            t = t.to(device())
         dist.broadcast(t, src)
     return [int(v) for v in t.tolist()]
 
 
 def allreduce_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-    if dist.is_initialized() and world() > 1:
-        dist.all_reduce(t, op=op)
-    return t
+    return all_reduce_(t, op)
 
 
 def max_float(v: float) -> float:
@@ -98,3 +98,51 @@ def min_packed_(packed: torch.Tensor) -> torch.Tensor:
     signed int64 MIN equals the unsigned one (reference: MPI_Reduce MIN, kdtree_mpi.cpp:253,
     which drops the id; here the id rides along)."""
     return allreduce_(packed, dist.ReduceOp.MIN)
+
+
+# ---- collectives used by the global decomposition ---------------------------------------
+# RCCL ("nccl") takes device tensors directly. gloo (CPU tests, and the multi-rank GPU tests
+# that run every rank on one card) only gets host tensors: device tensors are staged.
+def _staged(t: torch.Tensor) -> bool:
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    if not dist.is_initialized() or world() == 1:
+        return t
+    if _staged(t):
+        c = t.cpu()
+        dist.all_reduce(c, op=op)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
+def all_gather_into_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    """out[r * t.numel():(r + 1) * t.numel()] = t of rank r (fixed-size all-gather)."""
+    P = world()
+    if not dist.is_initialized() or P == 1:
+        out.view(-1)[: t.numel()].copy_(t.view(-1))
+        return out
+    if _staged(t) or dist.get_backend() == "gloo":
+        c = t.cpu().contiguous()
+        parts = [torch.empty_like(c) for _ in range(P)]
+        dist.all_gather(parts, c)
+        out.view(-1).copy_(torch.cat([p.view(-1) for p in parts]))
+    else:
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
+    return out
+
+
+def all_to_all_single_(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> torch.Tensor:
+    if not dist.is_initialized() or world() == 1:
+        out.copy_(inp)
+        return out
+    if _staged(inp):
+        co = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(co, inp.cpu(), out_splits, in_splits)
+        out.copy_(co)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits)
+    return out

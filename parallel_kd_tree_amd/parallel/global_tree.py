@@ -20,6 +20,7 @@ CPU tests, where the per-rank device ops run as torch code with identical arithm
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -76,21 +77,13 @@ def _route_cpu(rows, dim, node, pivots_signed, axis):
     return node
 
 
-class _Backend:
-    """Per-rank device ops: HIP kernels on GPU tensors, torch reference code on CPU tensors."""
+class _HostOps:
+    """Per-rank top-level ops on host tensors (gloo tests): the torch reference of the HIP
+    kernels in csrc/gpu/dist_ops.hip (same bucketing arithmetic, same routing)."""
 
-    def __init__(self, device: torch.device):
-        self.gpu = device.type == "cuda"
-        self.device = device
-
-    def route_hist(self, rows, dim, node, level, pivots_u64, prev_axis, axis, params, bins):
+    @staticmethod
+    def route_hist(rows, dim, node, level, pivots_u64, prev_axis, axis, params, bins):
         nodes = 1 << level
-        if self.gpu:
-            hist = torch.zeros(nodes * bins, dtype=torch.int32, device=self.device)
-            piv = torch.from_numpy(pivots_u64.view(np.int64)).to(self.device)
-            prm = torch.from_numpy(params.reshape(-1)).to(self.device)
-            ops.native().top_route_hist(rows, dim, node, level, piv, prev_axis, axis, prm, bins, hist)
-            return hist
         if level > 0:
             piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
             _route_cpu(rows, dim, node, piv, prev_axis)
@@ -100,20 +93,9 @@ class _Backend:
         b = _bucket_cpu(rows[live, axis], prm[j, 0], prm[j, 1], bins)
         return torch.bincount(j * bins + b, minlength=nodes * bins).to(torch.int32)
 
-    def collect_middle(self, rows, dim, node, level, axis, params, bins, bstar):
+    @staticmethod
+    def collect_middle(rows, dim, node, level, axis, params, bins, bstar):
         nodes = 1 << level
-        if self.gpu:
-            prm = torch.from_numpy(params.reshape(-1)).to(self.device)
-            bs = torch.from_numpy(bstar.astype(np.int32)).to(self.device)
-            cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
-            cap = 4096
-            while True:
-                out = torch.empty((cap, dim + 2), dtype=torch.float32, device=self.device)
-                ops.native().top_collect_middle(rows, dim, node, level, axis, prm, bins, bs, out, cnt)
-                c = int(cnt.item())
-                if c <= cap:
-                    return out[:c]
-                cap = c
         live = (node != DONE).nonzero().flatten()
         j = node[live] - (nodes - 1)
         prm = torch.from_numpy(params)
@@ -124,16 +106,8 @@ class _Backend:
         out[:, dim + 1] = node[sel].to(torch.int32).view(torch.float32)
         return out
 
-    def pack(self, rows, dim, node, levels, pivots_u64, last_axis, P):
-        if self.gpu:
-            n = rows.shape[0]
-            out = torch.empty_like(rows)
-            counts = torch.empty(P, dtype=torch.int32, device=self.device)
-            scratch = torch.empty(ops.native().top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=self.device)
-            piv = torch.from_numpy(pivots_u64.view(np.int64)).to(self.device)
-            ops.native().top_pack(rows, dim, node, levels, piv, last_axis, P, out, counts, scratch)
-            c = counts.to(torch.int64)
-            return out[: int(c.sum().item())], c
+    @staticmethod
+    def pack(rows, dim, node, levels, pivots_u64, last_axis, P):
         piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
         _route_cpu(rows, dim, node, piv, last_axis)
         live = (node != DONE).nonzero().flatten()
@@ -225,39 +199,170 @@ def _all_gather_var(t: torch.Tensor) -> List[torch.Tensor]:
     if P == 1:
         return [t]
     cnt = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    cnts = [torch.zeros_like(cnt) for _ in range(P)]
-    dist.all_gather(cnts, cnt)
-    sizes = [int(c.item()) for c in cnts]
+    cnts = torch.empty(P, dtype=torch.int64, device=t.device)
+    comm.all_gather_into_(cnts, cnt)
+    sizes = cnts.tolist()
     mx = max(sizes)
     pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     pad[: t.shape[0]] = t
-    outs = [torch.empty_like(pad) for _ in range(P)]
-    dist.all_gather(outs, pad)
-    return [o[:s] for o, s in zip(outs, sizes)]
+    outs = torch.empty((P,) + tuple(pad.shape), dtype=t.dtype, device=t.device)
+    comm.all_gather_into_(outs, pad)
+    return [outs[r, :s] for r, s in enumerate(sizes)]
 
 
 class GlobalTreeBuilder:
-    """Builds the global tree; reusable across builds of the same (n_total, dim)."""
+    """Builds the global tree; reusable across builds of the same (n_total, dim).
 
-    def __init__(self, n_total: int, dim: int, device: Optional[torch.device] = None, depth0: int = 0):
+    On GPU every top-level decision is made on the device (csrc/gpu/dist_ops.hip): per level
+    one route+histogram pass, an allreduce(SUM) of the histogram, the median bucket per node,
+    one compaction pass of that bucket, a fixed-size all-gather of the compacted rows and a
+    radix select of the exact pivot. Nothing is read back until the all-to-all needs its split
+    sizes. Host tensors (gloo tests) take the torch reference path with the same arithmetic.
+    """
+
+    def __init__(self, n_total: int, dim: int, device: Optional[torch.device] = None, depth0: int = 0,
+                 timings: bool = False):
         self.P = comm.world()
         self.rank = comm.rank()
         if self.P & (self.P - 1):
             raise ValueError(f"global decomposition needs a power-of-two world size, got {self.P}")
+        if self.P > 64:
+            raise ValueError("global decomposition supports at most 64 ranks")
         self.L = int(math.log2(self.P))
         self.n_total, self.dim, self.depth0 = int(n_total), int(dim), int(depth0)
+        if self.n_total >= 1 << 32:
+            raise ValueError("point ids are 32-bit: at most 2^32 - 1 points")
         self.device = device if device is not None else comm.device()
-        self.backend = _Backend(self.device)
         leaf = self.P - 1 + self.rank
         self.slot_lo, self.n_leaf = segment(self.n_total, leaf)
+        self.top_slots = [median_slot(self.n_total, h) if segment(self.n_total, h)[1] > 0 else -1
+                          for h in range(self.P - 1)]
+        self.record_timings = timings
         self._builder = None
+        self._ws: Dict[str, torch.Tensor] = {}
         if self.device.type == "cuda" and self.n_leaf > 0:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
 
     # ------------------------------------------------------------------------------------
     def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
+        if self.device.type == "cuda":
+            return self._build_device(points, ids, id_base)
+        return self._build_host(points, ids, id_base)
+
+    # ---------------------------------------------------------------- device (HIP + RCCL) path
+    def _cap(self, level: int, scale: int) -> int:
+        """Middle-bucket rows a rank may contribute at `level` (uniform data: about
+        n_total * 2^level / (8192 * P)); overflow is detected and the build retried. Must be
+        the same on every rank: it sizes the all-gather."""
+        expect = self.n_total * (1 << level) // (TOP_BINS * self.P) + 1
+        return int(min(max(2048, 3 * expect) * scale, max(self.n_total, 1)))
+
+    def _buf(self, name: str, shape, dtype) -> torch.Tensor:
+        t = self._ws.get(name)
+        n = int(np.prod(shape))
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(n, dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:n].view(shape)
+
+    def _tick(self, timings: Dict[str, float], name: str, t0: List[float]) -> None:
+        if self.record_timings:
+            torch.cuda.synchronize(self.device)
+            now = time.perf_counter()
+            timings[name] = timings.get(name, 0.0) + (now - t0[0]) * 1e3
+            t0[0] = now
+
+    def _top_device(self, pts, idt, id_base, scale, timings, t0):
+        nat = ops.native()
+        dim, P, L = self.dim, self.P, self.L
+        n_local = pts.shape[0]
+        dev = self.device
+        box = self._buf("box", (2 * dim,), torch.int64)
+        box.fill_(0xFFFFFFFF)
+        nat.top_bbox(pts, box)
+        comm.all_reduce_(box, dist.ReduceOp.MIN)
+        cells = self._buf("cells", ((2 * P - 1) * dim * 2,), torch.float32)
+        nat.top_root_cell(box, dim, cells)
+        node = self._buf("node", (max(n_local, 1),), torch.int32)
+        pivots = torch.full((max(P - 1, 1),), -1, dtype=torch.int64, device=dev)
+        top_rows = torch.zeros((max(P - 1, 1), dim + 1), dtype=torch.float32, device=dev)
+        err = self._buf("err", (4,), torch.int32)
+        err.zero_()
+        sel = self._buf("sel", (32 * 4,), torch.int32)
+        hist = self._buf("hist", (TOP_BINS,), torch.int32)
+        self._tick(timings, "bbox", t0)
+        for level in range(L):
+            nodes = 1 << level
+            bins = TOP_BINS // nodes
+            axis = (self.depth0 + level) % dim
+            prev_axis = (self.depth0 + level - 1) % dim
+            sizes = [segment(self.n_total, nodes - 1 + j)[1] for j in range(nodes)]
+            h = hist[: nodes * bins]
+            h.zero_()
+            nat.top_route_hist(pts, idt, id_base, node, level, pivots, prev_axis, axis, cells, bins, h)
+            comm.all_reduce_(h, dist.ReduceOp.SUM)
+            nat.top_select(h, level, bins, sizes, sel, err)
+            cap = self._cap(level, scale)
+            words = nat.top_middle_words(dim, cap)
+            buf = self._buf("mid", (words,), torch.float32)
+            nat.top_collect(pts, idt, id_base, node, level, axis, cells, bins, sel, buf, cap)
+            gathered = self._buf("gathered", (P * words,), torch.float32)
+            comm.all_gather_into_(gathered, buf)
+            nat.top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err)
+            self._tick(timings, f"top_level{level}", t0)
+        last_axis = (self.depth0 + L - 1) % dim
+        send = self._buf("send", (max(n_local, 1), dim + 1), torch.float32)
+        counts = torch.empty(2 * P, dtype=torch.int64, device=dev)
+        scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, P),), torch.uint8)
+        nat.top_pack(pts, idt, id_base, node, L, pivots, last_axis, P, send, counts, err, scratch)
+        recv_counts = torch.empty_like(counts)
+        comm.all_to_all_single_(recv_counts, counts)
+        both = torch.cat([counts, recv_counts]).cpu()  # the only host read-back of the build
+        self._tick(timings, "pack", t0)
+        errs = 0
+        for v in both[1::2].tolist():
+            errs |= int(v)
+        if errs & 2:
+            raise RuntimeError("global top levels: histogram totals disagree with the tree geometry")
+        if errs & 1:
+            return None  # a middle bucket overflowed its all-gather slot: retry larger
+        in_splits = both[0:2 * P:2].tolist()
+        out_splits = both[2 * P::2].tolist()
+        return send[: sum(in_splits)], in_splits, out_splits, top_rows
+
+    def _build_device(self, points, ids, id_base) -> DistTree:
         dim, P, L = self.dim, self.P, self.L
         timings: Dict[str, float] = {}
+        t0 = [time.perf_counter()]
+        pts = points.to(self.device, torch.float32).contiguous()
+        idt = None if ids is None else ids.to(self.device, torch.int32).contiguous()
+        scale = 1
+        while True:
+            res = self._top_device(pts, idt, int(id_base), scale, timings, t0)
+            if res is not None:
+                break
+            if all(self._cap(l, scale) >= self.n_total for l in range(L)):
+                raise RuntimeError("global top levels: middle buckets inconsistent at full capacity")
+            scale *= 8
+        send, in_splits, out_splits, top_rows = res
+        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=self.device)
+        comm.all_to_all_single_(recv, send, out_splits, in_splits)
+        self._tick(timings, "all_to_all", t0)
+        if recv.shape[0] != self.n_leaf:
+            raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
+        if self.n_leaf == 0:
+            tp = torch.empty((0, dim), dtype=torch.float32, device=self.device)
+            ti = torch.empty((0,), dtype=torch.int32, device=self.device)
+        else:
+            tp, ti = self._builder.build_rows(recv)
+        self._tick(timings, "local_build", t0)
+        return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
+                        list(self.top_slots), top_rows[: P - 1], timings)
+
+    # ---------------------------------------------------------------- host (gloo) reference path
+    def _build_host(self, points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) -> DistTree:
+        dim, P, L = self.dim, self.P, self.L
+        ops_h = _HostOps
         rows = _to_rows(points.to(torch.float32), ids, id_base)
         n_local = rows.shape[0]
         # 1. bounding box
@@ -265,16 +370,15 @@ class GlobalTreeBuilder:
             lo = points.amin(0).to(torch.float32)
             hi = points.amax(0).to(torch.float32)
         else:
-            lo = torch.full((dim,), float("inf"), device=points.device)
-            hi = torch.full((dim,), float("-inf"), device=points.device)
-        comm.allreduce_(lo, dist.ReduceOp.MIN)
-        comm.allreduce_(hi, dist.ReduceOp.MAX)
-        root_cell = np.stack([lo.cpu().numpy(), hi.cpu().numpy()], 1).astype(np.float32)  # [dim][2]
+            lo = torch.full((dim,), float("inf"))
+            hi = torch.full((dim,), float("-inf"))
+        comm.all_reduce_(lo, dist.ReduceOp.MIN)
+        comm.all_reduce_(hi, dist.ReduceOp.MAX)
+        root_cell = np.stack([lo.numpy(), hi.numpy()], 1).astype(np.float32)  # [dim][2]
         cells = {0: root_cell}
-        node = torch.zeros(n_local, dtype=torch.int64 if not self.backend.gpu else torch.int32, device=rows.device)
+        node = torch.zeros(n_local, dtype=torch.int64)
         pivots = np.zeros(max(P - 1, 1), dtype=np.uint64)
         top_rows = torch.zeros((max(P - 1, 1), dim + 1), dtype=torch.float32)
-        top_slots = [-1] * max(P - 1, 1)
         # 2. top levels
         for level in range(L):
             nodes = 1 << level
@@ -286,9 +390,9 @@ class GlobalTreeBuilder:
             for j in range(nodes):
                 c = cells.get(first + j, root_cell)
                 params[j] = make_params(c[axis, 0], c[axis, 1], bins)
-            hist = self.backend.route_hist(rows, dim, node, level, pivots, prev_axis, axis, params, bins)
-            comm.allreduce_(hist, dist.ReduceOp.SUM)
-            hh = hist.cpu().numpy().astype(np.int64).reshape(nodes, bins)
+            hist = ops_h.route_hist(rows, dim, node, level, pivots, prev_axis, axis, params, bins)
+            comm.all_reduce_(hist, dist.ReduceOp.SUM)
+            hh = hist.numpy().astype(np.int64).reshape(nodes, bins)
             bstar = np.zeros(nodes, dtype=np.int64)
             cless = np.zeros(nodes, dtype=np.int64)
             sizes = [segment(self.n_total, first + j)[1] for j in range(nodes)]
@@ -303,9 +407,9 @@ class GlobalTreeBuilder:
                 b = int(np.searchsorted(cum, r, side="right"))
                 bstar[j] = b
                 cless[j] = int(cum[b - 1]) if b > 0 else 0
-            mid_local = self.backend.collect_middle(rows, dim, node, level, axis, params, bins,
-                                                    np.where(bstar < 0, bins + 1, bstar))
-            mids = torch.cat(_all_gather_var(mid_local), 0).cpu()
+            mid_local = ops_h.collect_middle(rows, dim, node, level, axis, params, bins,
+                                             np.where(bstar < 0, bins + 1, bstar))
+            mids = torch.cat(_all_gather_var(mid_local), 0)
             mnode = mids[:, dim + 1].contiguous().view(torch.int32).numpy().astype(np.int64) & 0xFFFFFFFF
             mid_np = mids.numpy()
             for j in range(nodes):
@@ -323,7 +427,6 @@ class GlobalTreeBuilder:
                 pr = sel[order[t]]
                 pivots[h] = keys[order[t]]
                 top_rows[h] = torch.from_numpy(pr[:dim + 1].copy())
-                top_slots[h] = median_slot(self.n_total, h)
                 cl = cells.get(h, root_cell).copy()
                 cr = cl.copy()
                 cl[axis, 1] = pr[axis]
@@ -332,23 +435,21 @@ class GlobalTreeBuilder:
                 cells[2 * h + 2] = cr
         # 3. exchange
         last_axis = (self.depth0 + L - 1) % dim
-        send, counts = self.backend.pack(rows, dim, node, L, pivots, last_axis, P)
+        send, counts = ops_h.pack(rows, dim, node, L, pivots, last_axis, P)
         recv_counts = torch.empty_like(counts)
-        dist.all_to_all_single(recv_counts, counts)
-        in_splits = counts.cpu().tolist()
-        out_splits = recv_counts.cpu().tolist()
-        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=rows.device)
-        dist.all_to_all_single(recv, send, out_splits, in_splits)
+        comm.all_to_all_single_(recv_counts, counts)
+        in_splits = counts.tolist()
+        out_splits = recv_counts.tolist()
+        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32)
+        comm.all_to_all_single_(recv, send, out_splits, in_splits)
         if recv.shape[0] != self.n_leaf:
             raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
         # 4. local subtree
         if self.n_leaf == 0:
-            tp = torch.empty((0, dim), dtype=torch.float32, device=rows.device)
-            ti = torch.empty((0,), dtype=torch.int32, device=rows.device)
-        elif self._builder is not None:
-            tp, ti = self._builder.build_rows(recv)
+            tp = torch.empty((0, dim), dtype=torch.float32)
+            ti = torch.empty((0,), dtype=torch.int32)
         else:
             tp, ti = ops.build_cpu(recv[:, :dim].contiguous(), recv[:, dim].contiguous().view(torch.int32), "exact",
                                    self.depth0 + L, 1)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
-                        top_slots[: P - 1], top_rows[: P - 1], timings)
+                        list(self.top_slots), top_rows[: P - 1], {})

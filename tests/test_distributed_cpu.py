@@ -25,7 +25,7 @@ def _worker(rank, world, port, fn, args, q):
     try:
         torch.set_num_threads(1)
         from parallel_kd_tree_amd.parallel import comm
-        comm.init(backend="gloo")
+        comm.init(backend="gloo", timeout_s=150)
         fn(rank, world, *args)
         comm.barrier()
         comm.destroy()
@@ -41,7 +41,15 @@ def run(world, fn, *args):
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    errs = [q.get(timeout=600) for _ in range(world)]
+    errs = []
+    try:
+        for _ in range(world):
+            errs.append(q.get(timeout=240))
+    except Exception:  # a rank died or hangs in a collective: end the group instead of hanging
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        raise AssertionError(f"only {len(errs)} of {world} ranks finished: {[e for _, e in errs if e]}")
     for p in procs:
         p.join(60)
     bad = [e for _, e in errs if e]

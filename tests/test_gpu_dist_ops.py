@@ -1,83 +1,174 @@
-"""The global decomposition's HIP kernels (csrc/gpu/dist_ops.hip) against the torch reference
-ops that the multi-process CPU tests validate end to end. Single GPU: ranks are not needed to
-check the per-rank kernels; the 8-GPU path is exercised by the driver's scaling run."""
+"""The global decomposition's HIP kernels (csrc/gpu/dist_ops.hip) against the torch/numpy
+reference path that the multi-process CPU tests validate end to end. The kernels are per-rank
+code, so one process checks them; test_gpu_multirank.py runs the whole pipeline with several
+ranks sharing the card."""
 import numpy as np
 import pytest
 import torch
 
 import parallel_kd_tree_amd as pk
-from parallel_kd_tree_amd.parallel.geometry import composite_u64, make_params
-from parallel_kd_tree_amd.parallel.global_tree import _Backend, _to_rows
+from parallel_kd_tree_amd import ops
+from parallel_kd_tree_amd.parallel.geometry import composite_u64, make_params, segment
+from parallel_kd_tree_amd.parallel.global_tree import DONE, _HostOps, _to_rows
 
 pytestmark = pytest.mark.gpu
 
 
-def _setup(n, dim, level, seed=1):
-    x = pk.generate_problem(seed, dim, n)
-    rows = _to_rows(x, None, 1)
-    nodes = 1 << level
-    first = nodes - 1
-    # fake pivots: medians of random subsets per heap node (exact composite keys of points)
+def _pivots(x, n, dim, levels, seed):
+    """Fake but valid pivots: composite keys of random points, per heap node."""
     rng = np.random.default_rng(seed)
-    piv = np.zeros(max(2 * nodes - 1, 1), dtype=np.uint64)
-    for h in range(first):
+    piv = np.zeros(max((1 << levels) - 1, 1), dtype=np.uint64)
+    for h in range((1 << levels) - 1):
         i = int(rng.integers(0, n))
         ax = ((h + 1).bit_length() - 1) % dim
         piv[h] = composite_u64(x[i:i + 1, ax].numpy(), np.array([i + 1], dtype=np.uint32))[0]
-    return x, rows, piv
+    return piv
+
+
+def _cells(nodes_total, dim, seed):
+    rng = np.random.default_rng(seed)
+    lo = rng.uniform(-120, -20, size=(nodes_total, dim)).astype(np.float32)
+    hi = rng.uniform(20, 120, size=(nodes_total, dim)).astype(np.float32)
+    return np.stack([lo, hi], -1).astype(np.float32)  # [h][dim][2]
+
+
+def test_bbox(gpu_device):
+    x = pk.generate_problem(3, 5, 123_457)
+    x[17, 2] = -0.0
+    box = torch.full((10,), 0xFFFFFFFF, dtype=torch.int64, device=gpu_device)
+    nat = ops.native()
+    nat.top_bbox(x.to(gpu_device), box)
+    cells = torch.zeros(10, dtype=torch.float32, device=gpu_device)
+    nat.top_root_cell(box, 5, cells)
+    c = cells.cpu().view(5, 2)
+    assert torch.equal(c[:, 0], x.amin(0)) and torch.equal(c[:, 1], x.amax(0))
 
 
 @pytest.mark.parametrize("level,dim", [(0, 3), (1, 3), (2, 3), (3, 2), (2, 8)])
-def test_route_hist_matches_cpu(gpu_device, level, dim):
-    n = 50_000
-    x, rows, piv = _setup(n, dim, level)
-    nodes = 1 << level
-    bins = 8192 // nodes
-    params = np.stack([np.array(make_params(-100.0 + j, 100.0 - j, bins)) for j in range(nodes)]).astype(np.float32)
-    cpu, gpu = _Backend(torch.device("cpu")), _Backend(gpu_device)
-    axis, prev = level % dim, (level - 1) % dim
-    # route down to `level` one level at a time on both backends
+def test_route_hist_select_collect_pivot(gpu_device, level, dim):
+    n = 60_000
+    x = pk.generate_problem(level + 7, dim, n)
+    rows = _to_rows(x, None, 1)
+    piv = _pivots(x, n, dim, level, level)
+    cells = _cells(4 << level, dim, level)
+    nat = ops.native()
+    xg = x.to(gpu_device)
     node_c = torch.zeros(n, dtype=torch.int64)
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
-    rows_g = rows.to(gpu_device)
+    cells_g = torch.from_numpy(cells.reshape(-1).copy()).to(gpu_device)
+    piv_g = torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device)
     for l in range(level + 1):
         nl = 1 << l
-        b = 8192 // nl
-        pr = np.stack([np.array(make_params(-100.0 + j, 100.0 - j, b)) for j in range(nl)]).astype(np.float32)
-        hc = cpu.route_hist(rows, dim, node_c, l, piv, (l - 1) % dim, l % dim, pr, b)
-        hg = gpu.route_hist(rows_g, dim, node_g, l, piv, (l - 1) % dim, l % dim, pr, b)
+        bins = 8192 // nl
+        axis, prev = l % dim, (l - 1) % dim
+        params = np.stack([np.array(make_params(cells[nl - 1 + j, axis, 0], cells[nl - 1 + j, axis, 1], bins))
+                           for j in range(nl)]).astype(np.float32)
+        hc = _HostOps.route_hist(rows, dim, node_c, l, piv, prev, axis, params, bins)
+        hg = torch.zeros(nl * bins, dtype=torch.int32, device=gpu_device)
+        nat.top_route_hist(xg, None, 1, node_g, l, piv_g, prev, axis, cells_g, bins, hg)
         assert torch.equal(hc, hg.cpu()), f"histogram mismatch at level {l}"
-        assert torch.equal(node_c.to(torch.int32), node_g.cpu()), f"routing mismatch at level {l}"
-    bstar = np.array([int(torch.argmax(hc[j * bins:(j + 1) * bins])) for j in range(nodes)])
-    mc = cpu.collect_middle(rows, dim, node_c, level, axis, params, bins, bstar)
-    mg = gpu.collect_middle(rows_g, dim, node_g, level, axis, params, bins, bstar).cpu()
-    key = lambda m: sorted(map(tuple, m.view(torch.int32).tolist()))
-    assert key(mc) == key(mg)
+        if l > 0:
+            assert torch.equal(node_c.to(torch.int32), node_g.cpu()), f"routing mismatch at level {l}"
+    # select: per node the bucket holding rank size/2 of the (local, here global) histogram
+    nl = 1 << level
+    bins = 8192 // nl
+    hh = hc.numpy().astype(np.int64).reshape(nl, bins)
+    sizes = [int(v) for v in hh.sum(1)]
+    sel = torch.zeros(128, dtype=torch.int32, device=gpu_device)
+    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
+    nat.top_select(hg, level, bins, sizes, sel, err)
+    s = sel.cpu().numpy().reshape(32, 4)
+    for j in range(nl):
+        if sizes[j] == 0:
+            continue
+        cum = np.cumsum(hh[j])
+        b = int(np.searchsorted(cum, sizes[j] // 2, side="right"))
+        assert s[j, 0] == b and s[j, 1] == (cum[b - 1] if b else 0) and s[j, 2] == hh[j, b]
+    assert int(err[0]) == 0
+    # collect + pivot (one rank: the gathered buffer is the local one)
+    axis = level % dim
+    cap = 8192
+    words = nat.top_middle_words(dim, cap)
+    buf = torch.empty(words, dtype=torch.float32, device=gpu_device)
+    nat.top_collect(xg, None, 1, node_g, level, axis, cells_g, bins, sel, buf, cap)
+    pivots = torch.full((2 * nl,), -1, dtype=torch.int64, device=gpu_device)
+    top_rows = torch.zeros((2 * nl, dim + 1), dtype=torch.float32, device=gpu_device)
+    cg = cells_g.clone()
+    nat.top_pivot(buf, 1, cap, level, axis, dim, sizes, sel, pivots, top_rows, cg, err)
+    assert int(err[0]) == 0
+    pv = pivots.cpu().numpy().view(np.uint64)
+    ids = np.arange(1, n + 1, dtype=np.uint32)
+    nodes_np = node_c.numpy()
+    for j in range(nl):
+        h = nl - 1 + j
+        mask = (nodes_np == h) if level > 0 else np.ones(n, bool)
+        if sizes[j] == 0:
+            assert pv[h] == np.uint64(0xFFFFFFFFFFFFFFFF)
+            continue
+        keys = np.sort(composite_u64(x.numpy()[mask, axis], ids[mask]))
+        assert pv[h] == keys[sizes[j] // 2], f"node {h}: wrong pivot"
+        i = int(pv[h] & np.uint64(0xFFFFFFFF)) - 1
+        tr = top_rows.cpu()[h]
+        assert torch.equal(tr[:dim], x[i]) and int(tr[dim].view(torch.int32)) == i + 1
+        c = cg.cpu().view(-1, dim, 2)
+        assert float(c[2 * h + 1, axis, 1]) == float(x[i, axis]) and float(c[2 * h + 2, axis, 0]) == float(x[i, axis])
 
 
 @pytest.mark.parametrize("P,dim", [(2, 3), (4, 3), (8, 3), (8, 5)])
-def test_pack_matches_cpu(gpu_device, P, dim):
+def test_pack_matches_host(gpu_device, P, dim):
     n = 100_000
     L = P.bit_length() - 1
-    x, rows, piv = _setup(n, dim, L, seed=P)
-    cpu, gpu = _Backend(torch.device("cpu")), _Backend(gpu_device)
-    # nodes at level L-1: route from the root with the fake pivots
+    x = pk.generate_problem(P, dim, n)
+    rows = _to_rows(x, None, 1)
+    piv = _pivots(x, n, dim, L, P)
+    nat = ops.native()
     node_c = torch.zeros(n, dtype=torch.int64)
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
-    rows_g = rows.to(gpu_device)
+    xg = x.to(gpu_device)
+    piv_g = torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device)
+    cells_g = torch.from_numpy(np.tile(np.array([-100, 100], np.float32), 2 * P * dim)).to(gpu_device)
     for l in range(L):
         nl = 1 << l
         pr = np.tile(np.array(make_params(-100, 100, 8192 // nl), dtype=np.float32), (nl, 1))
-        cpu.route_hist(rows, dim, node_c, l, piv, (l - 1) % dim, l % dim, pr, 8192 // nl)
-        gpu.route_hist(rows_g, dim, node_g, l, piv, (l - 1) % dim, l % dim, pr, 8192 // nl)
-    sc, cc = cpu.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P)
-    sg, cg = gpu.pack(rows_g, dim, node_g, L, piv, (L - 1) % dim, P)
-    assert torch.equal(cc, cg.cpu())
-    assert torch.equal(sc.view(torch.int32), sg.cpu().view(torch.int32)), "pack must be stable by destination"
+        _HostOps.route_hist(rows, dim, node_c, l, piv, (l - 1) % dim, l % dim, pr, 8192 // nl)
+        hg = torch.zeros(8192, dtype=torch.int32, device=gpu_device)
+        nat.top_route_hist(xg, None, 1, node_g, l, piv_g, (l - 1) % dim, l % dim, cells_g, 8192 // nl, hg)
+    sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P)
+    out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
+    counts = torch.empty(2 * P, dtype=torch.int64, device=gpu_device)
+    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
+    scratch = torch.empty(nat.top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=gpu_device)
+    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, P, out, counts, err, scratch)
+    cg = counts.cpu()
+    assert torch.equal(cc, cg[0::2]) and int(cg[1::2].abs().sum()) == 0
+    k = int(cc.sum())
+    assert torch.equal(sc.view(torch.int32), out[:k].cpu().view(torch.int32)), "pack must be stable by destination"
+
+
+def test_explicit_ids(gpu_device):
+    """Explicit id arrays route ties by id exactly like implicit ones."""
+    n, dim = 20_000, 2
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 4, (n, dim), generator=g).float()  # massive ties
+    ids = torch.randperm(n, generator=g).to(torch.int32) + 10
+    rows = torch.cat([x, ids.view(torch.float32)[:, None]], 1)
+    keys = composite_u64(x[:, 0].numpy(), ids.numpy().view(np.uint32))
+    piv = np.array([np.sort(keys)[n // 2]], dtype=np.uint64)
+    node_c = torch.zeros(n, dtype=torch.int64)
+    _HostOps.pack(rows, dim, node_c, 1, piv, 0, 2)
+    nat = ops.native()
+    node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
+    out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
+    counts = torch.empty(4, dtype=torch.int64, device=gpu_device)
+    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
+    scratch = torch.empty(nat.top_pack_scratch_bytes(n, 2), dtype=torch.uint8, device=gpu_device)
+    nat.top_pack(x.to(gpu_device), ids.to(gpu_device), 0, node_g, 1,
+                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, 2, out, counts, err, scratch)
+    assert torch.equal(node_c.to(torch.int32), node_g.cpu())
+    assert counts.cpu()[0::2].tolist() == [n // 2, n - n // 2 - 1]
 
 
 def test_build_rows_equals_build(gpu_device):
-    from parallel_kd_tree_amd import ops
     x = pk.generate_problem(4, 3, 200_000)
     ids = torch.arange(200_000, dtype=torch.int32) * 3 + 7
     b = ops.GpuTreeBuilder(200_000, 3, 2)
