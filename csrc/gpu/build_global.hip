@@ -14,6 +14,8 @@
 // Replaces build_tree_rec's per-node std::sort (kdtree_sequential.cpp:30-66).
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <string>
 #include <sstream>
 
 #include "device_utils.hpp"
@@ -36,6 +38,8 @@ constexpr int kChunk = kBlock * kItems;     // 4096 points per partition chunk
 constexpr int kMaxBins = 4096;              // per-segment histogram bins (global levels)
 constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one workgroup
 constexpr int kRadixBits = 11;
+constexpr i64 kLevelBlocks = 2048;          // partition-type grids of the top levels
+constexpr int kPairBins = 2048;             // bins of a level whose histogram a paired pass fuses (4 children)
 constexpr int kRadixBins = 1 << kRadixBits;
 
 struct SegState {
@@ -49,6 +53,7 @@ struct SegState {
   u32 sbstar;                 // stage 2: sub-bucket holding the median
   float p2lo, p2scale;        // stage 2: bucketing of the median bucket's value range
   u32 pad2;
+  unsigned long long pivot;   // paired levels: composite key of the median (set by k_pivot*)
 };
 
 constexpr int kBins2 = 4096;  // stage-2 sub-buckets
@@ -300,7 +305,18 @@ __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ 
   const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
   const BucketParams p = a.params[h];
   const float* key = a.src + i64(a.axis) * a.ncol + lo;
-  for (i64 e = b0 + threadIdx.x; e < b1; e += kBlock) atomicAdd(&sh[bucket_of(key[e], p, a.bins)], 1u);
+  constexpr int U = 8;
+  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
+    float k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock;
+      k[u] = e < b1 ? key[e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (e0 + i64(u) * kBlock < b1) atomicAdd(&sh[bucket_of(k[u], p, a.bins)], 1u);
+  }
   __syncthreads();
   for (int b = threadIdx.x; b < a.bins; b += kBlock) {
     const u32 v = sh[b];
@@ -533,10 +549,21 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     // read per point, served from the Infinity Cache on the second pass) and reserve once.
     u32 cnt0 = 0, cnt1 = 0;
     const float* kc = src + i64(axis) * nc + lo;
-    for (i64 e = b0 + threadIdx.x; e < b1; e += kBlock) {
-      const u32 z = zone_of(kc[e], prm, a.bins, bstar, stage2, p2, sbstar);
-      cnt0 += z == 0 ? 1u : 0u;
-      cnt1 += z == 1 ? 1u : 0u;
+    constexpr int U = 8;
+    for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
+      float k[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const i64 e = e0 + i64(u) * kBlock;
+        k[u] = e < b1 ? kc[e] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (e0 + i64(u) * kBlock >= b1) continue;
+        const u32 z = zone_of(k[u], prm, a.bins, bstar, stage2, p2, sbstar);
+        cnt0 += z == 0 ? 1u : 0u;
+        cnt1 += z == 1 ? 1u : 0u;
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -926,6 +953,427 @@ __global__ __launch_bounds__(kBlock) void k_refine_small(LevelArgs a, i64 segs) 
   }
 }
 
+// =====================================================================================
+// Paired global levels: levels l and l+1 are moved by ONE scatter pass instead of two.
+//   k_scan       keys of l and l+1 only (8 B / row): rows of level l's median bucket are
+//                compacted into their middle-zone area of dst (scratch), every other row
+//                adds its level-(l+1) key to its child's histogram (fused, LDS);
+//   k_pivot*     exact median of level l among the compacted rows (wave ranking, or a radix
+//                select over the composite key): written to the output, its composite key
+//                kept as the segment's pivot, the other middle rows complete the children's
+//                histograms, children cells set;
+//   k_select     level l+1 as usual;
+//   k_partition2 one read + one write of every row: child (level l, from the bucket or the
+//                pivot comparison) and zone inside the child (level l+1) give 6 destination
+//                zones; the level-(l+2) histograms of the 4 grandchildren are fused in;
+//   k_refine*    level l+1's middle zones as usual.
+// Traffic per two levels: 8 + 16 + 16 B / row instead of 2 x (16 + 16).
+struct PairArgs {
+  int bins1;             // level l+1 bins
+  int axis2;             // level l+2 axis
+  int bins2;             // level l+2 bins (0: l+2 is the subtree level)
+  u32* hist2n;           // level l+2 histograms [4 * segs][bins2]
+};
+
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
+  extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
+  constexpr int D = NCOL - 1;
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const int nb = a.next_bins;
+  for (int b = threadIdx.x; b < 2 * nb; b += kBlock) nh[b] = 0;
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  SegState* st = a.state + h;
+  const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const BucketParams prm = a.params[h];
+  const BucketParams cp0 = a.params[2 * h + 1], cp1 = a.params[2 * h + 2];
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  const i64 nc = a.ncol;
+  const float* kc = src + i64(a.axis) * nc + lo;
+  const float* nkc = src + i64(a.next_axis) * nc + lo;
+  const int ln = dev::lane();
+  __syncthreads();
+  constexpr int U = 8;
+  for (i64 e0 = b0; e0 < b1; e0 += kBlock * U) {
+    float k[U], nk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock + threadIdx.x;
+      k[u] = e < b1 ? kc[e] : 0.0f;
+      nk[u] = e < b1 ? nkc[e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock + threadIdx.x;
+      const u32 z = e < b1 ? zone_of(k[u], prm, a.bins, bstar, stage2, p2, sbstar) : 3u;
+      if (z == 0) atomicAdd(&nh[bucket_of(nk[u], cp0, nb)], 1u);
+      if (z == 2) atomicAdd(&nh[nb + bucket_of(nk[u], cp1, nb)], 1u);
+      const u64 m = __ballot(z == 1);
+      if (m) {  // rare: compact the median bucket's rows
+        const int leader = __ffsll((long long)m) - 1;
+        u32 base = 0;
+        if (ln == leader) base = atomicAdd(&st->cur[1], u32(__popcll(m)));
+        base = __shfl(base, leader, 64);
+        if (z == 1) {
+          const i64 q = lo + base + mbcnt(m);
+          if (i64(base + mbcnt(m)) >= n) {
+            atomicOr(a.err, 1u);
+          } else {
+#pragma unroll
+            for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + q] = src[i64(c) * nc + lo + e];
+          }
+          const u32 id = reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e];
+          const u64 ck = composite_key(k[u], id);
+          atomicMin(&st->mid_min, (unsigned long long)ck);
+          atomicMax(&st->mid_max, (unsigned long long)ck);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  u32* hn = a.hist_next + (2 * s) * nb;
+  for (int b = threadIdx.x; b < 2 * nb; b += kBlock) {
+    const u32 v = nh[b];
+    if (v) atomicAdd(&hn[b], v);
+  }
+}
+
+// Median row of a paired level found: output slot, pivot key, children cells.
+template <int NCOL>
+__device__ __forceinline__ void pivot_found(const LevelArgs& a, i64 h, i64 lo, i64 n, const float* row, u64 ck) {
+  constexpr int D = NCOL - 1;
+  const i64 mpos = lo + n / 2;
+#pragma unroll
+  for (int c = 0; c < D; ++c) a.out_pts[mpos * D + c] = row[c];
+  a.out_ids[mpos] = __float_as_uint(row[D]);
+  a.state[h].pivot = ck;
+  float split = row[0];
+#pragma unroll
+  for (int c = 1; c < D; ++c) split = c == a.axis ? row[c] : split;
+  const float* cell = a.cells + h * 2 * D;
+  float* cl_ = a.cells + (2 * h + 1) * 2 * D;
+  float* cr_ = a.cells + (2 * h + 2) * 2 * D;
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    const float clo = cell[2 * c], chi = cell[2 * c + 1];
+    cl_[2 * c] = clo;
+    cl_[2 * c + 1] = c == a.axis ? split : chi;
+    cr_[2 * c] = c == a.axis ? split : clo;
+    cr_[2 * c + 1] = chi;
+  }
+}
+
+// One wave per segment whose median bucket holds <= 64 rows.
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_pivot_small(LevelArgs a, i64 segs) {
+  constexpr int D = NCOL - 1;
+  const i64 s = i64(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  if (s >= segs) return;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  if (n <= 0) return;
+  const SegState st = a.state[h];
+  if (st.cnt_mid > 64) return;
+  const i64 lo = a.seg_lo[h];
+  const int zc = int(st.cnt_mid);
+  const int t = int(n / 2 - i64(st.cnt_less));
+  const i64 zlo = lo + st.cnt_less;
+  const i64 nc = a.ncol;
+  const int l = dev::lane();
+  const bool valid = l < zc;
+  float row[NCOL];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) row[c] = valid ? a.dst[i64(c) * nc + zlo + l] : 0.0f;
+  float key = row[0], nkey = row[0];
+#pragma unroll
+  for (int c = 1; c < D; ++c) {
+    key = c == a.axis ? row[c] : key;
+    nkey = c == a.next_axis ? row[c] : nkey;
+  }
+  const u64 k = valid ? composite_key(key, __float_as_uint(row[D])) : ~0ull;
+  u32 rank = 0;
+  for (int j = 0; j < zc; ++j) rank += dev::shfl_u64(k, j) < k ? 1u : 0u;
+  if (!valid) return;
+  if (int(rank) == t) pivot_found<NCOL>(a, h, lo, n, row, k);
+  else if (a.next_bins > 0) add_next_hist(a, s, h, int(rank) < t ? 0 : 1, nkey);
+}
+
+// One workgroup per segment with a larger median bucket: radix select (11-bit digits) of
+// the rank-t composite key, rows read in place (no staging).
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_pivot(LevelArgs a) {
+  constexpr int D = NCOL - 1;
+  __shared__ u32 rh[kRadixBins];
+  __shared__ u32 sh4[4];
+  __shared__ u32 info[3];
+  const i64 s = blockIdx.x;
+  const i64 h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  if (n <= 0) return;
+  const SegState st = a.state[h];
+  if (st.cnt_mid <= 64) return;
+  const i64 lo = a.seg_lo[h];
+  const i64 nc = a.ncol;
+  const float* __restrict__ dst = a.dst;
+  const i64 zlo = lo + st.cnt_less, zc = st.cnt_mid;
+  u64 t = u64(n / 2 - i64(st.cnt_less));
+  auto ckey = [&](i64 p) -> u64 {
+    float key = dst[p];
+#pragma unroll
+    for (int c = 1; c < D; ++c) key = c == a.axis ? dst[i64(c) * nc + p] : key;
+    return composite_key(key, reinterpret_cast<const u32*>(dst)[i64(D) * nc + p]);
+  };
+  const u64 diff = u64(st.mid_min) ^ u64(st.mid_max);
+  int hb = diff ? 63 - __builtin_clzll(diff) : -1;
+  u64 prefix = hb >= 63 ? 0ull : (u64(st.mid_min) & ~((2ull << hb) - 1ull));
+  if (hb < 0) prefix = u64(st.mid_min);
+  while (hb >= 0) {
+    const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
+    const u64 himask = hb >= 63 ? 0ull : ~((2ull << hb) - 1ull);
+    for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
+    __syncthreads();
+    for (i64 e = threadIdx.x; e < zc; e += kBlock) {
+      const u64 key = ckey(zlo + e);
+      if ((key & himask) == prefix) atomicAdd(&rh[u32(key >> shift) & (kRadixBins - 1)], 1u);
+    }
+    __syncthreads();
+    const int per = kRadixBins / kBlock;
+    u32 sum = 0;
+    for (int b = 0; b < per; ++b) sum += rh[threadIdx.x * per + b];
+    u32 total;
+    const u32 excl = block_excl_scan(sum, sh4, &total);
+    if (t >= excl && t < u64(excl) + sum) {
+      u32 c = excl;
+      for (int b = 0; b < per; ++b) {
+        const u32 v = rh[threadIdx.x * per + b];
+        if (t < u64(c) + v) {
+          info[0] = u32(threadIdx.x * per + b);
+          info[1] = c;
+          break;
+        }
+        c += v;
+      }
+    }
+    __syncthreads();
+    const u32 digit = info[0];
+    t -= info[1];
+    const int width = hb - shift + 1;
+    prefix |= u64(digit & ((1u << width) - 1u)) << shift;
+    hb = shift - 1;
+    __syncthreads();
+  }
+  const u64 pivot = prefix;
+  for (i64 e = threadIdx.x; e < zc; e += kBlock) {
+    const i64 p = zlo + e;
+    float row[NCOL];
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) row[c] = dst[i64(c) * nc + p];
+    float key = row[0], nkey = row[0];
+#pragma unroll
+    for (int c = 1; c < D; ++c) {
+      key = c == a.axis ? row[c] : key;
+      nkey = c == a.next_axis ? row[c] : nkey;
+    }
+    const u64 k = composite_key(key, __float_as_uint(row[D]));
+    if (k == pivot) pivot_found<NCOL>(a, h, lo, n, row, k);
+    else if (a.next_bins > 0) add_next_hist(a, s, h, k < pivot ? 0 : 1, nkey);
+  }
+}
+
+// Pass B of a pair: a = level l (src -> dst), children states/params are level l+1's.
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
+  extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
+  __shared__ u32 gcnt[6][64];
+  __shared__ u32 bcur[6];
+  constexpr int D = NCOL - 1;
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const int nb2 = pa.bins2;
+  const bool fuse = nb2 > 0;
+  if (fuse)
+    for (int b = threadIdx.x; b < 4 * nb2; b += kBlock) nh[b] = 0;
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const SegState* st = a.state + h;
+  const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
+  const u64 pivot = st->pivot;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const BucketParams prm = a.params[h];
+  // children (level l+1)
+  SegState* cst[2] = {a.state + 2 * h + 1, a.state + 2 * h + 2};
+  u32 cbs[2], cs2[2], csb[2];
+  BucketParams cpr[2], cp2[2], gpr[4];
+  i64 clo[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    cbs[c] = cst[c]->bstar;
+    cs2[c] = cst[c]->stage2;
+    csb[c] = cst[c]->sbstar;
+    cp2[c].lo = cst[c]->p2lo;
+    cp2[c].scale = cst[c]->p2scale;
+    cpr[c] = a.params[2 * h + 1 + c];
+    clo[c] = a.seg_lo[2 * h + 1 + c];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) gpr[2 * c + g] = fuse ? a.params[2 * (2 * h + 1 + c) + 1 + g] : BucketParams{0.f, 0.f};
+  }
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  const i64 nc = a.ncol;
+  const int axis = a.axis, ax1 = a.next_axis, ax2 = pa.axis2;
+  const int w = threadIdx.x / 64;
+  const int ln = dev::lane();
+  auto classify = [&](float k0, float k1, u32 id, bool valid) -> u32 {  // 6 * 0 + q, or 7 (none)
+    if (!valid) return 7u;
+    const u32 z0 = zone_of(k0, prm, a.bins, bstar, stage2, p2, sbstar);
+    u32 c = z0 == 0 ? 0u : 1u;
+    if (z0 == 1) {
+      const u64 ck = composite_key(k0, id);
+      if (ck == pivot) return 7u;
+      c = ck < pivot ? 0u : 1u;
+    }
+    const u32 z1 = c == 0 ? zone_of(k1, cpr[0], pa.bins1, cbs[0], cs2[0], cp2[0], csb[0])
+                          : zone_of(k1, cpr[1], pa.bins1, cbs[1], cs2[1], cp2[1], csb[1]);
+    return 3 * c + z1;
+  };
+  if (a.block_reserve) {
+    u32 cnt[6] = {0, 0, 0, 0, 0, 0};
+    const float* kc = src + i64(axis) * nc + lo;
+    const float* k1c = src + i64(ax1) * nc + lo;
+    const u32* idc = reinterpret_cast<const u32*>(src) + i64(D) * nc + lo;
+    constexpr int U = 8;
+    for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
+      float k0[U], k1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const i64 e = e0 + i64(u) * kBlock;
+        k0[u] = e < b1 ? kc[e] : 0.0f;
+        k1[u] = e < b1 ? k1c[e] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const i64 e = e0 + i64(u) * kBlock;
+        if (e >= b1) continue;
+        const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
+        const u32 q = classify(k0[u], k1[u], z0 == 1 ? idc[e] : 0u, true);
+#pragma unroll
+        for (int z = 0; z < 6; ++z) cnt[z] += q == u32(z) ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int z = 0; z < 6; ++z) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt[z] += __shfl_xor(cnt[z], o, 64);
+      if (ln == 0) gcnt[z][w] = cnt[z];
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      u32 tz = 0;
+      for (int k = 0; k < kBlock / 64; ++k) tz += gcnt[threadIdx.x][k];
+      const int c = threadIdx.x / 3, z = threadIdx.x % 3;
+      bcur[threadIdx.x] = tz ? atomicAdd(&cst[c]->cur[z], tz) : 0u;
+    }
+  }
+  __syncthreads();
+
+  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+    float row[kItems][NCOL];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const i64 e = c0 + i * kBlock + threadIdx.x;
+      const i64 p = lo + (e < b1 ? e : b0);
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) row[i][c] = src[i64(c) * nc + p];
+    }
+    u32 zone_pre[kItems];  // (q << 16) | rank-in-wave
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const i64 e = c0 + i * kBlock + threadIdx.x;
+      float k0 = row[i][0], k1 = row[i][0], k2 = row[i][0];
+#pragma unroll
+      for (int c = 1; c < D; ++c) {
+        k0 = c == axis ? row[i][c] : k0;
+        k1 = c == ax1 ? row[i][c] : k1;
+        k2 = c == ax2 ? row[i][c] : k2;
+      }
+      const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), e < b1);
+      u32 my = 0;
+#pragma unroll
+      for (int z = 0; z < 6; ++z) {
+        const u64 m = __ballot(q == u32(z));
+        if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
+        if (q == u32(z)) my = mbcnt(m);
+      }
+      zone_pre[i] = (q << 16) | my;
+      if (q < 6) {
+        const u32 c = q / 3, z1 = q % 3;
+        if (z1 == 1) {  // level l+1 middle zone: track its composite key range
+          const u64 ck = composite_key(k1, __float_as_uint(row[i][D]));
+          atomicMin(&cst[c]->mid_min, (unsigned long long)ck);
+          atomicMax(&cst[c]->mid_max, (unsigned long long)ck);
+        } else if (fuse) {
+          const u32 g = 2 * c + (z1 == 2 ? 1u : 0u);
+          atomicAdd(&nh[g * nb2 + bucket_of(k2, gpr[g], nb2)], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    for (int z = w; z < 6; z += kBlock / 64) {  // wave w scans zones w, w+4
+      const u32 v = gcnt[z][ln];
+      const u32 incl = dev::wave_incl_scan(v);
+      const u32 tot = __shfl(incl, 63, 64);
+      u32 base = 0;
+      if (a.block_reserve) {
+        base = bcur[z];
+        if (ln == 0) bcur[z] = base + tot;
+      } else {
+        if (ln == 0 && tot) base = atomicAdd(&cst[z / 3]->cur[z % 3], tot);
+        base = __shfl(base, 0, 64);
+      }
+      gcnt[z][ln] = base + incl - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const u32 q = zone_pre[i] >> 16;
+      i64 dest = -1;
+      if (q < 6) {
+        const u32 c = q / 3;
+        const u32 off = gcnt[q][i * 4 + w] + (zone_pre[i] & 0xffffu);
+        const i64 cn = c == 0 ? n / 2 : n - n / 2 - 1;
+        if (i64(off) >= cn) {
+          atomicOr(a.err, 1u);
+        } else {
+          dest = (c == 0 ? clo[0] : clo[1]) + off;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c)
+        if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
+    }
+    __syncthreads();
+  }
+  if (fuse) {
+    u32* hn = pa.hist2n + (4 * s) * nb2;
+    for (int b = threadIdx.x; b < 4 * nb2; b += kBlock) {
+      const u32 v = nh[b];
+      if (v) atomicAdd(&hn[b], v);
+    }
+  }
+}
+
 int pow2_floor(i64 v) {
   int p = 1;
   while (i64(p) * 2 <= v) p *= 2;
@@ -956,8 +1404,9 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.nmax = n_ >> l;
     lp.bins = global_bins(lp.nmax);
     lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
-    const i64 range = std::max<i64>(kChunk * 16, i64(kChunk));
-    lp.bps = int(std::max<i64>(1, (lp.nmax + range - 1) / range));
+    // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
+    // 256 CUs) while segments are few; one block per segment below that.
+    lp.bps = int(std::max<i64>(1, kLevelBlocks / lp.segs));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
     lp.stage2 = lp.nmax / lp.bins > kRefineCap;
@@ -965,6 +1414,24 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     levels_.push_back(lp);
     max_bins_ = std::max(max_bins_, lp.bins);
     max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
+  }
+  // Pair level l with l+1 (one fused scatter pass) when rows fit the register path and
+  // l+1 needs no second-stage histogram.
+  const char* pe = std::getenv("PKD_PAIR");
+  const bool pairs = dim <= 4 && !(pe && std::string(pe) == "0");
+  for (int l = 0; pairs && l + 1 < lg_; ++l) {
+    if (levels_[size_t(l + 1)].stage2) continue;
+    levels_[size_t(l)].pair = true;
+    if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
+      LevelPlan& g = levels_[size_t(l + 2)];
+      g.bins = std::min(g.bins, kPairBins);
+      levels_[size_t(l + 1)].next_bins = g.bins;
+    }
+    ++l;  // l+1 is the second level of the pair
+  }
+  for (size_t l = 0; l < levels_.size(); ++l) {
+    max_bins_ = std::max(max_bins_, levels_[l].bins);
+    max_hist_ = std::max<i64>(max_hist_, levels_[l].segs * levels_[l].bins);
   }
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -995,7 +1462,8 @@ std::string GpuBuilder::describe() const {
      << ", workspace=" << ws_bytes_ << "B)";
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
-       << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "");
+       << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
+       << (lp.pair ? " pair" : "");
   return os.str();
 }
 
@@ -1092,7 +1560,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
 
   float* src = colsA;
   float* dst = colsB;
-  for (int l = 0; l < lg_; ++l) {
+  auto level_args = [&](int l) {
     const LevelPlan& lp = levels_[size_t(l)];
     LevelArgs a;
     a.src = src;
@@ -1116,12 +1584,37 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.out_ids = out_ids;
     a.err = err;
     a.block_reserve = (lp.segs <= 8 && lp.bps > 4) ? 1 : 0;  // only where cursor contention is high
+    a.small_done = 0;
+    a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
+    return a;
+  };
+  auto refine = [&](LevelArgs& a, i64 segs) {
+    a.small_done = dim_ <= 8 ? 1 : 0;
+    if (a.small_done) {
+      const int g = int((segs + 3) / 4);
+      switch (dim_) {
+        case 1: k_refine_small<2><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 2: k_refine_small<3><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 3: k_refine_small<4><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 4: k_refine_small<5><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 5: k_refine_small<6><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 6: k_refine_small<7><<<g, kBlock, 0, stream>>>(a, segs); break;
+        case 7: k_refine_small<8><<<g, kBlock, 0, stream>>>(a, segs); break;
+        default: k_refine_small<9><<<g, kBlock, 0, stream>>>(a, segs); break;
+      }
+      PKD_LAUNCH_CHECK();
+    }
+    k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
+    PKD_LAUNCH_CHECK();
+  };
+  for (int l = 0; l < lg_;) {
+    const LevelPlan& lp = levels_[size_t(l)];
+    LevelArgs a = level_args(l);
     if (l == 0) {
       PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
       k_hist<<<int(lp.segs * lp.bps), kBlock, size_t(lp.bins) * 4, stream>>>(a, hist[0]);
       PKD_LAUNCH_CHECK();
     }
-    a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
     k_select<<<int(lp.segs), kBlock, 0, stream>>>(a);
     PKD_LAUNCH_CHECK();
     if (lp.stage2) {
@@ -1131,8 +1624,47 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       k_select2<<<int(lp.segs), kBlock, 0, stream>>>(a);
       PKD_LAUNCH_CHECK();
     }
-    const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
     const int grid = int(lp.segs * lp.bps);
+    if (lp.pair) {
+      const LevelPlan& lq = levels_[size_t(l + 1)];
+      const size_t lds_a = size_t(2 * lp.next_bins) * 4;
+      const int gs = int((lp.segs + 3) / 4);
+      switch (dim_) {
+        case 1: k_scan<2><<<grid, kBlock, lds_a, stream>>>(a); break;
+        case 2: k_scan<3><<<grid, kBlock, lds_a, stream>>>(a); break;
+        case 3: k_scan<4><<<grid, kBlock, lds_a, stream>>>(a); break;
+        default: k_scan<5><<<grid, kBlock, lds_a, stream>>>(a); break;
+      }
+      PKD_LAUNCH_CHECK();
+      switch (dim_) {
+        case 1: k_pivot_small<2><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<2><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
+        case 2: k_pivot_small<3><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<3><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
+        case 3: k_pivot_small<4><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<4><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
+        default: k_pivot_small<5><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<5><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
+      }
+      PKD_LAUNCH_CHECK();
+      LevelArgs b = level_args(l + 1);
+      k_select<<<int(lq.segs), kBlock, 0, stream>>>(b);
+      PKD_LAUNCH_CHECK();
+      PairArgs pa;
+      pa.bins1 = lq.bins;
+      pa.axis2 = (opt_.depth0 + l + 2) % dim_;
+      pa.bins2 = lq.next_bins;
+      pa.hist2n = hist[l & 1];
+      const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
+      switch (dim_) {
+        case 1: k_partition2<2><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+        case 2: k_partition2<3><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+        case 3: k_partition2<4><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+        default: k_partition2<5><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+      }
+      PKD_LAUNCH_CHECK();
+      refine(b, lq.segs);
+      std::swap(src, dst);
+      l += 2;
+      continue;
+    }
+    const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
     switch (dim_) {
       case 1: k_partition<2><<<grid, kBlock, lds, stream>>>(a); break;
       case 2: k_partition<3><<<grid, kBlock, lds, stream>>>(a); break;
@@ -1141,24 +1673,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       default: k_partition<0><<<grid, kBlock, lds, stream>>>(a); break;
     }
     PKD_LAUNCH_CHECK();
-    a.small_done = dim_ <= 8 ? 1 : 0;
-    if (a.small_done) {
-      const int g = int((lp.segs + 3) / 4);
-      switch (dim_) {
-        case 1: k_refine_small<2><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 2: k_refine_small<3><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 3: k_refine_small<4><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 4: k_refine_small<5><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 5: k_refine_small<6><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 6: k_refine_small<7><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        case 7: k_refine_small<8><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-        default: k_refine_small<9><<<g, kBlock, 0, stream>>>(a, lp.segs); break;
-      }
-      PKD_LAUNCH_CHECK();
-    }
-    k_refine<kRefineCap><<<int(lp.segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
-    PKD_LAUNCH_CHECK();
+    refine(a, lp.segs);
     std::swap(src, dst);
+    l += 1;
   }
   const i64 heap0 = (i64(1) << lg_) - 1;
   launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,

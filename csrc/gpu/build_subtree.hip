@@ -56,7 +56,7 @@ struct SubArgs {
   float* out_pts;
   u32* out_ids;
   u32* err;
-  unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][8] s_memtime
+  unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][kStampSlots] s_memtime
 };
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
@@ -112,8 +112,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+constexpr int kStampSlots = 32;
+constexpr int kStampBlocks = 4096;
+// slot 0 start, 1 rows loaded, 2 + t after level t (rank kernel), 30 before the store, 31 end
 __device__ __forceinline__ void stamp(const SubArgs& a, int i) {
-  if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memtime();
+  if (a.stamps && threadIdx.x == 0 && blockIdx.x < kStampBlocks)
+    a.stamps[blockIdx.x * kStampSlots + i] = __builtin_amdgcn_s_memtime();
 }
 
 __device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
@@ -585,7 +589,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
     }
   }
   __syncthreads();
-  stamp(a, 3);
+  stamp(a, 30);
   // in-order rows out, AoS, coalesced
   const i64 total = i64(n) * dim;
   float* outp = a.out_pts + glo * dim;
@@ -596,9 +600,308 @@ __global__ __launch_bounds__(THREADS) void k_subtree(SubArgs a) {
   }
   for (int k = tid; k < n; k += THREADS) a.out_ids[glo + k] = idrow[slot[k] & 0xffffu];
   __syncthreads();
-  stamp(a, 4);
+  stamp(a, 31);
   (void)W;
 }
+
+// =====================================================================================
+// Rank-based subtree kernel (default). Points never move inside LDS: every level only
+// computes each live point's exact rank inside its current sub-segment on the level's axis,
+// which decides left / median / right at once.
+//   * The first `dim` levels (first use of each axis) rank with a per-sub-segment linear
+//     bucket histogram (range from the sub-segment's LDS min/max), a block scan, a
+//     bucket-ordered index list and exact (key, id) comparisons inside each bucket.
+//   * Every rank is stored, relative to the child it sends the point to, as a 16-bit
+//     "compressed rank" of that axis. When the axis comes round again d levels later the
+//     ranks of the points of any sub-segment are distinct small integers in the (key, id)
+//     order, so the rank inside the sub-segment is a prefix popcount over one LDS bitmap per
+//     sub-segment: one ds_or, one scan of word popcounts, one read per point.
+// The slot of a point is final when its rank is the median rank; the slot -> point table is
+// written then and streamed out at the end with coalesced stores.
+namespace rk {
+
+constexpr int kSmallSeg = 16;  // sub-segments up to this size rank by comparison in one bucket
+
+__host__ __device__ inline int bitlen(u32 v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+__device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32 - __clz(v - 1)); }
+
+// Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
+__host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
+
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+4 | aux nm | fin nm
+size_t lds_words(int dim, int nm) {
+  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 4 + 2 * size_t(nm);
+}
+
+// In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
+template <int THREADS>
+__device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
+  const int tid = threadIdx.x, w = tid / 64;
+  const int C = (m + THREADS - 1) / THREADS;
+  const int b0 = min(m, tid * C), b1 = min(m, b0 + C);
+  u32 s = 0;
+  for (int b = b0; b < b1; ++b) s += v[b];
+  const u32 incl = dev::wave_incl_scan(s);
+  if (dev::lane() == 63) wsum[w] = incl;
+  __syncthreads();
+  u32 run = incl - s;
+  for (int q = 0; q < w; ++q) run += wsum[q];
+  for (int b = b0; b < b1; ++b) {
+    const u32 x = v[b];
+    v[b] = run;
+    run += x;
+  }
+  if (tid == THREADS - 1) v[m] = run;
+}
+
+}  // namespace rk
+
+template <int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
+  extern __shared__ __align__(16) u32 smem[];
+  __shared__ u32 wsum[THREADS / 64];
+  constexpr int NM = ITEMS * THREADS;
+  const int dim = a.dim;
+  const i64 h = a.heap0 + blockIdx.x;
+  const int n = int(a.seg_n[h]);
+  if (n <= 0) return;
+  const i64 glo = a.seg_lo[h];
+  const int tid = threadIdx.x;
+  const int lsub = rk::bitlen(u32(n));  // levels of the implicit subtree of n points
+  const int kept_layout = rk::kept_axes(dim, NM);
+  const bool keep = dim < lsub;
+  float* rows = reinterpret_cast<float*>(smem);
+  const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
+  u16* crank = reinterpret_cast<u16*>(smem + size_t(dim + 1) * NM);
+  u32* work = smem + size_t(dim + 1) * NM + (size_t(kept_layout) * NM + 1) / 2;
+  u32* aux = work + NM + 4;
+  u32* fin = aux + NM;
+  stamp(a, 0);
+
+  for (int c = 0; c <= dim; ++c) {
+    const float* col = a.cols + i64(c) * a.ncol + glo;
+    float v[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int k = tid + i * THREADS;
+      v[i] = k < n ? col[k] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int k = tid + i * THREADS;
+      if (k < n) rows[c * NM + k] = v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int k = tid + i * THREADS;
+    if (k < n) fin[k] = 0xffffffffu;
+  }
+  u32 lo[ITEMS], nn[ITEMS], sg[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    lo[i] = 0;
+    sg[i] = 0;
+    nn[i] = (tid + i * THREADS) < n ? u32(n) : 0u;
+  }
+  __syncthreads();
+  stamp(a, 1);
+
+  for (int t = 0; t < lsub; ++t) {
+    const int axis = (a.depth_base + t) % dim;
+    const float* kcol = rows + axis * NM;
+    u16* cr = crank + size_t(axis) * NM;
+    const int S = 1 << t;
+    int Wt = 0;
+    if (keep && t >= dim) {
+      const u32 wbits = u32(n) >> (t - dim + 1);
+      const u32 words = rk::pow2_ceil((wbits + 31) / 32);
+      if (words <= 64 && u32(S) * words <= u32(NM)) Wt = int(words);
+    }
+    u32 rank[ITEMS];
+    if (Wt > 0) {
+      // ---- compressed ranks: one bitmap of Wt words per sub-segment ----
+      const int nw = S * Wt;
+      for (int w = tid; w < nw; w += THREADS) work[w] = 0;
+      __syncthreads();
+      u32 c[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        c[i] = 0;
+        if (nn[i]) {
+          c[i] = cr[tid + i * THREADS];
+          atomicOr(&work[sg[i] * Wt + (c[i] >> 5)], 1u << (c[i] & 31));
+        }
+      }
+      __syncthreads();
+      if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
+        const int g = dev::lane() & (Wt - 1);
+        for (int w0 = 0; w0 < nw; w0 += THREADS) {
+          const int w = w0 + tid;
+          const u32 v = w < nw ? u32(__popc(work[w])) : 0u;
+          u32 incl = v;
+          for (int o = 1; o < Wt; o <<= 1) {
+            const u32 tt = __shfl_up(incl, o, 64);
+            if (g >= o) incl += tt;
+          }
+          if (w < nw) aux[w] = incl - v;
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        rank[i] = 0;
+        if (nn[i]) {
+          const u32 wi = sg[i] * Wt + (c[i] >> 5);
+          rank[i] = (Wt > 1 ? aux[wi] : 0u) + u32(__popc(work[wi] & ((1u << (c[i] & 31)) - 1u)));
+        }
+      }
+    } else {
+      // ---- exact ranks from bucket histograms (first use of the axis) ----
+      const int maxsize = n >> t;
+      const int B = maxsize > rk::kSmallSeg ? max(2, pow2_floor_dev(maxsize / 2)) : 1;
+      const int nb = S * B;
+      u16* tmp = reinterpret_cast<u16*>(aux);
+      u32* mm = aux + NM / 2;
+      for (int w = tid; w <= nb; w += THREADS) work[w] = 0;
+      if (B > 1)
+        for (int q = tid; q < S; q += THREADS) {
+          mm[2 * q] = 0xffffffffu;
+          mm[2 * q + 1] = 0u;
+        }
+      __syncthreads();
+      u32 ok[ITEMS];
+      float kf[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        kf[i] = nn[i] ? kcol[tid + i * THREADS] : 0.0f;
+        ok[i] = orderable(kf[i]);
+      }
+      if (B > 1) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (nn[i]) {
+            atomicMin(&mm[2 * sg[i]], ok[i]);
+            atomicMax(&mm[2 * sg[i] + 1], ok[i]);
+          }
+        __syncthreads();
+      }
+      u32 bk[ITEMS], wi[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        bk[i] = 0;
+        wi[i] = 0;
+        if (nn[i]) {
+          u32 b = 0;
+          if (B > 1) {
+            const BucketParams pr = make_params(from_orderable(mm[2 * sg[i]]), from_orderable(mm[2 * sg[i] + 1]), B);
+            b = bucket_of(kf[i], pr, B);
+          }
+          bk[i] = sg[i] * B + b;
+          wi[i] = atomicAdd(&work[bk[i]], 1u);
+        }
+      }
+      __syncthreads();
+      rk::block_excl_scan<THREADS>(work, nb, wsum);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i)
+        if (nn[i]) tmp[work[bk[i]] + wi[i]] = u16(tid + i * THREADS);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        rank[i] = 0;
+        if (nn[i]) {
+          const u32 st = work[bk[i]], en = work[bk[i] + 1], base = work[sg[i] * B];
+          const u32 myid = idrow[tid + i * THREADS];
+          u32 r = st - base;
+          for (u32 k = st; k < en && k < st + u32(NM); ++k) {
+            const u32 q = tmp[k];
+            const u32 qk = orderable(kcol[q]);
+            r += (qk < ok[i] || (qk == ok[i] && idrow[q] < myid)) ? 1u : 0u;
+          }
+          rank[i] = r;
+        }
+      }
+    }
+    // ---- median / left / right ----
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      if (!nn[i]) continue;
+      const u32 mid = nn[i] / 2, r = rank[i];
+      if (r >= nn[i]) {
+        report(a.err, 0x400u, u32(t), r);
+        nn[i] = 0;
+        continue;
+      }
+      u32 nc;
+      if (r == mid) {
+        fin[lo[i] + mid] = u32(tid + i * THREADS);
+        nn[i] = 0;
+        continue;
+      } else if (r < mid) {
+        sg[i] = 2 * sg[i];
+        nn[i] = mid;
+        nc = r;
+      } else {
+        sg[i] = 2 * sg[i] + 1;
+        lo[i] += mid + 1;
+        nn[i] -= mid + 1;
+        nc = r - mid - 1;
+      }
+      if (keep) cr[tid + i * THREADS] = u16(nc);
+    }
+    __syncthreads();
+    if (t < 28) stamp(a, 2 + t);
+  }
+  stamp(a, 30);
+  // in-order rows out, AoS, coalesced
+  const i64 total = i64(n) * dim;
+  float* outp = a.out_pts + glo * dim;
+  for (i64 f = tid; f < total; f += THREADS) {
+    const int k = int(f / dim);
+    const int c = int(f - i64(k) * dim);
+    const u32 p = fin[k];
+    outp[f] = rows[c * NM + (p < u32(NM) ? p : 0u)];
+  }
+  for (int k = tid; k < n; k += THREADS) {
+    const u32 p = fin[k];
+    if (p >= u32(NM)) report(a.err, 0x800u, u32(k), p);
+    a.out_ids[glo + k] = idrow[p < u32(NM) ? p : 0u];
+  }
+  __syncthreads();
+  stamp(a, 31);
+}
+
+template <int ITEMS, int THREADS>
+void launch_rank_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
+  static bool attr_set = false;
+  const size_t lds = 4 * rk::lds_words(a.dim, ITEMS * THREADS);
+  if (!attr_set) {
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
+    attr_set = true;
+  }
+  k_subtree_rank<ITEMS, THREADS><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+  PKD_LAUNCH_CHECK();
+}
+
+bool use_hist_impl() {
+  static const bool v = [] {
+    const char* e = std::getenv("PKD_SUBTREE_IMPL");
+    return e && std::string(e) == "hist";
+  }();
+  return v;
+}
+
+size_t impl_lds_bytes(int dim, int nm) { return use_hist_impl() ? subtree_lds_bytes(dim, nm) : 4 * rk::lds_words(dim, nm); }
 
 template <int ITEMS, int THREADS>
 void launch_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
@@ -623,20 +926,34 @@ unsigned long long*& subtree_stamp_buffer() {
 std::string subtree_stamp_report() {
   unsigned long long* d = subtree_stamp_buffer();
   if (!d) return "stamps disabled (set PKD_SUBTREE_STAMPS=1)";
-  std::vector<unsigned long long> h(4096 * 8);
+  std::vector<unsigned long long> h(size_t(kStampBlocks) * kStampSlots);
   PKD_HIP_CHECK(hipDeviceSynchronize());
   PKD_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-  double acc[4] = {0, 0, 0, 0};
-  int cnt = 0;
-  for (int b = 0; b < 4096; ++b) {
-    const unsigned long long* s = &h[size_t(b) * 8];
-    if (!s[0] || !s[4]) continue;
-    for (int i = 0; i < 4; ++i) acc[i] += double(s[i + 1] - s[i]);
-    ++cnt;
+  // mean cycles between consecutive recorded slots, over blocks that recorded start and end
+  double acc[kStampSlots] = {};
+  int cnt[kStampSlots] = {};
+  for (int b = 0; b < kStampBlocks; ++b) {
+    const unsigned long long* s = &h[size_t(b) * kStampSlots];
+    if (!s[0] || !s[31]) continue;
+    int prev = 0;
+    for (int i = 1; i < kStampSlots; ++i) {
+      if (!s[i]) continue;
+      acc[i] += double(s[i] - s[prev]);
+      ++cnt[i];
+      prev = i;
+    }
   }
   std::ostringstream os;
-  os << "subtree stamps over " << cnt << " blocks (mean cycles): load " << acc[0] / cnt << ", block-phase "
-     << acc[1] / cnt << ", wave-phase " << acc[2] / cnt << ", store " << acc[3] / cnt;
+  os << "subtree stamps (mean cycles since the previous mark):";
+  for (int i = 1; i < kStampSlots; ++i) {
+    if (!cnt[i]) continue;
+    os << " ";
+    if (i == 1) os << "load";
+    else if (i == 30) os << "levels-end";
+    else if (i == 31) os << "store";
+    else os << "L" << (i - 2);
+    os << "=" << long(acc[i] / cnt[i]);
+  }
   return os.str();
 }
 
@@ -644,15 +961,15 @@ int subtree_capacity(int dim) {
   // Prefer two workgroups per CU (LDS <= ~78 KiB) so one block's barriers hide behind the
   // other's work; fall back to smaller capacities for high dimensions.
   for (int nm = 2048; nm >= 64; nm /= 2)
-    if (subtree_lds_bytes(dim, nm) <= kLdsMax / 2) return nm;
+    if (impl_lds_bytes(dim, nm) <= kLdsMax / 2) return nm;
   for (int nm = 64; nm >= 32; nm /= 2)
-    if (subtree_lds_bytes(dim, nm) <= kLdsMax) return nm;
+    if (impl_lds_bytes(dim, nm) <= kLdsMax) return nm;
   throw std::invalid_argument("pkdtree: dimension too large for the LDS subtree kernel");
 }
 
 int subtree_capacity_max(int dim) {
   for (int nm = 4096; nm >= 32; nm /= 2)
-    if (subtree_lds_bytes(dim, nm) <= kLdsMax) return nm;
+    if (impl_lds_bytes(dim, nm) <= kLdsMax) return nm;
   throw std::invalid_argument("pkdtree: dimension too large for the LDS subtree kernel");
 }
 
@@ -662,11 +979,21 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
   if (segs <= 0) return;
   static unsigned long long* stamps = nullptr;
   if (std::getenv("PKD_SUBTREE_STAMPS") && !stamps) {
-    PKD_HIP_CHECK(hipMalloc(&stamps, 4096 * 8 * sizeof(unsigned long long)));
-    PKD_HIP_CHECK(hipMemset(stamps, 0, 4096 * 8 * sizeof(unsigned long long)));
+    PKD_HIP_CHECK(hipMalloc(&stamps, size_t(kStampBlocks) * kStampSlots * sizeof(unsigned long long)));
+    PKD_HIP_CHECK(hipMemset(stamps, 0, size_t(kStampBlocks) * kStampSlots * sizeof(unsigned long long)));
   }
   subtree_stamp_buffer() = stamps;
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps};
+  if (!use_hist_impl()) {
+    if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);
+    else if (nmax > 1024) launch_rank_cfg<4, 512>(a, segs, stream);
+    else if (nmax > 512) launch_rank_cfg<4, 256>(a, segs, stream);
+    else if (nmax > 256) launch_rank_cfg<2, 256>(a, segs, stream);
+    else if (nmax > 128) launch_rank_cfg<1, 256>(a, segs, stream);
+    else if (nmax > 64) launch_rank_cfg<1, 128>(a, segs, stream);
+    else launch_rank_cfg<1, 64>(a, segs, stream);
+    return;
+  }
   if (nmax > 2048) launch_cfg<4, 1024>(a, segs, stream);
   else if (nmax > 1024) launch_cfg<4, 512>(a, segs, stream);
   else if (nmax > 512) launch_cfg<4, 256>(a, segs, stream);

@@ -26,6 +26,7 @@
 
 namespace pkdtree {
 
+using u16 = std::uint16_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 using i64 = int64_t;

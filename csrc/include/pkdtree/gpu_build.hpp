@@ -37,6 +37,7 @@ struct LevelPlan {
   int bps;          // partition blocks per segment
   int axis;         // split axis at this level
   bool stage2 = false;  // median bucket split by a second (key-only) histogram pass
+  bool pair = false;    // this level and the next are moved by ONE fused partition pass
 };
 
 class GpuBuilder {

@@ -12,6 +12,8 @@ one distributed tree (parallel/global_tree.py). Only rank 0 prints.
 from __future__ import annotations
 
 import argparse
+import contextlib
+import ctypes
 import json
 import os
 import sys
@@ -19,6 +21,23 @@ import time
 
 import numpy as np
 import torch
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Point fd 1 at stderr (C and C++ stdio included) for the duration of the block."""
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def main(argv=None) -> int:
@@ -30,6 +49,10 @@ def main(argv=None) -> int:
     ap.add_argument("--queries", type=int, default=10)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--metrics-json", action="store_true")
+    ap.add_argument("--save", default=None, help="write the built tree (PKDTREE file); forest: one file per rank "
+                    "(<path>.rank<r>), global: the assembled tree from rank 0")
+    ap.add_argument("--leaf-threshold", type=int, default=0,
+                    help="largest segment finished by the LDS subtree kernel (0 = auto from dim)")
     ap.add_argument("positional", nargs="*")
     a = ap.parse_args(argv)
     tick = time.perf_counter()
@@ -45,7 +68,9 @@ def main(argv=None) -> int:
 
     from .parallel import comm
     if world > 1:
-        comm.init(backend="nccl" if device.type == "cuda" else "gloo", device=device)
+        # gloo prints "[Gloo] Rank r is connected ..." on stdout; stdout belongs to the protocol
+        with _stdout_to_stderr():
+            comm.init(backend="nccl" if device.type == "cuda" else "gloo", device=device)
     from .utils import protocol
     debug = a.debug or bool(a.positional) or os.environ.get("KDTREE_DEBUG", "0") not in ("", "0")
     cfg = [0, 0, 0]
@@ -72,19 +97,27 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     t_build = time.perf_counter()
     if decomp == "single":
-        tree = pk.KDTree.build(x, id_base=1, mode=a.mode)
+        tree = pk.KDTree.build(x, id_base=1, mode=a.mode, subtree_max=a.leaf_threshold)
         from .parallel.global_tree import _local_packed
         packed = _local_packed(tree, q, a.query)
+        if a.save:
+            tree.save(a.save)
     elif decomp == "forest":
         from .parallel.forest import ForestTree
         f = ForestTree.build(x, first, n, id_base=1, mode=a.mode)
         packed = f.query_packed(q, a.query)
+        if a.save:
+            f.local.save(f"{a.save}.rank{rank}")
     else:
         if a.mode != "exact":
             raise SystemExit("--decomp global builds exact trees only")
         from .parallel.global_tree import GlobalTreeBuilder
         t = GlobalTreeBuilder(n, dim, device=device).build(x, id_base=first + 1)
         packed = t.query_packed(q, a.query)
+        if a.save:
+            tp, ti = t.gather_full()
+            if rank == 0:
+                pk.KDTree(tp.cpu(), ti.cpu(), 0, "exact").save(a.save)
     if device.type == "cuda":
         torch.cuda.synchronize()
     t_done = time.perf_counter()

@@ -1,0 +1,64 @@
+"""Python CLI (parallel_kd_tree_amd/cli.py): reference protocol single-process and under
+torchrun (forest / global decompositions over gloo), plus --save."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import parallel_kd_tree_amd as pk
+from test_cli_protocol import oracle_lines
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, nproc=1, stdin=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    if nproc == 1:
+        cmd = [sys.executable, "-m", "parallel_kd_tree_amd.cli", *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "parallel_kd_tree_amd.cli", *args]
+    return subprocess.run(cmd, input=stdin, capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+
+
+def test_single_debug_and_save(tmp_path):
+    path = tmp_path / "t.pkd"
+    r = _run(["--device", "cpu", "--save", str(path), "42", "3", "1024"])
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "READY" and lines[-1] == "DONE" and lines[-2].startswith("elapsed time ")
+    assert lines[1:11] == oracle_lines(42, 3, 1024)
+    t = pk.KDTree.load(path)
+    assert t.n == 1024 and t.invariant_violations() == 0
+    x = pk.generate_problem(42, 3, 1024)
+    assert torch.equal(torch.sort(t.tree_ids.long()).values, torch.arange(1, 1025))
+    assert torch.equal(t.tree_pts[torch.argsort(t.tree_ids.long())], x)
+
+
+@pytest.mark.parametrize("decomp,nproc", [("forest", 2), ("global", 2), ("global", 4)])
+def test_torchrun_decompositions(decomp, nproc):
+    r = _run(["--device", "cpu", "--decomp", decomp, "7", "3", "6000"], nproc=nproc)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert lines[0] == "READY" and lines[-1] == "DONE"
+    assert lines[1:11] == oracle_lines(7, 3, 6000)
+
+
+def test_eval_mode_stdin_metrics():
+    r = _run(["--device", "cpu", "--metrics-json", "--queries", "10"], stdin="3\n")
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "READY" and lines[-1] == "DONE" and len(lines) == 12
+    assert lines[1:11] == oracle_lines(3, 128, 500_000)
+    assert '"build_query_ms"' in r.stderr
