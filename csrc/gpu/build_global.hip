@@ -291,6 +291,20 @@ __device__ __forceinline__ u32 zone_of(float key, const BucketParams& prm, int b
   return sb < sbstar ? 0u : (sb == sbstar ? 1u : 2u);
 }
 
+// Wave-aggregated min / max of the composite keys of the `active` lanes, one pair of
+// atomics per wave (all lanes of the wave must call it).
+__device__ __forceinline__ void wave_minmax_atomic(bool active, u64 k, unsigned long long* mn,
+                                                   unsigned long long* mx) {
+  const u64 m = __ballot(active);
+  if (!m) return;
+  const u64 lo = dev::wave_min_u64(active ? k : ~0ull);
+  const u64 hi = dev::wave_max_u64(active ? k : 0ull);
+  if (dev::lane() == __ffsll((long long)m) - 1) {
+    atomicMin(mn, (unsigned long long)lo);
+    atomicMax(mx, (unsigned long long)hi);
+  }
+}
+
 // Histogram of a level's keys (used for the first global level only; later levels get
 // theirs from the fused partition pass).
 __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ hist) {
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ 
   for (int b = threadIdx.x; b < a.bins; b += kBlock) sh[b] = 0;
   __syncthreads();
   const i64 per = (n + a.bps - 1) / a.bps;
-  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   const BucketParams p = a.params[h];
   const float* key = a.src + i64(a.axis) * a.ncol + lo;
   constexpr int U = 8;
@@ -434,7 +448,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
   for (int b = threadIdx.x; b < kBins2; b += kBlock) sh[b] = 0;
   __syncthreads();
   const i64 per = (n + a.bps - 1) / a.bps;
-  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   const BucketParams p = a.params[h];
   const SegState* st = a.state + h;
   const u32 bstar = st->bstar;
@@ -523,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     for (int b = threadIdx.x; b < 2 * a.next_bins; b += kBlock) nh[b] = 0;
   }
   const i64 per = (n + a.bps - 1) / a.bps;
-  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   SegState* st = a.state + h;
   const u32 bstar = st->bstar;
   const u32 stage2 = st->stage2, sbstar = st->sbstar;
@@ -627,11 +641,10 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       }
       const u64 mz = z == 0 ? m0 : (z == 1 ? m1 : m2);
       zone_pre[i] = (z << 16) | mbcnt(mz);
-      if (m1 != 0 && z == 1) {  // rare: track the middle zone's composite key range
-        const u32 id = reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e];
-        const u64 k = composite_key(key, id);
-        atomicMin(&st->mid_min, (unsigned long long)k);
-        atomicMax(&st->mid_max, (unsigned long long)k);
+      if (m1 != 0) {  // rare: track the middle zone's composite key range
+        u64 k = 0;
+        if (z == 1) k = composite_key(key, reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e]);
+        wave_minmax_atomic(z == 1, k, &st->mid_min, &st->mid_max);
       }
       if (fuse && z < 3 && z != 1) {
         const int child = z == 0 ? 0 : 1;
@@ -986,7 +999,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
   const int nb = a.next_bins;
   for (int b = threadIdx.x; b < 2 * nb; b += kBlock) nh[b] = 0;
   const i64 per = (n + a.bps - 1) / a.bps;
-  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   SegState* st = a.state + h;
   const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
   BucketParams p2;
@@ -1022,6 +1035,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
         u32 base = 0;
         if (ln == leader) base = atomicAdd(&st->cur[1], u32(__popcll(m)));
         base = __shfl(base, leader, 64);
+        u64 ck = 0;
         if (z == 1) {
           const i64 q = lo + base + mbcnt(m);
           if (i64(base + mbcnt(m)) >= n) {
@@ -1030,11 +1044,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
 #pragma unroll
             for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + q] = src[i64(c) * nc + lo + e];
           }
-          const u32 id = reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e];
-          const u64 ck = composite_key(k[u], id);
-          atomicMin(&st->mid_min, (unsigned long long)ck);
-          atomicMax(&st->mid_max, (unsigned long long)ck);
+          ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e]);
         }
+        wave_minmax_atomic(z == 1, ck, &st->mid_min, &st->mid_max);
       }
     }
   }
@@ -1204,7 +1216,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   if (fuse)
     for (int b = threadIdx.x; b < 4 * nb2; b += kBlock) nh[b] = 0;
   const i64 per = (n + a.bps - 1) / a.bps;
-  const i64 b0 = i64(part) * per, b1 = min(n, b0 + per);
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   const SegState* st = a.state + h;
   const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
   const u64 pivot = st->pivot;
@@ -1212,18 +1224,21 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   p2.lo = st->p2lo;
   p2.scale = st->p2scale;
   const BucketParams prm = a.params[h];
-  // children (level l+1)
-  SegState* cst[2] = {a.state + 2 * h + 1, a.state + 2 * h + 2};
+  // children (level l+1); only compile-time indices below (a runtime index would put the
+  // arrays in scratch memory)
+  SegState* const cst0 = a.state + 2 * h + 1;
+  SegState* const cst1 = a.state + 2 * h + 2;
   u32 cbs[2], cs2[2], csb[2];
   BucketParams cpr[2], cp2[2], gpr[4];
   i64 clo[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    cbs[c] = cst[c]->bstar;
-    cs2[c] = cst[c]->stage2;
-    csb[c] = cst[c]->sbstar;
-    cp2[c].lo = cst[c]->p2lo;
-    cp2[c].scale = cst[c]->p2scale;
+    const SegState* cs = c == 0 ? cst0 : cst1;
+    cbs[c] = cs->bstar;
+    cs2[c] = cs->stage2;
+    csb[c] = cs->sbstar;
+    cp2[c].lo = cs->p2lo;
+    cp2[c].scale = cs->p2scale;
     cpr[c] = a.params[2 * h + 1 + c];
     clo[c] = a.seg_lo[2 * h + 1 + c];
 #pragma unroll
@@ -1283,7 +1298,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       u32 tz = 0;
       for (int k = 0; k < kBlock / 64; ++k) tz += gcnt[threadIdx.x][k];
       const int c = threadIdx.x / 3, z = threadIdx.x % 3;
-      bcur[threadIdx.x] = tz ? atomicAdd(&cst[c]->cur[z], tz) : 0u;
+      bcur[threadIdx.x] = tz ? atomicAdd(&(c == 0 ? cst0 : cst1)->cur[z], tz) : 0u;
     }
   }
   __syncthreads();
@@ -1317,16 +1332,15 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         if (q == u32(z)) my = mbcnt(m);
       }
       zone_pre[i] = (q << 16) | my;
-      if (q < 6) {
-        const u32 c = q / 3, z1 = q % 3;
-        if (z1 == 1) {  // level l+1 middle zone: track its composite key range
-          const u64 ck = composite_key(k1, __float_as_uint(row[i][D]));
-          atomicMin(&cst[c]->mid_min, (unsigned long long)ck);
-          atomicMax(&cst[c]->mid_max, (unsigned long long)ck);
-        } else if (fuse) {
-          const u32 g = 2 * c + (z1 == 2 ? 1u : 0u);
-          atomicAdd(&nh[g * nb2 + bucket_of(k2, gpr[g], nb2)], 1u);
-        }
+      if (fuse && q < 6 && q != 1 && q != 4) {
+        const u32 g = (q / 3) * 2 + (q % 3 == 2 ? 1u : 0u);
+        const BucketParams gp = g == 0 ? gpr[0] : (g == 1 ? gpr[1] : (g == 2 ? gpr[2] : gpr[3]));
+        atomicAdd(&nh[g * nb2 + bucket_of(k2, gp, nb2)], 1u);
+      }
+      if (__ballot(q == 1 || q == 4)) {  // level l+1 middle zones: track their composite key ranges
+        const u64 ck = composite_key(k1, __float_as_uint(row[i][D]));
+        wave_minmax_atomic(q == 1, ck, &cst0->mid_min, &cst0->mid_max);
+        wave_minmax_atomic(q == 4, ck, &cst1->mid_min, &cst1->mid_max);
       }
     }
     __syncthreads();
@@ -1339,7 +1353,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         base = bcur[z];
         if (ln == 0) bcur[z] = base + tot;
       } else {
-        if (ln == 0 && tot) base = atomicAdd(&cst[z / 3]->cur[z % 3], tot);
+        if (ln == 0 && tot) base = atomicAdd(&(z < 3 ? cst0 : cst1)->cur[z % 3], tot);
         base = __shfl(base, 0, 64);
       }
       gcnt[z][ln] = base + incl - v;
@@ -1406,7 +1420,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
     // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
     // 256 CUs) while segments are few; one block per segment below that.
-    lp.bps = int(std::max<i64>(1, kLevelBlocks / lp.segs));
+    lp.bps = int(std::max<i64>(1, std::min<i64>(kLevelBlocks / lp.segs, (lp.nmax + kChunk - 1) / kChunk)));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
     lp.stage2 = lp.nmax / lp.bins > kRefineCap;

@@ -635,9 +635,10 @@ __device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32
 // Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
 __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
 
-// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+4 | aux nm | fin nm
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+4 | aux nm | fin nm | tmpi u16 nm
 size_t lds_words(int dim, int nm) {
-  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 4 + 2 * size_t(nm);
+  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 4 + 2 * size_t(nm) +
+         size_t(nm) / 2;
 }
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
@@ -683,20 +684,39 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   u32* work = smem + size_t(dim + 1) * NM + (size_t(kept_layout) * NM + 1) / 2;
   u32* aux = work + NM + 4;
   u32* fin = aux + NM;
+  u16* tmpi = reinterpret_cast<u16*>(fin + NM);
   stamp(a, 0);
 
-  for (int c = 0; c <= dim; ++c) {
-    const float* col = a.cols + i64(c) * a.ncol + glo;
-    float v[ITEMS];
+  {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
+    constexpr int kLoadCols = 5;
+    float v[kLoadCols][ITEMS];
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int k = tid + i * THREADS;
-      v[i] = k < n ? col[k] : 0.0f;
-    }
+    for (int c = 0; c < kLoadCols; ++c)
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int k = tid + i * THREADS;
-      if (k < n) rows[c * NM + k] = v[i];
+      for (int i = 0; i < ITEMS; ++i) {
+        const int k = tid + i * THREADS;
+        v[c][i] = (c <= dim && k < n) ? a.cols[i64(c) * a.ncol + glo + k] : 0.0f;
+      }
+#pragma unroll
+    for (int c = 0; c < kLoadCols; ++c)
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int k = tid + i * THREADS;
+        if (c <= dim && k < n) rows[c * NM + k] = v[c][i];
+      }
+    for (int c = kLoadCols; c <= dim; ++c) {
+      const float* col = a.cols + i64(c) * a.ncol + glo;
+      float w[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int k = tid + i * THREADS;
+        w[i] = k < n ? col[k] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int k = tid + i * THREADS;
+        if (k < n) rows[c * NM + k] = w[i];
+      }
     }
   }
 #pragma unroll
@@ -765,67 +785,55 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       }
     } else {
       // ---- exact ranks from bucket histograms (first use of the axis) ----
+      // Bucket range: the block root's cell on this axis. On an axis's first use no split
+      // inside the block has narrowed it, so it is the sub-segment's own range; otherwise it
+      // is a valid (wider) range. Any monotone bucketing gives exact ranks.
+      // About one point per bucket (S * B <= NM): most buckets need no comparison at all.
       const int maxsize = n >> t;
-      const int B = maxsize > rk::kSmallSeg ? max(2, pow2_floor_dev(maxsize / 2)) : 1;
+      const int B = maxsize > rk::kSmallSeg ? int(rk::pow2_ceil(u32(maxsize))) : 1;
       const int nb = S * B;
-      u16* tmp = reinterpret_cast<u16*>(aux);
-      u32* mm = aux + NM / 2;
+      u32* tmpk = aux;  // orderable keys in bucket order
       for (int w = tid; w <= nb; w += THREADS) work[w] = 0;
-      if (B > 1)
-        for (int q = tid; q < S; q += THREADS) {
-          mm[2 * q] = 0xffffffffu;
-          mm[2 * q + 1] = 0u;
-        }
+      const float* rc = a.cells + (h * dim + axis) * 2;
+      const BucketParams pr = make_params(rc[0], rc[1], B);
       __syncthreads();
       u32 ok[ITEMS];
-      float kf[ITEMS];
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        kf[i] = nn[i] ? kcol[tid + i * THREADS] : 0.0f;
-        ok[i] = orderable(kf[i]);
-      }
-      if (B > 1) {
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-          if (nn[i]) {
-            atomicMin(&mm[2 * sg[i]], ok[i]);
-            atomicMax(&mm[2 * sg[i] + 1], ok[i]);
-          }
-        __syncthreads();
-      }
       u32 bk[ITEMS], wi[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
+        const float kf = nn[i] ? kcol[tid + i * THREADS] : 0.0f;
+        ok[i] = orderable(kf);
         bk[i] = 0;
         wi[i] = 0;
         if (nn[i]) {
-          u32 b = 0;
-          if (B > 1) {
-            const BucketParams pr = make_params(from_orderable(mm[2 * sg[i]]), from_orderable(mm[2 * sg[i] + 1]), B);
-            b = bucket_of(kf[i], pr, B);
-          }
-          bk[i] = sg[i] * B + b;
+          bk[i] = sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u);
           wi[i] = atomicAdd(&work[bk[i]], 1u);
         }
       }
       __syncthreads();
       rk::block_excl_scan<THREADS>(work, nb, wsum);
       __syncthreads();
+      u32 pos[ITEMS];
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i)
-        if (nn[i]) tmp[work[bk[i]] + wi[i]] = u16(tid + i * THREADS);
+      for (int i = 0; i < ITEMS; ++i) {
+        pos[i] = 0;
+        if (nn[i]) {
+          pos[i] = work[bk[i]] + wi[i];
+          tmpk[pos[i]] = ok[i];
+          tmpi[pos[i]] = u16(tid + i * THREADS);
+        }
+      }
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         rank[i] = 0;
         if (nn[i]) {
           const u32 st = work[bk[i]], en = work[bk[i] + 1], base = work[sg[i] * B];
-          const u32 myid = idrow[tid + i * THREADS];
           u32 r = st - base;
           for (u32 k = st; k < en && k < st + u32(NM); ++k) {
-            const u32 q = tmp[k];
-            const u32 qk = orderable(kcol[q]);
-            r += (qk < ok[i] || (qk == ok[i] && idrow[q] < myid)) ? 1u : 0u;
+            const u32 qk = tmpk[k];
+            r += qk < ok[i] ? 1u : 0u;
+            if (qk == ok[i] && k != pos[i]) r += idrow[tmpi[k]] < idrow[tid + i * THREADS] ? 1u : 0u;
           }
           rank[i] = r;
         }
@@ -862,19 +870,17 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
     if (t < 28) stamp(a, 2 + t);
   }
   stamp(a, 30);
-  // in-order rows out, AoS, coalesced
-  const i64 total = i64(n) * dim;
+  // in-order rows out: thread per slot, the row's dim floats (consecutive threads cover
+  // consecutive 4*dim-byte runs, merged in L2)
   float* outp = a.out_pts + glo * dim;
-  for (i64 f = tid; f < total; f += THREADS) {
-    const int k = int(f / dim);
-    const int c = int(f - i64(k) * dim);
-    const u32 p = fin[k];
-    outp[f] = rows[c * NM + (p < u32(NM) ? p : 0u)];
-  }
   for (int k = tid; k < n; k += THREADS) {
-    const u32 p = fin[k];
-    if (p >= u32(NM)) report(a.err, 0x800u, u32(k), p);
-    a.out_ids[glo + k] = idrow[p < u32(NM) ? p : 0u];
+    u32 p = fin[k];
+    if (p >= u32(NM)) {
+      report(a.err, 0x800u, u32(k), p);
+      p = 0;
+    }
+    for (int c = 0; c < dim; ++c) outp[i64(k) * dim + c] = rows[c * NM + p];
+    a.out_ids[glo + k] = idrow[p];
   }
   __syncthreads();
   stamp(a, 31);
@@ -985,7 +991,12 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
   subtree_stamp_buffer() = stamps;
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps};
   if (!use_hist_impl()) {
+    static const bool wide = [] {
+      const char* e = std::getenv("PKD_SUBTREE_WIDE");
+      return !(e && std::string(e) == "0");
+    }();
     if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);
+    else if (nmax > 1024 && wide) launch_rank_cfg<2, 1024>(a, segs, stream);
     else if (nmax > 1024) launch_rank_cfg<4, 512>(a, segs, stream);
     else if (nmax > 512) launch_rank_cfg<4, 256>(a, segs, stream);
     else if (nmax > 256) launch_rank_cfg<2, 256>(a, segs, stream);
