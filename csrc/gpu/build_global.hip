@@ -523,8 +523,10 @@ __global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
 // at a time (loads of a column batched before its stores). Loads and stores never
 // interleave per item: the compiler cannot prove src/dst disjoint and would otherwise
 // serialise each load behind the previous store.
-template <int NCOL>
+template <int NCOL, int KI>
 __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
+  constexpr int kItems = KI;
+  constexpr int kChunk = kBlock * KI;
   extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
   __shared__ u32 gcnt[3][64];
   const int dim = NCOL > 0 ? NCOL - 1 : a.dim;
@@ -653,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     }
     __syncthreads();
     if (w < 3) {  // wave w scans zone w over the 64 (item, wave) groups in slot order
-      const u32 v = gcnt[w][ln];
+      const u32 v = ln < kItems * 4 ? gcnt[w][ln] : 0u;
       const u32 incl = dev::wave_incl_scan(v);
       const u32 tot = __shfl(incl, 63, 64);
       u32 base = 0;
@@ -1201,8 +1203,10 @@ __global__ __launch_bounds__(kBlock) void k_pivot(LevelArgs a) {
 }
 
 // Pass B of a pair: a = level l (src -> dst), children states/params are level l+1's.
-template <int NCOL>
+template <int NCOL, int KI>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
+  constexpr int kItems = KI;
+  constexpr int kChunk = kBlock * KI;
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
   __shared__ u32 gcnt[6][64];
   __shared__ u32 bcur[6];
@@ -1224,26 +1228,15 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   p2.lo = st->p2lo;
   p2.scale = st->p2scale;
   const BucketParams prm = a.params[h];
-  // children (level l+1); only compile-time indices below (a runtime index would put the
-  // arrays in scratch memory)
+  // children (level l+1, never second-stage: a pair is only formed when l+1 has none);
+  // grandchild bucketing in LDS to keep the scalar register file from spilling
   SegState* const cst0 = a.state + 2 * h + 1;
   SegState* const cst1 = a.state + 2 * h + 2;
-  u32 cbs[2], cs2[2], csb[2];
-  BucketParams cpr[2], cp2[2], gpr[4];
-  i64 clo[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const SegState* cs = c == 0 ? cst0 : cst1;
-    cbs[c] = cs->bstar;
-    cs2[c] = cs->stage2;
-    csb[c] = cs->sbstar;
-    cp2[c].lo = cs->p2lo;
-    cp2[c].scale = cs->p2scale;
-    cpr[c] = a.params[2 * h + 1 + c];
-    clo[c] = a.seg_lo[2 * h + 1 + c];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) gpr[2 * c + g] = fuse ? a.params[2 * (2 * h + 1 + c) + 1 + g] : BucketParams{0.f, 0.f};
-  }
+  __shared__ BucketParams sgp[4];
+  if (fuse && threadIdx.x < 4) sgp[threadIdx.x] = a.params[2 * (2 * h + 1 + threadIdx.x / 2) + 1 + (threadIdx.x & 1)];
+  const u32 cbs0 = cst0->bstar, cbs1 = cst1->bstar;
+  const BucketParams cpr0 = a.params[2 * h + 1], cpr1 = a.params[2 * h + 2];
+  const i64 clo0 = a.seg_lo[2 * h + 1], clo1 = a.seg_lo[2 * h + 2];
   const float* __restrict__ src = a.src;
   float* __restrict__ dst = a.dst;
   const i64 nc = a.ncol;
@@ -1259,9 +1252,9 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       if (ck == pivot) return 7u;
       c = ck < pivot ? 0u : 1u;
     }
-    const u32 z1 = c == 0 ? zone_of(k1, cpr[0], pa.bins1, cbs[0], cs2[0], cp2[0], csb[0])
-                          : zone_of(k1, cpr[1], pa.bins1, cbs[1], cs2[1], cp2[1], csb[1]);
-    return 3 * c + z1;
+    const u32 b1 = c == 0 ? bucket_of(k1, cpr0, pa.bins1) : bucket_of(k1, cpr1, pa.bins1);
+    const u32 cb = c == 0 ? cbs0 : cbs1;
+    return 3 * c + (b1 < cb ? 0u : (b1 == cb ? 1u : 2u));
   };
   if (a.block_reserve) {
     u32 cnt[6] = {0, 0, 0, 0, 0, 0};
@@ -1334,8 +1327,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       zone_pre[i] = (q << 16) | my;
       if (fuse && q < 6 && q != 1 && q != 4) {
         const u32 g = (q / 3) * 2 + (q % 3 == 2 ? 1u : 0u);
-        const BucketParams gp = g == 0 ? gpr[0] : (g == 1 ? gpr[1] : (g == 2 ? gpr[2] : gpr[3]));
-        atomicAdd(&nh[g * nb2 + bucket_of(k2, gp, nb2)], 1u);
+        atomicAdd(&nh[g * nb2 + bucket_of(k2, sgp[g], nb2)], 1u);
       }
       if (__ballot(q == 1 || q == 4)) {  // level l+1 middle zones: track their composite key ranges
         const u64 ck = composite_key(k1, __float_as_uint(row[i][D]));
@@ -1345,7 +1337,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     }
     __syncthreads();
     for (int z = w; z < 6; z += kBlock / 64) {  // wave w scans zones w, w+4
-      const u32 v = gcnt[z][ln];
+      const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
       const u32 incl = dev::wave_incl_scan(v);
       const u32 tot = __shfl(incl, 63, 64);
       u32 base = 0;
@@ -1370,7 +1362,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         if (i64(off) >= cn) {
           atomicOr(a.err, 1u);
         } else {
-          dest = (c == 0 ? clo[0] : clo[1]) + off;
+          dest = (c == 0 ? clo0 : clo1) + off;
         }
       }
 #pragma unroll
@@ -1386,6 +1378,14 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       if (v) atomicAdd(&hn[b], v);
     }
   }
+}
+
+bool items16() {
+  static const bool v = [] {
+    const char* e = std::getenv("PKD_PART_ITEMS");
+    return e && std::string(e) == "16";
+  }();
+  return v;
 }
 
 int pow2_floor(i64 v) {
@@ -1666,11 +1666,20 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       pa.bins2 = lq.next_bins;
       pa.hist2n = hist[l & 1];
       const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
-      switch (dim_) {
-        case 1: k_partition2<2><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-        case 2: k_partition2<3><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-        case 3: k_partition2<4><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-        default: k_partition2<5><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+      if (items16()) {
+        switch (dim_) {
+          case 1: k_partition2<2, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          case 2: k_partition2<3, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          case 3: k_partition2<4, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          default: k_partition2<5, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+        }
+      } else {
+        switch (dim_) {
+          case 1: k_partition2<2, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          case 2: k_partition2<3, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          case 3: k_partition2<4, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+          default: k_partition2<5, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+        }
       }
       PKD_LAUNCH_CHECK();
       refine(b, lq.segs);
@@ -1679,12 +1688,22 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       continue;
     }
     const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
-    switch (dim_) {
-      case 1: k_partition<2><<<grid, kBlock, lds, stream>>>(a); break;
-      case 2: k_partition<3><<<grid, kBlock, lds, stream>>>(a); break;
-      case 3: k_partition<4><<<grid, kBlock, lds, stream>>>(a); break;
-      case 4: k_partition<5><<<grid, kBlock, lds, stream>>>(a); break;
-      default: k_partition<0><<<grid, kBlock, lds, stream>>>(a); break;
+    if (items16()) {
+      switch (dim_) {
+        case 1: k_partition<2, 16><<<grid, kBlock, lds, stream>>>(a); break;
+        case 2: k_partition<3, 16><<<grid, kBlock, lds, stream>>>(a); break;
+        case 3: k_partition<4, 16><<<grid, kBlock, lds, stream>>>(a); break;
+        case 4: k_partition<5, 16><<<grid, kBlock, lds, stream>>>(a); break;
+        default: k_partition<0, 16><<<grid, kBlock, lds, stream>>>(a); break;
+      }
+    } else {
+      switch (dim_) {
+        case 1: k_partition<2, 8><<<grid, kBlock, lds, stream>>>(a); break;
+        case 2: k_partition<3, 8><<<grid, kBlock, lds, stream>>>(a); break;
+        case 3: k_partition<4, 8><<<grid, kBlock, lds, stream>>>(a); break;
+        case 4: k_partition<5, 8><<<grid, kBlock, lds, stream>>>(a); break;
+        default: k_partition<0, 8><<<grid, kBlock, lds, stream>>>(a); break;
+      }
     }
     PKD_LAUNCH_CHECK();
     refine(a, lp.segs);
