@@ -529,6 +529,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   constexpr int kChunk = kBlock * KI;
   extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
   __shared__ u32 gcnt[3][64];
+  __shared__ unsigned long long bmin, bmax;  // block's middle-zone key range, flushed once
   const int dim = NCOL > 0 ? NCOL - 1 : a.dim;
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -559,6 +560,10 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   const int w = threadIdx.x / 64;
   const int ln = dev::lane();
   __shared__ u32 bcur[4];
+  if (threadIdx.x == 0) {
+    bmin = ~0ull;
+    bmax = 0ull;
+  }
   if (a.block_reserve) {
     // Few segments and many blocks per segment: per-chunk cursor atomics would all hit the
     // same three words. Count this block's zones from the key column first (an extra 4 B
@@ -646,7 +651,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       if (m1 != 0) {  // rare: track the middle zone's composite key range
         u64 k = 0;
         if (z == 1) k = composite_key(key, reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e]);
-        wave_minmax_atomic(z == 1, k, &st->mid_min, &st->mid_max);
+        wave_minmax_atomic(z == 1, k, &bmin, &bmax);
       }
       if (fuse && z < 3 && z != 1) {
         const int child = z == 0 ? 0 : 1;
@@ -705,6 +710,10 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (threadIdx.x == 0 && bmin != ~0ull) {
+    atomicMin(&st->mid_min, bmin);
+    atomicMax(&st->mid_max, bmax);
   }
   if (fuse) {
     u32* hn = a.hist_next + (2 * s) * a.next_bins;
@@ -1015,6 +1024,17 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
   const float* kc = src + i64(a.axis) * nc + lo;
   const float* nkc = src + i64(a.next_axis) * nc + lo;
   const int ln = dev::lane();
+  // middle rows are staged in LDS and reserved once per block (same-address atomics on the
+  // segment cursor from every wave would serialise in L2)
+  constexpr int kStage = 256;
+  __shared__ float mrow[kStage * NCOL];
+  __shared__ u32 mcnt, mbase;
+  __shared__ unsigned long long bmin, bmax;
+  if (threadIdx.x == 0) {
+    mcnt = 0;
+    bmin = ~0ull;
+    bmax = 0ull;
+  }
   __syncthreads();
   constexpr int U = 8;
   for (i64 e0 = b0; e0 < b1; e0 += kBlock * U) {
@@ -1032,27 +1052,52 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
       if (z == 0) atomicAdd(&nh[bucket_of(nk[u], cp0, nb)], 1u);
       if (z == 2) atomicAdd(&nh[nb + bucket_of(nk[u], cp1, nb)], 1u);
       const u64 m = __ballot(z == 1);
-      if (m) {  // rare: compact the median bucket's rows
+      if (m) {  // rare: stage the median bucket's rows
         const int leader = __ffsll((long long)m) - 1;
         u32 base = 0;
-        if (ln == leader) base = atomicAdd(&st->cur[1], u32(__popcll(m)));
+        if (ln == leader) base = atomicAdd(&mcnt, u32(__popcll(m)));
         base = __shfl(base, leader, 64);
         u64 ck = 0;
         if (z == 1) {
-          const i64 q = lo + base + mbcnt(m);
-          if (i64(base + mbcnt(m)) >= n) {
-            atomicOr(a.err, 1u);
-          } else {
+          const u32 slot = base + mbcnt(m);
+          if (slot < u32(kStage)) {
 #pragma unroll
-            for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + q] = src[i64(c) * nc + lo + e];
+            for (int c = 0; c < NCOL; ++c) mrow[slot * NCOL + c] = src[i64(c) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x];
+          } else {  // staging full: reserve directly
+            const u32 g = atomicAdd(&st->cur[1], 1u);
+            if (i64(g) >= n) {
+              atomicOr(a.err, 1u);
+            } else {
+#pragma unroll
+              for (int c = 0; c < NCOL; ++c)
+                dst[i64(c) * nc + lo + g] = src[i64(c) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x];
+            }
           }
-          ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e]);
+          ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x]);
         }
-        wave_minmax_atomic(z == 1, ck, &st->mid_min, &st->mid_max);
+        wave_minmax_atomic(z == 1, ck, &bmin, &bmax);
       }
     }
   }
   __syncthreads();
+  const u32 staged = min(mcnt, u32(kStage));
+  if (threadIdx.x == 0) {
+    mbase = staged ? atomicAdd(&st->cur[1], staged) : 0u;
+    if (bmin != ~0ull) {
+      atomicMin(&st->mid_min, bmin);
+      atomicMax(&st->mid_max, bmax);
+    }
+  }
+  __syncthreads();
+  for (u32 k2 = threadIdx.x; k2 < staged; k2 += kBlock) {
+    const i64 q = i64(mbase) + k2;
+    if (q >= n) {
+      atomicOr(a.err, 1u);
+      continue;
+    }
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + q] = mrow[k2 * NCOL + c];
+  }
   u32* hn = a.hist_next + (2 * s) * nb;
   for (int b = threadIdx.x; b < 2 * nb; b += kBlock) {
     const u32 v = nh[b];
@@ -1210,6 +1255,11 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
   __shared__ u32 gcnt[6][64];
   __shared__ u32 bcur[6];
+  __shared__ unsigned long long bmin[2], bmax[2];  // children's middle-zone key ranges, flushed once
+  if (threadIdx.x < 2) {
+    bmin[threadIdx.x] = ~0ull;
+    bmax[threadIdx.x] = 0ull;
+  }
   constexpr int D = NCOL - 1;
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -1331,8 +1381,8 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       }
       if (__ballot(q == 1 || q == 4)) {  // level l+1 middle zones: track their composite key ranges
         const u64 ck = composite_key(k1, __float_as_uint(row[i][D]));
-        wave_minmax_atomic(q == 1, ck, &cst0->mid_min, &cst0->mid_max);
-        wave_minmax_atomic(q == 4, ck, &cst1->mid_min, &cst1->mid_max);
+        wave_minmax_atomic(q == 1, ck, &bmin[0], &bmax[0]);
+        wave_minmax_atomic(q == 4, ck, &bmin[1], &bmax[1]);
       }
     }
     __syncthreads();
@@ -1370,6 +1420,11 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
     }
     __syncthreads();
+  }
+  if (threadIdx.x < 2 && bmin[threadIdx.x] != ~0ull) {
+    SegState* cs = threadIdx.x == 0 ? cst0 : cst1;
+    atomicMin(&cs->mid_min, bmin[threadIdx.x]);
+    atomicMax(&cs->mid_max, bmax[threadIdx.x]);
   }
   if (fuse) {
     u32* hn = pa.hist2n + (4 * s) * nb2;
