@@ -993,6 +993,7 @@ __global__ __launch_bounds__(kBlock) void k_refine_small(LevelArgs a, i64 segs) 
 //   k_refine*    level l+1's middle zones as usual.
 // Traffic per two levels: 8 + 16 + 16 B / row instead of 2 x (16 + 16).
 struct PairArgs {
+  int stage2_1;          // level l+1 median buckets split again (k_hist2p + k_select2)
   int bins1;             // level l+1 bins
   int axis2;             // level l+2 axis
   int bins2;             // level l+2 bins (0: l+2 is the subtree level)
@@ -1247,6 +1248,71 @@ __global__ __launch_bounds__(kBlock) void k_pivot(LevelArgs a) {
   }
 }
 
+// Second-stage histogram of level l+1 before a pair's scatter: rows are still grouped by
+// level-l segment, so each row is routed to its child first (bucket, or pivot comparison for
+// level l's median bucket); rows in the child's median bucket add to the child's sub-bucket
+// histogram (hist2 of level l+1, [2 * segs][kBins2]).
+__global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
+  __shared__ u32 sh[2 * kBins2];
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  for (int b = threadIdx.x; b < 2 * kBins2; b += kBlock) sh[b] = 0;
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
+  const SegState* st = a.state + h;
+  const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
+  const u64 pivot = st->pivot;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const BucketParams prm = a.params[h];
+  const SegState* c0 = a.state + 2 * h + 1;
+  const SegState* c1 = a.state + 2 * h + 2;
+  const BucketParams cpr0 = a.params[2 * h + 1], cpr1 = a.params[2 * h + 2];
+  const BucketParams q0{c0->p2lo, c0->p2scale}, q1{c1->p2lo, c1->p2scale};
+  const u32 cb0 = c0->bstar, cb1 = c1->bstar;
+  const i64 nc = a.ncol;
+  const float* kc = a.src + i64(a.axis) * nc + lo;
+  const float* k1c = a.src + i64(a.next_axis) * nc + lo;
+  const u32* idc = reinterpret_cast<const u32*>(a.src) + i64(a.dim) * nc + lo;
+  __syncthreads();
+  constexpr int U = 8;
+  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
+    float k0[U], k1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock;
+      k0[u] = e < b1 ? kc[e] : 0.0f;
+      k1[u] = e < b1 ? k1c[e] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + i64(u) * kBlock;
+      if (e >= b1) continue;
+      const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
+      u32 c = z0 == 0 ? 0u : 1u;
+      if (z0 == 1) {
+        const u64 ck = composite_key(k0[u], idc[e]);
+        if (ck == pivot) continue;
+        c = ck < pivot ? 0u : 1u;
+      }
+      if (c == 0) {
+        if (bucket_of(k1[u], cpr0, pa.bins1) == cb0) atomicAdd(&sh[bucket_of(k1[u], q0, kBins2)], 1u);
+      } else {
+        if (bucket_of(k1[u], cpr1, pa.bins1) == cb1) atomicAdd(&sh[kBins2 + bucket_of(k1[u], q1, kBins2)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  u32* hs = a.hist2 + (2 * s) * kBins2;
+  for (int b = threadIdx.x; b < 2 * kBins2; b += kBlock) {
+    const u32 v = sh[b];
+    if (v) atomicAdd(&hs[b], v);
+  }
+}
+
 // Pass B of a pair: a = level l (src -> dst), children states/params are level l+1's.
 template <int NCOL, int KI>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
@@ -1284,6 +1350,13 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   SegState* const cst1 = a.state + 2 * h + 2;
   __shared__ BucketParams sgp[4];
   if (fuse && threadIdx.x < 4) sgp[threadIdx.x] = a.params[2 * (2 * h + 1 + threadIdx.x / 2) + 1 + (threadIdx.x & 1)];
+  __shared__ BucketParams c2p[2];  // children's second-stage bucketing (pa.stage2_1)
+  __shared__ u32 c2sb[2];
+  if (pa.stage2_1 && threadIdx.x < 2) {
+    const SegState* cs = threadIdx.x == 0 ? cst0 : cst1;
+    c2p[threadIdx.x] = BucketParams{cs->p2lo, cs->p2scale};
+    c2sb[threadIdx.x] = cs->sbstar;
+  }
   const u32 cbs0 = cst0->bstar, cbs1 = cst1->bstar;
   const BucketParams cpr0 = a.params[2 * h + 1], cpr1 = a.params[2 * h + 2];
   const i64 clo0 = a.seg_lo[2 * h + 1], clo1 = a.seg_lo[2 * h + 2];
@@ -1304,7 +1377,12 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     }
     const u32 b1 = c == 0 ? bucket_of(k1, cpr0, pa.bins1) : bucket_of(k1, cpr1, pa.bins1);
     const u32 cb = c == 0 ? cbs0 : cbs1;
-    return 3 * c + (b1 < cb ? 0u : (b1 == cb ? 1u : 2u));
+    u32 z1 = b1 < cb ? 0u : (b1 == cb ? 1u : 2u);
+    if (pa.stage2_1 && z1 == 1) {
+      const u32 sb = bucket_of(k1, c2p[c], kBins2), sbs = c2sb[c];
+      z1 = sb < sbs ? 0u : (sb == sbs ? 1u : 2u);
+    }
+    return 3 * c + z1;
   };
   if (a.block_reserve) {
     u32 cnt[6] = {0, 0, 0, 0, 0, 0};
@@ -1489,7 +1567,6 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   const char* pe = std::getenv("PKD_PAIR");
   const bool pairs = dim <= 4 && !(pe && std::string(pe) == "0");
   for (int l = 0; pairs && l + 1 < lg_; ++l) {
-    if (levels_[size_t(l + 1)].stage2) continue;
     levels_[size_t(l)].pair = true;
     if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
       LevelPlan& g = levels_[size_t(l + 2)];
@@ -1716,10 +1793,18 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       k_select<<<int(lq.segs), kBlock, 0, stream>>>(b);
       PKD_LAUNCH_CHECK();
       PairArgs pa;
+      pa.stage2_1 = lq.stage2 ? 1 : 0;
       pa.bins1 = lq.bins;
       pa.axis2 = (opt_.depth0 + l + 2) % dim_;
       pa.bins2 = lq.next_bins;
       pa.hist2n = hist[l & 1];
+      if (lq.stage2) {
+        PKD_HIP_CHECK(hipMemsetAsync(b.hist2, 0, size_t(lq.segs) * kBins2 * 4, stream));
+        k_hist2p<<<grid, kBlock, 0, stream>>>(a, pa);
+        PKD_LAUNCH_CHECK();
+        k_select2<<<int(lq.segs), kBlock, 0, stream>>>(b);
+        PKD_LAUNCH_CHECK();
+      }
       const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
       if (items16()) {
         switch (dim_) {

@@ -635,29 +635,40 @@ __device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32
 // Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
 __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
 
-// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+4 | aux nm | fin nm | tmpi u16 nm
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+36 | aux nm+32 | fin nm+32 | tmpi u16 nm+32
 size_t lds_words(int dim, int nm) {
-  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 4 + 2 * size_t(nm) +
-         size_t(nm) / 2;
+  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 36 + 2 * (size_t(nm) + 32) +
+         size_t(nm) / 2 + 16;
 }
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
-template <int THREADS>
+// m <= CMAX * THREADS. Fixed-trip predicated loops and a shuffle reduction of the wave
+// totals: no per-lane loop bounds, so no exec-mask juggling on the (shared) scalar unit.
+template <int THREADS, int CMAX>
 __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
-  const int tid = threadIdx.x, w = tid / 64;
+  constexpr int W = THREADS / 64;
+  const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
   const int C = (m + THREADS - 1) / THREADS;
-  const int b0 = min(m, tid * C), b1 = min(m, b0 + C);
-  u32 s = 0;
-  for (int b = b0; b < b1; ++b) s += v[b];
+  const int b0 = tid * C;
+  u32 x[CMAX], s = 0;
+#pragma unroll
+  for (int j = 0; j < CMAX; ++j) {
+    const bool in = j < C && b0 + j < m;
+    x[j] = in ? v[in ? b0 + j : 0] : 0u;
+    s += x[j];
+  }
   const u32 incl = dev::wave_incl_scan(s);
-  if (dev::lane() == 63) wsum[w] = incl;
+  if (ln == 63) wsum[w] = incl;
   __syncthreads();
-  u32 run = incl - s;
-  for (int q = 0; q < w; ++q) run += wsum[q];
-  for (int b = b0; b < b1; ++b) {
-    const u32 x = v[b];
-    v[b] = run;
-    run += x;
+  u32 pw = ln < W && ln < w ? wsum[ln < W ? ln : 0] : 0u;  // prefix of the wave totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) pw += __shfl_xor(pw, o, 64);
+  u32 run = pw + incl - s;
+#pragma unroll
+  for (int j = 0; j < CMAX; ++j) {
+    const bool in = j < C && b0 + j < m;
+    if (in) v[b0 + j] = run;
+    run += x[j];
   }
   if (tid == THREADS - 1) v[m] = run;
 }
@@ -682,9 +693,10 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
   u16* crank = reinterpret_cast<u16*>(smem + size_t(dim + 1) * NM);
   u32* work = smem + size_t(dim + 1) * NM + (size_t(kept_layout) * NM + 1) / 2;
-  u32* aux = work + NM + 4;
-  u32* fin = aux + NM;
-  u16* tmpi = reinterpret_cast<u16*>(fin + NM);
+  u32* aux = work + NM + 4 + 32;  // work: NM buckets, sentinel, 32 per-lane dummy words
+  u32* fin = aux + NM + 32;           // aux / fin: NM entries + 32 per-lane dummies each
+  u16* tmpi = reinterpret_cast<u16*>(fin + NM + 32);  // NM + 32 entries
+  const u32 dummy = u32(NM + 4) + (tid & 31);
   stamp(a, 0);
 
   {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
@@ -751,14 +763,14 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       const int nw = S * Wt;
       for (int w = tid; w < nw; w += THREADS) work[w] = 0;
       __syncthreads();
-      u32 c[ITEMS];
+      // Branch-free (the scalar unit, shared by the CU's four SIMDs, is the bottleneck of
+      // exec-mask juggling): finished points OR 0 into a private dummy word per lane.
+      u32 c[ITEMS], wi[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        c[i] = 0;
-        if (nn[i]) {
-          c[i] = cr[tid + i * THREADS];
-          atomicOr(&work[sg[i] * Wt + (c[i] >> 5)], 1u << (c[i] & 31));
-        }
+        c[i] = cr[tid + i * THREADS];
+        wi[i] = nn[i] ? sg[i] * Wt + (c[i] >> 5) : dummy;
+        atomicOr(&work[wi[i]], nn[i] ? 1u << (c[i] & 31) : 0u);
       }
       __syncthreads();
       if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
@@ -776,13 +788,8 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         __syncthreads();
       }
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        rank[i] = 0;
-        if (nn[i]) {
-          const u32 wi = sg[i] * Wt + (c[i] >> 5);
-          rank[i] = (Wt > 1 ? aux[wi] : 0u) + u32(__popc(work[wi] & ((1u << (c[i] & 31)) - 1u)));
-        }
-      }
+      for (int i = 0; i < ITEMS; ++i)
+        rank[i] = (Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u) + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
     } else {
       // ---- exact ranks from bucket histograms (first use of the axis) ----
       // Bucket range: the block root's cell on this axis. On an axis's first use no split
@@ -793,78 +800,65 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       const int B = maxsize > rk::kSmallSeg ? int(rk::pow2_ceil(u32(maxsize))) : 1;
       const int nb = S * B;
       u32* tmpk = aux;  // orderable keys in bucket order
-      for (int w = tid; w <= nb; w += THREADS) work[w] = 0;
+#pragma unroll
+      for (int j = 0; j <= ITEMS; ++j) {
+        const int w = tid + j * THREADS;
+        if (w <= nb) work[w] = 0;
+      }
       const float* rc = a.cells + (h * dim + axis) * 2;
       const BucketParams pr = make_params(rc[0], rc[1], B);
       __syncthreads();
       u32 ok[ITEMS];
       u32 bk[ITEMS], wi[ITEMS];
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const float kf = nn[i] ? kcol[tid + i * THREADS] : 0.0f;
+      for (int i = 0; i < ITEMS; ++i) {  // finished points count into a per-lane dummy word
+        const float kf = kcol[tid + i * THREADS];
         ok[i] = orderable(kf);
-        bk[i] = 0;
-        wi[i] = 0;
-        if (nn[i]) {
-          bk[i] = sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u);
-          wi[i] = atomicAdd(&work[bk[i]], 1u);
-        }
+        bk[i] = nn[i] ? sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u) : dummy;
+        wi[i] = atomicAdd(&work[bk[i]], 1u);
       }
       __syncthreads();
-      rk::block_excl_scan<THREADS>(work, nb, wsum);
+      rk::block_excl_scan<THREADS, ITEMS>(work, nb, wsum);
       __syncthreads();
       u32 pos[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        pos[i] = 0;
-        if (nn[i]) {
-          pos[i] = work[bk[i]] + wi[i];
-          tmpk[pos[i]] = ok[i];
-          tmpi[pos[i]] = u16(tid + i * THREADS);
-        }
+        pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + (tid & 31);
+        tmpk[pos[i]] = ok[i];
+        tmpi[pos[i]] = u16(tid + i * THREADS);
       }
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        rank[i] = 0;
-        if (nn[i]) {
-          const u32 st = work[bk[i]], en = work[bk[i] + 1], base = work[sg[i] * B];
-          u32 r = st - base;
-          for (u32 k = st; k < en && k < st + u32(NM); ++k) {
-            const u32 qk = tmpk[k];
-            r += qk < ok[i] ? 1u : 0u;
-            if (qk == ok[i] && k != pos[i]) r += idrow[tmpi[k]] < idrow[tid + i * THREADS] ? 1u : 0u;
-          }
-          rank[i] = r;
+        const u32 bi = nn[i] ? bk[i] : 0u;
+        const u32 st = work[bi], en = nn[i] ? work[bi + 1] : st, base = work[nn[i] ? sg[i] * B : 0u];
+        const u32 cnt = en - st;
+        const u32 myid = idrow[tid + i * THREADS];
+        u32 r = st - base;
+        for (u32 j = 0;; ++j) {  // wave-uniform trip count (max bucket size in the wave)
+          const bool act = j < cnt;
+          if (!__ballot(act)) break;
+          const u32 k = act ? st + j : 0u;
+          const u32 qk = tmpk[k];
+          r += (act && qk < ok[i]) ? 1u : 0u;
+          const bool tie = act && qk == ok[i] && k != pos[i];
+          if (__ballot(tie)) r += (tie && idrow[tmpi[k]] < myid) ? 1u : 0u;
         }
+        rank[i] = r;
       }
     }
-    // ---- median / left / right ----
+    // ---- median / left / right (selects only; the median's slot write goes to a dummy
+    // word for every other point) ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      if (!nn[i]) continue;
-      const u32 mid = nn[i] / 2, r = rank[i];
-      if (r >= nn[i]) {
-        report(a.err, 0x400u, u32(t), r);
-        nn[i] = 0;
-        continue;
-      }
-      u32 nc;
-      if (r == mid) {
-        fin[lo[i] + mid] = u32(tid + i * THREADS);
-        nn[i] = 0;
-        continue;
-      } else if (r < mid) {
-        sg[i] = 2 * sg[i];
-        nn[i] = mid;
-        nc = r;
-      } else {
-        sg[i] = 2 * sg[i] + 1;
-        lo[i] += mid + 1;
-        nn[i] -= mid + 1;
-        nc = r - mid - 1;
-      }
-      if (keep) cr[tid + i * THREADS] = u16(nc);
+      const u32 n0 = nn[i], mid = n0 >> 1, r = rank[i];
+      const bool is_mid = n0 != 0 && r == mid;
+      const bool right = r > mid;
+      fin[is_mid ? lo[i] + mid : u32(NM) + (tid & 31)] = u32(tid + i * THREADS);
+      if (keep) cr[tid + i * THREADS] = u16(right ? r - mid - 1 : r);
+      lo[i] = right ? lo[i] + mid + 1 : lo[i];
+      sg[i] = 2 * sg[i] + (right ? 1u : 0u);
+      nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
     }
     __syncthreads();
     if (t < 28) stamp(a, 2 + t);
