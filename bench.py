@@ -101,6 +101,10 @@ def main():
     dt = time.perf_counter() - t0
     if world > 1:
         dt = comm.max_float(dt)
+    # the device error word of the last build (outside the timed region)
+    err = builder.read_error() if world > 1 else b.read_error()
+    if err:
+        sys.exit(f"bench.py: rank {rank}: device build reported error flags {err}")
     ms = dt * 1e3 / args.steps
     mpts = n / (ms / 1e3) / 1e6
     if rank == 0:

@@ -1360,6 +1360,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   const u32 cbs0 = cst0->bstar, cbs1 = cst1->bstar;
   const BucketParams cpr0 = a.params[2 * h + 1], cpr1 = a.params[2 * h + 2];
   const i64 clo0 = a.seg_lo[2 * h + 1], clo1 = a.seg_lo[2 * h + 2];
+  __syncthreads();  // c2p / c2sb / sgp are read by every wave below
   const float* __restrict__ src = a.src;
   float* __restrict__ dst = a.dst;
   const i64 nc = a.ncol;

@@ -243,6 +243,10 @@ class GlobalTreeBuilder:
         if self.device.type == "cuda" and self.n_leaf > 0:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
 
+    def read_error(self) -> int:
+        """Device error word of the last local subtree build (0 = ok). Synchronises."""
+        return self._builder.read_error() if self._builder is not None else 0
+
     # ------------------------------------------------------------------------------------
     def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
         if self.device.type == "cuda":

@@ -71,3 +71,9 @@ def test_queries_high_dim(gpu_device):
     tc = pk.KDTree.build(x[:30_000], id_base=1)
     dc, idc = tc.query(x[30_000:])
     assert torch.equal(d.cpu(), dc) and torch.equal(ids.cpu(), idc)
+
+
+def test_large_stage2_pairs(gpu_device):
+    # 20M points: levels 0 and 1 both need the second-stage histogram, so the first pair
+    # runs k_hist2p / k_select2 for its second level and the block-reserve count pass
+    check_same(pk.generate_problem(5, 3, 20_000_000), gpu_device)
