@@ -660,9 +660,9 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
   const u32 incl = dev::wave_incl_scan(s);
   if (ln == 63) wsum[w] = incl;
   __syncthreads();
-  u32 pw = ln < W && ln < w ? wsum[ln < W ? ln : 0] : 0u;  // prefix of the wave totals
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) pw += __shfl_xor(pw, o, 64);
+  // prefix of the wave totals: inclusive scan of wsum over lanes, read at lane w - 1
+  const u32 pin = dev::wave_incl_scan(ln < W ? wsum[ln < W ? ln : 0] : 0u);
+  const u32 pw = w > 0 ? u32(__builtin_amdgcn_readlane(int(pin), w - 1)) : 0u;
   u32 run = pw + incl - s;
 #pragma unroll
   for (int j = 0; j < CMAX; ++j) {
@@ -808,6 +808,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       const float* rc = a.cells + (h * dim + axis) * 2;
       const BucketParams pr = make_params(rc[0], rc[1], B);
       __syncthreads();
+      if (t == 0) stamp(a, 20);
       u32 ok[ITEMS];
       u32 bk[ITEMS], wi[ITEMS];
 #pragma unroll
@@ -818,8 +819,10 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         wi[i] = atomicAdd(&work[bk[i]], 1u);
       }
       __syncthreads();
+      if (t == 0) stamp(a, 21);
       rk::block_excl_scan<THREADS, ITEMS>(work, nb, wsum);
       __syncthreads();
+      if (t == 0) stamp(a, 22);
       u32 pos[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
@@ -828,24 +831,35 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         tmpi[pos[i]] = u16(tid + i * THREADS);
       }
       __syncthreads();
+      if (t == 0) stamp(a, 23);
+      u32 st[ITEMS], cnt[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 bi = nn[i] ? bk[i] : 0u;
-        const u32 st = work[bi], en = nn[i] ? work[bi + 1] : st, base = work[nn[i] ? sg[i] * B : 0u];
-        const u32 cnt = en - st;
-        const u32 myid = idrow[tid + i * THREADS];
-        u32 r = st - base;
-        for (u32 j = 0;; ++j) {  // wave-uniform trip count (max bucket size in the wave)
-          const bool act = j < cnt;
-          if (!__ballot(act)) break;
-          const u32 k = act ? st + j : 0u;
-          const u32 qk = tmpk[k];
-          r += (act && qk < ok[i]) ? 1u : 0u;
-          const bool tie = act && qk == ok[i] && k != pos[i];
-          if (__ballot(tie)) r += (tie && idrow[tmpi[k]] < myid) ? 1u : 0u;
-        }
-        rank[i] = r;
+        st[i] = work[bi];
+        const u32 en = nn[i] ? work[bi + 1] : st[i];
+        cnt[i] = en - st[i];
+        rank[i] = st[i] - work[nn[i] ? sg[i] * B : 0u];
       }
+      // all items' bucket scans advance together (their LDS reads overlap); wave-uniform
+      // trip count = largest bucket among the wave's items
+      for (u32 j = 0;; ++j) {
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) any |= j < cnt[i];
+        if (!__ballot(any)) break;
+        u32 qk[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) qk[i] = tmpk[j < cnt[i] ? st[i] + j : 0u];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+          const bool act = j < cnt[i];
+          rank[i] += (act && qk[i] < ok[i]) ? 1u : 0u;
+          const bool tie = act && qk[i] == ok[i] && st[i] + j != pos[i];
+          if (__ballot(tie)) rank[i] += (tie && idrow[tmpi[st[i] + j]] < idrow[tid + i * THREADS]) ? 1u : 0u;
+        }
+      }
+      if (t == 0) stamp(a, 24);
     }
     // ---- median / left / right (selects only; the median's slot write goes to a dummy
     // word for every other point) ----
@@ -861,7 +875,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
     }
     __syncthreads();
-    if (t < 28) stamp(a, 2 + t);
+    if (t < 18) stamp(a, 2 + t);
   }
   stamp(a, 30);
   // in-order rows out: thread per slot, the row's dim floats (consecutive threads cover
@@ -950,6 +964,7 @@ std::string subtree_stamp_report() {
     os << " ";
     if (i == 1) os << "load";
     else if (i == 30) os << "levels-end";
+    else if (i >= 20 && i <= 24) os << "L0." << (i - 20);
     else if (i == 31) os << "store";
     else os << "L" << (i - 2);
     os << "=" << long(acc[i] / cnt[i]);

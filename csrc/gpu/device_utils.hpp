@@ -17,13 +17,16 @@ __device__ __forceinline__ u32 mbcnt(u64 mask) {
   return __builtin_amdgcn_mbcnt_hi(u32(mask >> 32), __builtin_amdgcn_mbcnt_lo(u32(mask), 0u));
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP moves only (no LDS round trips): shifts of
+// 1, 2, 4, 8 inside each row of 16 lanes, then row_bcast:15 / row_bcast:31 carry the row
+// totals across rows (GFX9 DPP controls, available on CDNA4).
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
-  const int l = lane();
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const u32 t = __shfl_up(v, o, kWave);
-    if (l >= o) v += t;
-  }
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));  // row_shr:1
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));  // row_shr:2
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));  // row_shr:4
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));  // row_shr:8
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+  v += u32(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
