@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <sstream>
 
 #include "device_utils.hpp"
@@ -1514,6 +1515,23 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   }
 }
 
+// Calls f(std::integral_constant<int, dim + 1>) for dim <= 8 (rows in registers), else
+// f(std::integral_constant<int, 0>) (runtime dim).
+template <class F>
+void with_ncol(int dim, F&& f) {
+  switch (dim) {
+    case 1: f(std::integral_constant<int, 2>{}); break;
+    case 2: f(std::integral_constant<int, 3>{}); break;
+    case 3: f(std::integral_constant<int, 4>{}); break;
+    case 4: f(std::integral_constant<int, 5>{}); break;
+    case 5: f(std::integral_constant<int, 6>{}); break;
+    case 6: f(std::integral_constant<int, 7>{}); break;
+    case 7: f(std::integral_constant<int, 8>{}); break;
+    case 8: f(std::integral_constant<int, 9>{}); break;
+    default: f(std::integral_constant<int, 0>{}); break;
+  }
+}
+
 bool items16() {
   static const bool v = [] {
     const char* e = std::getenv("PKD_PART_ITEMS");
@@ -1566,7 +1584,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   // Pair level l with l+1 (one fused scatter pass) when rows fit the register path and
   // l+1 needs no second-stage histogram.
   const char* pe = std::getenv("PKD_PAIR");
-  const bool pairs = dim <= 4 && !(pe && std::string(pe) == "0");
+  const bool pairs = dim <= 8 && !(pe && std::string(pe) == "0");
   for (int l = 0; pairs && l + 1 < lg_; ++l) {
     levels_[size_t(l)].pair = true;
     if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
@@ -1739,16 +1757,10 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.small_done = dim_ <= 8 ? 1 : 0;
     if (a.small_done) {
       const int g = int((segs + 3) / 4);
-      switch (dim_) {
-        case 1: k_refine_small<2><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 2: k_refine_small<3><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 3: k_refine_small<4><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 4: k_refine_small<5><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 5: k_refine_small<6><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 6: k_refine_small<7><<<g, kBlock, 0, stream>>>(a, segs); break;
-        case 7: k_refine_small<8><<<g, kBlock, 0, stream>>>(a, segs); break;
-        default: k_refine_small<9><<<g, kBlock, 0, stream>>>(a, segs); break;
-      }
+      with_ncol(dim_, [&](auto nc) {
+        constexpr int NC = decltype(nc)::value > 0 ? decltype(nc)::value : 9;
+        k_refine_small<NC><<<g, kBlock, 0, stream>>>(a, segs);
+      });
       PKD_LAUNCH_CHECK();
     }
     k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
@@ -1776,20 +1788,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const LevelPlan& lq = levels_[size_t(l + 1)];
       const size_t lds_a = size_t(2 * lp.next_bins) * 4;
       const int gs = int((lp.segs + 3) / 4);
-      switch (dim_) {
-        case 1: k_scan<2><<<grid, kBlock, lds_a, stream>>>(a); break;
-        case 2: k_scan<3><<<grid, kBlock, lds_a, stream>>>(a); break;
-        case 3: k_scan<4><<<grid, kBlock, lds_a, stream>>>(a); break;
-        default: k_scan<5><<<grid, kBlock, lds_a, stream>>>(a); break;
-      }
-      PKD_LAUNCH_CHECK();
-      switch (dim_) {
-        case 1: k_pivot_small<2><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<2><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
-        case 2: k_pivot_small<3><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<3><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
-        case 3: k_pivot_small<4><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<4><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
-        default: k_pivot_small<5><<<gs, kBlock, 0, stream>>>(a, lp.segs); k_pivot<5><<<int(lp.segs), kBlock, 0, stream>>>(a); break;
-      }
-      PKD_LAUNCH_CHECK();
+      with_ncol(dim_, [&](auto nc) {
+        constexpr int NC = decltype(nc)::value;
+        if constexpr (NC > 0) {
+          k_scan<NC><<<grid, kBlock, lds_a, stream>>>(a);
+          PKD_LAUNCH_CHECK();
+          k_pivot_small<NC><<<gs, kBlock, 0, stream>>>(a, lp.segs);
+          k_pivot<NC><<<int(lp.segs), kBlock, 0, stream>>>(a);
+          PKD_LAUNCH_CHECK();
+        }
+      });
       LevelArgs b = level_args(l + 1);
       k_select<<<int(lq.segs), kBlock, 0, stream>>>(b);
       PKD_LAUNCH_CHECK();
@@ -1807,21 +1815,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         PKD_LAUNCH_CHECK();
       }
       const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
-      if (items16()) {
-        switch (dim_) {
-          case 1: k_partition2<2, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          case 2: k_partition2<3, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          case 3: k_partition2<4, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          default: k_partition2<5, 16><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
+      with_ncol(dim_, [&](auto nc) {
+        constexpr int NC = decltype(nc)::value;
+        if constexpr (NC > 0) {
+          if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, stream>>>(a, pa);
+          else if (NC <= 5) k_partition2<NC, 8><<<grid, kBlock, lds_b, stream>>>(a, pa);
+          else k_partition2<NC, 4><<<grid, kBlock, lds_b, stream>>>(a, pa);
         }
-      } else {
-        switch (dim_) {
-          case 1: k_partition2<2, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          case 2: k_partition2<3, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          case 3: k_partition2<4, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-          default: k_partition2<5, 8><<<grid, kBlock, lds_b, stream>>>(a, pa); break;
-        }
-      }
+      });
       PKD_LAUNCH_CHECK();
       refine(b, lq.segs);
       std::swap(src, dst);
@@ -1829,23 +1830,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       continue;
     }
     const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
-    if (items16()) {
-      switch (dim_) {
-        case 1: k_partition<2, 16><<<grid, kBlock, lds, stream>>>(a); break;
-        case 2: k_partition<3, 16><<<grid, kBlock, lds, stream>>>(a); break;
-        case 3: k_partition<4, 16><<<grid, kBlock, lds, stream>>>(a); break;
-        case 4: k_partition<5, 16><<<grid, kBlock, lds, stream>>>(a); break;
-        default: k_partition<0, 16><<<grid, kBlock, lds, stream>>>(a); break;
-      }
-    } else {
-      switch (dim_) {
-        case 1: k_partition<2, 8><<<grid, kBlock, lds, stream>>>(a); break;
-        case 2: k_partition<3, 8><<<grid, kBlock, lds, stream>>>(a); break;
-        case 3: k_partition<4, 8><<<grid, kBlock, lds, stream>>>(a); break;
-        case 4: k_partition<5, 8><<<grid, kBlock, lds, stream>>>(a); break;
-        default: k_partition<0, 8><<<grid, kBlock, lds, stream>>>(a); break;
-      }
-    }
+    with_ncol(dim_, [&](auto nc) {
+      constexpr int NC = decltype(nc)::value;
+      if (NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, stream>>>(a);
+      else if (NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, stream>>>(a);
+      else k_partition<NC, 4><<<grid, kBlock, lds, stream>>>(a);
+    });
     PKD_LAUNCH_CHECK();
     refine(a, lp.segs);
     std::swap(src, dst);
