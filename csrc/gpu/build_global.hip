@@ -83,6 +83,54 @@ __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i6
   seg_n[h] = m;
 }
 
+// Bounding boxes are reduced without global atomics: every prep block writes one partial row
+// part[block][2 * dim] (orderable min | max), k_bbox_reduce folds them. (Same-address atomics
+// from thousands of waves serialise in L2 and cost hundreds of microseconds.)
+constexpr int kMaxBoxParts = 4096;
+
+template <int D>
+__device__ __forceinline__ void block_box_partial(const u32 (&mn)[D], const u32 (&mx)[D], u32* part) {
+  __shared__ u32 red[kBlock / 64][2 * D];
+  const int w = threadIdx.x / 64;
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    const u32 a = dev::wave_min_u32(mn[c]), b = dev::wave_max_u32(mx[c]);
+    if (dev::lane() == 0) {
+      red[w][c] = a;
+      red[w][D + c] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * D) {
+    const int c = threadIdx.x;
+    u32 v = red[0][c];
+    for (int k = 1; k < kBlock / 64; ++k) v = c < D ? min(v, red[k][c]) : max(v, red[k][c]);
+    part[size_t(blockIdx.x) * 2 * D + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bbox_reduce(const u32* __restrict__ part, int nparts, int dim,
+                                                        u32* __restrict__ bbox) {
+  __shared__ u32 red[kBlock / 64];
+  for (int c = 0; c < 2 * dim; ++c) {
+    const bool is_min = c < dim;
+    u32 v = is_min ? 0xffffffffu : 0u;
+    for (int q = threadIdx.x; q < nparts; q += kBlock) {
+      const u32 x = part[size_t(q) * 2 * dim + c];
+      v = is_min ? min(v, x) : max(v, x);
+    }
+    v = is_min ? dev::wave_min_u32(v) : dev::wave_max_u32(v);
+    if (dev::lane() == 0) red[threadIdx.x / 64] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u32 r = red[0];
+      for (int k = 1; k < kBlock / 64; ++k) r = is_min ? min(r, red[k]) : max(r, red[k]);
+      bbox[c] = r;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // AoS input -> SoA working columns (+ ids column) and the bounding box (orderable u32).
 // D > 0: one thread per row, the row's D loads issued before its D column stores (each
@@ -116,14 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
       }
       idcol[r] = id;
     }
-#pragma unroll
-    for (int c = 0; c < DD; ++c) {
-      const u32 a = dev::wave_min_u32(mn[c]), b = dev::wave_max_u32(mx[c]);
-      if (dev::lane() == 0) {
-        atomicMin(&bbox[c], a);
-        atomicMax(&bbox[DD + c], b);
-      }
-    }
+    block_box_partial<DD>(mn, mx, bbox);
     return;
   }
   for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sbox[c] = (c < dim) ? 0xffffffffu : 0u;
@@ -141,10 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
   for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride)
     idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
   __syncthreads();
-  for (int c = threadIdx.x; c < dim; c += kBlock) {
-    atomicMin(&bbox[c], sbox[c]);
-    atomicMax(&bbox[dim + c], sbox[dim + c]);
-  }
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) bbox[size_t(blockIdx.x) * 2 * dim + c] = sbox[c];
 }
 
 // d = 3, contiguous AoS input: a thread moves 4 rows with three 16-B loads and four 16-B
@@ -209,19 +247,13 @@ __global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts
     }
     reinterpret_cast<u32*>(cols + 3 * ncol)[r] = ids ? ids[r] : id_base + u32(r);
   }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const u32 lo = dev::wave_min_u32(mn[c]), hi = dev::wave_max_u32(mx[c]);
-    if (dev::lane() == 0) {
-      atomicMin(&bbox[c], lo);
-      atomicMax(&bbox[3 + c], hi);
-    }
-  }
+  block_box_partial<3>(mn, mx, bbox);
 }
 
 // bbox over SoA columns (distributed path: points arrive already in SoA).
 __global__ __launch_bounds__(kBlock) void k_bbox_soa(const float* __restrict__ cols, i64 n, int dim,
-                                                     u32* __restrict__ bbox, i64 ncol) {
+                                                     u32* __restrict__ part, i64 ncol) {
+  __shared__ u32 red[kBlock / 64][2];
   const i64 stride = i64(gridDim.x) * kBlock;
   for (int c = 0; c < dim; ++c) {
     u32 mn = 0xffffffffu, mx = 0u;
@@ -233,17 +265,23 @@ __global__ __launch_bounds__(kBlock) void k_bbox_soa(const float* __restrict__ c
     mn = dev::wave_min_u32(mn);
     mx = dev::wave_max_u32(mx);
     if (dev::lane() == 0) {
-      atomicMin(&bbox[c], mn);
-      atomicMax(&bbox[dim + c], mx);
+      red[threadIdx.x / 64][0] = mn;
+      red[threadIdx.x / 64][1] = mx;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int k = 1; k < kBlock / 64; ++k) {
+        mn = min(red[0][0], red[k][0]);
+        mx = max(red[0][1], red[k][1]);
+        red[0][0] = mn;
+        red[0][1] = mx;
+      }
+      part[size_t(blockIdx.x) * 2 * dim + c] = red[0][0];
+      part[size_t(blockIdx.x) * 2 * dim + dim + c] = red[0][1];
+    }
+    __syncthreads();
   }
 }
-
-__global__ void k_bbox_init(u32* bbox, int dim) {
-  for (int c = threadIdx.x; c < 2 * dim; c += blockDim.x) bbox[c] = (c < dim) ? 0xffffffffu : 0u;
-}
-
-// Root cell = bounding box; root bucketing parameters for the level-0 axis.
 __global__ void k_root(const u32* __restrict__ bbox, int dim, float* __restrict__ cells,
                        BucketParams* __restrict__ params, int axis0, int bins0) {
   for (int c = threadIdx.x; c < dim; c += blockDim.x) {
@@ -1616,7 +1654,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   off_hist0_ = take(size_t(max_hist_) * 4);
   off_hist1_ = take(size_t(max_hist_) * 4);
   off_hist2_ = take(size_t(std::max<i64>(max_hist2_, 1)) * 4);
-  off_bbox_ = take(size_t(2 * dim) * 4);
+  off_bbox_ = take(size_t(2 * dim) * 4 * (1 + kMaxBoxParts));  // final box + per-block partials
   off_err_ = take(16);
   ws_bytes_ = off;
 }
@@ -1664,7 +1702,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
-  k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
+  u32* part = bbox + 2 * dim_;
   const i64 total = dim_ <= 8 ? n_ : n_ * dim_;
   const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
   const size_t lds = size_t(2 * dim_) * 4;
@@ -1672,22 +1710,26 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
-    k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, bbox);
+    k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part);
+    PKD_LAUNCH_CHECK();
+    k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, g, dim_, bbox);
     PKD_LAUNCH_CHECK();
     run_levels(out_pts, out_ids, ws, stream);
     return;
   }
   switch (dim_) {
-    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
-    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, bbox, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 1: k_prep<1><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 2: k_prep<2><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 3: k_prep<3><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 4: k_prep<4><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 5: k_prep<5><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
   }
+  PKD_LAUNCH_CHECK();
+  k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }
@@ -1697,9 +1739,11 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
-  k_bbox_init<<<1, 64, 0, stream>>>(bbox, dim_);
+  u32* part = bbox + 2 * dim_;
   const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
-  k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, bbox, ncol_);
+  k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, part, ncol_);
+  PKD_LAUNCH_CHECK();
+  k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }

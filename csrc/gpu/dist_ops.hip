@@ -426,7 +426,7 @@ int stream_grid(i64 n) { return int(std::max<i64>(1, std::min<i64>(512, (n + 163
 void top_bbox(const TopPoints& p, i64* box, hipStream_t stream) {
   if (p.n <= 0) return;
   const int dim = p.dim;
-  const i64 want = std::min<i64>(p.n * dim, i64(1024) * kBlock);
+  const i64 want = std::min<i64>(p.n * dim, i64(256) * kBlock);  // few blocks: one atomic pair each
   const i64 T = std::max<i64>(dim, (want / dim) * dim);
   const int grid = int((T + kBlock - 1) / kBlock);
   k_top_bbox<<<grid, kBlock, size_t(2) * dim * 4, stream>>>(p, T, box);
