@@ -11,8 +11,9 @@ resident in HBM to the finished implicit in-order tree (ids + coordinates) in HB
   all-to-all, and each GPU builds its subtree. Strong scaling: the total point count is
   fixed, so `value` is the whole-job throughput.
 
-Data: the reference generator stream (std::mt19937 + uniform_real<float>(-100,100), seed 42)
-generated on the host with jump-ahead per rank, then copied to the GPU (untimed).
+Data: the reference generator stream (std::mt19937 + uniform_real<float>(-100,100), seed 42),
+each rank's slice generated on its own GPU by the device generator (csrc/gpu/generator.hip,
+bit-identical to the host stream; untimed).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -39,7 +40,9 @@ def main():
     ap.add_argument("--points", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=3)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--data", choices=["reference", "device"], default="reference")
+    ap.add_argument("--data", choices=["reference", "reference-host", "device"], default="reference",
+                    help="reference: the reference stream generated on the GPU (bit-identical to the host "
+                         "generator); reference-host: same stream generated on the host; device: torch RNG")
     ap.add_argument("--profile-levels", action="store_true", help="print per-phase timings to stderr")
     args = ap.parse_args()
 
@@ -70,6 +73,8 @@ def main():
         first, count = 0, n
 
     if args.data == "reference":
+        x = pk.generate_slice(args.seed, dim, first, count, device=dev)
+    elif args.data == "reference-host":
         x = pk.generate_slice(args.seed, dim, first, count).to(dev)
     else:
         x = pk.uniform_points(count, dim, seed=args.seed * 1000 + rank, device=dev)
@@ -121,7 +126,7 @@ def main():
             "vs_baseline": round(mpts / BASELINE_MPTS, 1),
             "dtype": "fp32",
             "data": f"synthetic: reference generator stream (mt19937 seed {args.seed}, uniform(-100,100))"
-                    if args.data == "reference" else "synthetic: on-device uniform(-100,100), reference value map",
+                    if args.data.startswith("reference") else "synthetic: on-device uniform(-100,100), reference value map",
             "config": {"model": "exact median-split kd-tree, cycling axis (implicit in-order layout)",
                        "global_batch": n, "seq_len": dim, "n_points": n, "dim": dim,
                        "parallelism": f"global{world}" if world > 1 else "single"},

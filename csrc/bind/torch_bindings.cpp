@@ -13,6 +13,7 @@
 #include "pkdtree/cpu_tree.hpp"
 #include "pkdtree/generator.hpp"
 #include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
 
 namespace pkdtree {
@@ -112,6 +113,29 @@ torch::Tensor generate(int64_t seed, int64_t dim, int64_t rows, int64_t first, i
   TORCH_CHECK(dim > 0 && rows >= 0 && first >= 0, "bad generator arguments");
   torch::Tensor x = torch::empty({rows, dim}, torch::kFloat32);
   pk::generate_rows(int(seed), int(dim), first, rows, x.data_ptr<float>(), int(threads));
+  return x;
+}
+
+// Rows [first, first + rows) of the reference stream generated on `out`'s GPU.
+torch::Tensor generate_gpu(int64_t seed, int64_t first, torch::Tensor out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.dim() == 2,
+              "out must be a contiguous float32 [rows, dim] GPU tensor");
+  TORCH_CHECK(first >= 0, "first must be >= 0");
+  const c10::DeviceGuard guard(out.device());
+  const pk::DevGenPlan p = pk::devgen_plan(uint64_t(out.size(0)) * uint64_t(out.size(1)));
+  torch::Tensor ws = torch::empty({int64_t(pk::devgen_workspace_bytes(p)) + 1},
+                                  out.options().dtype(torch::kUInt8));
+  pk::generate_rows_device(uint32_t(seed), int(out.size(1)), first, out.size(0), out.data_ptr<float>(),
+                           ws.data_ptr(), cur_stream(out));
+  return out;
+}
+
+// The device algorithm on the host (CPU oracle for the kernels' arithmetic).
+torch::Tensor generate_emulated(int64_t seed, int64_t dim, int64_t rows, int64_t first) {
+  TORCH_CHECK(dim > 0 && rows >= 0 && first >= 0, "bad generator arguments");
+  torch::Tensor x = torch::empty({rows, dim}, torch::kFloat32);
+  pk::devgen_emulate(uint32_t(seed), uint64_t(first) * uint64_t(dim), uint64_t(rows) * uint64_t(dim),
+                     x.data_ptr<float>());
   return x;
 }
 
@@ -231,6 +255,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       });
   m.def("generate", &generate, py::arg("seed"), py::arg("dim"), py::arg("rows"), py::arg("first") = 0,
         py::arg("threads") = 0);
+  m.def("generate_gpu", &generate_gpu, py::arg("seed"), py::arg("first"), py::arg("out"));
+  m.def("generate_emulated", &generate_emulated, py::arg("seed"), py::arg("dim"), py::arg("rows"),
+        py::arg("first") = 0);
+  m.def("devgen_plan", [](int64_t total) {
+    const pk::DevGenPlan p = pk::devgen_plan(uint64_t(total));
+    return std::vector<int64_t>{int64_t(p.S), int64_t(p.C), int64_t(p.R)};
+  });
   m.def("build_cpu", &build_cpu, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("mode") = "exact",
         py::arg("depth0") = 0, py::arg("threads") = 1);
   m.def("search_cpu", &search_cpu, py::arg("tree_pts"), py::arg("queries"), py::arg("depth0") = 0,

@@ -27,6 +27,7 @@ struct Options {
   int num_queries = 10;            // kdtree_sequential.cpp:144
   bool metrics = false;            // per-phase timings as one JSON line on stderr
   int device = 0;
+  bool host_gen = false;           // generate on the host and copy (default: on the GPU)
   std::vector<char*> positional;   // argv[0] + positionals
 };
 
@@ -48,6 +49,7 @@ inline Options parse(int argc, char** argv) {
     else if (a.rfind("--query", 0) == 0) o.query = val("--query");
     else if (a.rfind("--threads", 0) == 0) o.threads = std::atoi(val("--threads").c_str());
     else if (a.rfind("--queries", 0) == 0) o.num_queries = std::atoi(val("--queries").c_str());
+    else if (a == "--host-gen") o.host_gen = true;
     else if (a.rfind("--device", 0) == 0) o.device = std::atoi(val("--device").c_str());
     else o.positional.push_back(argv[i]);
   }

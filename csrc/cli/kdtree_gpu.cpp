@@ -1,10 +1,12 @@
 // kdtree_gpu — single-MI355X executable with the reference's protocol
 // (kdtree_sequential.cpp:140-208): host generation of the reference data, level-synchronous
-// HIP build, exact GPU queries. --metrics-json prints per-phase times (hipEvents) on stderr.
+// HIP build, exact GPU queries. The reference data are generated on the GPU
+// (csrc/gpu/generator.hip, bit-identical to the host stream) unless --host-gen. --metrics-json prints per-phase times (hipEvents) on stderr.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cmath>
+#include <algorithm>
 #include <cstdio>
 #include <iostream>
 #include <vector>
@@ -12,6 +14,7 @@
 #include "cli_common.hpp"
 #include "pkdtree/generator.hpp"
 #include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
 #include "pkdtree/hip_check.hpp"
 
@@ -30,17 +33,29 @@ int main(int argc, char** argv) {
   const int dim = p.dim;
   try {
     PKD_HIP_CHECK(hipSetDevice(o.device));
-    const auto g0 = std::chrono::high_resolution_clock::now();
-    std::vector<float> x = generate_problem(p.seed, dim, N + Q);
-    const auto g1 = std::chrono::high_resolution_clock::now();
     hipStream_t s;
     PKD_HIP_CHECK(hipStreamCreate(&s));
+    const size_t total = size_t(N + Q) * size_t(dim);
+    const auto g0 = std::chrono::high_resolution_clock::now();
+    std::vector<float> x;
+    float* d_x = nullptr;
+    PKD_HIP_CHECK(hipMalloc(&d_x, total * 4));
+    if (o.host_gen) {
+      x = generate_problem(p.seed, dim, N + Q);
+    } else {
+      const DevGenPlan gp = devgen_plan(total);
+      void* gws = nullptr;
+      PKD_HIP_CHECK(hipMalloc(&gws, std::max<size_t>(1, devgen_workspace_bytes(gp))));
+      generate_rows_device(uint32_t(p.seed), dim, 0, N + Q, d_x, gws, s);
+      PKD_HIP_CHECK(hipStreamSynchronize(s));
+      PKD_HIP_CHECK(hipFree(gws));
+    }
+    const auto g1 = std::chrono::high_resolution_clock::now();
     GpuBuilder b(N, dim);
-    float *d_x = nullptr, *d_tree = nullptr;
+    float* d_tree = nullptr;
     u32* d_ids = nullptr;
     u64* d_res = nullptr;
     void* ws = nullptr;
-    PKD_HIP_CHECK(hipMalloc(&d_x, x.size() * 4));
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(N) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(N) * 4));
     PKD_HIP_CHECK(hipMalloc(&d_res, size_t(Q) * 8));
@@ -48,7 +63,7 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1, e2, e3;
     for (hipEvent_t* e : {&e0, &e1, &e2, &e3}) PKD_HIP_CHECK(hipEventCreate(e));
     PKD_HIP_CHECK(hipEventRecord(e0, s));
-    PKD_HIP_CHECK(hipMemcpyAsync(d_x, x.data(), x.size() * 4, hipMemcpyHostToDevice, s));
+    if (o.host_gen) PKD_HIP_CHECK(hipMemcpyAsync(d_x, x.data(), total * 4, hipMemcpyHostToDevice, s));
     PKD_HIP_CHECK(hipEventRecord(e1, s));
     b.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);  // reference point IDs are 1..N
     PKD_HIP_CHECK(hipEventRecord(e2, s));

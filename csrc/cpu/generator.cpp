@@ -208,6 +208,113 @@ void MT19937::jump(uint64_t n) {
   idx = N;
 }
 
+// ---- device generator host side -------------------------------------------------------
+DevGenPlan devgen_plan(uint64_t total) {
+  DevGenPlan p;
+  p.total = total;
+  if (total == 0) return p;
+  // >= 64 twists per chunk so the jump rounds stay small next to generation; at most
+  // 2048 chunks (8 workgroups per CU on 256 CUs).
+  const uint64_t min_chunk = uint64_t(kMtWords) * 64;
+  uint64_t C = std::min<uint64_t>(2048, std::max<uint64_t>(1, total / min_chunk));
+  p.S = (total + C - 1) / C;
+  p.C = int((total + p.S - 1) / p.S);
+  while ((1 << p.R) < p.C) ++p.R;
+  return p;
+}
+
+void mt_window_after(uint32_t seed, uint64_t n, uint32_t* out) {
+  MT19937 g(seed);  // idx == N: mt is the window after 0 draws
+  if (n >= 4 * uint64_t(MT19937::N)) {
+    g.jump(n);  // a fresh generator takes the Horner path: mt = window after n, idx == N
+    std::copy(g.mt, g.mt + MT19937::N, out);
+    return;
+  }
+  Lin s;
+  std::copy(g.mt, g.mt + MT19937::N, s.st);
+  s.i = 0;
+  for (uint64_t k = 0; k < n; ++k) s.step();
+  for (int k = 0; k < MT19937::N; ++k) out[k] = s.st[(s.i + k) % MT19937::N];
+}
+
+std::vector<uint32_t> mt_jump_polys(uint64_t S, int R) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<uint64_t, int>, std::vector<uint32_t>>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : cache)
+    if (e.first.first == S && e.first.second == R) return e.second;
+  const Poly& phi = charpoly();
+  const int dm = pdeg(phi);
+  std::vector<uint32_t> out(size_t(R) * kMtWords, 0u);
+  Poly q = x_pow_mod(S, phi);
+  for (int r = 0; r < R; ++r) {
+    if (r > 0) {
+      q = psquare(q);
+      pmod(q, phi, dm);
+    }
+    for (int k = 0; k <= pdeg(q); ++k)
+      if (pbit(q, size_t(k))) out[size_t(r) * kMtWords + size_t(k / 32)] |= 1u << (k % 32);
+  }
+  if (cache.size() > 8) cache.erase(cache.begin());
+  cache.push_back({{S, R}, out});
+  return out;
+}
+
+namespace {
+// In-place twist of a 624-word block: the next 624 untempered words.
+void twist_block(uint32_t* mt) {
+  MT19937 g;
+  std::copy(mt, mt + MT19937::N, g.mt);
+  g.twist();
+  std::copy(g.mt, g.mt + MT19937::N, mt);
+}
+}  // namespace
+
+void devgen_emulate(uint32_t seed, uint64_t first_draw, uint64_t total, float* out) {
+  const DevGenPlan p = devgen_plan(total);
+  if (p.C == 0) return;
+  const int N = MT19937::N;
+  std::vector<uint32_t> states(size_t(p.C) * N);
+  mt_window_after(seed, first_draw, states.data());
+  const std::vector<uint32_t> polys = mt_jump_polys(p.S, p.R);
+  std::vector<uint32_t> ext(kMtExtWords);
+  for (int r = 0; r < p.R; ++r) {
+    const int src = 1 << r;
+    for (int i = 0; i < src && src + i < p.C; ++i) {
+      // extension of state i: the window, then 32 twisted blocks
+      std::copy(&states[size_t(i) * N], &states[size_t(i) * N] + N, ext.begin());
+      for (int b = 1; b < kMtExtWords / N; ++b) {
+        std::copy(ext.begin() + (b - 1) * N, ext.begin() + b * N, ext.begin() + b * N);
+        twist_block(&ext[size_t(b) * N]);
+      }
+      uint32_t* dst = &states[size_t(src + i) * N];
+      std::fill(dst, dst + N, 0u);
+      const uint32_t* q = &polys[size_t(r) * kMtWords];
+      for (int wi = 0; wi < kMtWords; ++wi)
+        for (uint32_t word = q[wi]; word; word &= word - 1) {
+          const int k = wi * 32 + __builtin_ctz(word);
+          for (int m = 0; m < N; ++m) dst[m] ^= ext[size_t(k + m)];
+        }
+    }
+  }
+  for (int c = 0; c < p.C; ++c) {
+    uint32_t mt[624];
+    std::copy(&states[size_t(c) * N], &states[size_t(c) * N] + N, mt);
+    const uint64_t b = uint64_t(c) * p.S, e = std::min(p.total, b + p.S);
+    for (uint64_t pos = b; pos < e; pos += N) {
+      twist_block(mt);
+      for (int j = 0; j < N && pos + uint64_t(j) < e; ++j) {
+        uint32_t y = mt[j];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        out[pos + uint64_t(j)] = u32_to_uniform(y);
+      }
+    }
+  }
+}
+
 std::vector<float> generate_problem(int seed, int dim, int64_t rows) {
   std::vector<float> x(size_t(rows) * size_t(dim));
   generate_rows(seed, dim, 0, rows, x.data(), 0);

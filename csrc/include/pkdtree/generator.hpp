@@ -45,6 +45,33 @@ inline float u32_to_uniform(uint32_t x, float a = -100.0f, float b = 100.0f) {
   return t + a;
 }
 
+// ---- device generator support (csrc/gpu/generator.hip) ---------------------------------
+// The stream [first_draw, first_draw + total) is cut into C chunks of S draws. Chunk c
+// starts from the MT state after first_draw + c*S draws. Chunk 0's state is computed on the
+// host; the others come from log2(C) doubling rounds on the device: in round r, chunk
+// 2^r + i is chunk i advanced by S*2^r draws, i.e. q_r(f) applied to chunk i's state with
+// q_r = x^(S*2^r) mod phi. Applying q(f) to a state s is a GF(2) correlation with the
+// state's own extension w (the untempered word sequence starting at s):
+//   (q(f) s)[m] = XOR over k with q_k = 1 of w[k + m],   m = 0..623.
+struct DevGenPlan {
+  uint64_t total = 0;  // draws
+  uint64_t S = 0;      // draws per chunk
+  int C = 0;           // chunks
+  int R = 0;           // doubling rounds (2^R >= C)
+};
+constexpr int kMtWords = 624;
+constexpr int kMtExtWords = 624 * 33;  // >= 19937 + 623: extension window per source state
+DevGenPlan devgen_plan(uint64_t total);
+// Untempered window after n draws from seed (624 words, logical order; next twist outputs
+// draw n). O(log n) via jump-ahead.
+void mt_window_after(uint32_t seed, uint64_t n, uint32_t* out);
+// R jump polynomials x^(S * 2^r) mod phi, r = 0..R-1, 624 little-endian u32 words each
+// (bit k = coefficient of x^k). Cached per (S, R).
+std::vector<uint32_t> mt_jump_polys(uint64_t S, int R);
+// The device algorithm run on the host (same plan, rounds and chunk generation): a CPU
+// oracle for the GPU kernels' arithmetic. Writes total draws as floats.
+void devgen_emulate(uint32_t seed, uint64_t first_draw, uint64_t total, float* out);
+
 // Rows [0, rows) of the reference stream.
 std::vector<float> generate_problem(int seed, int dim, int64_t rows);
 // Rows [first, first+rows) of the reference stream (jump-ahead; any first).

@@ -48,6 +48,8 @@ def main(argv=None) -> int:
     ap.add_argument("--query", choices=["auto", "brute", "traverse"], default="auto")
     ap.add_argument("--queries", type=int, default=10)
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--host-gen", action="store_true", help="generate the data on the host (default on a GPU: "
+                                                            "the bit-identical device generator)")
     ap.add_argument("--metrics-json", action="store_true")
     ap.add_argument("--save", default=None, help="write the built tree (PKDTREE file); forest: one file per rank "
                     "(<path>.rank<r>), global: the assembled tree from rank 0")
@@ -91,8 +93,9 @@ def main(argv=None) -> int:
         first, cnt = 0, n
     else:
         first, cnt = comm.forest_slice(n, world, rank)
-    x = pk.generate_slice(seed, dim, first, cnt).to(device)
-    q = pk.generate_slice(seed, dim, n, Q).to(device)
+    gen_dev = device if (device.type == "cuda" and not a.host_gen) else None
+    x = pk.generate_slice(seed, dim, first, cnt, device=gen_dev).to(device)
+    q = pk.generate_slice(seed, dim, n, Q, device=gen_dev).to(device)
     if device.type == "cuda":
         torch.cuda.synchronize()
     t_build = time.perf_counter()

@@ -5,6 +5,9 @@
 (Utility.cpp:6-18), including per-rank slices (kdtree_mpi.cpp:19-41) reached by an O(log)
 jump-ahead instead of ``discard`` (csrc/cpu/generator.cpp).
 
+``generate_slice(..., device="cuda")`` produces the same bits on the GPU (csrc/gpu/generator.hip):
+chunked mt19937 with device-side jump-ahead rounds, no serial walk over the stream.
+
 ``uniform_points`` is the fast on-device synthetic generator for benchmarks: a different
 random stream, but the same value map (``float(u32) / 2^32`` clamped below 1, ``*200 - 100``)
 so values take the same ~22.5 M distinct levels per axis (ties as in the reference data).
@@ -21,9 +24,17 @@ def generate_problem(seed: int, dim: int, num_points: int, threads: int = 0) -> 
     return native().generate(int(seed), int(dim), int(num_points), 0, int(threads))
 
 
-def generate_slice(seed: int, dim: int, first: int, rows: int, threads: int = 0) -> torch.Tensor:
-    """Rows first..first+rows-1 of the reference stream."""
+def generate_slice(seed: int, dim: int, first: int, rows: int, threads: int = 0, device=None) -> torch.Tensor:
+    """Rows first..first+rows-1 of the reference stream (on `device` if it is a GPU)."""
+    if device is not None and torch.device(device).type == "cuda":
+        out = torch.empty((int(rows), int(dim)), dtype=torch.float32, device=device)
+        return native().generate_gpu(int(seed), int(first), out)
     return native().generate(int(seed), int(dim), int(rows), int(first), int(threads))
+
+
+def generate_emulated(seed: int, dim: int, first: int, rows: int) -> torch.Tensor:
+    """The device generator's algorithm (chunk plan, jump rounds, twists) run on the host."""
+    return native().generate_emulated(int(seed), int(dim), int(rows), int(first))
 
 
 def u32_to_uniform(u: torch.Tensor, lo: float = -100.0, hi: float = 100.0) -> torch.Tensor:

@@ -61,3 +61,25 @@ def test_uniform_value_map():
     u = torch.tensor([0, 1, 2**31, 2**32 - 1, 2**32 - 128], dtype=torch.int64)
     v = u32_to_uniform(u)
     assert v[0] == -100.0 and v.max() < 100.0 and v.min() >= -100.0
+
+
+@pytest.mark.parametrize("seed,first,rows,dim", [(5, 0, 10, 3), (5, 17, 40_000, 3), (42, 1, 333_333, 1),
+                                                  (3, 99_991, 100_000, 3), (11, 0, 7_000, 128)])
+def test_device_algorithm_emulated(seed, first, rows, dim):
+    """The device generator's chunk plan and jump rounds, run on the host, equal the stream."""
+    from parallel_kd_tree_amd.utils.generator import generate_emulated
+    from parallel_kd_tree_amd.ops import native
+    S, C, R = native().devgen_plan(rows * dim)
+    assert C * S >= rows * dim and (1 << R) >= C
+    assert torch.equal(generate_emulated(seed, dim, first, rows), pk.generate_slice(seed, dim, first, rows))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,first,rows,dim", [(5, 0, 10, 3), (5, 17, 40_000, 3), (42, 1, 333_333, 1),
+                                                  (3, 12_500_000, 2_000_000, 3), (11, 0, 7_000, 128),
+                                                  (42, 0, 25_000_000, 3)])
+def test_device_generator_bit_exact(seed, first, rows, dim):
+    x = pk.generate_slice(seed, dim, first, rows, device="cuda")
+    torch.cuda.synchronize()
+    assert x.is_cuda and x.shape == (rows, dim)
+    assert torch.equal(x.cpu(), pk.generate_slice(seed, dim, first, rows))

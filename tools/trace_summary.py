@@ -16,8 +16,13 @@ def short(n):
     return m.group(1) if m else n[:40]
 
 
-starts = [i for i, r in enumerate(rows) if "k_bbox_init" in r["Kernel_Name"]]
+first_kernel = next((k for k in ("k_bbox_init", "k_bbox_reduce", "k_prep") if any(k in r["Kernel_Name"] for r in rows)), None)
+starts = [i for i, r in enumerate(rows) if first_kernel and first_kernel in r["Kernel_Name"]]
 last = rows[starts[-1]:] if starts else rows
+# the build ends at its subtree kernel (later dispatches belong to the caller)
+ends = [i for i, r in enumerate(last) if "k_subtree" in r["Kernel_Name"]]
+if ends:
+    last = last[:ends[0] + 1]
 tot = defaultdict(float)
 cnt = defaultdict(int)
 print("timeline of the last build:")
