@@ -6,6 +6,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include <memory>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -181,6 +182,29 @@ std::vector<torch::Tensor> search_cpu(const torch::Tensor& tree_pts, const torch
   return {slots, d2};
 }
 
+// Reference tree dumps (Utility.cpp:21-63) of a CPU implicit tree, as a string.
+std::string tree_dump(const torch::Tensor& tree_pts, const torch::Tensor& tree_ids, const std::string& what) {
+  check_points(tree_pts, false);
+  TORCH_CHECK(tree_ids.scalar_type() == torch::kInt32 && tree_ids.is_contiguous() &&
+                  tree_ids.numel() == tree_pts.size(0) && !tree_ids.is_cuda(),
+              "tree_ids must be int32 [n] on the CPU");
+  std::ostringstream os;
+  const auto* ids = reinterpret_cast<const pk::u32*>(tree_ids.data_ptr<int32_t>());
+  if (what == "tree") pk::print_tree(os, tree_pts.data_ptr<float>(), ids, tree_pts.size(0), int(tree_pts.size(1)));
+  else if (what == "head_and_leaves")
+    pk::print_head_and_leaves(os, tree_pts.data_ptr<float>(), ids, tree_pts.size(0), int(tree_pts.size(1)));
+  else TORCH_CHECK(false, "what must be tree or head_and_leaves");
+  return os.str();
+}
+
+std::string point_str(int64_t id, const torch::Tensor& coords) {
+  TORCH_CHECK(coords.scalar_type() == torch::kFloat32 && coords.is_contiguous() && !coords.is_cuda() &&
+                  coords.dim() == 1, "coords must be a float32 CPU vector");
+  std::ostringstream os;
+  pk::print_point(os, id, coords.data_ptr<float>(), int(coords.numel()));
+  return os.str();
+}
+
 int64_t invariant_violations(const torch::Tensor& tree_pts, const torch::Tensor& tree_ids, int64_t depth0) {
   check_points(tree_pts, false);
   TORCH_CHECK(tree_ids.scalar_type() == torch::kInt32 && !tree_ids.is_cuda(), "tree_ids must be CPU int32");
@@ -266,6 +290,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("depth0") = 0, py::arg("threads") = 1);
   m.def("search_cpu", &search_cpu, py::arg("tree_pts"), py::arg("queries"), py::arg("depth0") = 0,
         py::arg("brute") = false);
+  m.def("tree_dump", &tree_dump, py::arg("tree_pts"), py::arg("tree_ids"), py::arg("what") = "tree");
+  m.def("point_str", &point_str, py::arg("id"), py::arg("coords"));
   m.def("invariant_violations", &invariant_violations, py::arg("tree_pts"), py::arg("tree_ids"),
         py::arg("depth0") = 0);
   m.def("nn", &nn_gpu, py::arg("points"), py::arg("ids"), py::arg("id_base"), py::arg("queries"),

@@ -176,4 +176,59 @@ i64 count_invariant_violations(const float* tree_pts, const u32* tree_ids, i64 n
   return bad;
 }
 
+// ---- tree utilities ----------------------------------------------------------------------
+void print_point(std::ostream& os, i64 id, const float* coords, int dim) {
+  constexpr int kMaxPrintDimension = 5;  // Node.hpp:5
+  os << "Point(ID=" << id << ", dimension=" << dim << ", coordinates=[";
+  for (int d = 0; d < dim - 1; ++d) {
+    os << coords[d] << ", ";
+    if (d >= kMaxPrintDimension - 1) {
+      os << ", ..., ";
+      break;
+    }
+  }
+  if (dim > 0) os << coords[dim - 1];
+  os << "])";
+}
+
+namespace {
+void print_tree_rec(std::ostream& os, const float* tree_pts, const u32* tree_ids, int dim, i64 lo, i64 n, int depth) {
+  if (n <= 0) return;
+  const i64 m = lo + n / 2;
+  for (int d = 0; d < depth; ++d) os << "\t";
+  os << "NODE(@depth=" << depth << "): ";
+  print_point(os, i64(tree_ids[m]), tree_pts + size_t(m) * size_t(dim), dim);
+  os << "\n";
+  print_tree_rec(os, tree_pts, tree_ids, dim, lo, n / 2, depth + 1);
+  print_tree_rec(os, tree_pts, tree_ids, dim, m + 1, n - n / 2 - 1, depth + 1);
+}
+}  // namespace
+
+void print_tree(std::ostream& os, const float* tree_pts, const u32* tree_ids, i64 n, int dim) {
+  print_tree_rec(os, tree_pts, tree_ids, dim, 0, n, 0);
+}
+
+void print_head_and_leaves(std::ostream& os, const float* tree_pts, const u32* tree_ids, i64 n, int dim) {
+  if (n <= 0) return;
+  auto pt = [&](i64 k) { print_point(os, i64(tree_ids[k]), tree_pts + size_t(k) * size_t(dim), dim); };
+  const i64 head = n / 2;
+  i64 lo = 0, m = n;  // left-most leaf: keep the left child while it exists
+  while (m / 2 > 0) m = m / 2;
+  const i64 left = lo + m / 2;
+  lo = 0;
+  m = n;  // right-most leaf: keep the right child while it exists
+  while (m - m / 2 - 1 > 0) {
+    lo = lo + m / 2 + 1;
+    m = m - m / 2 - 1;
+  }
+  const i64 right = lo + m / 2;
+  os << "\nHead: ";
+  pt(head);
+  os << "\nLeft Leaf: ";
+  pt(left);
+  os << "\nRight Leaf: ";
+  pt(right);
+  os << "\n\n";
+}
+
 }  // namespace pkdtree

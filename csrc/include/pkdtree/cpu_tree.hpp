@@ -11,6 +11,7 @@
 // * nn_brute_cpu         — exact brute force with the reference's distance summation order.
 #pragma once
 #include <cstdint>
+#include <ostream>
 #include <vector>
 
 #include "pkdtree/common.hpp"
@@ -40,5 +41,15 @@ NNResult nn_brute_cpu(const float* pts, i64 n, int dim, const float* q);
 // left subtree is < the node and every element of the right subtree is > the node under
 // the (key, id) order on the node's axis. O(n log n).
 i64 count_invariant_violations(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0);
+
+// ---- tree utilities (Utility.cpp:21-63, Node.cpp:16-28) on the implicit layout ----------
+// operator<<(Point): "Point(ID=.., dimension=.., coordinates=[..])", at most
+// MAX_PRINT_DIMENSION (5) leading coordinates, with the reference's ", , ..., " artifact.
+void print_point(std::ostream& os, i64 id, const float* coords, int dim);
+// print_tree / print_tree_rec: pre-order, one "NODE(@depth=d): <point>" line per node,
+// indented by d tabs.
+void print_tree(std::ostream& os, const float* tree_pts, const u32* tree_ids, i64 n, int dim);
+// print_head_and_leaves: the root and the left-most / right-most leaves.
+void print_head_and_leaves(std::ostream& os, const float* tree_pts, const u32* tree_ids, i64 n, int dim);
 
 }  // namespace pkdtree

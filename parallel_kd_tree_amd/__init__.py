@@ -7,8 +7,9 @@ kernels, and forest / global multi-GPU decompositions over RCCL.
 """
 from .models import KDTree, Node, Point, build_tree, nearest_neighbor, tree_height
 from .utils.generator import generate_problem, generate_slice, uniform_points
+from .utils.tree_print import free_tree, print_head_and_leaves, print_tree
 
 __version__ = "0.1.0"
 
 __all__ = ["KDTree", "Node", "Point", "build_tree", "nearest_neighbor", "tree_height", "generate_problem",
-           "generate_slice", "uniform_points", "__version__"]
+           "generate_slice", "uniform_points", "print_tree", "print_head_and_leaves", "free_tree", "__version__"]
