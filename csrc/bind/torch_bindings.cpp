@@ -16,6 +16,7 @@
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
+#include "pkdtree/trace.hpp"
 
 namespace pkdtree {
 std::string subtree_stamp_report();
@@ -206,8 +207,19 @@ std::string point_str(int64_t id, const torch::Tensor& coords) {
 }
 
 int64_t invariant_violations(const torch::Tensor& tree_pts, const torch::Tensor& tree_ids, int64_t depth0) {
+  TORCH_CHECK(tree_ids.scalar_type() == torch::kInt32 && tree_ids.is_contiguous() &&
+                  tree_ids.numel() == tree_pts.size(0) && tree_ids.device() == tree_pts.device(),
+              "tree_ids must be int32 [n] on the points' device");
+  if (tree_pts.is_cuda()) {  // the device checker (query.hip)
+    check_points(tree_pts, true);
+    const c10::DeviceGuard guard(tree_pts.device());
+    torch::Tensor cnt = torch::zeros({1}, tree_pts.options().dtype(torch::kInt64));
+    pk::check_tree(tree_pts.data_ptr<float>(), reinterpret_cast<const pk::u32*>(tree_ids.data_ptr<int32_t>()),
+                   tree_pts.size(0), int(tree_pts.size(1)), int(depth0),
+                   reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), cur_stream(tree_pts));
+    return cnt.item<int64_t>();
+  }
   check_points(tree_pts, false);
-  TORCH_CHECK(tree_ids.scalar_type() == torch::kInt32 && !tree_ids.is_cuda(), "tree_ids must be CPU int32");
   return pk::count_invariant_violations(tree_pts.data_ptr<float>(),
                                         reinterpret_cast<const pk::u32*>(tree_ids.data_ptr<int32_t>()),
                                         tree_pts.size(0), int(tree_pts.size(1)), int(depth0));
@@ -290,6 +302,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("depth0") = 0, py::arg("threads") = 1);
   m.def("search_cpu", &search_cpu, py::arg("tree_pts"), py::arg("queries"), py::arg("depth0") = 0,
         py::arg("brute") = false);
+  m.def("trace_push", [](const std::string& name) { pk::trace_push(name.c_str()); }, py::arg("name"));
+  m.def("trace_pop", &pk::trace_pop);
   m.def("tree_dump", &tree_dump, py::arg("tree_pts"), py::arg("tree_ids"), py::arg("what") = "tree");
   m.def("point_str", &point_str, py::arg("id"), py::arg("coords"));
   m.def("invariant_violations", &invariant_violations, py::arg("tree_pts"), py::arg("tree_ids"),

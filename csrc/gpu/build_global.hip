@@ -22,6 +22,7 @@
 #include "device_utils.hpp"
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/hip_check.hpp"
+#include "pkdtree/trace.hpp"
 #include "subtree.hpp"
 
 namespace pkdtree {
@@ -1699,6 +1700,7 @@ void GpuBuilder::build_rows(const float* rows, float* out_pts, u32* out_ids, voi
 void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base,
                               float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
+  TraceRange tr("pkd.build");
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
@@ -1736,6 +1738,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
 
 void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
+  TraceRange tr("pkd.build");
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
@@ -1810,8 +1813,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
     PKD_LAUNCH_CHECK();
   };
+  static const char* const kLevelNames[] = {"pkd.level0", "pkd.level1", "pkd.level2", "pkd.level3",
+                                            "pkd.level4", "pkd.level5", "pkd.level6", "pkd.level7",
+                                            "pkd.level8", "pkd.level9", "pkd.level10", "pkd.level11+"};
   for (int l = 0; l < lg_;) {
     const LevelPlan& lp = levels_[size_t(l)];
+    TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
     LevelArgs a = level_args(l);
     if (l == 0) {
       PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
@@ -1886,6 +1893,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     l += 1;
   }
   const i64 heap0 = (i64(1) << lg_) - 1;
+  TraceRange trs("pkd.subtree");
   launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
                  out_ids, err, stream);
 }

@@ -15,6 +15,7 @@
 #include "pkdtree/common.hpp"
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/hip_check.hpp"
+#include "pkdtree/trace.hpp"
 
 namespace pkdtree {
 namespace {
@@ -164,6 +165,7 @@ void generate_rows_device(uint32_t seed, int dim, int64_t first_row, int64_t row
   const u64 total = u64(rows) * u64(dim);
   const DevGenPlan p = devgen_plan(total);
   if (p.C == 0) return;
+  TraceRange tr("pkd.generate");
   const WsLayout l = layout(p);
   char* ws = static_cast<char*>(workspace);
   u32* states = reinterpret_cast<u32*>(ws + l.states);

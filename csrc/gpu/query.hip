@@ -4,6 +4,7 @@
 #include "device_utils.hpp"
 #include "pkdtree/gpu_query.hpp"
 #include "pkdtree/hip_check.hpp"
+#include "pkdtree/trace.hpp"
 
 namespace pkdtree {
 
@@ -124,7 +125,47 @@ __global__ void k_finalize(const u64* __restrict__ packed, i64 nq, float* __rest
   ids[i] = i64(packed_idx(p));
 }
 
+// One thread per slot: walk from the root to the slot, checking the slot's side at every
+// ancestor; violations are wave-aggregated before the global atomic.
+__global__ __launch_bounds__(kBlock) void k_check(const float* __restrict__ tree_pts, const u32* __restrict__ tree_ids,
+                                                  i64 n, int dim, int depth0, unsigned long long* __restrict__ count) {
+  u32 bad = 0;
+  for (i64 k = i64(blockIdx.x) * kBlock + threadIdx.x; k < n; k += i64(gridDim.x) * kBlock) {
+    i64 lo = 0, m = n;
+    int depth = depth0;
+    const u32 idk = tree_ids[k];
+    while (m > 0) {
+      const i64 mid = lo + m / 2;
+      if (mid == k) break;
+      const int axis = depth % dim;
+      const u64 ck = composite_key(tree_pts[k * dim + axis], idk);
+      const u64 cm = composite_key(tree_pts[mid * dim + axis], tree_ids[mid]);
+      if (k < mid) {
+        bad += ck < cm ? 0u : 1u;
+        m = m / 2;
+      } else {
+        bad += ck > cm ? 0u : 1u;
+        lo = mid + 1;
+        m = m - m / 2 - 1;
+      }
+      ++depth;
+    }
+  }
+  const u64 tot = __ballot(bad != 0) ? u64(bad) : 0u;
+  u64 s = tot;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (dev::lane() == 0 && s) atomicAdd(count, (unsigned long long)s);
+}
+
 }  // namespace
+
+void check_tree(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, unsigned long long* count,
+                hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = int(std::min<i64>(8192, (n + kBlock - 1) / kBlock));
+  k_check<<<grid, kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, count);
+  PKD_LAUNCH_CHECK();
+}
 
 void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t stream) {
   if (nq <= 0) return;
@@ -141,6 +182,7 @@ void nn_init(u64* out, i64 nq, hipStream_t stream) {
 void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq, u64* out,
               hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
+  TraceRange tr("pkd.nn_brute");
   const i64 tiles = (nq + kQTile - 1) / kQTile;
   // enough point blocks to fill 256 CUs several times over across all query tiles
   const i64 want = std::max<i64>(1, 2048 / tiles);
@@ -156,6 +198,7 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries, i64 nq,
                  u64* out, hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
+  TraceRange tr("pkd.nn_traverse");
   k_traverse<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries, nq,
                                                                     out);
   PKD_LAUNCH_CHECK();

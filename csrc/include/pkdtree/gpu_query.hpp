@@ -28,6 +28,14 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
                  i64 nq, u64* out, hipStream_t stream);
 
+// Exact-mode invariant checked on the device (a semantic race detector for the partition
+// scatters): every slot k walks down from the root of its tree; at each
+// ancestor m it must sit on the side its slot says (k < m -> (key, id) below m's, k > m ->
+// above) on m's axis. Adds the number of violating (slot, ancestor) pairs to *count.
+// O(n log n) work, one thread per slot.
+void check_tree(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, unsigned long long* count,
+                hipStream_t stream);
+
 // packed -> (sqrt(d2) correctly rounded, id)
 void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t stream);
 

@@ -48,7 +48,8 @@ def _torch_flags():
                                         "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
     libdir = Path(torch.__file__).parent / "lib"
     ldflags = [f"-L{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-               "-lamdhip64", f"-Wl,-rpath,{libdir}"]
+               "-lamdhip64", f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
+               f"-Wl,-rpath,{ROCM / 'lib'}"]
     return cflags, ldflags
 
 
@@ -133,7 +134,7 @@ def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, j
             o = [objs[s] for s in srcs]
             extra = ["-lrccl"] if name == "kdtree_dist" else []
             if _stale(exe, o + core, 0.0):
-                _run(["g++", "-o", exe, *o, *core, f"-L{ROCM / 'lib'}", "-lamdhip64", *extra,
+                _run(["g++", "-o", exe, *o, *core, f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx", *extra,
                       f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"], verbose)
             out[name] = str(exe)
     return out

@@ -139,9 +139,12 @@ class KDTree:
 
     # ------------------------------------------------------------------ checks / io
     def invariant_violations(self) -> int:
-        """Exact-mode invariant (left < node < right under (key, id) on the node's axis)."""
-        return int(ops.native().invariant_violations(self.tree_pts.detach().cpu().contiguous(),
-                                                     self.tree_ids.detach().cpu().contiguous(), self.depth0))
+        """Exact-mode invariant (left < node < right under (key, id) on the node's axis); 0 iff
+        it holds. Runs on the tree's device: a HIP kernel for GPU trees (csrc/gpu/query.hip,
+        counts violating (point, ancestor) pairs), the recursive checker for CPU trees (counts
+        violating node sides)."""
+        return int(ops.native().invariant_violations(self.tree_pts.detach().contiguous(),
+                                                     self.tree_ids.detach().contiguous(), self.depth0))
 
     def save(self, path) -> None:
         tio.save_tree(path, self.tree_pts, self.tree_ids, self.depth0, self.mode)

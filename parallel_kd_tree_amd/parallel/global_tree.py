@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..utils.trace import trace_range
 from . import comm
 from .geometry import composite_u64, make_params, median_slot, segment
 
@@ -342,7 +343,8 @@ class GlobalTreeBuilder:
         idt = None if ids is None else ids.to(self.device, torch.int32).contiguous()
         scale = 1
         while True:
-            res = self._top_device(pts, idt, int(id_base), scale, timings, t0)
+            with trace_range("pkd.dist.top_levels"):
+                res = self._top_device(pts, idt, int(id_base), scale, timings, t0)
             if res is not None:
                 break
             if all(self._cap(l, scale) >= self.n_total for l in range(L)):
@@ -350,7 +352,8 @@ class GlobalTreeBuilder:
             scale *= 8
         send, in_splits, out_splits, top_rows = res
         recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=self.device)
-        comm.all_to_all_single_(recv, send, out_splits, in_splits)
+        with trace_range("pkd.dist.all_to_all"):
+            comm.all_to_all_single_(recv, send, out_splits, in_splits)
         self._tick(timings, "all_to_all", t0)
         if recv.shape[0] != self.n_leaf:
             raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
@@ -358,7 +361,8 @@ class GlobalTreeBuilder:
             tp = torch.empty((0, dim), dtype=torch.float32, device=self.device)
             ti = torch.empty((0,), dtype=torch.int32, device=self.device)
         else:
-            tp, ti = self._builder.build_rows(recv)
+            with trace_range("pkd.dist.local_build"):
+                tp, ti = self._builder.build_rows(recv)
         self._tick(timings, "local_build", t0)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
                         list(self.top_slots), top_rows[: P - 1], timings)

@@ -94,3 +94,13 @@ def test_point_node_facade():
 def test_tree_height():
     for n, h in [(0, 0), (1, 1), (2, 2), (3, 2), (4, 3), (1023, 10), (1024, 11), (500000, 19)]:
         assert pk.tree_height(n) == h
+
+
+def test_cpu_invariant_checker_catches_corruption():
+    x = pk.generate_problem(3, 3, 5000)
+    t = pk.KDTree.build(x, id_base=1)
+    assert t.invariant_violations() == 0
+    tp, ti = t.tree_pts.clone(), t.tree_ids.clone()
+    tp[[10, 4000]] = tp[[4000, 10]]
+    ti[[10, 4000]] = ti[[4000, 10]]
+    assert pk.KDTree(tp, ti).invariant_violations() > 0

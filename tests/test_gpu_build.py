@@ -77,3 +77,21 @@ def test_large_stage2_pairs(gpu_device):
     # 20M points: levels 0 and 1 both need the second-stage histogram, so the first pair
     # runs k_hist2p / k_select2 for its second level and the block-reserve count pass
     check_same(pk.generate_problem(5, 3, 20_000_000), gpu_device)
+
+
+@pytest.mark.parametrize("n,dim,depth0", [(1, 3, 0), (1000, 3, 0), (200_000, 3, 0), (100_000, 5, 2), (30_000, 8, 0)])
+def test_device_invariant_checker(gpu_device, n, dim, depth0):
+    """The HIP checker (semantic race detector) passes on built trees and catches corruption."""
+    x = pk.generate_problem(n + dim, dim, n)
+    t = pk.KDTree.build(x.to(gpu_device), id_base=1, depth0=depth0)
+    assert t.invariant_violations() == 0
+    cpu = pk.KDTree(t.tree_pts.cpu(), t.tree_ids.cpu(), depth0)
+    assert cpu.invariant_violations() == 0
+    if n > 2:  # swap the root with its left neighbour: both sides break
+        r = n // 2
+        for a in (t.tree_pts, t.tree_ids):
+            tmp = a[r].clone()
+            a[r] = a[r - 1]
+            a[r - 1] = tmp
+        assert t.invariant_violations() > 0
+        assert pk.KDTree(t.tree_pts.cpu(), t.tree_ids.cpu(), depth0).invariant_violations() > 0
