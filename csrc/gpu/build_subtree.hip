@@ -635,10 +635,11 @@ __device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32
 // Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
 __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
 
-// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+36 | aux nm+32 | fin nm+32 | tmpi u16 nm+32
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+36 | aux nm+32 | fin nm+32 | tmpi u16 nm+32 |
+//               root cell 2*dim
 size_t lds_words(int dim, int nm) {
   return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 36 + 2 * (size_t(nm) + 32) +
-         size_t(nm) / 2 + 16;
+         size_t(nm) / 2 + 16 + 2 * size_t(dim);
 }
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
@@ -696,6 +697,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   u32* aux = work + NM + 4 + 32;  // work: NM buckets, sentinel, 32 per-lane dummy words
   u32* fin = aux + NM + 32;           // aux / fin: NM entries + 32 per-lane dummies each
   u16* tmpi = reinterpret_cast<u16*>(fin + NM + 32);  // NM + 32 entries
+  float* cellv = reinterpret_cast<float*>(tmpi + NM + 32);  // [dim][2] root cell of the segment
   const u32 dummy = u32(NM + 4) + (tid & 31);
   stamp(a, 0);
 
@@ -709,6 +711,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         const int k = tid + i * THREADS;
         v[c][i] = (c <= dim && k < n) ? a.cols[i64(c) * a.ncol + glo + k] : 0.0f;
       }
+    for (int k = tid; k < 2 * dim; k += THREADS) cellv[k] = a.cells[h * dim * 2 + k];
 #pragma unroll
     for (int c = 0; c < kLoadCols; ++c)
 #pragma unroll
@@ -805,8 +808,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         const int w = tid + j * THREADS;
         if (w <= nb) work[w] = 0;
       }
-      const float* rc = a.cells + (h * dim + axis) * 2;
-      const BucketParams pr = make_params(rc[0], rc[1], B);
+      const BucketParams pr = make_params(cellv[2 * axis], cellv[2 * axis + 1], B);
       __syncthreads();
       if (t == 0) stamp(a, 20);
       u32 ok[ITEMS];
@@ -841,22 +843,37 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         cnt[i] = en - st[i];
         rank[i] = st[i] - work[nn[i] ? sg[i] * B : 0u];
       }
-      // all items' bucket scans advance together (their LDS reads overlap); wave-uniform
-      // trip count = largest bucket among the wave's items
-      for (u32 j = 0;; ++j) {
+      // in-bucket comparisons, kU members per round: all items' reads of a round are issued
+      // together; wave-uniform trip count = largest bucket among the wave's items / kU
+      constexpr u32 kU = 2;
+      for (u32 j0 = 0;; j0 += kU) {
         bool any = false;
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) any |= j < cnt[i];
+        for (int i = 0; i < ITEMS; ++i) any |= j0 < cnt[i];
         if (!__ballot(any)) break;
-        u32 qk[ITEMS];
+        u32 qk[kU][ITEMS];
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) qk[i] = tmpk[j < cnt[i] ? st[i] + j : 0u];
+        for (u32 u = 0; u < kU; ++u)
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-          const bool act = j < cnt[i];
-          rank[i] += (act && qk[i] < ok[i]) ? 1u : 0u;
-          const bool tie = act && qk[i] == ok[i] && st[i] + j != pos[i];
-          if (__ballot(tie)) rank[i] += (tie && idrow[tmpi[st[i] + j]] < idrow[tid + i * THREADS]) ? 1u : 0u;
+          for (int i = 0; i < ITEMS; ++i) qk[u][i] = tmpk[j0 + u < cnt[i] ? st[i] + j0 + u : 0u];
+        bool tany = false;
+#pragma unroll
+        for (u32 u = 0; u < kU; ++u)
+#pragma unroll
+          for (int i = 0; i < ITEMS; ++i) {
+            const bool act = j0 + u < cnt[i];
+            rank[i] += (act && qk[u][i] < ok[i]) ? 1u : 0u;
+            tany |= act && qk[u][i] == ok[i] && st[i] + j0 + u != pos[i];
+          }
+        if (__ballot(tany)) {  // equal keys: the id decides
+#pragma unroll
+          for (u32 u = 0; u < kU; ++u)
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+              const u32 q = st[i] + j0 + u;
+              const bool tie = j0 + u < cnt[i] && qk[u][i] == ok[i] && q != pos[i];
+              rank[i] += (tie && idrow[tmpi[tie ? q : 0u]] < idrow[tid + i * THREADS]) ? 1u : 0u;
+            }
         }
       }
       if (t == 0) stamp(a, 24);

@@ -1,5 +1,5 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  gputests 600 'python -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu' \
-  marker 200 'rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d gpurun_out/marker -o run -- python3 tools/bench_build.py --n 12500000 --steps 2' \
+  gputests 600 'python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu' \
+  smoke 120 'python -c "import __graft_entry__ as g; g.smoke()"' \
   bench 300 'python bench.py'
