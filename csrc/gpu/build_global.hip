@@ -40,7 +40,7 @@ constexpr int kChunk = kBlock * kItems;     // 4096 points per partition chunk
 constexpr int kMaxBins = 4096;              // per-segment histogram bins (global levels)
 constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one workgroup
 constexpr int kRadixBits = 11;
-constexpr i64 kLevelBlocks = 2048;          // partition-type grids of the top levels
+constexpr i64 kLevelBlocks = 2048;          // partition-type grids of the top levels (large builds)
 constexpr int kPairBins = 2048;             // bins of a level whose histogram a paired pass fuses (4 children)
 constexpr int kRadixBins = 1 << kRadixBits;
 
@@ -835,12 +835,14 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
     for (int c = 0; c <= dim; ++c) to[i64(c) * nc + q] = from[i64(c) * nc + p];
   };
 
-  // Large middle zone (heavy duplicates, or a huge segment): radix passes over the
-  // composite key, 11 bits at a time starting at the highest differing bit.
-  if (zc > CAP) {
+  // Middle zones above one wave: radix passes over the composite key, 11 bits at a time
+  // starting at the highest differing bit, each keeping only the digit bucket that holds
+  // rank t (a median bucket of ~1-2k rows needs one pass; a full LDS sort of it would take
+  // one workgroup ~66 barrier stages).
+  if (zc > 64) {
     const u64 diff = u64(st.mid_min) ^ u64(st.mid_max);
     int hb = diff ? 63 - __builtin_clzll(diff) : 0;
-    while (zc > CAP) {
+    while (zc > 64) {
       const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
       for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
       __syncthreads();
@@ -1579,6 +1581,17 @@ bool items16() {
   return v;
 }
 
+// Workgroups of a partition-type grid at the top levels: two rounds of 4 per CU for large
+// builds, one round below 64M points. Every block flushes its fused LDS histograms (up to
+// 8192 bins) with global atomics, so blocks must keep many rows each: at 12.5M points (a
+// rank's share of 100M on 8 GPUs) 1024 blocks build 7% faster than 2048, 1280 or 768
+// (profiles/r1_level_blocks_sweep.txt). PKD_LEVEL_BLOCKS overrides.
+i64 level_blocks_for(i64 n) {
+  const char* e = std::getenv("PKD_LEVEL_BLOCKS");
+  if (e) return std::max<i64>(1, std::atoll(e));
+  return n >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2;
+}
+
 int pow2_floor(i64 v) {
   int p = 1;
   while (i64(p) * 2 <= v) p *= 2;
@@ -1602,6 +1615,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
   max_bins_ = 0;
   max_hist_ = 1;
+  const i64 level_blocks = level_blocks_for(n_);
   for (int l = 0; l < lg_; ++l) {
     LevelPlan lp;
     lp.level = l;
@@ -1611,7 +1625,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
     // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
     // 256 CUs) while segments are few; one block per segment below that.
-    lp.bps = int(std::max<i64>(1, std::min<i64>(kLevelBlocks / lp.segs, (lp.nmax + kChunk - 1) / kChunk)));
+    lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + kChunk - 1) / kChunk)));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
     lp.stage2 = lp.nmax / lp.bins > kRefineCap;

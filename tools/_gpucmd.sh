@@ -1,5 +1,4 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
   gputests 600 'python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu' \
-  smoke 120 'python -c "import __graft_entry__ as g; g.smoke()"' \
-  bench 300 'python bench.py'
+  sizes 120 'python tools/bench_build.py --n 12500000 25000000 100000000 --steps 10'
