@@ -1,0 +1,312 @@
+// kdtree_dist — native multi-GPU driver with the reference MPI program's behaviour
+// (kdtree_mpi.cpp:170-291), one process per MI355X, RCCL over xGMI instead of MPI.
+//
+//   kdtree_dist --gpus P [options] [SEED DIM_POINTS NUM_POINTS]
+//
+// The launcher process parses the configuration (eval protocol: READY, seed on stdin; debug
+// protocol: argv), never touches the GPU, and forks P ranks. Rank 0 creates the RCCL unique
+// id and hands it to the other ranks through pipes (MPI_Init / Comm_rank / Comm_size,
+// :177-183). Then, exactly as the reference's forest decomposition:
+//   * config broadcast from rank 0 (MPI_Bcast of {seed, dim, N}, :199)   -> ncclBroadcast
+//   * rank r generates its generation-order slice local = N / P (remainder to the last
+//     rank, :204-224) on its own GPU — jump-ahead device generator, no discard() walk —
+//     plus the 10 queries (rows N .. N+9)
+//   * rank r builds its own local kd-tree (HIP level-synchronous builder) with global ids
+//   * every rank answers the queries on its tree; packed (d2 << 32 | id) results are
+//     MIN-reduced to rank 0 (MPI_Reduce MIN of the distances, :253)             -> ncclReduce
+//   * rank 0 prints the protocol lines.
+// Ranks with no points (N < P, the reference's segfault F7) contribute +inf.
+// Every collective is waited on with a watchdog: the stream is polled and
+// ncclCommGetAsyncError checked until a deadline (--timeout seconds, default 300); a stuck or
+// failed collective aborts the communicator and the rank exits non-zero, after which the
+// launcher stops the remaining ranks and returns non-zero.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cli_common.hpp"
+#include "pkdtree/generator.hpp"
+#include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_generator.hpp"
+#include "pkdtree/gpu_query.hpp"
+#include "pkdtree/hip_check.hpp"
+
+using namespace pkdtree;
+
+namespace {
+
+int g_rank = -1;
+
+#define PKD_NCCL_CHECK(expr)                                                                        \
+  do {                                                                                              \
+    ncclResult_t r_ = (expr);                                                                       \
+    if (r_ != ncclSuccess)                                                                          \
+      throw std::runtime_error(std::string("rank ") + std::to_string(g_rank) + ": " #expr " -> " + \
+                               ncclGetErrorString(r_));                                             \
+  } while (0)
+
+struct Config {
+  int seed, dim, num_points;
+};
+
+// Waits for everything enqueued on `s` (collectives included) with a deadline, polling the
+// communicator's asynchronous error state (the failure detector of SURVEY.md §5.3).
+void watchdog_wait(hipStream_t s, ncclComm_t comm, double timeout_s, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(q));
+    ncclResult_t async = ncclSuccess;
+    PKD_NCCL_CHECK(ncclCommGetAsyncError(comm, &async));
+    if (async != ncclSuccess) {
+      ncclCommAbort(comm);
+      throw std::runtime_error(std::string("rank ") + std::to_string(g_rank) + ": " + what +
+                               ": asynchronous RCCL error " + ncclGetErrorString(async));
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > timeout_s) {
+      ncclCommAbort(comm);
+      throw std::runtime_error(std::string("rank ") + std::to_string(g_rank) + ": " + what + ": no progress for " +
+                               std::to_string(timeout_s) + " s (watchdog)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+void write_all(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n) {
+    const ssize_t w = ::write(fd, c, n);
+    if (w <= 0) throw std::runtime_error("pipe write failed");
+    c += w;
+    n -= size_t(w);
+  }
+}
+void read_all(int fd, void* p, size_t n) {
+  char* c = static_cast<char*>(p);
+  while (n) {
+    const ssize_t r = ::read(fd, c, n);
+    if (r <= 0) throw std::runtime_error("pipe read failed (rank 0 died before sharing the RCCL id?)");
+    c += r;
+    n -= size_t(r);
+  }
+}
+
+int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vector<int>& id_pipes, double timeout_s,
+             std::chrono::high_resolution_clock::time_point tick) {
+  g_rank = rank;
+  PKD_HIP_CHECK(hipSetDevice(o.device + rank));
+  // RCCL prints a version banner on stdout during initialisation; stdout carries only the
+  // protocol, so fd 1 points at stderr until the communicator is up.
+  std::fflush(stdout);
+  const int saved_stdout = ::dup(1);
+  ::dup2(2, 1);
+  ncclUniqueId uid;
+  if (rank == 0) {
+    PKD_NCCL_CHECK(ncclGetUniqueId(&uid));
+    for (int r = 1; r < P; ++r) write_all(id_pipes[size_t(2 * r + 1)], &uid, sizeof(uid));
+  } else {
+    read_all(id_pipes[size_t(2 * rank)], &uid, sizeof(uid));
+  }
+  ncclComm_t comm;
+  PKD_NCCL_CHECK(ncclCommInitRank(&comm, P, uid, rank));
+  std::fflush(stdout);
+  ::dup2(saved_stdout, 1);
+  ::close(saved_stdout);
+  hipStream_t s;
+  PKD_HIP_CHECK(hipStreamCreate(&s));
+
+  // MPI_Bcast of the configuration (kdtree_mpi.cpp:199): rank 0's values win.
+  int* d_cfg = nullptr;
+  PKD_HIP_CHECK(hipMalloc(&d_cfg, 3 * sizeof(int)));
+  const int hcfg[3] = {cfg.seed, cfg.dim, cfg.num_points};
+  PKD_HIP_CHECK(hipMemcpyAsync(d_cfg, hcfg, sizeof(hcfg), hipMemcpyHostToDevice, s));
+  PKD_NCCL_CHECK(ncclBroadcast(d_cfg, d_cfg, 3, ncclInt32, 0, comm, s));
+  int bcfg[3];
+  PKD_HIP_CHECK(hipMemcpyAsync(bcfg, d_cfg, sizeof(bcfg), hipMemcpyDeviceToHost, s));
+  watchdog_wait(s, comm, timeout_s, "config broadcast");
+  cfg = Config{bcfg[0], bcfg[1], bcfg[2]};
+  const int dim = cfg.dim, Q = o.num_queries;
+  const i64 N = cfg.num_points;
+
+  // forest slice (kdtree_mpi.cpp:204-224): equal parts, remainder to the last rank
+  i64 local = N / P;
+  const i64 first = local * rank;
+  if (rank == P - 1) local += N % P;
+
+  const auto g0 = std::chrono::high_resolution_clock::now();
+  float* d_x = nullptr;
+  PKD_HIP_CHECK(hipMalloc(&d_x, size_t(std::max<i64>(local, 1) + Q) * dim * 4));
+  {
+    const DevGenPlan gp = devgen_plan(size_t(std::max<i64>(local, Q)) * dim);
+    void* gws = nullptr;
+    PKD_HIP_CHECK(hipMalloc(&gws, std::max<size_t>(1, devgen_workspace_bytes(gp))));
+    if (local > 0) generate_rows_device(uint32_t(cfg.seed), dim, first, local, d_x, gws, s);
+    generate_rows_device(uint32_t(cfg.seed), dim, N, Q, d_x + size_t(local) * dim, gws, s);  // the queries
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    PKD_HIP_CHECK(hipFree(gws));
+  }
+  const auto g1 = std::chrono::high_resolution_clock::now();
+
+  u64* d_res = nullptr;
+  PKD_HIP_CHECK(hipMalloc(&d_res, size_t(Q) * 8));
+  hipEvent_t e0, e1, e2;
+  for (hipEvent_t* e : {&e0, &e1, &e2}) PKD_HIP_CHECK(hipEventCreate(e));
+  float* d_tree = nullptr;
+  u32* d_ids = nullptr;
+  void* ws = nullptr;
+  std::unique_ptr<GpuBuilder> b;
+  if (local > 0) {  // allocations outside the timed region
+    b = std::make_unique<GpuBuilder>(local, dim);
+    PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(local) * 4));
+    PKD_HIP_CHECK(hipMalloc(&ws, b->workspace_bytes()));
+  }
+  PKD_HIP_CHECK(hipEventRecord(e0, s));
+  nn_init(d_res, Q, s);
+  if (local > 0) b->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);  // global 1-based ids (kdtree_mpi.cpp:223)
+  PKD_HIP_CHECK(hipEventRecord(e1, s));
+  if (local > 0) {
+    const float* d_q = d_x + size_t(local) * dim;
+    const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
+    if (traverse) nn_traverse(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);
+    else nn_brute(d_tree, d_ids, 0, local, dim, d_q, Q, d_res, s);
+  }
+  // MPI_Reduce(MIN) to rank 0 (kdtree_mpi.cpp:253), the id riding along in the low bits
+  PKD_NCCL_CHECK(ncclReduce(d_res, d_res, size_t(Q), ncclUint64, ncclMin, 0, comm, s));
+  PKD_HIP_CHECK(hipEventRecord(e2, s));
+  std::vector<u64> res(static_cast<size_t>(Q));
+  PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
+  watchdog_wait(s, comm, timeout_s, "build + queries + reduce");
+
+  // per-rank timings, MAX-reduced (the slowest rank bounds the job)
+  float bld = 0, qry = 0;
+  PKD_HIP_CHECK(hipEventElapsedTime(&bld, e0, e1));
+  PKD_HIP_CHECK(hipEventElapsedTime(&qry, e1, e2));
+  const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
+  float* d_t = nullptr;
+  PKD_HIP_CHECK(hipMalloc(&d_t, 3 * sizeof(float)));
+  const float ht[3] = {gen, bld, qry};
+  PKD_HIP_CHECK(hipMemcpyAsync(d_t, ht, sizeof(ht), hipMemcpyHostToDevice, s));
+  PKD_NCCL_CHECK(ncclReduce(d_t, d_t, 3, ncclFloat32, ncclMax, 0, comm, s));
+  float mt[3];
+  PKD_HIP_CHECK(hipMemcpyAsync(mt, d_t, sizeof(mt), hipMemcpyDeviceToHost, s));
+  watchdog_wait(s, comm, timeout_s, "timing reduce");
+
+  if (rank == 0) {
+    for (int q = 0; q < Q; ++q) print_result_line(N + q, std::sqrt(packed_dist(res[size_t(q)])));
+    if (o.debug) {
+      const auto tock = std::chrono::high_resolution_clock::now();
+      print_elapsed(std::chrono::duration<double>(tock - tick).count());
+    }
+    print_done();
+    std::cout.flush();
+    if (o.metrics)
+      std::fprintf(stderr,
+                   "{\"ranks\": %d, \"decomp\": \"forest\", \"gen_ms\": %.3f, \"build_ms\": %.3f, "
+                   "\"query_reduce_ms\": %.3f, \"build_mpts_per_s\": %.2f, \"local_global_levels\": %d}\n",
+                   P, mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f), b ? b->global_levels() : 0);
+  }
+  (void)hipFree(d_x); (void)hipFree(d_res); (void)hipFree(d_cfg); (void)hipFree(d_t);
+  if (d_tree) (void)hipFree(d_tree);
+  if (d_ids) (void)hipFree(d_ids);
+  if (ws) (void)hipFree(ws);
+  PKD_NCCL_CHECK(ncclCommDestroy(comm));
+  (void)hipStreamDestroy(s);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  // --gpus / --timeout are ours; everything else goes to the shared front-end
+  int P = 1;
+  double timeout_s = 300.0;
+  std::vector<char*> rest{argv[0]};
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    if ((a == "--gpus" || a == "--timeout") && i + 1 < argc) {
+      (a == "--gpus" ? void(P = std::atoi(argv[++i])) : void(timeout_s = std::atof(argv[++i])));
+    } else if (a.rfind("--gpus=", 0) == 0) {
+      P = std::atoi(a.c_str() + 7);
+    } else if (a.rfind("--timeout=", 0) == 0) {
+      timeout_s = std::atof(a.c_str() + 10);
+    } else {
+      rest.push_back(argv[i]);
+    }
+  }
+  if (P < 1 || P > 64) {
+    std::cerr << "--gpus must be in [1, 64]" << std::endl;
+    return 1;
+  }
+  cli::Options o = cli::parse(int(rest.size()), rest.data());
+  if (o.mode != "exact") {
+    std::cerr << "kdtree_dist builds exact trees only; use kdtree_sequential --mode reference" << std::endl;
+    return 1;
+  }
+  const auto tick = std::chrono::high_resolution_clock::now();
+  const Problem p = cli::specify(o);  // launcher: protocol I/O only, no GPU call before fork
+  std::cout.flush();
+  std::fflush(stdout);
+  std::fflush(stderr);
+  const Config cfg{p.seed, p.dim, p.num_points};
+
+  std::vector<int> fds(size_t(2 * P), -1);
+  for (int r = 1; r < P; ++r)
+    if (::pipe(&fds[size_t(2 * r)]) != 0) {
+      std::perror("pipe");
+      return 2;
+    }
+  std::vector<pid_t> kids;
+  for (int r = 0; r < P; ++r) {
+    const pid_t pid = ::fork();
+    if (pid < 0) {
+      std::perror("fork");
+      for (pid_t k : kids) ::kill(k, SIGTERM);
+      return 2;
+    }
+    if (pid == 0) {
+      int rc = 0;
+      try {
+        rc = run_rank(r, P, cfg, o, fds, timeout_s, tick);
+      } catch (const std::exception& ex) {
+        std::cerr << "kdtree_dist: " << ex.what() << std::endl;
+        rc = 2;
+      }
+      std::cout.flush();
+      std::fflush(stderr);
+      ::_exit(rc);
+    }
+    kids.push_back(pid);
+  }
+  for (int fd : fds)
+    if (fd >= 0) ::close(fd);
+  int rc = 0;
+  for (size_t done = 0; done < kids.size(); ++done) {
+    int st = 0;
+    const pid_t w = ::wait(&st);
+    if (w < 0) break;
+    const bool ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
+    if (!ok && rc == 0) {
+      rc = WIFEXITED(st) ? WEXITSTATUS(st) : 3;
+      for (pid_t k : kids)
+        if (k != w) ::kill(k, SIGTERM);  // a failed rank: stop the others (they would block in RCCL)
+    }
+  }
+  return rc;
+}

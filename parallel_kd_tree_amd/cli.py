@@ -12,8 +12,6 @@ one distributed tree (parallel/global_tree.py). Only rank 0 prints.
 from __future__ import annotations
 
 import argparse
-import contextlib
-import ctypes
 import json
 import os
 import sys
@@ -21,23 +19,6 @@ import time
 
 import numpy as np
 import torch
-
-
-@contextlib.contextmanager
-def _stdout_to_stderr():
-    """Point fd 1 at stderr (C and C++ stdio included) for the duration of the block."""
-    libc = ctypes.CDLL(None)
-    sys.stdout.flush()
-    libc.fflush(None)
-    saved = os.dup(1)
-    os.dup2(2, 1)
-    try:
-        yield
-    finally:
-        sys.stdout.flush()
-        libc.fflush(None)
-        os.dup2(saved, 1)
-        os.close(saved)
 
 
 def main(argv=None) -> int:
@@ -70,9 +51,7 @@ def main(argv=None) -> int:
 
     from .parallel import comm
     if world > 1:
-        # gloo prints "[Gloo] Rank r is connected ..." on stdout; stdout belongs to the protocol
-        with _stdout_to_stderr():
-            comm.init(backend="nccl" if device.type == "cuda" else "gloo", device=device)
+        comm.init(backend="nccl" if device.type == "cuda" else "gloo", device=device)
     from .utils import protocol
     debug = a.debug or bool(a.positional) or os.environ.get("KDTREE_DEBUG", "0") not in ("", "0")
     cfg = [0, 0, 0]

@@ -8,8 +8,11 @@ histograms) except the all-to-all redistribution of the global decomposition.
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
 import datetime
 import os
+import sys
 from typing import List, Optional, Tuple
 
 import torch
@@ -18,8 +21,28 @@ import torch.distributed as dist
 _device: Optional[torch.device] = None
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Point fd 1 at stderr (C and C++ stdio included) for the duration of the block: gloo
+    ("[Gloo] Rank r is connected ...") and RCCL (its version banner) print on stdout during
+    initialisation, and stdout carries only the protocol / the bench JSON line."""
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def init(backend: Optional[str] = None, device: Optional[torch.device] = None, timeout_s: int = 600) -> None:
-    """Initialise the default process group from the environment (idempotent)."""
+    """Initialise the default process group from the environment (idempotent). With the
+    nccl backend the communicator is created eagerly (device_id), inside the stdout guard."""
     global _device
     if dist.is_initialized():
         return
@@ -30,7 +53,11 @@ def init(backend: Optional[str] = None, device: Optional[torch.device] = None, t
     kw = {}
     if backend == "nccl" and device is not None:
         kw["device_id"] = device
-    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    with stdout_to_stderr():
+        dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if backend == "nccl":
+            # first collective on the communicator: any lazy RCCL setup prints here, not later
+            dist.barrier(device_ids=[device.index] if device is not None else None)
     _device = device if device is not None else torch.device("cpu")
 
 

@@ -21,3 +21,20 @@ def test_gpu_cli_eval_mode(bin_dir):
     a = out(bin_dir / "kdtree_gpu", [], stdin="3\n")
     b = out(bin_dir / "kdtree_sequential", ["--threads", "16"], stdin="3\n")
     assert a == b and a[0] == "READY" and a[-1] == "DONE"
+
+
+@pytest.mark.parametrize("cfg", [(42, 3, 1024), (3, 8, 200000), (1, 3, 1)])
+def test_dist_cli_one_rank(bin_dir, cfg):
+    """kdtree_dist (native RCCL forest driver, kdtree_mpi.cpp's protocol) with one rank: same
+    lines as the CPU executable; the RCCL init / broadcast / reduce path runs for real."""
+    assert out(bin_dir / "kdtree_dist", ["--gpus", 1, *cfg]) == out(bin_dir / "kdtree_sequential", cfg)
+
+
+def test_dist_cli_eval_mode_and_metrics(bin_dir):
+    r = subprocess.run([str(bin_dir / "kdtree_dist"), "--gpus", "1", "--metrics-json"], input="3\n",
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    b = out(bin_dir / "kdtree_sequential", ["--threads", "16"], stdin="3\n")
+    assert lines == b and lines[0] == "READY" and lines[-1] == "DONE"
+    assert '"decomp": "forest"' in r.stderr and '"ranks": 1' in r.stderr
