@@ -241,6 +241,7 @@ class GlobalTreeBuilder:
         self.record_timings = timings
         self._builder = None
         self._ws: Dict[str, torch.Tensor] = {}
+        self._scale = 1
         if self.device.type == "cuda" and self.n_leaf > 0:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
 
@@ -341,7 +342,7 @@ class GlobalTreeBuilder:
         t0 = [time.perf_counter()]
         pts = points.to(self.device, torch.float32).contiguous()
         idt = None if ids is None else ids.to(self.device, torch.int32).contiguous()
-        scale = 1
+        scale = self._scale  # sticky: a skewed input pays its all-gather retry once, not per build
         while True:
             with trace_range("pkd.dist.top_levels"):
                 res = self._top_device(pts, idt, int(id_base), scale, timings, t0)
@@ -350,6 +351,7 @@ class GlobalTreeBuilder:
             if all(self._cap(l, scale) >= self.n_total for l in range(L)):
                 raise RuntimeError("global top levels: middle buckets inconsistent at full capacity")
             scale *= 8
+        self._scale = scale
         send, in_splits, out_splits, top_rows = res
         recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=self.device)
         with trace_range("pkd.dist.all_to_all"):
