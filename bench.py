@@ -52,12 +52,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    # Rehearsal knobs for a one-GPU box (never set by the driver): PKD_BENCH_SHARE_GPU=1 puts
+    # every rank on cuda:0 and PKD_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks
+    # on one device. The timing is then meaningless; the control flow is the real one.
+    if os.environ.get("PKD_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     from parallel_kd_tree_amd.parallel import comm
     if world > 1:
-        comm.init(backend="nccl", device=dev)
+        comm.init(backend=os.environ.get("PKD_BENCH_BACKEND", "nccl"), device=dev)
     if rank == 0 and os.environ.get("PKD_SKIP_BUILD") != "1":
         from parallel_kd_tree_amd import _build
         _build.build()  # no-op when the in-tree extension is up to date
