@@ -1,5 +1,4 @@
 export TMPDIR=/tmp
-export PKD_BENCH_SHARE_GPU=1 PKD_BENCH_BACKEND=gloo
 python tools/gpu_steps.py \
-  bench2 300 'python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 3 --warmup 1' \
-  bench4 300 'python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --steps 3 --warmup 1'
+  graphtest 300 'python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_build.py -m gpu -k graphed' \
+  graphbench 200 'python tools/bench_graph.py 100000 1000000 4000000 12500000 100000000'
