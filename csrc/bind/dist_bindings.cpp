@@ -3,6 +3,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <optional>
 #include <vector>
 
@@ -102,16 +103,52 @@ void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level,
 
 void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base, torch::Tensor node,
           int64_t levels, const torch::Tensor& pivots, int64_t last_axis, int64_t P, torch::Tensor out,
-          torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
+          std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
   const c10::DeviceGuard g(pts.device());
   TopPoints p = points_of(pts, ids, id_base);
   check_cuda(out, torch::kFloat32, "out");
-  TORCH_CHECK(out.size(0) >= p.n && out.size(1) == p.dim + 1, "out must be [>= n, dim+1]");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= p.n && (out.size(1) == p.dim + 1 || out.size(1) == p.dim),
+              "out must be [>= n, dim+1] or [>= n, dim]");
   check_cuda(counts, torch::kInt64, "counts");
-  TORCH_CHECK(counts.numel() == 2 * P, "counts must have 2*P entries");
+  TORCH_CHECK(counts.numel() == 4 * P, "counts must have 4*P entries");
   TORCH_CHECK(size_t(scratch.numel()) >= top_pack_scratch_bytes(p.n, int(P)), "scratch too small");
-  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), out.data_ptr<float>(),
-           counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
+  u32* bm = nullptr;
+  int64_t words = 0;
+  if (bitmaps && bitmaps->defined()) {
+    check_cuda(*bitmaps, torch::kInt32, "bitmaps");
+    TORCH_CHECK(bitmaps->dim() == 2 && bitmaps->size(0) == P && bitmaps->size(1) * 32 >= p.n, "bitmaps must be [P, >= n/32]");
+    bm = u32p(*bitmaps);
+    words = bitmaps->size(1);
+  }
+  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), out.data_ptr<float>(), int(out.size(1)),
+           bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
+}
+
+// bitmaps: all sources' words back to back; per source (row offset, rows, word offset, words, id base)
+void ids_from_bm(const torch::Tensor& bitmaps, const std::vector<int64_t>& off, const std::vector<int64_t>& cnt,
+                 const std::vector<int64_t>& bm_off, const std::vector<int64_t>& words,
+                 const std::vector<int64_t>& base, torch::Tensor ids, torch::Tensor scratch, torch::Tensor err) {
+  const c10::DeviceGuard g(bitmaps.device());
+  check_cuda(bitmaps, torch::kInt32, "bitmaps");
+  check_cuda(ids, torch::kInt32, "ids");
+  const size_t P = off.size();
+  TORCH_CHECK(P >= 1 && P <= size_t(kBmMaxSources) && cnt.size() == P && bm_off.size() == P && words.size() == P &&
+                  base.size() == P,
+              "one row offset / count / bitmap offset / word count / id base per source");
+  BmSources src{};
+  int64_t max_words = 0;
+  for (size_t s = 0; s < P; ++s) {
+    src.off[s] = off[s];
+    src.cnt[s] = cnt[s];
+    src.bm_off[s] = bm_off[s];
+    src.words[s] = words[s];
+    src.base[s] = u32(base[s]);
+    TORCH_CHECK(off[s] >= 0 && off[s] + cnt[s] <= ids.numel(), "ids too small");
+    TORCH_CHECK(bm_off[s] >= 0 && bm_off[s] + words[s] <= bitmaps.numel(), "bitmap buffer too small");
+    max_words = std::max(max_words, words[s]);
+  }
+  TORCH_CHECK(size_t(scratch.numel()) >= ids_from_bitmaps_scratch_bytes(max_words, int(P)), "scratch too small");
+  ids_from_bitmaps(cu32p(bitmaps), int(P), src, u32p(ids), scratch.data_ptr(), u32p(err), stream_of(bitmaps));
 }
 
 }  // namespace
@@ -126,6 +163,9 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("top_pack", &pack);
   m.def("top_middle_words", [](int64_t dim, int64_t cap) { return int64_t(top_middle_words(int(dim), cap)); });
   m.def("top_pack_scratch_bytes", [](int64_t n, int64_t P) { return int64_t(top_pack_scratch_bytes(n, int(P))); });
+  m.def("ids_from_bitmaps", &ids_from_bm);
+  m.def("ids_from_bitmaps_scratch_bytes",
+        [](int64_t words, int64_t P) { return int64_t(ids_from_bitmaps_scratch_bytes(words, int(P))); });
 }
 
 }  // namespace pkdtree

@@ -1592,6 +1592,11 @@ i64 level_blocks_for(i64 n) {
   return n >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2;
 }
 
+i64 stage2_min() {
+  const char* e = std::getenv("PKD_STAGE2_MIN");
+  return e ? std::max<i64>(1, std::atoll(e)) : i64(kRefineCap);
+}
+
 int pow2_floor(i64 v) {
   int p = 1;
   while (i64(p) * 2 <= v) p *= 2;
@@ -1628,7 +1633,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + kChunk - 1) / kChunk)));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
-    lp.stage2 = lp.nmax / lp.bins > kRefineCap;
+    lp.stage2 = lp.nmax / lp.bins > stage2_min();
     if (lp.stage2) max_hist2_ = std::max<i64>(max_hist2_, lp.segs * kBins2);
     levels_.push_back(lp);
     max_bins_ = std::max(max_bins_, lp.bins);

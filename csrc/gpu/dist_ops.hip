@@ -364,8 +364,8 @@ __global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u
     u32 s = 0;
     for (int b = 0; b < blocks; ++b) s += bcount[i64(b) * P + d];
     tot[d] = s;
-    counts[2 * d] = i64(s);
-    counts[2 * d + 1] = i64(*err);
+    counts[4 * d] = i64(s);
+    counts[4 * d + 1] = i64(*err);
   }
   __syncthreads();
   if (d < P) {
@@ -380,7 +380,7 @@ __global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u
 
 __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int P,
                                                          i64 per_block, const u32* __restrict__ offsets,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out, int rs) {
   __shared__ u32 cur[64];
   __shared__ u32 wcnt[kBlock / 64][64];
   const u32 first = u32(P - 1);
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   __syncthreads();
   const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const int w = threadIdx.x / 64, ln = dev::lane();
-  const int dim = p.dim, rs = dim + 1;
+  const int dim = p.dim;
   for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
     const i64 i = c0 + threadIdx.x;
     const u32 h = i < b1 ? node[i] : kTopDone;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
       float* o = out + i64(off + my) * rs;
       const float* r = p.pts + i * dim;
       for (int c = 0; c < dim; ++c) o[c] = r[c];
-      o[dim] = __uint_as_float(point_id(p, i));
+      if (rs > dim) o[dim] = __uint_as_float(point_id(p, i));
     }
     __syncthreads();
     if (threadIdx.x < P) {
@@ -416,6 +416,97 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
     }
     __syncthreads();
   }
+}
+
+// Destination bitmaps of the compact exchange: bm[d][w] bit j = row 32w + j goes to leaf d.
+// One wave per 64 rows (two words), one ballot per destination; rows >= n give zero words,
+// so the grid covers the whole padded stride.
+__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int P, i64 ws,
+                                                        u32* __restrict__ bm) {
+  const i64 wave = (i64(blockIdx.x) * kBlock + threadIdx.x) / 64;
+  const int ln = dev::lane();
+  const i64 row = wave * 64 + ln;
+  const u32 first = u32(P - 1);
+  const u32 h = row < n ? node[row] : kTopDone;
+  const int d = h == kTopDone ? -1 : int(h - first);
+  for (int e = 0; e < P; ++e) {
+    const u64 m = __ballot(d == e);
+    const i64 w = 2 * wave + (ln & 1);
+    if (ln < 2 && w < ws) bm[i64(e) * ws + w] = ln == 0 ? u32(m) : u32(m >> 32);
+  }
+}
+
+// Receiver side: popcount sums of kBmWords-word blocks of every source's bitmap.
+constexpr int kBmWords = 2048;  // words per block (8 per thread)
+__global__ __launch_bounds__(kBlock) void k_bm_block_sums(const u32* __restrict__ bm, BmSources srcs, int nblk,
+                                                          u32* __restrict__ bsum) {
+  const int s = blockIdx.y, b = blockIdx.x;
+  const u32* src = bm + srcs.bm_off[s];
+  const i64 ws = srcs.words[s];
+  u32 c = 0;
+  for (int k = threadIdx.x; k < kBmWords; k += kBlock) {
+    const i64 w = i64(b) * kBmWords + k;
+    c += w < ws ? u32(__popc(src[w])) : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ u32 part[kBlock / 64];
+  if (dev::lane() == 0) part[threadIdx.x / 64] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 t = 0;
+    for (int v = 0; v < kBlock / 64; ++v) t += part[v];
+    bsum[i64(s) * nblk + b] = t;
+  }
+}
+
+// ids[recv_off[s] + k] = id_base[s] + (position of the k-th set bit of source s's bitmap):
+// the rows of a source arrive in its stable pack order, i.e. by increasing source row.
+__global__ __launch_bounds__(kBlock) void k_bm_ids(const u32* __restrict__ bm, int nblk, const u32* __restrict__ bsum,
+                                                   BmSources src, u32* __restrict__ ids, u32* __restrict__ err) {
+  constexpr int kPer = kBmWords / kBlock;
+  const int s = blockIdx.y, b = blockIdx.x;
+  const i64 ws = src.words[s];
+  const i64 last = ws > 0 ? (ws - 1) / kBmWords : 0;  // this source's last block
+  if (b > last) return;
+  __shared__ u32 part[kBlock / 64];
+  __shared__ u32 wtot[kBlock / 64];
+  // words of blocks before b
+  u32 pre = 0;
+  for (int k = threadIdx.x; k < b; k += kBlock) pre += bsum[i64(s) * nblk + k];
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (dev::lane() == 0) part[threadIdx.x / 64] = pre;
+  const u32* sb = bm + src.bm_off[s];
+  const i64 w0 = i64(b) * kBmWords + i64(threadIdx.x) * kPer;
+  u32 words[kPer], cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    words[j] = w0 + j < ws ? sb[w0 + j] : 0u;
+    cnt += u32(__popc(words[j]));
+  }
+  const u32 incl = dev::wave_incl_scan(cnt);
+  if (dev::lane() == 63) wtot[threadIdx.x / 64] = incl;
+  __syncthreads();
+  u32 base = 0, before = 0;
+  for (int v = 0; v < kBlock / 64; ++v) {
+    base += part[v];
+    if (v < int(threadIdx.x / 64)) before += wtot[v];
+  }
+  u32 k = base + before + incl - cnt;  // rank of this thread's first set bit within source s
+  const i64 off = src.off[s];
+  const u32 idb = src.base[s];
+  const i64 cap = src.cnt[s];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    u32 x = words[j];
+    while (x) {
+      const int t = __ffs(int(x)) - 1;
+      x &= x - 1;
+      if (i64(k) < cap) ids[off + k] = idb + u32((w0 + j) * 32 + t);
+      else atomicOr(err, 8u);
+      ++k;
+    }
+  }
+  if (b == last && threadIdx.x == kBlock - 1 && i64(k) != cap) atomicOr(err, 8u);
 }
 
 int pack_blocks(i64 n) { return int(std::max<i64>(1, std::min<i64>(2048, (n + 8191) / 8192))); }
@@ -482,8 +573,11 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
 size_t top_pack_scratch_bytes(i64 n, int P) { return size_t(2) * pack_blocks(n) * size_t(P) * 4; }
 
 void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
-              i64* counts, const u32* err, void* scratch, hipStream_t stream) {
+              int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch,
+              hipStream_t stream) {
   if (P > 64 || P != (1 << levels)) throw std::invalid_argument("top_pack: P must be 2^levels <= 64");
+  if (row_stride != p.dim && row_stride != p.dim + 1) throw std::invalid_argument("top_pack: row stride dim or dim+1");
+  if (bitmaps && bitmap_words * 32 < p.n) throw std::invalid_argument("top_pack: bitmap stride too small");
   const int blocks = pack_blocks(p.n);
   const i64 per_block = (std::max<i64>(p.n, 1) + blocks - 1) / blocks;
   u32* bcount = static_cast<u32*>(scratch);
@@ -492,7 +586,29 @@ void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int 
   PKD_LAUNCH_CHECK();
   k_pack_scan<<<1, 64, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
   PKD_LAUNCH_CHECK();
-  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, per_block, offsets, out_rows);
+  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, per_block, offsets, out_rows, row_stride);
+  PKD_LAUNCH_CHECK();
+  if (bitmaps) {
+    const i64 waves = (bitmap_words + 1) / 2;
+    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, P, bitmap_words, bitmaps);
+    PKD_LAUNCH_CHECK();
+  }
+}
+
+size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P) {
+  return size_t(P) * size_t(std::max<i64>(1, (max_words + kBmWords - 1) / kBmWords)) * 4;
+}
+
+void ids_from_bitmaps(const u32* bitmaps, int P, const BmSources& src, u32* ids, void* scratch, u32* err,
+                      hipStream_t stream) {
+  if (P > kBmMaxSources) throw std::invalid_argument("ids_from_bitmaps: too many sources");
+  i64 max_words = 0;
+  for (int s = 0; s < P; ++s) max_words = std::max(max_words, src.words[s]);
+  const int nblk = int(std::max<i64>(1, (max_words + kBmWords - 1) / kBmWords));
+  u32* bsum = static_cast<u32*>(scratch);
+  k_bm_block_sums<<<dim3(nblk, P), kBlock, 0, stream>>>(bitmaps, src, nblk, bsum);
+  PKD_LAUNCH_CHECK();
+  k_bm_ids<<<dim3(nblk, P), kBlock, 0, stream>>>(bitmaps, nblk, bsum, src, ids, err);
   PKD_LAUNCH_CHECK();
 }
 

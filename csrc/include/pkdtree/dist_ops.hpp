@@ -71,10 +71,31 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream);
 
 // Final routing below the last top level + counting sort of rows by destination leaf
-// (dest = node - (P - 1)): out_rows [n_kept][dim+1] grouped by destination (stable),
-// counts [P][2] int64 = (rows for dest, err word). Pivot points are dropped.
+// (dest = node - (P - 1)): out_rows [n_kept][row_stride] grouped by destination (stable),
+// row_stride = dim + 1 (coordinates, id bits) or dim (compact: coordinates only). counts
+// [P][4] int64 = (rows for dest, err word, 2 words left to the caller). Pivot points are dropped. With
+// `bitmaps` ([P][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the destination of every
+// row is also written as one bit per (dest, row): the compact exchange sends 12-B rows plus
+// n / 8 bytes per destination instead of 16-B rows, and the receiver rebuilds the ids.
 size_t top_pack_scratch_bytes(i64 n, int P);
 void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
-              i64* counts, const u32* err, void* scratch, hipStream_t stream);
+              int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch,
+              hipStream_t stream);
+
+// Receiver of the compact exchange: rows from source s occupy [off[s], off[s] + cnt[s]) of
+// the receive buffer in increasing source-row order, so the k-th row from s has the id
+// base[s] + (position of the k-th set bit of s's bitmap, words [bm_off[s], bm_off[s] +
+// words[s]) of `bitmaps`). err |= 8 if a bitmap's popcount differs from cnt[s].
+constexpr int kBmMaxSources = 64;
+struct BmSources {
+  i64 off[kBmMaxSources];
+  i64 cnt[kBmMaxSources];
+  i64 bm_off[kBmMaxSources];
+  i64 words[kBmMaxSources];
+  u32 base[kBmMaxSources];
+};
+size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P);
+void ids_from_bitmaps(const u32* bitmaps, int P, const BmSources& src, u32* ids, void* scratch, u32* err,
+                      hipStream_t stream);
 
 }  // namespace pkdtree

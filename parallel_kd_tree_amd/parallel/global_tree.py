@@ -20,6 +20,7 @@ CPU tests, where the per-rank device ops run as torch code with identical arithm
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -246,8 +247,12 @@ class GlobalTreeBuilder:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
 
     def read_error(self) -> int:
-        """Device error word of the last local subtree build (0 = ok). Synchronises."""
-        return self._builder.read_error() if self._builder is not None else 0
+        """Device error word of the last build (0 = ok): the local subtree build's, plus 8 if the
+        compact exchange's id bitmaps disagreed with the received row counts. Synchronises."""
+        e = self._builder.read_error() if self._builder is not None else 0
+        if "err" in self._ws:
+            e |= int(self._ws["err"][0].item()) & 8
+        return e
 
     # ------------------------------------------------------------------------------------
     def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
@@ -317,24 +322,38 @@ class GlobalTreeBuilder:
             nat.top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err)
             self._tick(timings, f"top_level{level}", t0)
         last_axis = (self.depth0 + L - 1) % dim
-        send = self._buf("send", (max(n_local, 1), dim + 1), torch.float32)
-        counts = torch.empty(2 * P, dtype=torch.int64, device=dev)
+        # Compact exchange (implicit ids): 12-B rows plus one bit per (source row, destination);
+        # the receiver rebuilds the ids from the bitmaps (csrc/gpu/dist_ops.hip, ids_from_bitmaps).
+        compact = idt is None and os.environ.get("PKD_COMPACT_EXCHANGE", "1") != "0"
+        rs = dim if compact else dim + 1
+        send = self._buf("send_c" if compact else "send", (max(n_local, 1), rs), torch.float32)
+        counts = torch.empty(4 * P, dtype=torch.int64, device=dev)  # per dest: rows, err, id base, n_local
+        cv = counts.view(P, 4)
+        cv[:, 2] = int(id_base)
+        cv[:, 3] = int(n_local)
+        words = max(1, (n_local + 31) // 32)
+        bm = None
+        if compact:
+            bm = self._buf("bm", (P, words), torch.int32)
         scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, P),), torch.uint8)
-        nat.top_pack(pts, idt, id_base, node, L, pivots, last_axis, P, send, counts, err, scratch)
+        nat.top_pack(pts, idt, id_base, node, L, pivots, last_axis, P, send, bm, counts, err, scratch)
         recv_counts = torch.empty_like(counts)
         comm.all_to_all_single_(recv_counts, counts)
         both = torch.cat([counts, recv_counts]).cpu()  # the only host read-back of the build
         self._tick(timings, "pack", t0)
+        mine, theirs = both[:4 * P].view(P, 4), both[4 * P:].view(P, 4)
         errs = 0
-        for v in both[1::2].tolist():
+        for v in torch.cat([mine[:, 1], theirs[:, 1]]).tolist():
             errs |= int(v)
         if errs & 2:
             raise RuntimeError("global top levels: histogram totals disagree with the tree geometry")
         if errs & 1:
             return None  # a middle bucket overflowed its all-gather slot: retry larger
-        in_splits = both[0:2 * P:2].tolist()
-        out_splits = both[2 * P::2].tolist()
-        return send[: sum(in_splits)], in_splits, out_splits, top_rows
+        in_splits = mine[:, 0].tolist()
+        out_splits = theirs[:, 0].tolist()
+        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err,
+              "src_base": theirs[:, 2].tolist(), "src_n": theirs[:, 3].tolist()}
+        return send[: sum(in_splits)], in_splits, out_splits, top_rows, ex
 
     def _build_device(self, points, ids, id_base) -> DistTree:
         dim, P, L = self.dim, self.P, self.L
@@ -352,10 +371,14 @@ class GlobalTreeBuilder:
                 raise RuntimeError("global top levels: middle buckets inconsistent at full capacity")
             scale *= 8
         self._scale = scale
-        send, in_splits, out_splits, top_rows = res
-        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32, device=self.device)
+        send, in_splits, out_splits, top_rows, ex = res
+        recv = torch.empty((sum(out_splits), ex["rs"]), dtype=torch.float32, device=self.device)
         with trace_range("pkd.dist.all_to_all"):
             comm.all_to_all_single_(recv, send, out_splits, in_splits)
+            if ex["compact"]:
+                src_words = [max(1, (int(v) + 31) // 32) for v in ex["src_n"]]
+                recv_bm = self._buf("recv_bm", (sum(src_words),), torch.int32)
+                comm.all_to_all_single_(recv_bm, ex["bm"].view(-1), src_words, [ex["words"]] * P)
         self._tick(timings, "all_to_all", t0)
         if recv.shape[0] != self.n_leaf:
             raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
@@ -364,7 +387,18 @@ class GlobalTreeBuilder:
             ti = torch.empty((0,), dtype=torch.int32, device=self.device)
         else:
             with trace_range("pkd.dist.local_build"):
-                tp, ti = self._builder.build_rows(recv)
+                if ex["compact"]:
+                    nat = ops.native()
+                    off = np.concatenate([[0], np.cumsum(out_splits)[:-1]]).astype(np.int64).tolist()
+                    bm_off = np.concatenate([[0], np.cumsum(src_words)[:-1]]).astype(np.int64).tolist()
+                    ids = self._buf("ids", (self.n_leaf,), torch.int32)
+                    scr = self._buf("bm_scratch", (nat.ids_from_bitmaps_scratch_bytes(max(src_words), P),),
+                                    torch.uint8)
+                    nat.ids_from_bitmaps(recv_bm, off, out_splits, bm_off, src_words, ex["src_base"], ids, scr,
+                                         ex["err"])
+                    tp, ti = self._builder.build(recv, ids, 0)
+                else:
+                    tp, ti = self._builder.build_rows(recv)
         self._tick(timings, "local_build", t0)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
                         list(self.top_slots), top_rows[: P - 1], timings)

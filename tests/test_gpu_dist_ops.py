@@ -135,14 +135,40 @@ def test_pack_matches_host(gpu_device, P, dim):
         nat.top_route_hist(xg, None, 1, node_g, l, piv_g, (l - 1) % dim, l % dim, cells_g, 8192 // nl, hg)
     sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
-    counts = torch.empty(2 * P, dtype=torch.int64, device=gpu_device)
+    counts = torch.empty(4 * P, dtype=torch.int64, device=gpu_device)
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=gpu_device)
-    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, P, out, counts, err, scratch)
-    cg = counts.cpu()
-    assert torch.equal(cc, cg[0::2]) and int(cg[1::2].abs().sum()) == 0
+    node_keep = node_g.clone()
+    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, P, out, None, counts, err, scratch)
+    cg = counts.cpu().view(P, 4)
+    assert torch.equal(cc, cg[:, 0]) and int(cg[:, 1].abs().sum()) == 0
     k = int(cc.sum())
     assert torch.equal(sc.view(torch.int32), out[:k].cpu().view(torch.int32)), "pack must be stable by destination"
+
+    # compact exchange: coordinates only + destination bitmaps; ids rebuilt on the receiver side
+    words = (n + 31) // 32 + 3  # any stride >= n / 32
+    bm = torch.full((P, words), -1, dtype=torch.int32, device=gpu_device)
+    outc = torch.empty((n, dim), dtype=torch.float32, device=gpu_device)
+    nat.top_pack(xg, None, 1, node_keep, L, piv_g, (L - 1) % dim, P, outc, bm, counts, err, scratch)
+    assert torch.equal(outc[:k].cpu(), sc[:, :dim])
+    dest = node_keep.cpu().to(torch.int64) - (P - 1)
+    bits = ((bm.cpu().to(torch.int64) & 0xFFFFFFFF)[:, :, None] >> torch.arange(32)) & 1
+    bits = bits.reshape(P, -1)
+    for d in range(P):
+        assert torch.equal(bits[d, :n].bool(), dest == d) and int(bits[d, n:].sum()) == 0
+    # the receiver: every source is this same rank here, with its own id base
+    bases = [1 + 1000 * s for s in range(P)]
+    off = [0] + np.cumsum(cc.tolist())[:-1].tolist()
+    rows_per = cc.tolist()
+    # bitmap of source s for receiver d: here receiver d == s's row of the bitmap block
+    recv_bm = torch.cat([bm[d, :words] for d in range(P)])
+    ids = torch.full((k,), -1, dtype=torch.int32, device=gpu_device)
+    scr = torch.empty(nat.ids_from_bitmaps_scratch_bytes(words, P), dtype=torch.uint8, device=gpu_device)
+    err.zero_()
+    nat.ids_from_bitmaps(recv_bm, off, rows_per, [d * words for d in range(P)], [words] * P, bases, ids, scr, err)
+    want = torch.cat([torch.nonzero(dest == d).flatten() + bases[d] for d in range(P)]).to(torch.int32)
+    assert int(err.cpu()[0]) == 0
+    assert torch.equal(ids.cpu(), want)
 
 
 def test_explicit_ids(gpu_device):
@@ -159,13 +185,13 @@ def test_explicit_ids(gpu_device):
     nat = ops.native()
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
-    counts = torch.empty(4, dtype=torch.int64, device=gpu_device)
+    counts = torch.empty(8, dtype=torch.int64, device=gpu_device)
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, 2), dtype=torch.uint8, device=gpu_device)
     nat.top_pack(x.to(gpu_device), ids.to(gpu_device), 0, node_g, 1,
-                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, 2, out, counts, err, scratch)
+                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, 2, out, None, counts, err, scratch)
     assert torch.equal(node_c.to(torch.int32), node_g.cpu())
-    assert counts.cpu()[0::2].tolist() == [n // 2, n - n // 2 - 1]
+    assert counts.cpu()[0::4].tolist() == [n // 2, n - n // 2 - 1]
 
 
 def test_build_rows_equals_build(gpu_device):

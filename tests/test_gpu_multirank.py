@@ -12,7 +12,7 @@ from test_distributed_cpu import run
 pytestmark = pytest.mark.gpu
 
 
-def _case(rank, world, n, dim, seed, dupes):
+def _case(rank, world, n, dim, seed, dupes, explicit=False):
     import parallel_kd_tree_amd as pk
     from parallel_kd_tree_amd import ops
     from parallel_kd_tree_amd.parallel import comm
@@ -27,8 +27,12 @@ def _case(rank, world, n, dim, seed, dupes):
         full = pk.generate_problem(seed, dim, n + 10)
     x = full[first:first + cnt].to(dev)
     b = GlobalTreeBuilder(n, dim, device=dev, timings=True)
-    t = b.build(x, id_base=first + 1)
-    t = b.build(x, id_base=first + 1)  # reuse of the builder's workspaces
+    # implicit ids take the compact exchange (12-B rows + destination bitmaps), explicit ids
+    # the 16-B rows
+    ids = (torch.arange(cnt, dtype=torch.int32) + first + 1).to(dev) if explicit else None
+    t = b.build(x, ids, id_base=first + 1)
+    t = b.build(x, ids, id_base=first + 1)  # reuse of the builder's workspaces
+    assert b.read_error() == 0
     assert t.tree_pts.is_cuda and set(t.timings) >= {"bbox", "pack", "all_to_all", "local_build"}
     tp, ti = t.gather_full()
     cp, ci = ops.build_cpu(full[:n], None, "exact", 0, 1)
@@ -45,3 +49,7 @@ def _case(rank, world, n, dim, seed, dupes):
                                                (4, 50_001, 5, False), (2, 40_000, 2, True), (4, 7, 3, False)])
 def test_global_tree_gpu(world, n, dim, dupes):
     run(world, _case, n, dim, 21, dupes)
+
+
+def test_global_tree_gpu_explicit_ids():
+    run(4, _case, 300_000, 3, 22, False, True)
