@@ -88,6 +88,7 @@ __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i6
 // part[block][2 * dim] (orderable min | max), k_bbox_reduce folds them. (Same-address atomics
 // from thousands of waves serialise in L2 and cost hundreds of microseconds.)
 constexpr int kMaxBoxParts = 4096;
+constexpr int kPrepRows = 64;  // rows per LDS transpose tile of the runtime-dim prep (one wave per column)
 
 template <int D>
 __device__ __forceinline__ void block_box_partial(const u32 (&mn)[D], const u32 (&mx)[D], u32* part) {
@@ -110,25 +111,26 @@ __device__ __forceinline__ void block_box_partial(const u32 (&mn)[D], const u32 
   }
 }
 
+// One block per output word c (column min for c < dim, max above): 2 * dim blocks, so a
+// 128-D box (256 words x thousands of partial rows) folds in one pass instead of 256
+// sequential block-wide reductions.
 __global__ __launch_bounds__(kBlock) void k_bbox_reduce(const u32* __restrict__ part, int nparts, int dim,
                                                         u32* __restrict__ bbox) {
   __shared__ u32 red[kBlock / 64];
-  for (int c = 0; c < 2 * dim; ++c) {
-    const bool is_min = c < dim;
-    u32 v = is_min ? 0xffffffffu : 0u;
-    for (int q = threadIdx.x; q < nparts; q += kBlock) {
-      const u32 x = part[size_t(q) * 2 * dim + c];
-      v = is_min ? min(v, x) : max(v, x);
-    }
-    v = is_min ? dev::wave_min_u32(v) : dev::wave_max_u32(v);
-    if (dev::lane() == 0) red[threadIdx.x / 64] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      u32 r = red[0];
-      for (int k = 1; k < kBlock / 64; ++k) r = is_min ? min(r, red[k]) : max(r, red[k]);
-      bbox[c] = r;
-    }
-    __syncthreads();
+  const int c = blockIdx.x;
+  const bool is_min = c < dim;
+  u32 v = is_min ? 0xffffffffu : 0u;
+  for (int q = threadIdx.x; q < nparts; q += kBlock) {
+    const u32 x = part[size_t(q) * 2 * dim + c];
+    v = is_min ? min(v, x) : max(v, x);
+  }
+  v = is_min ? dev::wave_min_u32(v) : dev::wave_max_u32(v);
+  if (dev::lane() == 0) red[threadIdx.x / 64] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 r = red[0];
+    for (int k = 1; k < kBlock / 64; ++k) r = is_min ? min(r, red[k]) : max(r, red[k]);
+    bbox[c] = r;
   }
 }
 
@@ -184,6 +186,49 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
     idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * dim; c += kBlock) bbox[size_t(blockIdx.x) * 2 * dim + c] = sbox[c];
+}
+
+// Runtime dim (> 8): tiles of kPrepRows rows are transposed through LDS, so both the row
+// loads (contiguous rows) and the column stores (kPrepRows consecutive floats per column) are
+// coalesced; the box is reduced per (wave, column) with one LDS atomic pair. (k_prep<0>
+// stores one float per thread with a column stride between lanes: 10x slower at 128-D.)
+__global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                       u32 id_base, float* __restrict__ cols, i64 n, int dim,
+                                                       u32* __restrict__ bbox, int rs, int ids_in_row, i64 ncol) {
+  extern __shared__ __align__(16) u32 sbox[];  // [2*dim] box | [dim][kPrepRows + 1] tile
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * ncol);
+  u32* sb = sbox;                                           // [2 * dim]
+  float* tile = reinterpret_cast<float*>(sbox + 2 * dim);   // [dim][kPrepRows + 1]
+  constexpr int TR = kPrepRows;
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sb[c] = (c < dim) ? 0xffffffffu : 0u;
+  const int ln = dev::lane();
+  for (i64 r0 = i64(blockIdx.x) * TR; r0 < n; r0 += i64(gridDim.x) * TR) {
+    const int rows = int(min<i64>(TR, n - r0));
+    __syncthreads();  // previous tile consumed (and sb initialised)
+    for (int k = threadIdx.x; k < rows * dim; k += kBlock) {
+      const int rr = k / dim, c = k - rr * dim;
+      tile[c * (TR + 1) + rr] = pts[(r0 + rr) * rs + c];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < dim * TR; k += kBlock) {  // a wave = 64 rows of one column
+      const int c = k / TR, rr = k - c * TR;
+      const bool ok = rr < rows;
+      const float v = tile[c * (TR + 1) + rr];
+      if (ok) cols[i64(c) * ncol + r0 + rr] = v;
+      const u32 kv = ok ? orderable(v) : 0xffffffffu;
+      const u32 mn = dev::wave_min_u32(kv), mx = dev::wave_max_u32(ok ? orderable(v) : 0u);
+      if (ln == 0) {
+        atomicMin(&sb[c], mn);
+        atomicMax(&sb[dim + c], mx);
+      }
+    }
+    for (int rr = threadIdx.x; rr < rows; rr += kBlock) {
+      const i64 r = r0 + rr;
+      idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) bbox[size_t(blockIdx.x) * 2 * dim + c] = sb[c];
 }
 
 // d = 3, contiguous AoS input: a thread moves 4 rows with three 16-B loads and four 16-B
@@ -737,16 +782,24 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
         }
       }
     } else {
-      for (int c = 0; c <= dim; ++c) {
-        float v[kItems];
+      // runtime dim: kColGroup columns per round, all of a round's loads issued before its
+      // stores (one HBM latency per round instead of per column)
+      constexpr int kColGroup = 8;
+      for (int cg = 0; cg <= dim; cg += kColGroup) {
+        float v[kColGroup][kItems];
 #pragma unroll
-        for (int i = 0; i < kItems; ++i) {
-          const i64 e = c0 + i * kBlock + threadIdx.x;
-          v[i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
-        }
+        for (int j = 0; j < kColGroup; ++j)
 #pragma unroll
-        for (int i = 0; i < kItems; ++i)
-          if (zone_pre[i] != 0xffffffffu) dst[i64(c) * nc + lo + zone_pre[i]] = v[i];
+          for (int i = 0; i < kItems; ++i) {
+            const i64 e = c0 + i * kBlock + threadIdx.x;
+            const int c = cg + j <= dim ? cg + j : dim;
+            v[j][i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
+          }
+#pragma unroll
+        for (int j = 0; j < kColGroup; ++j)
+#pragma unroll
+          for (int i = 0; i < kItems; ++i)
+            if (cg + j <= dim && zone_pre[i] != 0xffffffffu) dst[i64(cg + j) * nc + lo + zone_pre[i]] = v[j][i];
       }
     }
     __syncthreads();
@@ -834,6 +887,30 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   auto copy_row = [&](float* to, i64 q, const float* from, i64 p) {
     for (int c = 0; c <= dim; ++c) to[i64(c) * nc + q] = from[i64(c) * nc + p];
   };
+  // Whole-block column-major moves of the zone's rows [zlo, zlo + cnt): consecutive threads
+  // touch consecutive rows of one column, so every load is independent of the others (a row
+  // per thread would chain dim + 1 load/store pairs, ~130 HBM latencies at 128-D).
+  constexpr u32 kNoSlot = 0xffffffffu;
+  const int ncols = dim + 1;
+  auto scatter_cols = [&](float* to, const float* from, int cnt) {  // to[idx[e]] = from[e]
+    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
+      const int c = k / cnt, e = k - c * cnt;
+      const u32 d = idx[e];
+      if (d != kNoSlot) to[i64(c) * nc + zlo + d] = from[i64(c) * nc + zlo + e];
+    }
+  };
+  auto gather_cols = [&](float* to, const float* from, int cnt) {  // to[e] = from[idx[e]]
+    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
+      const int c = k / cnt, e = k - c * cnt;
+      to[i64(c) * nc + zlo + e] = from[i64(c) * nc + zlo + idx[e]];
+    }
+  };
+  auto copy_cols = [&](float* to, const float* from, int cnt) {
+    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
+      const int c = k / cnt, e = k - c * cnt;
+      to[i64(c) * nc + zlo + e] = from[i64(c) * nc + zlo + e];
+    }
+  };
 
   // Middle zones above one wave: radix passes over the composite key, 11 bits at a time
   // starting at the highest differing bit, each keeping only the digit bucket that holds
@@ -844,6 +921,7 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
     int hb = diff ? 63 - __builtin_clzll(diff) : 0;
     while (zc > 64) {
       const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
+      const bool coop = zc <= CAP;  // destinations fit the LDS map: move rows column-major
       for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
       __syncthreads();
       for (i64 e = threadIdx.x; e < zc; e += kBlock)
@@ -901,12 +979,21 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
           z = 3;
         }
         if (z < 3) {
-          copy_row(alt, zlo + dest, dst, zlo + e);
+          if (coop) idx[e] = dest;  // rows move below, column by column
+          else copy_row(alt, zlo + dest, dst, zlo + e);
           if (fuse && z != 1) add_next_hist(a, s, h, z == 0 ? 0 : 1, dst[i64(a.next_axis) * nc + zlo + e]);
+        } else if (coop && e < zc) {
+          idx[e] = kNoSlot;
         }
       }
       __syncthreads();
-      for (i64 e = threadIdx.x; e < zc; e += kBlock) copy_row(dst, zlo + e, alt, zlo + e);
+      if (coop) {
+        scatter_cols(alt, dst, int(zc));
+        __syncthreads();
+        copy_cols(dst, alt, int(zc));
+      } else {
+        for (i64 e = threadIdx.x; e < zc; e += kBlock) copy_row(dst, zlo + e, alt, zlo + e);
+      }
       __syncthreads();
       zlo += cl;
       zc = ce;
@@ -925,8 +1012,10 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
       const u64 k = valid ? ckey(zlo + l) : ~0ull;
       u32 rank = 0;
       for (int j = 0; j < zc; ++j) rank += dev::shfl_u64(k, j) < k ? 1u : 0u;
-      if (valid && rank < zc) copy_row(alt, zlo + rank, dst, zlo + l);
+      if (valid) idx[l] = rank < zc ? rank : kNoSlot;
     }
+    __syncthreads();
+    scatter_cols(alt, dst, int(zc));
   } else {
     for (i64 e = threadIdx.x; e < zc; e += kBlock) {
       keys[e] = ckey(zlo + e);
@@ -934,12 +1023,12 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
     }
     __syncthreads();
     block_bitonic(keys, idx, int(zc), CAP);
-    for (i64 k = threadIdx.x; k < zc; k += kBlock) copy_row(alt, zlo + k, dst, zlo + idx[k]);
+    gather_cols(alt, dst, int(zc));
   }
   __syncthreads();
+  copy_cols(dst, alt, int(zc));
   for (i64 e = threadIdx.x; e < zc; e += kBlock) {
     const i64 q = zlo + e;
-    copy_row(dst, q, alt, q);
     if (e == t) {
       for (int c = 0; c < dim; ++c) a.out_pts[mpos * dim + c] = alt[i64(c) * nc + q];
       a.out_ids[mpos] = reinterpret_cast<const u32*>(alt)[i64(dim) * nc + q];
@@ -1597,6 +1686,8 @@ i64 stage2_min() {
   return e ? std::max<i64>(1, std::atoll(e)) : i64(kRefineCap);
 }
 
+size_t tiled_prep_lds(int dim) { return size_t(2 * dim) * 4 + size_t(dim) * (kPrepRows + 1) * 4; }
+
 int pow2_floor(i64 v) {
   int p = 1;
   while (i64(p) * 2 <= v) p *= 2;
@@ -1630,7 +1721,10 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
     // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
     // 256 CUs) while segments are few; one block per segment below that.
-    lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + kChunk - 1) / kChunk)));
+    // rows per block-chunk of the partition kernel used for this dim (runtime-dim rows are
+    // wide, so their blocks take 1024-row chunks and more blocks share a segment)
+    const i64 chunk = dim <= 8 ? i64(kChunk) : i64(kBlock) * 4;
+    lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + chunk - 1) / chunk)));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
     lp.stage2 = lp.nmax / lp.bins > stage2_min();
@@ -1724,16 +1818,25 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   u32* part = bbox + 2 * dim_;
-  const i64 total = dim_ <= 8 ? n_ : n_ * dim_;
-  const int grid = int(std::min<i64>(4096, std::max<i64>(1, (total + kBlock - 1) / kBlock)));
-  const size_t lds = size_t(2 * dim_) * 4;
+  const bool tiled = dim_ > 8 && tiled_prep_lds(dim_) <= size_t(96 * 1024);  // LDS transpose tiles
+  const int grid = tiled ? int(std::min<i64>(kMaxBoxParts, std::max<i64>(1, (n_ + kPrepRows - 1) / kPrepRows)))
+                         : int(std::min<i64>(kMaxBoxParts, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
+  const size_t lds = tiled ? tiled_prep_lds(dim_) : size_t(2 * dim_) * 4;
+  if (tiled) {
+    static bool attr = false;
+    if (!attr) {
+      PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_prep_tiled),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+      attr = true;
+    }
+  }
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
     k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part);
     PKD_LAUNCH_CHECK();
-    k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, g, dim_, bbox);
+    k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, g, dim_, bbox);
     PKD_LAUNCH_CHECK();
     run_levels(out_pts, out_ids, ws, stream);
     return;
@@ -1747,10 +1850,13 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     case 6: k_prep<6><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
     case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
     case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
-    default: k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
+    default:
+      if (tiled) k_prep_tiled<<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_);
+      else k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_);
+      break;
   }
   PKD_LAUNCH_CHECK();
-  k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, grid, dim_, bbox);
+  k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }
@@ -1765,7 +1871,7 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
   k_bbox_soa<<<grid, kBlock, 0, stream>>>(colsA, n_, dim_, part, ncol_);
   PKD_LAUNCH_CHECK();
-  k_bbox_reduce<<<1, kBlock, 0, stream>>>(part, grid, dim_, bbox);
+  k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
   run_levels(out_pts, out_ids, ws, stream);
 }
@@ -1902,8 +2008,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
     with_ncol(dim_, [&](auto nc) {
       constexpr int NC = decltype(nc)::value;
-      if (NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, stream>>>(a);
-      else if (NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, stream>>>(a);
+      if (NC > 0 && NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, stream>>>(a);
+      else if (NC > 0 && NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, stream>>>(a);
       else k_partition<NC, 4><<<grid, kBlock, lds, stream>>>(a);
     });
     PKD_LAUNCH_CHECK();

@@ -1,4 +1,7 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  prof100 200 'rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof100b -o run -- python3 tools/bench_build.py --n 100000000 --steps 3 --data reference' \
-  prof12 200 'rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof12b -o run -- python3 tools/bench_build.py --n 12500000 --steps 3 --data reference'
+  buildtests 300 'python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_build.py tests/test_gpu_cli.py -m gpu' \
+  d128 200 'python tools/bench_build.py --n 500000 2000000 --dim 128 --steps 5' \
+  d16 200 'python tools/bench_build.py --n 10000000 --dim 16 --steps 5' \
+  d3 200 'python tools/bench_build.py --n 12500000 100000000 --dim 3 --steps 5' \
+  eval 120 'echo 42 | bin/kdtree_gpu --metrics-json'
