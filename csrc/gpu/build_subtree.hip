@@ -1021,11 +1021,22 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
       const char* e = std::getenv("PKD_SUBTREE_WIDE");
       return !(e && std::string(e) == "0");
     }();
+    static const std::string cfg = [] {
+      const char* e = std::getenv("PKD_SUBTREE_CFG");
+      return std::string(e ? e : "");
+    }();
     if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);
     else if (nmax > 1024 && wide) launch_rank_cfg<2, 1024>(a, segs, stream);
     else if (nmax > 1024) launch_rank_cfg<4, 512>(a, segs, stream);
-    else if (nmax > 512) launch_rank_cfg<4, 256>(a, segs, stream);
-    else if (nmax > 256) launch_rank_cfg<2, 256>(a, segs, stream);
+    // Segments of 513..1024 / 257..512 points (dims >= 4, whose rows fill the LDS sooner): the
+    // higher the dim, the more levels are first uses of an axis (latency-bound histogram
+    // ranking), so more waves per segment win: 100M x 8D 31.4 -> 28.1 ms with 1024 threads
+    // instead of 256 (profiles/r1_subtree_config_sweep.txt). PKD_SUBTREE_CFG overrides.
+    else if (nmax > 512 && (cfg == "4x256")) launch_rank_cfg<4, 256>(a, segs, stream);
+    else if (nmax > 512 && (cfg == "2x512" || (cfg.empty() && dim <= 5))) launch_rank_cfg<2, 512>(a, segs, stream);
+    else if (nmax > 512) launch_rank_cfg<1, 1024>(a, segs, stream);
+    else if (nmax > 256 && cfg == "2x256") launch_rank_cfg<2, 256>(a, segs, stream);
+    else if (nmax > 256) launch_rank_cfg<1, 512>(a, segs, stream);
     else if (nmax > 128) launch_rank_cfg<1, 256>(a, segs, stream);
     else if (nmax > 64) launch_rank_cfg<1, 128>(a, segs, stream);
     else launch_rank_cfg<1, 64>(a, segs, stream);
