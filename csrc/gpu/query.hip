@@ -1,5 +1,7 @@
 // Exact 1-NN kernels (see gpu_query.hpp).
 #include <algorithm>
+#include <cstdint>
+#include <stdexcept>
 
 #include "device_utils.hpp"
 #include "pkdtree/gpu_query.hpp"
@@ -12,6 +14,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kQTile = 16;     // queries per brute-force tile (registers per thread)
+constexpr int kDimChunk = 32;  // point coordinates held in registers per round of the brute-force kernel
 constexpr int kStack = 64;     // traversal stack (tree height <= 33 for n < 2^32)
 
 __global__ void k_init(u64* out, i64 nq) {
@@ -19,37 +22,100 @@ __global__ void k_init(u64* out, i64 nq) {
   if (i < nq) out[i] = kPackedInf;
 }
 
-// grid.x: point blocks, grid.y: query tiles. Queries of the tile are staged in LDS.
+// grid.x: point blocks, grid.y: query tiles. Queries of the tile are staged in LDS; every
+// thread owns one point at a time and holds kDimChunk of its coordinates in registers (one
+// 128-B line per lane, loaded with back-to-back 16-B loads), then runs the whole query tile
+// over them. Each query's sum runs over i = 0..dim-1 in order with separately rounded
+// multiply and add, exactly as sq_dist (common.hpp) and the reference's distance loop.
+// (A row per lane read coordinate by coordinate touches 64 cache lines per instruction and,
+// at 128-D, makes L2 re-fetch every line ~32 times; queries re-read from LDS per coordinate
+// left one LDS round trip per multiply.) VEC: dim % 4 == 0, rows and query rows 16-B aligned.
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_brute(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                   u32 id_base, i64 n, int dim, const float* __restrict__ queries,
                                                   i64 nq, u64* __restrict__ out) {
   extern __shared__ __align__(16) float qs[];  // [kQTile][dim]
   const i64 q0 = i64(blockIdx.y) * kQTile;
-  const int qt = int(std::min<i64>(kQTile, nq - q0));
-  for (int f = threadIdx.x; f < qt * dim; f += kBlock) qs[f] = queries[q0 * dim + f];
+  const int qt = int(std::min<i64>(kQTile, nq - q0));  // queries of this tile
+  for (int f = threadIdx.x; f < kQTile * dim; f += kBlock) qs[f] = f < qt * dim ? queries[q0 * dim + f] : 0.0f;
   __syncthreads();
   u64 best[kQTile];
 #pragma unroll
   for (int k = 0; k < kQTile; ++k) best[k] = kPackedInf;
   const i64 stride = i64(gridDim.x) * kBlock;
   for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += stride) {
-    const float* p = pts + r * dim;
+    const float* row = pts + r * dim;
+    float acc[kQTile];
+#pragma unroll
+    for (int k = 0; k < kQTile; ++k) acc[k] = 0.0f;
+    int c0 = 0;
+    for (; c0 + kDimChunk <= dim; c0 += kDimChunk) {
+      float pv[kDimChunk];
+      if (VEC) {
+#pragma unroll
+        for (int j = 0; j < kDimChunk / 4; ++j) {
+          const float4 v = reinterpret_cast<const float4*>(row + c0)[j];
+          pv[4 * j] = v.x;
+          pv[4 * j + 1] = v.y;
+          pv[4 * j + 2] = v.z;
+          pv[4 * j + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kDimChunk; ++j) pv[j] = row[c0 + j];
+      }
+#pragma unroll
+      for (int k = 0; k < kQTile; ++k) {
+        const float* qk = qs + k * dim + c0;
+#pragma unroll
+        for (int j = 0; j < kDimChunk; j += 4) {
+          float4 q4;
+          if (VEC) {
+            q4 = reinterpret_cast<const float4*>(qk)[j / 4];
+          } else {
+            q4 = make_float4(qk[j], qk[j + 1], qk[j + 2], qk[j + 3]);
+          }
+          const float t0 = pv[j] - q4.x, t1 = pv[j + 1] - q4.y, t2 = pv[j + 2] - q4.z, t3 = pv[j + 3] - q4.w;
+          const float s0 = t0 * t0, s1 = t1 * t1, s2 = t2 * t2, s3 = t3 * t3;
+          acc[k] = acc[k] + s0;
+          acc[k] = acc[k] + s1;
+          acc[k] = acc[k] + s2;
+          acc[k] = acc[k] + s3;
+        }
+      }
+    }
+    for (; c0 < dim; ++c0) {  // tail coordinates
+      const float pi = row[c0];
+#pragma unroll
+      for (int k = 0; k < kQTile; ++k) {
+        const float t = pi - qs[k * dim + c0];
+        const float sq = t * t;
+        acc[k] = acc[k] + sq;
+      }
+    }
     const u32 id = ids ? ids[r] : id_base + u32(r);
 #pragma unroll
     for (int k = 0; k < kQTile; ++k) {
       if (k < qt) {
-        const float d2 = sq_dist(p, qs + k * dim, dim);
-        const u64 v = pack_dist_idx(d2, id);
+        const u64 v = pack_dist_idx(acc[k], id);
         best[k] = v < best[k] ? v : best[k];
       }
     }
   }
+  // block minimum per query, then ONE 64-bit atomic per (block, query): same-address atomics
+  // serialise in L2, and with few queries every block would otherwise hit the same words
+  __shared__ u64 wmin[kBlock / 64][kQTile];
+  const int w = threadIdx.x / 64;
 #pragma unroll
   for (int k = 0; k < kQTile; ++k) {
-    if (k < qt) {
-      const u64 v = dev::wave_min_u64(best[k]);
-      if (dev::lane() == 0 && v != kPackedInf) atomicMin((unsigned long long*)&out[q0 + k], (unsigned long long)v);
-    }
+    const u64 v = dev::wave_min_u64(best[k]);
+    if (dev::lane() == 0) wmin[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < qt) {
+    u64 v = wmin[0][threadIdx.x];
+    for (int x = 1; x < kBlock / 64; ++x) v = wmin[x][threadIdx.x] < v ? wmin[x][threadIdx.x] : v;
+    if (v != kPackedInf) atomicMin((unsigned long long*)&out[q0 + threadIdx.x], (unsigned long long)v);
   }
 }
 
@@ -185,12 +251,28 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   TraceRange tr("pkd.nn_brute");
   const i64 tiles = (nq + kQTile - 1) / kQTile;
   // enough point blocks to fill 256 CUs several times over across all query tiles
-  const i64 want = std::max<i64>(1, 2048 / tiles);
+  // ~2048 blocks over all query tiles, but at most 512 per tile: every block adds one atomic
+  // per query of its tile, and those serialise per query word
+  const i64 want = std::max<i64>(1, std::min<i64>(512, 2048 / tiles));
   const int gx = int(std::min<i64>(want, (n + kBlock - 1) / kBlock));
+  const size_t lds = size_t(kQTile) * dim * 4;
+  if (lds > size_t(150) * 1024) throw std::invalid_argument("nn_brute: dimension too large for the LDS query tile");
+  const bool vec = dim % 4 == 0 && reinterpret_cast<uintptr_t>(pts) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(queries) % 16 == 0;
+  static bool attr = false;
+  if (!attr) {
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_brute<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_brute<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+    attr = true;
+  }
   for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
     const i64 ty = std::min<i64>(65535, tiles - t0);
-    k_brute<<<dim3(unsigned(gx), unsigned(ty)), kBlock, size_t(kQTile) * dim * 4, stream>>>(
-        pts, ids, id_base, n, dim, queries + t0 * kQTile * dim, nq - t0 * kQTile, out + t0 * kQTile);
+    const dim3 grid{unsigned(gx), unsigned(ty), 1u};
+    const float* qt = queries + t0 * kQTile * dim;
+    if (vec) k_brute<true><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, n, dim, qt, nq - t0 * kQTile, out + t0 * kQTile);
+    else k_brute<false><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, n, dim, qt, nq - t0 * kQTile, out + t0 * kQTile);
     PKD_LAUNCH_CHECK();
   }
 }
