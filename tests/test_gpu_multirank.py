@@ -46,7 +46,8 @@ def _case(rank, world, n, dim, seed, dupes, explicit=False):
 
 
 @pytest.mark.parametrize("world,n,dim,dupes", [(2, 300_000, 3, False), (4, 400_000, 3, False),
-                                               (4, 50_001, 5, False), (2, 40_000, 2, True), (4, 7, 3, False)])
+                                               (4, 50_001, 5, False), (2, 40_000, 2, True), (4, 7, 3, False),
+                                               (8, 800_003, 3, False)])
 def test_global_tree_gpu(world, n, dim, dupes):
     run(world, _case, n, dim, 21, dupes)
 
