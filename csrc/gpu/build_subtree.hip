@@ -635,11 +635,12 @@ __device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32
 // Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
 __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
 
-// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+36 | aux nm+32 | fin nm+32 | tmpi u16 nm+32 |
-//               root cell 2*dim
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+68 | aux nm+64 | fin nm+64 | tmpi u16 nm+64 |
+//               root cell 2*dim. The 64 dummy entries at the end of work / aux / fin / tmpi take the writes
+//               of finished points, one per lane, so those writes never share an address.
 size_t lds_words(int dim, int nm) {
-  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 36 + 2 * (size_t(nm) + 32) +
-         size_t(nm) / 2 + 16 + 2 * size_t(dim);
+  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 68 + 2 * (size_t(nm) + 64) +
+         size_t(nm) / 2 + 32 + 2 * size_t(dim);
 }
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
@@ -692,13 +693,17 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const bool keep = dim < lsub;
   float* rows = reinterpret_cast<float*>(smem);
   const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
+  // crank[axis][...]: a thread's compressed ranks are private to it; with 2 items per thread
+  // they sit side by side (index 2 * tid + i), so one ds_read_b32 / ds_write_b32 moves both and
+  // no two lanes share a dword
   u16* crank = reinterpret_cast<u16*>(smem + size_t(dim + 1) * NM);
   u32* work = smem + size_t(dim + 1) * NM + (size_t(kept_layout) * NM + 1) / 2;
-  u32* aux = work + NM + 4 + 32;  // work: NM buckets, sentinel, 32 per-lane dummy words
-  u32* fin = aux + NM + 32;           // aux / fin: NM entries + 32 per-lane dummies each
-  u16* tmpi = reinterpret_cast<u16*>(fin + NM + 32);  // NM + 32 entries
-  float* cellv = reinterpret_cast<float*>(tmpi + NM + 32);  // [dim][2] root cell of the segment
-  const u32 dummy = u32(NM + 4) + (tid & 31);
+  u32* aux = work + NM + 4 + 64;  // work: NM buckets, sentinel, 64 per-lane dummy words
+  u32* fin = aux + NM + 64;           // aux / fin: NM entries + 64 per-lane dummies each
+  u16* tmpi = reinterpret_cast<u16*>(fin + NM + 64);  // NM + 64 entries
+  float* cellv = reinterpret_cast<float*>(tmpi + NM + 64);  // [dim][2] root cell of the segment
+  const u32 lane_dummy = u32(dev::lane());
+  const u32 dummy = u32(NM + 4) + lane_dummy;
   stamp(a, 0);
 
   {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
@@ -769,9 +774,16 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       // Branch-free (the scalar unit, shared by the CU's four SIMDs, is the bottleneck of
       // exec-mask juggling): finished points OR 0 into a private dummy word per lane.
       u32 c[ITEMS], wi[ITEMS];
+      if (ITEMS == 2) {
+        const u32 both = reinterpret_cast<const u32*>(cr)[tid];
+        c[0] = both & 0xffffu;
+        c[ITEMS - 1] = both >> 16;
+      } else {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) c[i] = cr[tid + i * THREADS];
+      }
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        c[i] = cr[tid + i * THREADS];
         wi[i] = nn[i] ? sg[i] * Wt + (c[i] >> 5) : dummy;
         atomicOr(&work[wi[i]], nn[i] ? 1u << (c[i] & 31) : 0u);
       }
@@ -828,7 +840,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       u32 pos[ITEMS];
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + (tid & 31);
+        pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + lane_dummy;
         tmpk[pos[i]] = ok[i];
         tmpi[pos[i]] = u16(tid + i * THREADS);
       }
@@ -880,17 +892,20 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
     }
     // ---- median / left / right (selects only; the median's slot write goes to a dummy
     // word for every other point) ----
+    u32 cn[ITEMS];
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const u32 n0 = nn[i], mid = n0 >> 1, r = rank[i];
       const bool is_mid = n0 != 0 && r == mid;
       const bool right = r > mid;
-      fin[is_mid ? lo[i] + mid : u32(NM) + (tid & 31)] = u32(tid + i * THREADS);
-      if (keep) cr[tid + i * THREADS] = u16(right ? r - mid - 1 : r);
+      fin[is_mid ? lo[i] + mid : u32(NM) + lane_dummy] = u32(tid + i * THREADS);
+      cn[i] = right ? r - mid - 1 : r;
+      if (keep && ITEMS != 2) cr[tid + i * THREADS] = u16(cn[i]);
       lo[i] = right ? lo[i] + mid + 1 : lo[i];
       sg[i] = 2 * sg[i] + (right ? 1u : 0u);
       nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
     }
+    if (keep && ITEMS == 2) reinterpret_cast<u32*>(cr)[tid] = (cn[0] & 0xffffu) | (cn[ITEMS - 1] << 16);
     __syncthreads();
     if (t < 18) stamp(a, 2 + t);
   }
