@@ -103,7 +103,8 @@ void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level,
 
 void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base, torch::Tensor node,
           int64_t levels, const torch::Tensor& pivots, int64_t last_axis, int64_t P, torch::Tensor out,
-          std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
+          std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch,
+          int64_t pipe_k) {
   const c10::DeviceGuard g(pts.device());
   TopPoints p = points_of(pts, ids, id_base);
   check_cuda(out, torch::kFloat32, "out");
@@ -120,8 +121,8 @@ void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int
     bm = u32p(*bitmaps);
     words = bitmaps->size(1);
   }
-  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), out.data_ptr<float>(), int(out.size(1)),
-           bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
+  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), int(pipe_k), out.data_ptr<float>(),
+           int(out.size(1)), bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
 }
 
 // bitmaps: all sources' words back to back; per source (row offset, rows, word offset, words, id base)
@@ -160,7 +161,10 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("top_select", &select);
   m.def("top_collect", &collect);
   m.def("top_pivot", &pivot);
-  m.def("top_pack", &pack);
+  m.def("top_pack", &pack, pybind11::arg("pts"), pybind11::arg("ids"), pybind11::arg("id_base"), pybind11::arg("node"),
+        pybind11::arg("levels"), pybind11::arg("pivots"), pybind11::arg("last_axis"), pybind11::arg("P"),
+        pybind11::arg("out"), pybind11::arg("bitmaps"), pybind11::arg("counts"), pybind11::arg("err"),
+        pybind11::arg("scratch"), pybind11::arg("pipe_k") = 0);
   m.def("top_middle_words", [](int64_t dim, int64_t cap) { return int64_t(top_middle_words(int(dim), cap)); });
   m.def("top_pack_scratch_bytes", [](int64_t n, int64_t P) { return int64_t(top_pack_scratch_bytes(n, int(P))); });
   m.def("ids_from_bitmaps", &ids_from_bm);

@@ -338,9 +338,18 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
 }
 
 // ---- counting sort by destination (P <= 64) -------------------------------------------
+// Destination slot of top-level leaf l. With a pipelined exchange (pipe_k > 0) rank r owns the
+// 2^pipe_k leaves r * 2^pipe_k + j, sent in round j; slots are ordered (round, rank) so each
+// round's rows are one contiguous run in rank order.
+__device__ __forceinline__ int dest_slot(u32 l, int P, int pipe_k) {
+  if (pipe_k == 0) return int(l);
+  const u32 mask = (1u << pipe_k) - 1u;
+  return int((l & mask) * u32(P >> pipe_k) + (l >> pipe_k));
+}
+
 __global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restrict__ node, int levels,
                                                        const u64* __restrict__ pivots, int last_axis, int P,
-                                                       i64 per_block, u32* __restrict__ bcount) {
+                                                       int pipe_k, i64 per_block, u32* __restrict__ bcount) {
   __shared__ u32 cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restr
   for (i64 i = b0 + threadIdx.x; i < b1; i += kBlock) {
     const u32 h = route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots);
     node[i] = h;
-    if (h != kTopDone) atomicAdd(&cnt[h - first], 1u);
+    if (h != kTopDone) atomicAdd(&cnt[dest_slot(h - first, P, pipe_k)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < P) bcount[i64(blockIdx.x) * P + threadIdx.x] = cnt[threadIdx.x];
@@ -379,7 +388,7 @@ __global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int P,
-                                                         i64 per_block, const u32* __restrict__ offsets,
+                                                         int pipe_k, i64 per_block, const u32* __restrict__ offsets,
                                                          float* __restrict__ out, int rs) {
   __shared__ u32 cur[64];
   __shared__ u32 wcnt[kBlock / 64][64];
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
     const i64 i = c0 + threadIdx.x;
     const u32 h = i < b1 ? node[i] : kTopDone;
-    const int d = h == kTopDone ? -1 : int(h - first);
+    const int d = h == kTopDone ? -1 : dest_slot(h - first, P, pipe_k);
     u32 my = 0;
     for (int e = 0; e < P; ++e) {  // stable rank among same-destination points of the chunk
       const u64 m = __ballot(d == e);
@@ -421,14 +430,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
 // Destination bitmaps of the compact exchange: bm[d][w] bit j = row 32w + j goes to leaf d.
 // One wave per 64 rows (two words), one ballot per destination; rows >= n give zero words,
 // so the grid covers the whole padded stride.
-__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int P, i64 ws,
-                                                        u32* __restrict__ bm) {
+__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int P, int pipe_k,
+                                                        i64 ws, u32* __restrict__ bm) {
   const i64 wave = (i64(blockIdx.x) * kBlock + threadIdx.x) / 64;
   const int ln = dev::lane();
   const i64 row = wave * 64 + ln;
   const u32 first = u32(P - 1);
   const u32 h = row < n ? node[row] : kTopDone;
-  const int d = h == kTopDone ? -1 : int(h - first);
+  const int d = h == kTopDone ? -1 : dest_slot(h - first, P, pipe_k);
   for (int e = 0; e < P; ++e) {
     const u64 m = __ballot(d == e);
     const i64 w = 2 * wave + (ln & 1);
@@ -572,25 +581,27 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
 
 size_t top_pack_scratch_bytes(i64 n, int P) { return size_t(2) * pack_blocks(n) * size_t(P) * 4; }
 
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
-              int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch,
-              hipStream_t stream) {
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, int pipe_k,
+              float* out_rows, int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
+              void* scratch, hipStream_t stream) {
   if (P > 64 || P != (1 << levels)) throw std::invalid_argument("top_pack: P must be 2^levels <= 64");
+  if (pipe_k < 0 || pipe_k > levels) throw std::invalid_argument("top_pack: pipe_k out of range");
   if (row_stride != p.dim && row_stride != p.dim + 1) throw std::invalid_argument("top_pack: row stride dim or dim+1");
   if (bitmaps && bitmap_words * 32 < p.n) throw std::invalid_argument("top_pack: bitmap stride too small");
   const int blocks = pack_blocks(p.n);
   const i64 per_block = (std::max<i64>(p.n, 1) + blocks - 1) / blocks;
   u32* bcount = static_cast<u32*>(scratch);
   u32* offsets = bcount + size_t(blocks) * P;
-  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, P, per_block, bcount);
+  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, P, pipe_k, per_block, bcount);
   PKD_LAUNCH_CHECK();
   k_pack_scan<<<1, 64, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
   PKD_LAUNCH_CHECK();
-  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, per_block, offsets, out_rows, row_stride);
+  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, pipe_k, per_block, offsets, out_rows, row_stride);
   PKD_LAUNCH_CHECK();
   if (bitmaps) {
     const i64 waves = (bitmap_words + 1) / 2;
-    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, P, bitmap_words, bitmaps);
+    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, P, pipe_k, bitmap_words,
+                                                                                  bitmaps);
     PKD_LAUNCH_CHECK();
   }
 }

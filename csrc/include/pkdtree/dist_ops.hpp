@@ -77,10 +77,12 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
 // `bitmaps` ([P][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the destination of every
 // row is also written as one bit per (dest, row): the compact exchange sends 12-B rows plus
 // n / 8 bytes per destination instead of 16-B rows, and the receiver rebuilds the ids.
+// pipe_k > 0 (pipelined exchange): P = ranks * 2^pipe_k leaves, rank r owns leaves
+// r * 2^pipe_k + j, and destination slots (rows, counts, bitmaps) are ordered (j, r).
 size_t top_pack_scratch_bytes(i64 n, int P);
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, float* out_rows,
-              int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch,
-              hipStream_t stream);
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, int pipe_k,
+              float* out_rows, int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
+              void* scratch, hipStream_t stream);
 
 // Receiver of the compact exchange: rows from source s occupy [off[s], off[s] + cnt[s]) of
 // the receive buffer in increasing source-row order, so the k-th row from s has the id

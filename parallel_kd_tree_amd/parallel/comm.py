@@ -162,6 +162,16 @@ def all_gather_into_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def all_to_all_single_async(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
+    """Starts an all-to-all and returns a handle whose wait() orders the caller's current
+    stream after it (RCCL runs it on its own stream, overlapping later compute). gloo
+    staging is synchronous; its handle is None."""
+    if not dist.is_initialized() or world() == 1 or _staged(inp):
+        all_to_all_single_(out, inp, out_splits, in_splits)
+        return None
+    return dist.all_to_all_single(out, inp, out_splits, in_splits, async_op=True)
+
+
 def all_to_all_single_(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> torch.Tensor:
     if not dist.is_initialized() or world() == 1:
         out.copy_(inp)

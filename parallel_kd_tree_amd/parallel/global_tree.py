@@ -243,13 +243,17 @@ class GlobalTreeBuilder:
         self._builder = None
         self._ws: Dict[str, torch.Tensor] = {}
         self._scale = 1
+        self._leaf_builders: Dict[Tuple[int, int], ops.GpuTreeBuilder] = {}  # pipelined exchange
+        self._main_used = False  # the one-round exchange's builder has built at least once
         if self.device.type == "cuda" and self.n_leaf > 0:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
 
     def read_error(self) -> int:
         """Device error word of the last build (0 = ok): the local subtree build's, plus 8 if the
         compact exchange's id bitmaps disagreed with the received row counts. Synchronises."""
-        e = self._builder.read_error() if self._builder is not None else 0
+        e = self._builder.read_error() if (self._builder is not None and self._main_used) else 0
+        for b in self._leaf_builders.values():
+            e |= b.read_error()
         if "err" in self._ws:
             e |= int(self._ws["err"][0].item()) & 8
         return e
@@ -283,26 +287,43 @@ class GlobalTreeBuilder:
             timings[name] = timings.get(name, 0.0) + (now - t0[0]) * 1e3
             t0[0] = now
 
-    def _top_device(self, pts, idt, id_base, scale, timings, t0):
+    def pipeline_k(self) -> int:
+        """Exchange rounds 2^k per build: each rank's subtree is split k more levels down by
+        the distributed top levels, and the leaf subtrees are built one by one while the next
+        leaf's rows are in flight. The exchange only dominates at P = 2 (300 MB per direction
+        over the one xGMI link between the two GPUs, ~4-5 ms, next to a 7.2 ms local build), so
+        P = 2 takes two rounds (half the exchange hidden behind the first leaf's build, for
+        ~0.2 ms of extra top level and the slightly lower efficiency of two 25 M builds); at
+        P >= 4 the exchange is short and one round is kept. PKD_PIPELINE_K overrides."""
+        env = os.environ.get("PKD_PIPELINE_K")
+        k = int(env) if env is not None else {2: 1}.get(self.P, 0)
+        k = max(0, min(k, 6 - self.L))  # at most 64 leaves (32 nodes per top level)
+        if self.P == 1:
+            k = 0
+        return k
+
+    def _top_device(self, pts, idt, id_base, scale, timings, t0, k):
         nat = ops.native()
         dim, P, L = self.dim, self.P, self.L
+        LL, R = L + k, 1 << k
+        leaves = P << k
         n_local = pts.shape[0]
         dev = self.device
         box = self._buf("box", (2 * dim,), torch.int64)
         box.fill_(0xFFFFFFFF)
         nat.top_bbox(pts, box)
         comm.all_reduce_(box, dist.ReduceOp.MIN)
-        cells = self._buf("cells", ((2 * P - 1) * dim * 2,), torch.float32)
+        cells = self._buf("cells", ((2 * leaves - 1) * dim * 2,), torch.float32)
         nat.top_root_cell(box, dim, cells)
         node = self._buf("node", (max(n_local, 1),), torch.int32)
-        pivots = torch.full((max(P - 1, 1),), -1, dtype=torch.int64, device=dev)
-        top_rows = torch.zeros((max(P - 1, 1), dim + 1), dtype=torch.float32, device=dev)
+        pivots = torch.full((max(leaves - 1, 1),), -1, dtype=torch.int64, device=dev)
+        top_rows = torch.zeros((max(leaves - 1, 1), dim + 1), dtype=torch.float32, device=dev)
         err = self._buf("err", (4,), torch.int32)
         err.zero_()
         sel = self._buf("sel", (32 * 4,), torch.int32)
         hist = self._buf("hist", (TOP_BINS,), torch.int32)
         self._tick(timings, "bbox", t0)
-        for level in range(L):
+        for level in range(LL):
             nodes = 1 << level
             bins = TOP_BINS // nodes
             axis = (self.depth0 + level) % dim
@@ -321,39 +342,48 @@ class GlobalTreeBuilder:
             comm.all_gather_into_(gathered, buf)
             nat.top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err)
             self._tick(timings, f"top_level{level}", t0)
-        last_axis = (self.depth0 + L - 1) % dim
+        last_axis = (self.depth0 + LL - 1) % dim
         # Compact exchange (implicit ids): 12-B rows plus one bit per (source row, destination);
         # the receiver rebuilds the ids from the bitmaps (csrc/gpu/dist_ops.hip, ids_from_bitmaps).
         compact = idt is None and os.environ.get("PKD_COMPACT_EXCHANGE", "1") != "0"
         rs = dim if compact else dim + 1
         send = self._buf("send_c" if compact else "send", (max(n_local, 1), rs), torch.float32)
-        counts = torch.empty(4 * P, dtype=torch.int64, device=dev)  # per dest: rows, err, id base, n_local
-        cv = counts.view(P, 4)
+        # per destination slot (round j, rank r): rows, err, id base, n_local
+        counts = torch.empty(4 * leaves, dtype=torch.int64, device=dev)
+        cv = counts.view(leaves, 4)
         cv[:, 2] = int(id_base)
         cv[:, 3] = int(n_local)
         words = max(1, (n_local + 31) // 32)
-        bm = None
-        if compact:
-            bm = self._buf("bm", (P, words), torch.int32)
-        scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, P),), torch.uint8)
-        nat.top_pack(pts, idt, id_base, node, L, pivots, last_axis, P, send, bm, counts, err, scratch)
-        recv_counts = torch.empty_like(counts)
-        comm.all_to_all_single_(recv_counts, counts)
-        both = torch.cat([counts, recv_counts]).cpu()  # the only host read-back of the build
+        bm = self._buf("bm", (leaves, words), torch.int32) if compact else None
+        scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, leaves),), torch.uint8)
+        nat.top_pack(pts, idt, id_base, node, LL, pivots, last_axis, leaves, send, bm, counts, err, scratch, k)
+        by_rank = counts.view(R, P, 4).transpose(0, 1).contiguous()  # [rank][round][4]
+        recv_counts = torch.empty_like(by_rank)
+        comm.all_to_all_single_(recv_counts, by_rank)
+        both = torch.cat([by_rank.view(-1), recv_counts.view(-1)]).cpu()  # the only host read-back of the build
         self._tick(timings, "pack", t0)
-        mine, theirs = both[:4 * P].view(P, 4), both[4 * P:].view(P, 4)
+        mine, theirs = both[:4 * leaves].view(P, R, 4), both[4 * leaves:].view(P, R, 4)
         errs = 0
-        for v in torch.cat([mine[:, 1], theirs[:, 1]]).tolist():
+        for v in torch.cat([mine[:, :, 1].reshape(-1), theirs[:, :, 1].reshape(-1)]).tolist():
             errs |= int(v)
+        if errs & 1:
+            # a middle bucket overflowed its all-gather slot: that level's pivot (and every level
+            # routed through it, hence a possible err 2 below it) is void; retry larger
+            return None
         if errs & 2:
             raise RuntimeError("global top levels: histogram totals disagree with the tree geometry")
-        if errs & 1:
-            return None  # a middle bucket overflowed its all-gather slot: retry larger
-        in_splits = mine[:, 0].tolist()
-        out_splits = theirs[:, 0].tolist()
-        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err,
-              "src_base": theirs[:, 2].tolist(), "src_n": theirs[:, 3].tolist()}
-        return send[: sum(in_splits)], in_splits, out_splits, top_rows, ex
+        in_splits = [mine[:, j, 0].tolist() for j in range(R)]    # rows to each rank in round j
+        out_splits = [theirs[:, j, 0].tolist() for j in range(R)]  # rows from each rank in round j
+        starts = np.concatenate([[0], np.cumsum([sum(v) for v in in_splits])]).astype(np.int64).tolist()
+        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err, "R": R, "LL": LL,
+              "src_base": theirs[:, 0, 2].tolist(), "src_n": theirs[:, 0, 3].tolist(), "starts": starts}
+        return send, in_splits, out_splits, top_rows, ex
+
+    def _leaf_builder(self, n: int, depth: int):
+        b = self._leaf_builders.get((n, depth))
+        if b is None:
+            b = self._leaf_builders[(n, depth)] = ops.GpuTreeBuilder(n, self.dim, depth)
+        return b
 
     def _build_device(self, points, ids, id_base) -> DistTree:
         dim, P, L = self.dim, self.P, self.L
@@ -361,44 +391,98 @@ class GlobalTreeBuilder:
         t0 = [time.perf_counter()]
         pts = points.to(self.device, torch.float32).contiguous()
         idt = None if ids is None else ids.to(self.device, torch.int32).contiguous()
+        k = self.pipeline_k()
         scale = self._scale  # sticky: a skewed input pays its all-gather retry once, not per build
         while True:
             with trace_range("pkd.dist.top_levels"):
-                res = self._top_device(pts, idt, int(id_base), scale, timings, t0)
+                res = self._top_device(pts, idt, int(id_base), scale, timings, t0, k)
             if res is not None:
                 break
-            if all(self._cap(l, scale) >= self.n_total for l in range(L)):
+            if all(self._cap(l, scale) >= self.n_total for l in range(L + k)):
                 raise RuntimeError("global top levels: middle buckets inconsistent at full capacity")
             scale *= 8
         self._scale = scale
         send, in_splits, out_splits, top_rows, ex = res
-        recv = torch.empty((sum(out_splits), ex["rs"]), dtype=torch.float32, device=self.device)
-        with trace_range("pkd.dist.all_to_all"):
-            comm.all_to_all_single_(recv, send, out_splits, in_splits)
+        R, LL, rs = ex["R"], ex["LL"], ex["rs"]
+        if R == 1 and sum(out_splits[0]) != self.n_leaf:
+            raise RuntimeError(f"rank {self.rank}: received {sum(out_splits[0])} points for a subtree of {self.n_leaf}")
+        src_words = [max(1, (int(v) + 31) // 32) for v in ex["src_n"]]
+        bm_off = np.concatenate([[0], np.cumsum(src_words)[:-1]]).astype(np.int64).tolist()
+        nat = ops.native()
+
+        def issue(j):
+            """Start round j: the rows of leaf j of every rank (+ their id bitmaps)."""
+            recv = self._buf(f"recv{j}", (sum(out_splits[j]), rs), torch.float32)
+            a, b = ex["starts"][j], ex["starts"][j + 1]
+            handles = [comm.all_to_all_single_async(recv, send[a:b], out_splits[j], in_splits[j])]
+            recv_bm = None
             if ex["compact"]:
-                src_words = [max(1, (int(v) + 31) // 32) for v in ex["src_n"]]
-                recv_bm = self._buf("recv_bm", (sum(src_words),), torch.int32)
-                comm.all_to_all_single_(recv_bm, ex["bm"].view(-1), src_words, [ex["words"]] * P)
-        self._tick(timings, "all_to_all", t0)
-        if recv.shape[0] != self.n_leaf:
-            raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
-        if self.n_leaf == 0:
-            tp = torch.empty((0, dim), dtype=torch.float32, device=self.device)
-            ti = torch.empty((0,), dtype=torch.int32, device=self.device)
-        else:
-            with trace_range("pkd.dist.local_build"):
-                if ex["compact"]:
-                    nat = ops.native()
-                    off = np.concatenate([[0], np.cumsum(out_splits)[:-1]]).astype(np.int64).tolist()
-                    bm_off = np.concatenate([[0], np.cumsum(src_words)[:-1]]).astype(np.int64).tolist()
-                    ids = self._buf("ids", (self.n_leaf,), torch.int32)
-                    scr = self._buf("bm_scratch", (nat.ids_from_bitmaps_scratch_bytes(max(src_words), P),),
-                                    torch.uint8)
-                    nat.ids_from_bitmaps(recv_bm, off, out_splits, bm_off, src_words, ex["src_base"], ids, scr,
-                                         ex["err"])
-                    tp, ti = self._builder.build(recv, ids, 0)
+                recv_bm = self._buf(f"recv_bm{j}", (sum(src_words),), torch.int32)
+                handles.append(comm.all_to_all_single_async(recv_bm, ex["bm"][j * P:(j + 1) * P].reshape(-1),
+                                                            src_words, [ex["words"]] * P))
+            return recv, recv_bm, handles
+
+        def local_tree(recv, recv_bm, j, n_j, builder, out_pts=None, out_ids=None):
+            if ex["compact"]:
+                off = np.concatenate([[0], np.cumsum(out_splits[j])[:-1]]).astype(np.int64).tolist()
+                lids = self._buf("ids", (max(n_j, 1),), torch.int32)[:n_j]
+                scr = self._buf("bm_scratch", (nat.ids_from_bitmaps_scratch_bytes(max(src_words), P),), torch.uint8)
+                nat.ids_from_bitmaps(recv_bm, off, out_splits[j], bm_off, src_words, ex["src_base"], lids, scr,
+                                     ex["err"])
+                return builder.build(recv, lids, 0, out_pts, out_ids)
+            if out_pts is None:
+                return builder.build_rows(recv)
+            tp_, ti_ = builder.build_rows(recv)
+            out_pts.copy_(tp_)
+            out_ids.copy_(ti_)
+            return out_pts, out_ids
+
+        with trace_range("pkd.dist.exchange_and_build"):
+            if R == 1:
+                recv, recv_bm, handles = issue(0)
+                for hd in handles:
+                    if hd is not None:
+                        hd.wait()
+                self._tick(timings, "all_to_all", t0)
+                if self.n_leaf == 0:
+                    tp = torch.empty((0, dim), dtype=torch.float32, device=self.device)
+                    ti = torch.empty((0,), dtype=torch.int32, device=self.device)
                 else:
-                    tp, ti = self._builder.build_rows(recv)
+                    tp, ti = local_tree(recv, recv_bm, 0, self.n_leaf, self._builder)
+                    self._main_used = True
+            else:
+                # my subtree: node m = P - 1 + rank at depth L; its 2^k leaves at depth LL are the
+                # heap nodes first_leaf + j; the R - 1 pivots between them come from top_rows
+                m = P - 1 + self.rank
+                first_leaf = (m + 1) * R - 1
+                tp = torch.empty((self.n_leaf, dim), dtype=torch.float32, device=self.device)
+                ti = torch.empty((self.n_leaf,), dtype=torch.int32, device=self.device)
+                inner = [h for lvl in range(k) for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1)]
+                slots = [median_slot(self.n_total, h) - self.slot_lo for h in inner]
+                keep = [(s, h) for s, h in zip(slots, inner) if segment(self.n_total, h)[1] > 0]
+                if keep:
+                    si = torch.tensor([s for s, _ in keep], dtype=torch.int64, device=self.device)
+                    hi = torch.tensor([h for _, h in keep], dtype=torch.int64, device=self.device)
+                    rows = top_rows[hi]
+                    tp[si] = rows[:, :dim]
+                    ti[si] = rows[:, dim].contiguous().view(torch.int32)
+                pending = issue(0)
+                for j in range(R):
+                    recv, recv_bm, handles = pending
+                    for hd in handles:
+                        if hd is not None:
+                            hd.wait()
+                    if j + 1 < R:
+                        pending = issue(j + 1)  # in flight while leaf j builds
+                    lo_j, n_j = segment(self.n_total, first_leaf + j)
+                    if recv.shape[0] != n_j:
+                        raise RuntimeError(f"rank {self.rank}: round {j} received {recv.shape[0]} points for a "
+                                           f"leaf of {n_j}")
+                    if n_j > 0:
+                        a = lo_j - self.slot_lo
+                        local_tree(recv, recv_bm, j, n_j, self._leaf_builder(n_j, self.depth0 + LL),
+                                   tp[a:a + n_j], ti[a:a + n_j])
+                self._tick(timings, "all_to_all", t0)
         self._tick(timings, "local_build", t0)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
                         list(self.top_slots), top_rows[: P - 1], timings)

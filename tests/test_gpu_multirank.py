@@ -54,3 +54,12 @@ def test_global_tree_gpu(world, n, dim, dupes):
 
 def test_global_tree_gpu_explicit_ids():
     run(4, _case, 300_000, 3, 22, False, True)
+
+
+@pytest.mark.parametrize("world,k", [(2, 0), (2, 3), (4, 2), (8, 1)])
+def test_global_tree_gpu_pipeline_depth(monkeypatch, world, k):
+    """Exchange rounds: every rank's subtree split k levels further by the distributed top
+    levels, leaf subtrees built while the next leaf's rows are in flight (k = 0: one
+    all-to-all). Same tree for every k."""
+    monkeypatch.setenv("PKD_PIPELINE_K", str(k))
+    run(world, _case, 200_001, 3, 23, False)
