@@ -243,7 +243,7 @@ class GlobalTreeBuilder:
         self._builder = None
         self._ws: Dict[str, torch.Tensor] = {}
         self._scale = 1
-        self._leaf_builders: Dict[Tuple[int, int], ops.GpuTreeBuilder] = {}  # pipelined exchange
+        self._leaf_builders: Dict[tuple, object] = {}  # pipelined exchange: leaf builders, pivot slots
         self._main_used = False  # the one-round exchange's builder has built at least once
         if self.device.type == "cuda" and self.n_leaf > 0:
             self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
@@ -253,7 +253,8 @@ class GlobalTreeBuilder:
         compact exchange's id bitmaps disagreed with the received row counts. Synchronises."""
         e = self._builder.read_error() if (self._builder is not None and self._main_used) else 0
         for b in self._leaf_builders.values():
-            e |= b.read_error()
+            if isinstance(b, ops.GpuTreeBuilder):
+                e |= b.read_error()
         if "err" in self._ws:
             e |= int(self._ws["err"][0].item()) & 8
         return e
@@ -379,6 +380,22 @@ class GlobalTreeBuilder:
               "src_base": theirs[:, 0, 2].tolist(), "src_n": theirs[:, 0, 3].tolist(), "starts": starts}
         return send, in_splits, out_splits, top_rows, ex
 
+    def _inner_pivots(self, k: int):
+        """(output slots, heap nodes) of the pivots inside this rank's subtree above its 2^k
+        pipelined leaves, as device index tensors (geometry only, cached)."""
+        key = ("inner", k)
+        if key not in self._leaf_builders:
+            m = self.P - 1 + self.rank
+            inner = [h for lvl in range(k) for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1)]
+            keep = [(median_slot(self.n_total, h) - self.slot_lo, h) for h in inner if segment(self.n_total, h)[1] > 0]
+            if keep:
+                si = torch.tensor([a for a, _ in keep], dtype=torch.int64, device=self.device)
+                hi = torch.tensor([h for _, h in keep], dtype=torch.int64, device=self.device)
+                self._leaf_builders[key] = (si, hi)
+            else:
+                self._leaf_builders[key] = (None, None)
+        return self._leaf_builders[key]
+
     def _leaf_builder(self, n: int, depth: int):
         b = self._leaf_builders.get((n, depth))
         if b is None:
@@ -457,12 +474,8 @@ class GlobalTreeBuilder:
                 first_leaf = (m + 1) * R - 1
                 tp = torch.empty((self.n_leaf, dim), dtype=torch.float32, device=self.device)
                 ti = torch.empty((self.n_leaf,), dtype=torch.int32, device=self.device)
-                inner = [h for lvl in range(k) for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1)]
-                slots = [median_slot(self.n_total, h) - self.slot_lo for h in inner]
-                keep = [(s, h) for s, h in zip(slots, inner) if segment(self.n_total, h)[1] > 0]
-                if keep:
-                    si = torch.tensor([s for s, _ in keep], dtype=torch.int64, device=self.device)
-                    hi = torch.tensor([h for _, h in keep], dtype=torch.int64, device=self.device)
+                si, hi = self._inner_pivots(k)
+                if si is not None:
                     rows = top_rows[hi]
                     tp[si] = rows[:, :dim]
                     ti[si] = rows[:, dim].contiguous().view(torch.int32)

@@ -1,4 +1,3 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  gputests 600 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu' \
-  bench 300 'python bench.py'
+  mr 500 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -m gpu'
