@@ -1129,6 +1129,12 @@ struct PairArgs {
   int axis2;             // level l+2 axis
   int bins2;             // level l+2 bins (0: l+2 is the subtree level)
   u32* hist2n;           // level l+2 histograms [4 * segs][bins2]
+  // Prefix placement (top pairs with a second-stage level l+1): k_hist2p counts each block's
+  // rows whose zone is already certain (child known, level-(l+1) bucket != the child's median
+  // bucket) per (child, left/right) into bcnt[block][4]; k_block_bases turns them into
+  // per-block write offsets bbase[block][4], so k_partition2 needs no counting pass.
+  u32* bcnt = nullptr;
+  u32* bbase = nullptr;
 };
 
 template <int NCOL>
@@ -1408,6 +1414,9 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
   const float* kc = a.src + i64(a.axis) * nc + lo;
   const float* k1c = a.src + i64(a.next_axis) * nc + lo;
   const u32* idc = reinterpret_cast<const u32*>(a.src) + i64(a.dim) * nc + lo;
+  __shared__ u32 bc[4];
+  if (threadIdx.x < 4) bc[threadIdx.x] = 0;
+  u32 cnt[4] = {0, 0, 0, 0};  // certain rows: child 0 left / right, child 1 left / right
   __syncthreads();
   constexpr int U = 8;
   for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
@@ -1429,14 +1438,24 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
         if (ck == pivot) continue;
         c = ck < pivot ? 0u : 1u;
       }
-      if (c == 0) {
-        if (bucket_of(k1[u], cpr0, pa.bins1) == cb0) atomicAdd(&sh[bucket_of(k1[u], q0, kBins2)], 1u);
+      const u32 b1 = bucket_of(k1[u], c == 0 ? cpr0 : cpr1, pa.bins1), cb = c == 0 ? cb0 : cb1;
+      if (b1 == cb) {
+        atomicAdd(&sh[c * kBins2 + bucket_of(k1[u], c == 0 ? q0 : q1, kBins2)], 1u);
       } else {
-        if (bucket_of(k1[u], cpr1, pa.bins1) == cb1) atomicAdd(&sh[kBins2 + bucket_of(k1[u], q1, kBins2)], 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cnt[k] += u32(k) == 2 * c + (b1 > cb ? 1u : 0u) ? 1u : 0u;
       }
     }
   }
+  if (pa.bcnt) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32 v = dev::wave_incl_scan(cnt[k]);  // lane 63 holds the wave's total
+      if (dev::lane() == 63 && v) atomicAdd(&bc[k], v);
+    }
+  }
   __syncthreads();
+  if (pa.bcnt && threadIdx.x < 4) pa.bcnt[i64(blockIdx.x) * 4 + threadIdx.x] = bc[threadIdx.x];
   u32* hs = a.hist2 + (2 * s) * kBins2;
   for (int b = threadIdx.x; b < 2 * kBins2; b += kBlock) {
     const u32 v = sh[b];
@@ -1444,13 +1463,60 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
   }
 }
 
+// Per-block write offsets of the certain rows (one workgroup per level-l segment): for each
+// (child, left/right zone) an exclusive scan of the blocks' counts from the zone's start;
+// the zone cursor then points past all certain rows, where the uncertain rows (the
+// child's median bucket, placed by the second stage) are appended with atomics.
+__global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa) {
+  __shared__ u32 sh4[4];
+  const i64 s = blockIdx.x;
+  const i64 h = a.heap0 + s;
+  if (a.seg_n[h] <= 0) return;
+  const u32* cnt = pa.bcnt + s * a.bps * 4;
+  u32* base = pa.bbase + s * a.bps * 4;
+  // thread t owns blocks [t * per, t * per + per): all loads of a thread are issued together
+  const int per = (a.bps + kBlock - 1) / kBlock;
+  const int b0 = min(a.bps, int(threadIdx.x) * per), b1 = min(a.bps, b0 + per);
+  u32 sum[4] = {0, 0, 0, 0};
+  for (int b = b0; b < b1; ++b) {
+    const uint4 v = reinterpret_cast<const uint4*>(cnt)[b];
+    sum[0] += v.x;
+    sum[1] += v.y;
+    sum[2] += v.z;
+    sum[3] += v.w;
+  }
+  u32 off[4], start[4], tot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    start[k] = a.state[2 * h + 1 + k / 2].cur[(k & 1) ? 2 : 0];
+    off[k] = start[k] + block_excl_scan(sum[k], sh4, &tot[k]);
+    __syncthreads();  // sh4 is reused by the next scan
+  }
+  for (int b = b0; b < b1; ++b) {
+    const uint4 v = reinterpret_cast<const uint4*>(cnt)[b];
+    reinterpret_cast<uint4*>(base)[b] = make_uint4(off[0], off[1], off[2], off[3]);
+    off[0] += v.x;
+    off[1] += v.y;
+    off[2] += v.z;
+    off[3] += v.w;
+  }
+  if (threadIdx.x < 4) {
+    const int k = int(threadIdx.x);
+    a.state[2 * h + 1 + k / 2].cur[(k & 1) ? 2 : 0] = start[k] + tot[k];
+  }
+}
+
 // Pass B of a pair: a = level l (src -> dst), children states/params are level l+1's.
-template <int NCOL, int KI>
+// PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
+// offsets; rows in a child's median bucket (their zone is decided by the second stage)
+// form 6 more pseudo-zones placed with cursor atomics.
+template <int NCOL, int KI, bool PFX = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
+  constexpr int NZ = PFX ? 12 : 6;
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
-  __shared__ u32 gcnt[6][64];
+  __shared__ u32 gcnt[NZ][64];
   __shared__ u32 bcur[6];
   __shared__ unsigned long long bmin[2], bmax[2];  // children's middle-zone key ranges, flushed once
   if (threadIdx.x < 2) {
@@ -1498,7 +1564,9 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   const int axis = a.axis, ax1 = a.next_axis, ax2 = pa.axis2;
   const int w = threadIdx.x / 64;
   const int ln = dev::lane();
-  auto classify = [&](float k0, float k1, u32 id, bool valid) -> u32 {  // 6 * 0 + q, or 7 (none)
+  // 3 * child + zone, or 7 (none); unc: the row lies in the child's median bucket
+  auto classify = [&](float k0, float k1, u32 id, bool valid, bool& unc) -> u32 {
+    unc = false;
     if (!valid) return 7u;
     const u32 z0 = zone_of(k0, prm, a.bins, bstar, stage2, p2, sbstar);
     u32 c = z0 == 0 ? 0u : 1u;
@@ -1510,13 +1578,19 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     const u32 b1 = c == 0 ? bucket_of(k1, cpr0, pa.bins1) : bucket_of(k1, cpr1, pa.bins1);
     const u32 cb = c == 0 ? cbs0 : cbs1;
     u32 z1 = b1 < cb ? 0u : (b1 == cb ? 1u : 2u);
+    unc = z1 == 1;
     if (pa.stage2_1 && z1 == 1) {
       const u32 sb = bucket_of(k1, c2p[c], kBins2), sbs = c2sb[c];
       z1 = sb < sbs ? 0u : (sb == sbs ? 1u : 2u);
     }
     return 3 * c + z1;
   };
-  if (a.block_reserve) {
+  if (PFX) {
+    if (threadIdx.x < 6) {
+      const int t = int(threadIdx.x);
+      bcur[t] = (t == 1 || t == 4) ? 0u : pa.bbase[i64(blockIdx.x) * 4 + (t / 3) * 2 + (t % 3 == 2 ? 1 : 0)];
+    }
+  } else if (a.block_reserve) {
     u32 cnt[6] = {0, 0, 0, 0, 0, 0};
     const float* kc = src + i64(axis) * nc + lo;
     const float* k1c = src + i64(ax1) * nc + lo;
@@ -1535,7 +1609,8 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         const i64 e = e0 + i64(u) * kBlock;
         if (e >= b1) continue;
         const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
-        const u32 q = classify(k0[u], k1[u], z0 == 1 ? idc[e] : 0u, true);
+        bool unc;
+        const u32 q = classify(k0[u], k1[u], z0 == 1 ? idc[e] : 0u, true, unc);
 #pragma unroll
         for (int z = 0; z < 6; ++z) cnt[z] += q == u32(z) ? 1u : 0u;
       }
@@ -1565,7 +1640,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
 #pragma unroll
       for (int c = 0; c < NCOL; ++c) row[i][c] = src[i64(c) * nc + p];
     }
-    u32 zone_pre[kItems];  // (q << 16) | rank-in-wave
+    u32 zone_pre[kItems];  // (zone index << 16) | rank-in-wave; index q, or 6 + q (PFX uncertain), 15 none
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
       const i64 e = c0 + i * kBlock + threadIdx.x;
@@ -1576,15 +1651,17 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         k1 = c == ax1 ? row[i][c] : k1;
         k2 = c == ax2 ? row[i][c] : k2;
       }
-      const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), e < b1);
+      bool unc;
+      const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), e < b1, unc);
+      const u32 zi = q >= 6 ? 15u : (PFX && unc ? q + 6 : q);
       u32 my = 0;
 #pragma unroll
-      for (int z = 0; z < 6; ++z) {
-        const u64 m = __ballot(q == u32(z));
+      for (int z = 0; z < NZ; ++z) {
+        const u64 m = __ballot(zi == u32(z));
         if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
-        if (q == u32(z)) my = mbcnt(m);
+        if (zi == u32(z)) my = mbcnt(m);
       }
-      zone_pre[i] = (q << 16) | my;
+      zone_pre[i] = (zi << 16) | my;
       if (fuse && q < 6 && q != 1 && q != 4) {
         const u32 g = (q / 3) * 2 + (q % 3 == 2 ? 1u : 0u);
         atomicAdd(&nh[g * nb2 + bucket_of(k2, sgp[g], nb2)], 1u);
@@ -1596,12 +1673,15 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       }
     }
     __syncthreads();
-    for (int z = w; z < 6; z += kBlock / 64) {  // wave w scans zones w, w+4
+    for (int z = w; z < NZ; z += kBlock / 64) {  // wave w scans zones w, w+4 (, w+8)
       const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
       const u32 incl = dev::wave_incl_scan(v);
       const u32 tot = __shfl(incl, 63, 64);
       u32 base = 0;
-      if (a.block_reserve) {
+      if (PFX && z >= 6) {
+        if (ln == 0 && tot) base = atomicAdd(&(z < 9 ? cst0 : cst1)->cur[(z - 6) % 3], tot);
+        base = __shfl(base, 0, 64);
+      } else if (PFX || a.block_reserve) {
         base = bcur[z];
         if (ln == 0) bcur[z] = base + tot;
       } else {
@@ -1613,11 +1693,11 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
-      const u32 q = zone_pre[i] >> 16;
+      const u32 zi = zone_pre[i] >> 16;
       i64 dest = -1;
-      if (q < 6) {
-        const u32 c = q / 3;
-        const u32 off = gcnt[q][i * 4 + w] + (zone_pre[i] & 0xffffu);
+      if (zi < u32(NZ)) {
+        const u32 c = (zi % 6) / 3;
+        const u32 off = gcnt[zi][i * 4 + w] + (zone_pre[i] & 0xffffu);
         const i64 cn = c == 0 ? n / 2 : n - n / 2 - 1;
         if (i64(off) >= cn) {
           atomicOr(a.err, 1u);
@@ -1660,6 +1740,11 @@ void with_ncol(int dim, F&& f) {
     case 8: f(std::integral_constant<int, 9>{}); break;
     default: f(std::integral_constant<int, 0>{}); break;
   }
+}
+
+bool prefix_placement() {  // read per build (tests switch it)
+  const char* e = std::getenv("PKD_PART_PREFIX");
+  return !(e && std::string(e) == "0");
 }
 
 bool items16() {
@@ -1770,6 +1855,9 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   off_hist2_ = take(size_t(std::max<i64>(max_hist2_, 1)) * 4);
   off_bbox_ = take(size_t(2 * dim) * 4 * (1 + kMaxBoxParts));  // final box + per-block partials
   off_err_ = take(16);
+  i64 max_grid = 1;
+  for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
+  off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
   ws_bytes_ = off;
 }
 
@@ -1983,6 +2071,13 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       pa.axis2 = (opt_.depth0 + l + 2) % dim_;
       pa.bins2 = lq.next_bins;
       pa.hist2n = hist[l & 1];
+      // the second-stage pass of level l+1 reads what the block-reserve count pass would:
+      // it also counts each block's certain rows, and the scatter writes from prefix offsets
+      const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
+      if (pfx) {
+        pa.bcnt = reinterpret_cast<u32*>(ws + off_bcnt_);
+        pa.bbase = pa.bcnt + size_t(grid) * 4;
+      }
       if (lq.stage2) {
         PKD_HIP_CHECK(hipMemsetAsync(b.hist2, 0, size_t(lq.segs) * kBins2 * 4, stream));
         k_hist2p<<<grid, kBlock, 0, stream>>>(a, pa);
@@ -1990,13 +2085,18 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         k_select2<<<int(lq.segs), kBlock, 0, stream>>>(b);
         PKD_LAUNCH_CHECK();
       }
+      if (pfx) {
+        k_block_bases<<<int(lp.segs), kBlock, 0, stream>>>(a, pa);
+        PKD_LAUNCH_CHECK();
+      }
       const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
       with_ncol(dim_, [&](auto nc) {
         constexpr int NC = decltype(nc)::value;
         if constexpr (NC > 0) {
-          if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, stream>>>(a, pa);
-          else if (NC <= 5) k_partition2<NC, 8><<<grid, kBlock, lds_b, stream>>>(a, pa);
-          else k_partition2<NC, 4><<<grid, kBlock, lds_b, stream>>>(a, pa);
+          constexpr int KI = NC <= 5 ? 8 : 4;
+          if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, stream>>>(a, pa);
+          else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, stream>>>(a, pa);
+          else k_partition2<NC, KI><<<grid, kBlock, lds_b, stream>>>(a, pa);
         }
       });
       PKD_LAUNCH_CHECK();

@@ -89,7 +89,7 @@ class GpuBuilder {
   i64 max_hist2_ = 0;
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
-         off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0,
+         off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,
          ws_bytes_ = 0;
 };
 

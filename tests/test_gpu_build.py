@@ -79,6 +79,17 @@ def test_large_stage2_pairs(gpu_device):
     check_same(pk.generate_problem(5, 3, 20_000_000), gpu_device)
 
 
+@pytest.mark.parametrize("prefix", ["1", "0"])
+def test_large_stage2_pairs_prefix_placement(gpu_device, monkeypatch, prefix):
+    # prefix placement of the top pairs (per-block offsets from k_hist2p's counts) on skewed
+    # data: one axis takes few distinct values, so median buckets are huge and many rows are
+    # appended with cursor atomics after the certain rows; PKD_PART_PREFIX=0 is the counting pass
+    monkeypatch.setenv("PKD_PART_PREFIX", prefix)
+    x = pk.generate_problem(6, 3, 18_000_000)
+    x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
+    check_same(x, gpu_device)
+
+
 @pytest.mark.parametrize("n,dim,depth0", [(1, 3, 0), (1000, 3, 0), (200_000, 3, 0), (100_000, 5, 2), (30_000, 8, 0)])
 def test_device_invariant_checker(gpu_device, n, dim, depth0):
     """The HIP checker (semantic race detector) passes on built trees and catches corruption."""
