@@ -1162,10 +1162,12 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
   const float* kc = src + i64(a.axis) * nc + lo;
   const float* nkc = src + i64(a.next_axis) * nc + lo;
   const int ln = dev::lane();
-  // middle rows are staged in LDS and reserved once per block (same-address atomics on the
-  // segment cursor from every wave would serialise in L2)
-  constexpr int kStage = 256;
-  __shared__ float mrow[kStage * NCOL];
+  // Middle rows (the median bucket) are only noted during the sweep (their offsets in LDS);
+  // after it the block reserves them once (same-address atomics on the segment cursor from
+  // every wave would serialise in L2) and copies them with all threads, so no wave stalls
+  // on row loads inside the sweep.
+  constexpr int kStage = 512;
+  __shared__ u32 sidx[kStage];
   __shared__ u32 mcnt, mbase;
   __shared__ unsigned long long bmin, bmax;
   if (threadIdx.x == 0) {
@@ -1190,51 +1192,62 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
       if (z == 0) atomicAdd(&nh[bucket_of(nk[u], cp0, nb)], 1u);
       if (z == 2) atomicAdd(&nh[nb + bucket_of(nk[u], cp1, nb)], 1u);
       const u64 m = __ballot(z == 1);
-      if (m) {  // rare: stage the median bucket's rows
+      if (m) {  // rare: note the median bucket's rows
         const int leader = __ffsll((long long)m) - 1;
         u32 base = 0;
         if (ln == leader) base = atomicAdd(&mcnt, u32(__popcll(m)));
         base = __shfl(base, leader, 64);
-        u64 ck = 0;
-        if (z == 1) {
-          const u32 slot = base + mbcnt(m);
-          if (slot < u32(kStage)) {
-#pragma unroll
-            for (int c = 0; c < NCOL; ++c) mrow[slot * NCOL + c] = src[i64(c) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x];
-          } else {  // staging full: reserve directly
+        const u32 slot = base + mbcnt(m);
+        const bool direct = z == 1 && slot >= u32(kStage);
+        if (z == 1 && !direct) sidx[slot] = u32(e - b0);
+        if (__ballot(direct)) {  // staging full: reserve and copy directly
+          u64 ck = 0;
+          if (direct) {
             const u32 g = atomicAdd(&st->cur[1], 1u);
             if (i64(g) >= n) {
               atomicOr(a.err, 1u);
             } else {
 #pragma unroll
-              for (int c = 0; c < NCOL; ++c)
-                dst[i64(c) * nc + lo + g] = src[i64(c) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x];
+              for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + g] = src[i64(c) * nc + lo + e];
             }
+            ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e]);
           }
-          ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e0 + i64(u) * kBlock + threadIdx.x]);
+          wave_minmax_atomic(direct, ck, &bmin, &bmax);
         }
-        wave_minmax_atomic(z == 1, ck, &bmin, &bmax);
       }
     }
   }
   __syncthreads();
   const u32 staged = min(mcnt, u32(kStage));
-  if (threadIdx.x == 0) {
-    mbase = staged ? atomicAdd(&st->cur[1], staged) : 0u;
-    if (bmin != ~0ull) {
-      atomicMin(&st->mid_min, bmin);
-      atomicMax(&st->mid_max, bmax);
+  if (threadIdx.x == 0) mbase = staged ? atomicAdd(&st->cur[1], staged) : 0u;
+  __syncthreads();
+  for (u32 r0 = 0; r0 < staged; r0 += kBlock) {  // uniform trip count: every lane reaches the wave ops
+    const u32 k2 = r0 + threadIdx.x;
+    const bool act = k2 < staged;
+    const i64 q = i64(mbase) + k2;
+    u64 ck = 0;
+    if (act) {
+      const i64 e = b0 + sidx[k2];
+      float row[NCOL];
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) row[c] = src[i64(c) * nc + lo + e];
+      if (q >= n) {
+        atomicOr(a.err, 1u);
+      } else {
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + q] = row[c];
+      }
+      float key = row[0];
+#pragma unroll
+      for (int c = 1; c < D; ++c) key = c == a.axis ? row[c] : key;
+      ck = composite_key(key, __float_as_uint(row[D]));
     }
+    wave_minmax_atomic(act, ck, &bmin, &bmax);
   }
   __syncthreads();
-  for (u32 k2 = threadIdx.x; k2 < staged; k2 += kBlock) {
-    const i64 q = i64(mbase) + k2;
-    if (q >= n) {
-      atomicOr(a.err, 1u);
-      continue;
-    }
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + q] = mrow[k2 * NCOL + c];
+  if (threadIdx.x == 0 && bmin != ~0ull) {
+    atomicMin(&st->mid_min, bmin);
+    atomicMax(&st->mid_max, bmax);
   }
   u32* hn = a.hist_next + (2 * s) * nb;
   for (int b = threadIdx.x; b < 2 * nb; b += kBlock) {
