@@ -735,7 +735,9 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       zone_pre[i] = (z << 16) | mbcnt(mz);
       if (m1 != 0) {  // rare: track the middle zone's composite key range
         u64 k = 0;
-        if (z == 1) k = composite_key(key, reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e]);
+        if (z == 1)  // the id is in the register row when the dim is compile-time
+          k = composite_key(key, NCOL > 0 ? __float_as_uint(row[i][NR - 1])
+                                          : reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e]);
         wave_minmax_atomic(z == 1, k, &bmin, &bmax);
       }
       if (fuse && z < 3 && z != 1) {
@@ -1755,6 +1757,14 @@ void with_ncol(int dim, F&& f) {
   }
 }
 
+// k_scan runs on half the scatter's blocks per segment: its per-block histogram flush (2 x
+// next_bins global atomics) halves, and the sweep stays bandwidth-bound (100M x 3D: k_scan
+// 1.57 -> 1.51 ms). PKD_SCAN_DIV overrides.
+int scan_div() {
+  const char* e = std::getenv("PKD_SCAN_DIV");
+  return e ? std::max(1, std::atoi(e)) : 2;
+}
+
 bool prefix_placement() {  // read per build (tests switch it)
   const char* e = std::getenv("PKD_PART_PREFIX");
   return !(e && std::string(e) == "0");
@@ -2068,7 +2078,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       with_ncol(dim_, [&](auto nc) {
         constexpr int NC = decltype(nc)::value;
         if constexpr (NC > 0) {
-          k_scan<NC><<<grid, kBlock, lds_a, stream>>>(a);
+          LevelArgs as = a;  // the scan's own block split (its histogram flush scales with blocks)
+          as.bps = std::max(1, lp.bps / scan_div());
+          k_scan<NC><<<int(lp.segs * as.bps), kBlock, lds_a, stream>>>(as);
           PKD_LAUNCH_CHECK();
           k_pivot_small<NC><<<gs, kBlock, 0, stream>>>(a, lp.segs);
           k_pivot<NC><<<int(lp.segs), kBlock, 0, stream>>>(a);

@@ -1,5 +1,6 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  new 200 'python -u tools/bench_build.py --n 100000000 12500000 --dim 8 3 --steps 10' \
-  old 200 'cd old_wt && python -u tools/bench_build.py --n 100000000 12500000 --dim 8 3 --steps 10' \
-  new2 200 'python -u tools/bench_build.py --n 100000000 12500000 --dim 8 3 --steps 10'
+  p1 100 'PKD_SCAN_DIV=1 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa1 -o run -- python3 tools/bench_build.py --n 100000000 --dim 3 --steps 3' \
+  p2 100 'PKD_SCAN_DIV=2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa2 -o run -- python3 tools/bench_build.py --n 100000000 --dim 3 --steps 3' \
+  p3 100 'PKD_SCAN_DIV=1 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa3 -o run -- python3 tools/bench_build.py --n 100000000 --dim 3 --steps 3' \
+  p4 100 'PKD_SCAN_DIV=2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa4 -o run -- python3 tools/bench_build.py --n 100000000 --dim 3 --steps 3'
