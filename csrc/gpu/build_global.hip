@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
 // column stores (x, y, z, id), all fully coalesced; columns are 256-B aligned (ncol % 64 == 0).
 __global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                    u32 id_base, float* __restrict__ cols, i64 n, i64 ncol,
-                                                   u32* __restrict__ bbox) {
+                                                   u32* __restrict__ bbox, int write_ids) {
   const i64 nq = n / 4;
   const i64 stride = i64(gridDim.x) * kBlock;
   u32 mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts
       cx[t] = x;
       cy[t] = y;
       cz[t] = z;
-      ci[t] = id[u];
+      if (write_ids) ci[t] = id[u];
       upd(0, x.x); upd(0, x.y); upd(0, x.z); upd(0, x.w);
       upd(1, y.x); upd(1, y.y); upd(1, y.z); upd(1, y.w);
       upd(2, z.x); upd(2, z.y); upd(2, z.z); upd(2, z.w);
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void k_prep3v(const float* __restrict__ pts
       cols[i64(c) * ncol + r] = v;
       upd(c, v);
     }
-    reinterpret_cast<u32*>(cols + 3 * ncol)[r] = ids ? ids[r] : id_base + u32(r);
+    if (write_ids) reinterpret_cast<u32*>(cols + 3 * ncol)[r] = ids ? ids[r] : id_base + u32(r);
   }
   block_box_partial<3>(mn, mx, bbox);
 }
@@ -363,7 +363,18 @@ struct LevelArgs {
   int block_reserve;     // 1: count the block's zones first and reserve once per block
   int small_done;        // 1: k_refine_small already resolved middle zones of <= 64 points
   u32* hist2;            // stage-2 histograms [segs][kBins2] (levels with stage2)
+  int id_implicit;       // 1 (first level only): src has no id column, id of column row p = id_base0 + p
+  u32 id_base0;
 };
+
+// Id of src column row p (absolute), materialised or implicit (first level of a build whose
+// prep skipped the id column).
+__device__ __forceinline__ u32 src_id(const LevelArgs& a, i64 p) {
+  return a.id_implicit ? a.id_base0 + u32(p) : reinterpret_cast<const u32*>(a.src)[i64(a.dim) * a.ncol + p];
+}
+__device__ __forceinline__ float src_col(const LevelArgs& a, int c, i64 p) {
+  return (c == a.dim && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : a.src[i64(c) * a.ncol + p];
+}
 
 // Zone of a point: 0 left of the median bucket, 1 inside (the middle zone), 2 right.
 // Stage 2 splits the median bucket once more with its own linear sub-buckets.
@@ -1210,9 +1221,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
               atomicOr(a.err, 1u);
             } else {
 #pragma unroll
-              for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + g] = src[i64(c) * nc + lo + e];
+              for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + g] = src_col(a, c, lo + e);
             }
-            ck = composite_key(k[u], reinterpret_cast<const u32*>(src)[i64(D) * nc + lo + e]);
+            ck = composite_key(k[u], src_id(a, lo + e));
           }
           wave_minmax_atomic(direct, ck, &bmin, &bmax);
         }
@@ -1232,7 +1243,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
       const i64 e = b0 + sidx[k2];
       float row[NCOL];
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c) row[c] = src[i64(c) * nc + lo + e];
+      for (int c = 0; c < NCOL; ++c) row[c] = src_col(a, c, lo + e);
       if (q >= n) {
         atomicOr(a.err, 1u);
       } else {
@@ -1428,7 +1439,6 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
   const i64 nc = a.ncol;
   const float* kc = a.src + i64(a.axis) * nc + lo;
   const float* k1c = a.src + i64(a.next_axis) * nc + lo;
-  const u32* idc = reinterpret_cast<const u32*>(a.src) + i64(a.dim) * nc + lo;
   __shared__ u32 bc[4];
   if (threadIdx.x < 4) bc[threadIdx.x] = 0;
   u32 cnt[4] = {0, 0, 0, 0};  // certain rows: child 0 left / right, child 1 left / right
@@ -1449,7 +1459,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
       const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
       u32 c = z0 == 0 ? 0u : 1u;
       if (z0 == 1) {
-        const u64 ck = composite_key(k0[u], idc[e]);
+        const u64 ck = composite_key(k0[u], src_id(a, lo + e));
         if (ck == pivot) continue;
         c = ck < pivot ? 0u : 1u;
       }
@@ -1609,7 +1619,6 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     u32 cnt[6] = {0, 0, 0, 0, 0, 0};
     const float* kc = src + i64(axis) * nc + lo;
     const float* k1c = src + i64(ax1) * nc + lo;
-    const u32* idc = reinterpret_cast<const u32*>(src) + i64(D) * nc + lo;
     constexpr int U = 8;
     for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
       float k0[U], k1[U];
@@ -1625,7 +1634,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         if (e >= b1) continue;
         const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
         bool unc;
-        const u32 q = classify(k0[u], k1[u], z0 == 1 ? idc[e] : 0u, true, unc);
+        const u32 q = classify(k0[u], k1[u], z0 == 1 ? src_id(a, lo + e) : 0u, true, unc);
 #pragma unroll
         for (int z = 0; z < 6; ++z) cnt[z] += q == u32(z) ? 1u : 0u;
       }
@@ -1653,7 +1662,8 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       const i64 e = c0 + i * kBlock + threadIdx.x;
       const i64 p = lo + (e < b1 ? e : b0);
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c) row[i][c] = src[i64(c) * nc + p];
+      for (int c = 0; c < NCOL; ++c)
+        row[i][c] = (c == D && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : src[i64(c) * nc + p];
     }
     u32 zone_pre[kItems];  // (zone index << 16) | rank-in-wave; index q, or 6 + q (PFX uncertain), 15 none
 #pragma unroll
@@ -1760,6 +1770,11 @@ void with_ncol(int dim, F&& f) {
 // k_scan runs on half the scatter's blocks per segment: its per-block histogram flush (2 x
 // next_bins global atomics) halves, and the sweep stays bandwidth-bound (100M x 3D: k_scan
 // 1.57 -> 1.51 ms). PKD_SCAN_DIV overrides.
+bool implicit_ids_enabled() {
+  const char* e = std::getenv("PKD_IMPLICIT_IDS");
+  return !(e && std::string(e) == "0");
+}
+
 int scan_div() {
   const char* e = std::getenv("PKD_SCAN_DIV");
   return e ? std::max(1, std::atoi(e)) : 2;
@@ -1945,11 +1960,14 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
-    k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part);
+    // generated ids are synthesised by the first pair's kernels instead of written here
+    // (-4 B written and -4 B read per point); the first level must be a pair for that
+    const bool implicit = ids == nullptr && lg_ >= 2 && levels_[0].pair && implicit_ids_enabled();
+    k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part, implicit ? 0 : 1);
     PKD_LAUNCH_CHECK();
     k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, g, dim_, bbox);
     PKD_LAUNCH_CHECK();
-    run_levels(out_pts, out_ids, ws, stream);
+    run_levels(out_pts, out_ids, ws, stream, implicit, id_base);
     return;
   }
   switch (dim_) {
@@ -1987,7 +2005,8 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   run_levels(out_pts, out_ids, ws, stream);
 }
 
-void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const {
+void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
+                            u32 id_base) const {
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
@@ -2034,6 +2053,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.block_reserve = (lp.segs <= 8 && lp.bps > 4) ? 1 : 0;  // only where cursor contention is high
     a.small_done = 0;
     a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
+    a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
+    a.id_base0 = id_base;
     return a;
   };
   auto refine = [&](LevelArgs& a, i64 segs) {

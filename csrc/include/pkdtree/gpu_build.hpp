@@ -74,7 +74,10 @@ class GpuBuilder {
  private:
   void prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base, float* out_pts,
                     u32* out_ids, void* workspace, hipStream_t stream) const;
-  void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream) const;
+  // implicit_ids: the prep left the id column unwritten (ids = id_base + input row); the
+  // first pair's kernels synthesise them.
+  void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
+                  u32 id_base = 0) const;
 
   i64 n_;
   i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)
