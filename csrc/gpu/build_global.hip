@@ -905,25 +905,38 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   // per thread would chain dim + 1 load/store pairs, ~130 HBM latencies at 128-D).
   constexpr u32 kNoSlot = 0xffffffffu;
   const int ncols = dim + 1;
-  auto scatter_cols = [&](float* to, const float* from, int cnt) {  // to[idx[e]] = from[e]
-    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
-      const int c = k / cnt, e = k - c * cnt;
-      const u32 d = idx[e];
-      if (d != kNoSlot) to[i64(c) * nc + zlo + d] = from[i64(c) * nc + zlo + e];
+  // kMoveU elements per thread per round, all loads of a round before its stores (a loop of
+  // single load/store pairs would pay one HBM latency per element per thread: at 128-D a
+  // 40-row zone is 20 such rounds per move)
+  constexpr int kMoveU = 8;
+  auto move_cols = [&](float* to, const float* from, int cnt, int mode) {  // 0 scatter, 1 gather, 2 copy
+    const int total = cnt * ncols;
+    for (int k0 = threadIdx.x; k0 < total; k0 += kBlock * kMoveU) {
+      float v[kMoveU];
+      u32 dd[kMoveU];
+#pragma unroll
+      for (int u = 0; u < kMoveU; ++u) {
+        const int k = k0 + u * kBlock;
+        const int c = k / max(cnt, 1), e = k - c * cnt;
+        dd[u] = kNoSlot;
+        v[u] = 0.0f;
+        if (k < total) {
+          const u32 src_e = mode == 1 ? idx[e] : u32(e);
+          dd[u] = mode == 0 ? idx[e] : u32(e);
+          v[u] = from[i64(c) * nc + zlo + src_e];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kMoveU; ++u) {
+        const int k = k0 + u * kBlock;
+        const int c = k / max(cnt, 1);
+        if (k < total && dd[u] != kNoSlot) to[i64(c) * nc + zlo + dd[u]] = v[u];
+      }
     }
   };
-  auto gather_cols = [&](float* to, const float* from, int cnt) {  // to[e] = from[idx[e]]
-    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
-      const int c = k / cnt, e = k - c * cnt;
-      to[i64(c) * nc + zlo + e] = from[i64(c) * nc + zlo + idx[e]];
-    }
-  };
-  auto copy_cols = [&](float* to, const float* from, int cnt) {
-    for (int k = threadIdx.x; k < cnt * ncols; k += kBlock) {
-      const int c = k / cnt, e = k - c * cnt;
-      to[i64(c) * nc + zlo + e] = from[i64(c) * nc + zlo + e];
-    }
-  };
+  auto scatter_cols = [&](float* to, const float* from, int cnt) { move_cols(to, from, cnt, 0); };  // to[idx[e]] = from[e]
+  auto gather_cols = [&](float* to, const float* from, int cnt) { move_cols(to, from, cnt, 1); };   // to[e] = from[idx[e]]
+  auto copy_cols = [&](float* to, const float* from, int cnt) { move_cols(to, from, cnt, 2); };
 
   // Middle zones above one wave: radix passes over the composite key, 11 bits at a time
   // starting at the highest differing bit, each keeping only the digit bucket that holds
@@ -1018,6 +1031,8 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
 
   // Final ranking of the (small) middle zone.
   const i64 mpos = lo + n / 2;
+  constexpr int kInPlaceU = 32;  // zones of up to 32 * kBlock values are permuted in registers
+  const bool inplace = zc <= 64 && zc * ncols <= kInPlaceU * kBlock;
   if (zc <= 64) {
     if (threadIdx.x < 64) {
       const int l = dev::lane();
@@ -1028,7 +1043,25 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
       if (valid) idx[l] = rank < zc ? rank : kNoSlot;
     }
     __syncthreads();
-    scatter_cols(alt, dst, int(zc));
+    if (inplace) {  // every value of the zone in registers, one barrier, then the permuted stores
+      const int cnt = max(int(zc), 1), total = int(zc) * ncols;
+      float v[kInPlaceU];
+#pragma unroll
+      for (int u = 0; u < kInPlaceU; ++u) {
+        const int k = int(threadIdx.x) + u * kBlock;
+        const int c = k / cnt, e = k - c * cnt;
+        v[u] = k < total ? dst[i64(c) * nc + zlo + e] : 0.0f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kInPlaceU; ++u) {
+        const int k = int(threadIdx.x) + u * kBlock;
+        const int c = k / cnt, e = k - c * cnt;
+        if (k < total && idx[e] != kNoSlot) dst[i64(c) * nc + zlo + idx[e]] = v[u];
+      }
+    } else {
+      scatter_cols(alt, dst, int(zc));
+    }
   } else {
     for (i64 e = threadIdx.x; e < zc; e += kBlock) {
       keys[e] = ckey(zlo + e);
@@ -1039,18 +1072,21 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
     gather_cols(alt, dst, int(zc));
   }
   __syncthreads();
-  copy_cols(dst, alt, int(zc));
-  for (i64 e = threadIdx.x; e < zc; e += kBlock) {
-    const i64 q = zlo + e;
-    if (e == t) {
-      for (int c = 0; c < dim; ++c) a.out_pts[mpos * dim + c] = alt[i64(c) * nc + q];
-      a.out_ids[mpos] = reinterpret_cast<const u32*>(alt)[i64(dim) * nc + q];
-    } else if (fuse) {
-      add_next_hist(a, s, h, e < t ? 0 : 1, alt[i64(a.next_axis) * nc + q]);
-    }
+  if (!inplace) copy_cols(dst, alt, int(zc));
+  const float* zb = inplace ? dst : alt;  // the ordered zone (same values in both after the copy)
+  __syncthreads();
+  // the median row: one column per thread (a single thread would chain dim dependent
+  // load/store pairs)
+  for (int c = threadIdx.x; c <= dim; c += kBlock) {
+    const float v = zb[i64(c) * nc + zlo + t];
+    if (c < dim) a.out_pts[mpos * dim + c] = v;
+    else a.out_ids[mpos] = __float_as_uint(v);
   }
+  if (fuse)
+    for (i64 e = threadIdx.x; e < zc; e += kBlock)
+      if (e != t) add_next_hist(a, s, h, e < t ? 0 : 1, zb[i64(a.next_axis) * nc + zlo + e]);
   // Children cells: the split value bounds the split axis.
-  const float split = alt[i64(a.axis) * nc + zlo + t];
+  const float split = zb[i64(a.axis) * nc + zlo + t];
   const float* cell = a.cells + h * 2 * dim;
   float* cl_ = a.cells + (2 * h + 1) * 2 * dim;
   float* cr_ = a.cells + (2 * h + 2) * 2 * dim;
