@@ -363,6 +363,7 @@ struct LevelArgs {
   int block_reserve;     // 1: count the block's zones first and reserve once per block
   int small_done;        // 1: k_refine_small already resolved middle zones of <= 64 points
   u32* hist2;            // stage-2 histograms [segs][kBins2] (levels with stage2)
+  int colgroup;          // runtime-dim partition: columns moved per load round (8, 16, 32)
   int id_implicit;       // 1 (first level only): src has no id column, id of column row p = id_base0 + p
   u32 id_base0;
 };
@@ -795,25 +796,30 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
         }
       }
     } else {
-      // runtime dim: kColGroup columns per round, all of a round's loads issued before its
-      // stores (one HBM latency per round instead of per column)
-      constexpr int kColGroup = 8;
-      for (int cg = 0; cg <= dim; cg += kColGroup) {
-        float v[kColGroup][kItems];
+      // runtime dim: G columns per round, all of a round's loads issued before its stores
+      // (one HBM latency per round instead of per column)
+      auto move = [&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        for (int cg = 0; cg <= dim; cg += G) {
+          float v[G][kItems];
 #pragma unroll
-        for (int j = 0; j < kColGroup; ++j)
+          for (int j = 0; j < G; ++j)
 #pragma unroll
-          for (int i = 0; i < kItems; ++i) {
-            const i64 e = c0 + i * kBlock + threadIdx.x;
-            const int c = cg + j <= dim ? cg + j : dim;
-            v[j][i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
-          }
+            for (int i = 0; i < kItems; ++i) {
+              const i64 e = c0 + i * kBlock + threadIdx.x;
+              const int c = cg + j <= dim ? cg + j : dim;
+              v[j][i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
+            }
 #pragma unroll
-        for (int j = 0; j < kColGroup; ++j)
+          for (int j = 0; j < G; ++j)
 #pragma unroll
-          for (int i = 0; i < kItems; ++i)
-            if (cg + j <= dim && zone_pre[i] != 0xffffffffu) dst[i64(cg + j) * nc + lo + zone_pre[i]] = v[j][i];
-      }
+            for (int i = 0; i < kItems; ++i)
+              if (cg + j <= dim && zone_pre[i] != 0xffffffffu) dst[i64(cg + j) * nc + lo + zone_pre[i]] = v[j][i];
+        }
+      };
+      if (a.colgroup >= 32) move(std::integral_constant<int, 32>{});
+      else if (a.colgroup >= 16) move(std::integral_constant<int, 16>{});
+      else move(std::integral_constant<int, 8>{});
     }
     __syncthreads();
   }
@@ -1813,6 +1819,15 @@ bool implicit_ids_enabled() {
 
 // First-level histogram on half the blocks (its 4096-bin flush per block is the cost beyond
 // the key read): 100M x 3D k_hist 130 -> 115 us. PKD_HIST_DIV overrides.
+// Columns per load round of the runtime-dim partition: more bytes in flight per thread for
+// wide rows (1M x 64D 2.67 -> 2.56 ms with 16, 500k x 128D 2.76 -> 2.62 ms with 32; 16D
+// keeps 8). PKD_COLGROUP overrides.
+int colgroup(int dim) {
+  const char* e = std::getenv("PKD_COLGROUP");
+  if (e) return std::atoi(e);
+  return dim >= 96 ? 32 : (dim >= 48 ? 16 : 8);
+}
+
 int hist_div() {
   const char* e = std::getenv("PKD_HIST_DIV");
   return e ? std::max(1, std::atoi(e)) : 2;
@@ -2097,6 +2112,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.small_done = 0;
     a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
     a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
+    a.colgroup = colgroup(dim_);
     a.id_base0 = id_base;
     return a;
   };

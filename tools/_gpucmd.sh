@@ -1,5 +1,6 @@
 export TMPDIR=/tmp
-python tools/gpu_steps.py \
-  t 600 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_build.py -m gpu' \
-  b 200 'python tools/bench_build.py --n 500000 --dim 128 --steps 20 --data reference && python tools/bench_build.py --n 1000000 --dim 16 32 64 --steps 10' \
-  p 100 'rocprofv3 --kernel-trace --output-format csv -d gpurun_out/p128b -o run -- python3 tools/bench_build.py --n 500000 --dim 128 --steps 3 --data reference'
+for g in 8 16 32 8 16 32; do
+PKD_COLGROUP=$g timeout -k 10 100 python tools/bench_build.py --n 500000 --dim 128 --steps 20 --data reference > gpurun_out/cg_$g.log 2>&1 || exit 1
+PKD_COLGROUP=$g timeout -k 10 100 python tools/bench_build.py --n 1000000 --dim 16 64 --steps 10 >> gpurun_out/cg_$g.log 2>&1 || exit 1
+echo "cg $g"; grep -o '"dim": [0-9]*\|"ms": [0-9.]*' gpurun_out/cg_$g.log | paste - - | tail -3
+done
