@@ -1,6 +1,6 @@
 export TMPDIR=/tmp
-for g in 8 16 32 8 16 32; do
-PKD_COLGROUP=$g timeout -k 10 100 python tools/bench_build.py --n 500000 --dim 128 --steps 20 --data reference > gpurun_out/cg_$g.log 2>&1 || exit 1
-PKD_COLGROUP=$g timeout -k 10 100 python tools/bench_build.py --n 1000000 --dim 16 64 --steps 10 >> gpurun_out/cg_$g.log 2>&1 || exit 1
-echo "cg $g"; grep -o '"dim": [0-9]*\|"ms": [0-9.]*' gpurun_out/cg_$g.log | paste - - | tail -3
-done
+python tools/gpu_steps.py \
+  t 900 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/ -m gpu' \
+  smoke 200 'python -c "import __graft_entry__ as g; g.smoke()"' \
+  bench 200 'python bench.py --steps 20 --warmup 3' \
+  sizes 300 'python tools/bench_build.py --n 12500000 25000000 50000000 100000000 --dim 3 --steps 10 && python tools/bench_build.py --n 100000000 --dim 8 --steps 5 && python tools/bench_build.py --n 500000 --dim 128 --steps 20 --data reference && python tools/bench_build.py --n 1000000000 --dim 3 --steps 3'
