@@ -192,11 +192,17 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
 // loads (contiguous rows) and the column stores (kPrepRows consecutive floats per column) are
 // coalesced; the box is reduced per (wave, column) with one LDS atomic pair. (k_prep<0>
 // stores one float per thread with a column stride between lanes: 10x slower at 128-D.)
+// narrow_k > 0 (narrow columns): coordinate c is written only if it is the key of a global
+// level j < narrow_k (axis (depth0 + j) % dim, so column j), then the id column (narrow_k) and
+// the input row index (narrow_k + 1); the box still covers every coordinate.
 __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                        u32 id_base, float* __restrict__ cols, i64 n, int dim,
-                                                       u32* __restrict__ bbox, int rs, int ids_in_row, i64 ncol) {
+                                                       u32* __restrict__ bbox, int rs, int ids_in_row, i64 ncol,
+                                                       int narrow_k, int depth0) {
   extern __shared__ __align__(16) u32 sbox[];  // [2*dim] box | [dim][kPrepRows + 1] tile
-  u32* idcol = reinterpret_cast<u32*>(cols + i64(dim) * ncol);
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(narrow_k > 0 ? narrow_k : dim) * ncol);
+  auto out_col = [&](int c) { return narrow_k > 0 ? (c - depth0 % dim + dim) % dim : c; };
+  const int ncol_out = narrow_k > 0 ? narrow_k : dim;
   u32* sb = sbox;                                           // [2 * dim]
   float* tile = reinterpret_cast<float*>(sbox + 2 * dim);   // [dim][kPrepRows + 1]
   constexpr int TR = kPrepRows;
@@ -214,7 +220,8 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
       const int c = k / TR, rr = k - c * TR;
       const bool ok = rr < rows;
       const float v = tile[c * (TR + 1) + rr];
-      if (ok) cols[i64(c) * ncol + r0 + rr] = v;
+      const int oc = out_col(c);
+      if (ok && oc < ncol_out) cols[i64(oc) * ncol + r0 + rr] = v;
       const u32 kv = ok ? orderable(v) : 0xffffffffu;
       const u32 mn = dev::wave_min_u32(kv), mx = dev::wave_max_u32(ok ? orderable(v) : 0u);
       if (ln == 0) {
@@ -225,6 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
     for (int rr = threadIdx.x; rr < rows; rr += kBlock) {
       const i64 r = r0 + rr;
       idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
+      if (narrow_k > 0) idcol[ncol + r] = u32(r);
     }
   }
   __syncthreads();
@@ -364,6 +372,16 @@ struct LevelArgs {
   int small_done;        // 1: k_refine_small already resolved middle zones of <= 64 points
   u32* hist2;            // stage-2 histograms [segs][kBins2] (levels with stage2)
   int colgroup;          // runtime-dim partition: columns moved per load round (8, 16, 32)
+  // Column roles in src/dst. Classic: column c = coordinate c, column dim = id. Narrow
+  // (high-dim AoS input): only the keys of the global levels travel (column l = level l's
+  // key), then the id and the input row index; full rows are gathered from `in_rows` by
+  // index where a median is written out.
+  int kcol, nkcol;       // this / the next level's key column
+  int idcol;             // id column
+  int ncols;             // columns moved per row
+  int narrow;            // 1: narrow columns (idcol + 1 holds the input row index)
+  const float* in_rows;  // narrow: the AoS input, row stride in_rs floats
+  i64 in_rs;
   int id_implicit;       // 1 (first level only): src has no id column, id of column row p = id_base0 + p
   u32 id_base0;
 };
@@ -371,10 +389,10 @@ struct LevelArgs {
 // Id of src column row p (absolute), materialised or implicit (first level of a build whose
 // prep skipped the id column).
 __device__ __forceinline__ u32 src_id(const LevelArgs& a, i64 p) {
-  return a.id_implicit ? a.id_base0 + u32(p) : reinterpret_cast<const u32*>(a.src)[i64(a.dim) * a.ncol + p];
+  return a.id_implicit ? a.id_base0 + u32(p) : reinterpret_cast<const u32*>(a.src)[i64(a.idcol) * a.ncol + p];
 }
 __device__ __forceinline__ float src_col(const LevelArgs& a, int c, i64 p) {
-  return (c == a.dim && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : a.src[i64(c) * a.ncol + p];
+  return (c == a.idcol && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : a.src[i64(c) * a.ncol + p];
 }
 
 // Zone of a point: 0 left of the median bucket, 1 inside (the middle zone), 2 right.
@@ -415,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ 
   const i64 per = (n + a.bps - 1) / a.bps;
   const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   const BucketParams p = a.params[h];
-  const float* key = a.src + i64(a.axis) * a.ncol + lo;
+  const float* key = a.src + i64(a.kcol) * a.ncol + lo;
   constexpr int U = 8;
   for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
     float k[U];
@@ -552,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
   BucketParams p2;
   p2.lo = st->p2lo;
   p2.scale = st->p2scale;
-  const float* key = a.src + i64(a.axis) * a.ncol + lo;
+  const float* key = a.src + i64(a.kcol) * a.ncol + lo;
   constexpr int U = 8;
   for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
     float k[U];
@@ -666,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
     // same three words. Count this block's zones from the key column first (an extra 4 B
     // read per point, served from the Infinity Cache on the second pass) and reserve once.
     u32 cnt0 = 0, cnt1 = 0;
-    const float* kc = src + i64(axis) * nc + lo;
+    const float* kc = src + i64(a.kcol) * nc + lo;
     constexpr int U = 8;
     for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
       float k[U];
@@ -717,8 +735,8 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
 #pragma unroll
         for (int c = 0; c < NR; ++c) row[i][c] = src[i64(c) * nc + p];
       } else {
-        kk[i] = src[i64(axis) * nc + p];
-        nkk[i] = src[i64(naxis) * nc + p];
+        kk[i] = src[i64(a.kcol) * nc + p];
+        nkk[i] = src[i64(a.nkcol) * nc + p];
       }
     }
     u32 zone_pre[kItems];  // (zone << 16) | rank-in-wave
@@ -749,7 +767,7 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
         u64 k = 0;
         if (z == 1)  // the id is in the register row when the dim is compile-time
           k = composite_key(key, NCOL > 0 ? __float_as_uint(row[i][NR - 1])
-                                          : reinterpret_cast<const u32*>(src)[i64(dim) * nc + lo + e]);
+                                          : reinterpret_cast<const u32*>(src)[i64(a.idcol) * nc + lo + e]);
         wave_minmax_atomic(z == 1, k, &bmin, &bmax);
       }
       if (fuse && z < 3 && z != 1) {
@@ -800,21 +818,22 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
       // (one HBM latency per round instead of per column)
       auto move = [&](auto gc) {
         constexpr int G = decltype(gc)::value;
-        for (int cg = 0; cg <= dim; cg += G) {
+        const int lastc = a.ncols - 1;
+        for (int cg = 0; cg <= lastc; cg += G) {
           float v[G][kItems];
 #pragma unroll
           for (int j = 0; j < G; ++j)
 #pragma unroll
             for (int i = 0; i < kItems; ++i) {
               const i64 e = c0 + i * kBlock + threadIdx.x;
-              const int c = cg + j <= dim ? cg + j : dim;
+              const int c = cg + j <= lastc ? cg + j : lastc;
               v[j][i] = src[i64(c) * nc + lo + (e < b1 ? e : b0)];
             }
 #pragma unroll
           for (int j = 0; j < G; ++j)
 #pragma unroll
             for (int i = 0; i < kItems; ++i)
-              if (cg + j <= dim && zone_pre[i] != 0xffffffffu) dst[i64(cg + j) * nc + lo + zone_pre[i]] = v[j][i];
+              if (cg + j <= lastc && zone_pre[i] != 0xffffffffu) dst[i64(cg + j) * nc + lo + zone_pre[i]] = v[j][i];
         }
       };
       if (a.colgroup >= 32) move(std::integral_constant<int, 32>{});
@@ -900,17 +919,17 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   i64 zc = st.cnt_mid;
   i64 t = n / 2 - i64(st.cnt_less);
   auto ckey = [&](i64 p) -> u64 {
-    const u32 id = reinterpret_cast<const u32*>(dst)[i64(dim) * nc + p];
-    return composite_key(dst[i64(a.axis) * nc + p], id);
+    const u32 id = reinterpret_cast<const u32*>(dst)[i64(a.idcol) * nc + p];
+    return composite_key(dst[i64(a.kcol) * nc + p], id);
   };
   auto copy_row = [&](float* to, i64 q, const float* from, i64 p) {
-    for (int c = 0; c <= dim; ++c) to[i64(c) * nc + q] = from[i64(c) * nc + p];
+    for (int c = 0; c < a.ncols; ++c) to[i64(c) * nc + q] = from[i64(c) * nc + p];
   };
   // Whole-block column-major moves of the zone's rows [zlo, zlo + cnt): consecutive threads
   // touch consecutive rows of one column, so every load is independent of the others (a row
   // per thread would chain dim + 1 load/store pairs, ~130 HBM latencies at 128-D).
   constexpr u32 kNoSlot = 0xffffffffu;
-  const int ncols = dim + 1;
+  const int ncols = a.ncols;
   // kMoveU elements per thread per round, all loads of a round before its stores (a loop of
   // single load/store pairs would pay one HBM latency per element per thread: at 128-D a
   // 40-row zone is 20 such rounds per move)
@@ -1013,7 +1032,7 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
         if (z < 3) {
           if (coop) idx[e] = dest;  // rows move below, column by column
           else copy_row(alt, zlo + dest, dst, zlo + e);
-          if (fuse && z != 1) add_next_hist(a, s, h, z == 0 ? 0 : 1, dst[i64(a.next_axis) * nc + zlo + e]);
+          if (fuse && z != 1) add_next_hist(a, s, h, z == 0 ? 0 : 1, dst[i64(a.nkcol) * nc + zlo + e]);
         } else if (coop && e < zc) {
           idx[e] = kNoSlot;
         }
@@ -1083,16 +1102,22 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   __syncthreads();
   // the median row: one column per thread (a single thread would chain dim dependent
   // load/store pairs)
-  for (int c = threadIdx.x; c <= dim; c += kBlock) {
-    const float v = zb[i64(c) * nc + zlo + t];
-    if (c < dim) a.out_pts[mpos * dim + c] = v;
-    else a.out_ids[mpos] = __float_as_uint(v);
+  if (a.narrow) {  // gathered from the input row
+    const u32 r = reinterpret_cast<const u32*>(zb)[i64(a.idcol + 1) * nc + zlo + t];
+    for (int c = threadIdx.x; c < dim; c += kBlock) a.out_pts[mpos * dim + c] = a.in_rows[i64(r) * a.in_rs + c];
+    if (threadIdx.x == 0) a.out_ids[mpos] = reinterpret_cast<const u32*>(zb)[i64(a.idcol) * nc + zlo + t];
+  } else {
+    for (int c = threadIdx.x; c <= dim; c += kBlock) {
+      const float v = zb[i64(c) * nc + zlo + t];
+      if (c < dim) a.out_pts[mpos * dim + c] = v;
+      else a.out_ids[mpos] = __float_as_uint(v);
+    }
   }
   if (fuse)
     for (i64 e = threadIdx.x; e < zc; e += kBlock)
-      if (e != t) add_next_hist(a, s, h, e < t ? 0 : 1, zb[i64(a.next_axis) * nc + zlo + e]);
+      if (e != t) add_next_hist(a, s, h, e < t ? 0 : 1, zb[i64(a.nkcol) * nc + zlo + e]);
   // Children cells: the split value bounds the split axis.
-  const float split = zb[i64(a.axis) * nc + zlo + t];
+  const float split = zb[i64(a.kcol) * nc + zlo + t];
   const float* cell = a.cells + h * 2 * dim;
   float* cl_ = a.cells + (2 * h + 1) * 2 * dim;
   float* cr_ = a.cells + (2 * h + 2) * 2 * dim;
@@ -1822,6 +1847,12 @@ bool implicit_ids_enabled() {
 // Columns per load round of the runtime-dim partition: more bytes in flight per thread for
 // wide rows (1M x 64D 2.67 -> 2.56 ms with 16, 500k x 128D 2.76 -> 2.62 ms with 32; 16D
 // keeps 8). PKD_COLGROUP overrides.
+bool narrow_enabled() {
+  const char* e = std::getenv("PKD_NARROW");
+  const char* impl = std::getenv("PKD_SUBTREE_IMPL");
+  return !(e && std::string(e) == "0") && !(impl && std::string(impl) == "hist");
+}
+
 int colgroup(int dim) {
   const char* e = std::getenv("PKD_COLGROUP");
   if (e) return std::atoi(e);
@@ -2014,6 +2045,10 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
       attr = true;
     }
   }
+  // High-dim AoS input: only the global levels' keys, the ids and the input row index travel
+  // through the global levels (lg_ + 2 columns instead of dim + 1); the subtree kernel and the
+  // median writes gather whole rows from the input, which outlives the build.
+  const int narrow_k = (tiled && lg_ >= 1 && 2 * (lg_ + 2) < dim_ + 1 && narrow_enabled()) ? lg_ : 0;
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
@@ -2038,14 +2073,16 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     case 7: k_prep<7><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
     case 8: k_prep<8><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_); break;
     default:
-      if (tiled) k_prep_tiled<<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_);
+      if (tiled)
+        k_prep_tiled<<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0,
+                                                    ncol_, narrow_k, opt_.depth0);
       else k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_);
       break;
   }
   PKD_LAUNCH_CHECK();
   k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
-  run_levels(out_pts, out_ids, ws, stream);
+  run_levels(out_pts, out_ids, ws, stream, false, 0, narrow_k, pts, rs);
 }
 
 void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
@@ -2064,7 +2101,7 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
 }
 
 void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
-                            u32 id_base) const {
+                            u32 id_base, int narrow_k, const float* in_rows, i64 in_rs) const {
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
@@ -2112,7 +2149,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.small_done = 0;
     a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
     a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
-    a.colgroup = colgroup(dim_);
+    a.narrow = narrow_k > 0 ? 1 : 0;
+    a.kcol = a.narrow ? l : a.axis;
+    a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
+    a.idcol = a.narrow ? narrow_k : dim_;
+    a.ncols = a.narrow ? narrow_k + 2 : dim_ + 1;
+    a.colgroup = colgroup(a.ncols - 1);
+    a.in_rows = in_rows;
+    a.in_rs = in_rs;
     a.id_base0 = id_base;
     return a;
   };
@@ -2227,7 +2271,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   const i64 heap0 = (i64(1) << lg_) - 1;
   TraceRange trs("pkd.subtree");
   launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
-                 out_ids, err, stream);
+                 out_ids, err, stream, narrow_k, in_rows, in_rs);
 }
 
 }  // namespace pkdtree

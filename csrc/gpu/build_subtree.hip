@@ -57,6 +57,9 @@ struct SubArgs {
   u32* out_ids;
   u32* err;
   unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][kStampSlots] s_memtime
+  int narrow_k;                // > 0: narrow columns, rows gathered from in_rows by input row index
+  const float* in_rows;
+  i64 in_rs;
 };
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
@@ -706,7 +709,33 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const u32 dummy = u32(NM + 4) + lane_dummy;
   stamp(a, 0);
 
-  {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
+  if (a.narrow_k > 0) {  // ids and input row indices, then whole rows gathered from the input
+    u32* ridx = work;       // scratch until the first level
+    u32* idw = reinterpret_cast<u32*>(rows + dim * NM);
+    const u32* idc = reinterpret_cast<const u32*>(a.cols) + i64(a.narrow_k) * a.ncol + glo;
+    for (int k = tid; k < n; k += THREADS) {
+      idw[k] = idc[k];
+      ridx[k] = idc[a.ncol + k];
+    }
+    for (int k = tid; k < 2 * dim; k += THREADS) cellv[k] = a.cells[h * dim * 2 + k];
+    __syncthreads();
+    constexpr int kG = 8;  // loads in flight per thread
+    const int total = n * dim;
+    for (int e0 = tid; e0 < total; e0 += THREADS * kG) {
+      float v[kG];
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int e = e0 + u * THREADS, k = e / dim, c = e - k * dim;
+        v[u] = e < total ? a.in_rows[i64(ridx[k]) * a.in_rs + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int e = e0 + u * THREADS, k = e / dim, c = e - k * dim;
+        if (e < total) rows[c * NM + k] = v[u];
+      }
+    }
+    __syncthreads();  // ridx (work) is reused by the levels
+  } else {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
     constexpr int kLoadCols = 5;
     float v[kLoadCols][ITEMS];
 #pragma unroll
@@ -1022,7 +1051,7 @@ int subtree_capacity_max(int dim) {
 
 void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, const i64* seg_n, const float* cells,
                     i64 heap0, i64 segs, int depth_base, int nmax, float* out_pts, u32* out_ids, u32* err,
-                    hipStream_t stream) {
+                    hipStream_t stream, int narrow_k, const float* in_rows, i64 in_rs) {
   if (segs <= 0) return;
   static unsigned long long* stamps = nullptr;
   if (std::getenv("PKD_SUBTREE_STAMPS") && !stamps) {
@@ -1030,7 +1059,9 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     PKD_HIP_CHECK(hipMemset(stamps, 0, size_t(kStampBlocks) * kStampSlots * sizeof(unsigned long long)));
   }
   subtree_stamp_buffer() = stamps;
-  SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps};
+  if (narrow_k > 0 && use_hist_impl()) throw std::runtime_error("pkdtree: narrow columns need the rank subtree kernel");
+  SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
+            narrow_k, in_rows, in_rs};
   if (!use_hist_impl()) {
     static const bool wide = [] {
       const char* e = std::getenv("PKD_SUBTREE_WIDE");

@@ -76,8 +76,10 @@ class GpuBuilder {
                     u32* out_ids, void* workspace, hipStream_t stream) const;
   // implicit_ids: the prep left the id column unwritten (ids = id_base + input row); the
   // first pair's kernels synthesise them.
+  // narrow_k > 0: narrow columns (keys of the global levels, ids, input row index) gathered
+  // back to full rows from the AoS input `in_rows` (stride in_rs floats).
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
-                  u32 id_base = 0) const;
+                  u32 id_base = 0, int narrow_k = 0, const float* in_rows = nullptr, i64 in_rs = 0) const;
 
   i64 n_;
   i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)

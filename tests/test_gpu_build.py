@@ -79,6 +79,27 @@ def test_large_stage2_pairs(gpu_device):
     check_same(pk.generate_problem(5, 3, 20_000_000), gpu_device)
 
 
+@pytest.mark.parametrize("dim,n,depth0", [(32, 100_000, 0), (64, 60_000, 5), (128, 100_000, 0), (128, 33_333, 127)])
+def test_narrow_columns(gpu_device, dim, n, depth0):
+    # high-dim AoS input: the global levels move only their keys, the ids and the input row index;
+    # medians and subtree rows are gathered from the input
+    check_same(pk.generate_problem(dim + depth0, dim, n), gpu_device, depth0=depth0)
+
+
+def test_narrow_columns_explicit_ids(gpu_device, monkeypatch):
+    dim, n = 96, 50_000
+    x = pk.generate_problem(11, dim, n)
+    ids = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32) + 7
+    cp, ci = ops.build_cpu(x, ids, "exact", 0, 8)
+    for narrow in ("1", "0"):
+        monkeypatch.setenv("PKD_NARROW", narrow)
+        b = ops.GpuTreeBuilder(n, dim, 0, 0)
+        tp, ti = b.build(x.to(gpu_device), ids.to(gpu_device))
+        torch.cuda.synchronize()
+        assert b.read_error() == 0
+        assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+
+
 @pytest.mark.parametrize("prefix", ["1", "0"])
 def test_large_stage2_pairs_prefix_placement(gpu_device, monkeypatch, prefix):
     # prefix placement of the top pairs (per-block offsets from k_hist2p's counts) on skewed
