@@ -192,17 +192,17 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float* __restrict__ pts, 
 // loads (contiguous rows) and the column stores (kPrepRows consecutive floats per column) are
 // coalesced; the box is reduced per (wave, column) with one LDS atomic pair. (k_prep<0>
 // stores one float per thread with a column stride between lanes: 10x slower at 128-D.)
-// narrow_k > 0 (narrow columns): coordinate c is written only if it is the key of a global
+// narrow (narrow columns): coordinate c is written only if it is the key of a global
 // level j < narrow_k (axis (depth0 + j) % dim, so column j), then the id column (narrow_k) and
 // the input row index (narrow_k + 1); the box still covers every coordinate.
 __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                        u32 id_base, float* __restrict__ cols, i64 n, int dim,
                                                        u32* __restrict__ bbox, int rs, int ids_in_row, i64 ncol,
-                                                       int narrow_k, int depth0) {
+                                                       int narrow, int narrow_k, int depth0) {
   extern __shared__ __align__(16) u32 sbox[];  // [2*dim] box | [dim][kPrepRows + 1] tile
-  u32* idcol = reinterpret_cast<u32*>(cols + i64(narrow_k > 0 ? narrow_k : dim) * ncol);
-  auto out_col = [&](int c) { return narrow_k > 0 ? (c - depth0 % dim + dim) % dim : c; };
-  const int ncol_out = narrow_k > 0 ? narrow_k : dim;
+  u32* idcol = reinterpret_cast<u32*>(cols + i64(narrow ? narrow_k : dim) * ncol);
+  auto out_col = [&](int c) { return narrow ? (c - depth0 % dim + dim) % dim : c; };
+  const int ncol_out = narrow ? narrow_k : dim;
   u32* sb = sbox;                                           // [2 * dim]
   float* tile = reinterpret_cast<float*>(sbox + 2 * dim);   // [dim][kPrepRows + 1]
   constexpr int TR = kPrepRows;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
     for (int rr = threadIdx.x; rr < rows; rr += kBlock) {
       const i64 r = r0 + rr;
       idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
-      if (narrow_k > 0) idcol[ncol + r] = u32(r);
+      if (narrow) idcol[ncol + r] = u32(r);
     }
   }
   __syncthreads();
@@ -1918,6 +1918,18 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity_max(dim)) : subtree_capacity(dim);
+  // High dims: narrow columns (the global levels move lg + 2 columns instead of dim + 1) and the
+  // key-slot subtree kernel, whose LDS holds only its own levels' keys, so segments are larger
+  if (dim > 8 && tiled_prep_lds(dim) <= size_t(96 * 1024) && narrow_enabled()) {
+    const int capn = subtree_capacity_narrow(dim);
+    const int cap = opt.subtree_max > 0 ? std::min(opt.subtree_max, capn) : capn;
+    int lg = 0;
+    while (cap > 0 && (n_ >> lg) > cap) ++lg;
+    if (cap > 0 && 2 * (lg + 2) < dim + 1) {
+      narrow_ = true;
+      nsub_ = cap;
+    }
+  }
   lg_ = 0;
   while ((n_ >> lg_) > nsub_) ++lg_;
   heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
@@ -2048,7 +2060,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   // High-dim AoS input: only the global levels' keys, the ids and the input row index travel
   // through the global levels (lg_ + 2 columns instead of dim + 1); the subtree kernel and the
   // median writes gather whole rows from the input, which outlives the build.
-  const int narrow_k = (tiled && lg_ >= 1 && 2 * (lg_ + 2) < dim_ + 1 && narrow_enabled()) ? lg_ : 0;
+  const bool narrow = narrow_ && tiled;
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
@@ -2075,18 +2087,19 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     default:
       if (tiled)
         k_prep_tiled<<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0,
-                                                    ncol_, narrow_k, opt_.depth0);
+                                                    ncol_, narrow ? 1 : 0, lg_, opt_.depth0);
       else k_prep<0><<<grid, kBlock, lds, stream>>>(pts, ids, id_base, colsA, n_, dim_, part, rs, ids_in_row ? 1 : 0, ncol_);
       break;
   }
   PKD_LAUNCH_CHECK();
   k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, grid, dim_, bbox);
   PKD_LAUNCH_CHECK();
-  run_levels(out_pts, out_ids, ws, stream, false, 0, narrow_k, pts, rs);
+  run_levels(out_pts, out_ids, ws, stream, false, 0, narrow ? pts : nullptr, rs);
 }
 
 void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
+  if (narrow_) throw std::runtime_error("pkdtree: build_from_soa needs the full-column layout (set PKD_NARROW=0)");
   TraceRange tr("pkd.build");
   char* ws = static_cast<char*>(workspace);
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
@@ -2101,7 +2114,8 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
 }
 
 void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
-                            u32 id_base, int narrow_k, const float* in_rows, i64 in_rs) const {
+                            u32 id_base, const float* in_rows, i64 in_rs) const {
+  const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
   float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
@@ -2149,7 +2163,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     a.small_done = 0;
     a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
     a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
-    a.narrow = narrow_k > 0 ? 1 : 0;
+    a.narrow = in_rows ? 1 : 0;
     a.kcol = a.narrow ? l : a.axis;
     a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
     a.idcol = a.narrow ? narrow_k : dim_;
@@ -2271,7 +2285,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   const i64 heap0 = (i64(1) << lg_) - 1;
   TraceRange trs("pkd.subtree");
   launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
-                 out_ids, err, stream, narrow_k, in_rows, in_rs);
+                 out_ids, err, stream, in_rows ? narrow_k : -1, in_rows, in_rs);
 }
 
 }  // namespace pkdtree

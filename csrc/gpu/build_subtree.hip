@@ -57,9 +57,10 @@ struct SubArgs {
   u32* out_ids;
   u32* err;
   unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][kStampSlots] s_memtime
-  int narrow_k;                // > 0: narrow columns, rows gathered from in_rows by input row index
+  int narrow_k;                // narrow (ldim > 0): id column; the input row index follows it
   const float* in_rows;
   i64 in_rs;
+  int ldim;                    // narrow: LDS key slots (slot t = key of subtree level t), 0 otherwise
 };
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
@@ -645,6 +646,10 @@ size_t lds_words(int dim, int nm) {
   return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 68 + 2 * (size_t(nm) + 64) +
          size_t(nm) / 2 + 32 + 2 * size_t(dim);
 }
+// narrow mode: ldim key slots + ids + input row indices, no compressed ranks (ldim <= dim)
+size_t lds_words_narrow(int dim, int nm, int ldim) {
+  return size_t(ldim + 2) * nm + size_t(nm) + 68 + 2 * (size_t(nm) + 64) + size_t(nm) / 2 + 32 + 2 * size_t(dim);
+}
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
 // m <= CMAX * THREADS. Fixed-trip predicated loops and a shuffle reduction of the wave
@@ -694,13 +699,20 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const int lsub = rk::bitlen(u32(n));  // levels of the implicit subtree of n points
   const int kept_layout = rk::kept_axes(dim, NM);
   const bool keep = dim < lsub;
+  // Narrow mode (high dim): LDS holds only the keys of the subtree's own levels (slot t = level
+  // t's axis; a.ldim >= lsub and no axis repeats, so keep is false), the ids and the input row
+  // indices; output rows are copied from the input. Classic: all dim coordinates + ids.
+  const bool narrow = a.ldim > 0;
+  const int kslots = narrow ? a.ldim : dim;
+  const int rcols = narrow ? a.ldim + 2 : dim + 1;
   float* rows = reinterpret_cast<float*>(smem);
-  const u32* idrow = reinterpret_cast<const u32*>(rows + dim * NM);
+  const u32* idrow = reinterpret_cast<const u32*>(rows + kslots * NM);
+  u32* ridx = reinterpret_cast<u32*>(rows + (kslots + 1) * NM);  // narrow only
   // crank[axis][...]: a thread's compressed ranks are private to it; with 2 items per thread
   // they sit side by side (index 2 * tid + i), so one ds_read_b32 / ds_write_b32 moves both and
   // no two lanes share a dword
-  u16* crank = reinterpret_cast<u16*>(smem + size_t(dim + 1) * NM);
-  u32* work = smem + size_t(dim + 1) * NM + (size_t(kept_layout) * NM + 1) / 2;
+  u16* crank = reinterpret_cast<u16*>(smem + size_t(rcols) * NM);
+  u32* work = smem + size_t(rcols) * NM + (size_t(kept_layout) * NM + 1) / 2;
   u32* aux = work + NM + 4 + 64;  // work: NM buckets, sentinel, 64 per-lane dummy words
   u32* fin = aux + NM + 64;           // aux / fin: NM entries + 64 per-lane dummies each
   u16* tmpi = reinterpret_cast<u16*>(fin + NM + 64);  // NM + 64 entries
@@ -709,9 +721,8 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const u32 dummy = u32(NM + 4) + lane_dummy;
   stamp(a, 0);
 
-  if (a.narrow_k > 0) {  // ids and input row indices, then whole rows gathered from the input
-    u32* ridx = work;       // scratch until the first level
-    u32* idw = reinterpret_cast<u32*>(rows + dim * NM);
+  if (narrow) {  // ids and input row indices, then the subtree levels' keys from the input rows
+    u32* idw = reinterpret_cast<u32*>(rows + kslots * NM);
     const u32* idc = reinterpret_cast<const u32*>(a.cols) + i64(a.narrow_k) * a.ncol + glo;
     for (int k = tid; k < n; k += THREADS) {
       idw[k] = idc[k];
@@ -720,21 +731,20 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
     for (int k = tid; k < 2 * dim; k += THREADS) cellv[k] = a.cells[h * dim * 2 + k];
     __syncthreads();
     constexpr int kG = 8;  // loads in flight per thread
-    const int total = n * dim;
+    const int total = n * kslots;
     for (int e0 = tid; e0 < total; e0 += THREADS * kG) {
       float v[kG];
 #pragma unroll
       for (int u = 0; u < kG; ++u) {
-        const int e = e0 + u * THREADS, k = e / dim, c = e - k * dim;
-        v[u] = e < total ? a.in_rows[i64(ridx[k]) * a.in_rs + c] : 0.0f;
+        const int e = e0 + u * THREADS, k = e / kslots, t = e - k * kslots;
+        v[u] = e < total ? a.in_rows[i64(ridx[k]) * a.in_rs + (a.depth_base + t) % dim] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < kG; ++u) {
-        const int e = e0 + u * THREADS, k = e / dim, c = e - k * dim;
-        if (e < total) rows[c * NM + k] = v[u];
+        const int e = e0 + u * THREADS, k = e / kslots, t = e - k * kslots;
+        if (e < total) rows[t * NM + k] = v[u];
       }
     }
-    __syncthreads();  // ridx (work) is reused by the levels
   } else {  // rows -> LDS: every load of the first kLoadCols columns issued before any LDS store
     constexpr int kLoadCols = 5;
     float v[kLoadCols][ITEMS];
@@ -785,7 +795,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
 
   for (int t = 0; t < lsub; ++t) {
     const int axis = (a.depth_base + t) % dim;
-    const float* kcol = rows + axis * NM;
+    const float* kcol = rows + (narrow ? t : axis) * NM;
     u16* cr = crank + size_t(axis) * NM;
     const int S = 1 << t;
     int Wt = 0;
@@ -942,23 +952,57 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   // in-order rows out: thread per slot, the row's dim floats (consecutive threads cover
   // consecutive 4*dim-byte runs, merged in L2)
   float* outp = a.out_pts + glo * dim;
-  for (int k = tid; k < n; k += THREADS) {
-    u32 p = fin[k];
-    if (p >= u32(NM)) {
-      report(a.err, 0x800u, u32(k), p);
-      p = 0;
+  if (narrow) {  // slot -> input row index, then rows copied from the input (coalesced per row)
+    for (int k = tid; k < n; k += THREADS) {
+      u32 p = fin[k];
+      if (p >= u32(NM)) {
+        report(a.err, 0x800u, u32(k), p);
+        p = 0;
+      }
+      a.out_ids[glo + k] = idrow[p];
+      work[k] = ridx[p];
     }
-    for (int c = 0; c < dim; ++c) outp[i64(k) * dim + c] = rows[c * NM + p];
-    a.out_ids[glo + k] = idrow[p];
+    __syncthreads();
+    constexpr int kG = 8;
+    const int total = n * dim;
+    for (int e0 = tid; e0 < total; e0 += THREADS * kG) {
+      float v[kG];
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int e = e0 + u * THREADS, k = e / dim, c = e - k * dim;
+        v[u] = e < total ? a.in_rows[i64(work[k]) * a.in_rs + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int e = e0 + u * THREADS;
+        if (e < total) outp[e] = v[u];
+      }
+    }
+  } else {
+    for (int k = tid; k < n; k += THREADS) {
+      u32 p = fin[k];
+      if (p >= u32(NM)) {
+        report(a.err, 0x800u, u32(k), p);
+        p = 0;
+      }
+      for (int c = 0; c < dim; ++c) outp[i64(k) * dim + c] = rows[c * NM + p];
+      a.out_ids[glo + k] = idrow[p];
+    }
   }
   __syncthreads();
   stamp(a, 31);
 }
 
 template <int ITEMS, int THREADS>
-void launch_rank_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
+void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
+  SubArgs a = a0;
+  if (a.ldim > 0) {  // a key slot for every level a segment of this capacity can have
+    a.ldim = std::max(a.ldim, rk::bitlen(u32(ITEMS * THREADS)));
+    if (a.ldim > a.dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
+  }
   static bool attr_set = false;
-  const size_t lds = 4 * rk::lds_words(a.dim, ITEMS * THREADS);
+  const size_t lds = 4 * (a.ldim > 0 ? rk::lds_words_narrow(a.dim, ITEMS * THREADS, a.ldim)
+                                     : rk::lds_words(a.dim, ITEMS * THREADS));
   if (!attr_set) {
     PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
@@ -1043,6 +1087,15 @@ int subtree_capacity(int dim) {
   throw std::invalid_argument("pkdtree: dimension too large for the LDS subtree kernel");
 }
 
+int subtree_capacity_narrow(int dim) {
+  if (use_hist_impl()) return 0;
+  for (int nm = 2048; nm >= 64; nm /= 2) {
+    const int ldim = rk::bitlen(u32(nm));
+    if (ldim <= dim && 4 * rk::lds_words_narrow(dim, nm, ldim) <= kLdsMax / 2) return nm;
+  }
+  return 0;
+}
+
 int subtree_capacity_max(int dim) {
   for (int nm = 4096; nm >= 32; nm /= 2)
     if (impl_lds_bytes(dim, nm) <= kLdsMax) return nm;
@@ -1051,7 +1104,7 @@ int subtree_capacity_max(int dim) {
 
 void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, const i64* seg_n, const float* cells,
                     i64 heap0, i64 segs, int depth_base, int nmax, float* out_pts, u32* out_ids, u32* err,
-                    hipStream_t stream, int narrow_k, const float* in_rows, i64 in_rs) {
+                    hipStream_t stream, int narrow_idcol, const float* in_rows, i64 in_rs) {
   if (segs <= 0) return;
   static unsigned long long* stamps = nullptr;
   if (std::getenv("PKD_SUBTREE_STAMPS") && !stamps) {
@@ -1059,9 +1112,13 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     PKD_HIP_CHECK(hipMemset(stamps, 0, size_t(kStampBlocks) * kStampSlots * sizeof(unsigned long long)));
   }
   subtree_stamp_buffer() = stamps;
-  if (narrow_k > 0 && use_hist_impl()) throw std::runtime_error("pkdtree: narrow columns need the rank subtree kernel");
+  if (narrow_idcol >= 0 && use_hist_impl()) throw std::runtime_error("pkdtree: narrow columns need the rank subtree kernel");
+  // narrow: one key slot per subtree level (no axis repeats: the host enables narrow
+  // columns only for dim >= the subtree's levels)
+  const int ldim = narrow_idcol >= 0 ? rk::bitlen(u32(std::max(nmax, 1))) : 0;
+  if (ldim > dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
-            narrow_k, in_rows, in_rs};
+            std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
   if (!use_hist_impl()) {
     static const bool wide = [] {
       const char* e = std::getenv("PKD_SUBTREE_WIDE");

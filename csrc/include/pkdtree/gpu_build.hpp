@@ -76,10 +76,10 @@ class GpuBuilder {
                     u32* out_ids, void* workspace, hipStream_t stream) const;
   // implicit_ids: the prep left the id column unwritten (ids = id_base + input row); the
   // first pair's kernels synthesise them.
-  // narrow_k > 0: narrow columns (keys of the global levels, ids, input row index) gathered
-  // back to full rows from the AoS input `in_rows` (stride in_rs floats).
+  // in_rows != nullptr: narrow columns (the lg_ global levels' keys, ids, input row index);
+  // full rows are gathered from the AoS input `in_rows` (stride in_rs floats).
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
-                  u32 id_base = 0, int narrow_k = 0, const float* in_rows = nullptr, i64 in_rs = 0) const;
+                  u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0) const;
 
   i64 n_;
   i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)
@@ -92,6 +92,7 @@ class GpuBuilder {
   int max_bins_ = 0;
   i64 max_hist_ = 0;
   i64 max_hist2_ = 0;
+  bool narrow_ = false;  // high-dim: narrow columns + key-slot subtree (capacity nsub_ sized for it)
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,
