@@ -685,7 +685,9 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
 
 }  // namespace rk
 
-template <int ITEMS, int THREADS>
+// NARROW is a template parameter so the classic (low-dim) instantiation carries none of the
+// narrow path's registers: a runtime flag cost the 100M x 3D build's subtree kernel 3.7 -> 5.65 ms.
+template <int ITEMS, int THREADS, bool NARROW>
 __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   extern __shared__ __align__(16) u32 smem[];
   __shared__ u32 wsum[THREADS / 64];
@@ -702,7 +704,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   // Narrow mode (high dim): LDS holds only the keys of the subtree's own levels (slot t = level
   // t's axis; a.ldim >= lsub and no axis repeats, so keep is false), the ids and the input row
   // indices; output rows are copied from the input. Classic: all dim coordinates + ids.
-  const bool narrow = a.ldim > 0;
+  constexpr bool narrow = NARROW;
   const int kslots = narrow ? a.ldim : dim;
   const int rcols = narrow ? a.ldim + 2 : dim + 1;
   float* rows = reinterpret_cast<float*>(smem);
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   const u32 dummy = u32(NM + 4) + lane_dummy;
   stamp(a, 0);
 
-  if (narrow) {  // ids and input row indices, then the subtree levels' keys from the input rows
+  if constexpr (NARROW) {  // ids and input row indices, then the subtree levels' keys from the input rows
     u32* idw = reinterpret_cast<u32*>(rows + kslots * NM);
     const u32* idc = reinterpret_cast<const u32*>(a.cols) + i64(a.narrow_k) * a.ncol + glo;
     for (int k = tid; k < n; k += THREADS) {
@@ -952,7 +954,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   // in-order rows out: thread per slot, the row's dim floats (consecutive threads cover
   // consecutive 4*dim-byte runs, merged in L2)
   float* outp = a.out_pts + glo * dim;
-  if (narrow) {  // slot -> input row index, then rows copied from the input (coalesced per row)
+  if constexpr (NARROW) {  // slot -> input row index, then rows copied from the input (coalesced per row)
     for (int k = tid; k < n; k += THREADS) {
       u32 p = fin[k];
       if (p >= u32(NM)) {
@@ -1000,15 +1002,20 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
     a.ldim = std::max(a.ldim, rk::bitlen(u32(ITEMS * THREADS)));
     if (a.ldim > a.dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
   }
-  static bool attr_set = false;
   const size_t lds = 4 * (a.ldim > 0 ? rk::lds_words_narrow(a.dim, ITEMS * THREADS, a.ldim)
                                      : rk::lds_words(a.dim, ITEMS * THREADS));
-  if (!attr_set) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
-    attr_set = true;
+  static bool attr_set[2] = {false, false};
+  const bool nar = a.ldim > 0;
+  const void* fn = nar ? reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, true>)
+                       : reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false>);
+  if (!attr_set[nar]) {
+    PKD_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
+    attr_set[nar] = true;
   }
-  k_subtree_rank<ITEMS, THREADS><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+  if (nar)
+    k_subtree_rank<ITEMS, THREADS, true><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+  else
+    k_subtree_rank<ITEMS, THREADS, false><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
   PKD_LAUNCH_CHECK();
 }
 
