@@ -687,12 +687,13 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
 
 // NARROW is a template parameter so the classic (low-dim) instantiation carries none of the
 // narrow path's registers: a runtime flag cost the 100M x 3D build's subtree kernel 3.7 -> 5.65 ms.
-template <int ITEMS, int THREADS, bool NARROW>
+// DIMC > 0: the dimension as a compile-time constant (d = 3 headline shape), else a.dim.
+template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0>
 __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   extern __shared__ __align__(16) u32 smem[];
   __shared__ u32 wsum[THREADS / 64];
   constexpr int NM = ITEMS * THREADS;
-  const int dim = a.dim;
+  const int dim = DIMC > 0 ? DIMC : a.dim;
   const i64 h = a.heap0 + blockIdx.x;
   const int n = int(a.seg_n[h]);
   if (n <= 0) return;
@@ -1012,10 +1013,28 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
     PKD_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
     attr_set[nar] = true;
   }
-  if (nar)
+  static const bool dim3c = [] {
+    const char* e = std::getenv("PKD_SUBTREE_DIM3");
+    return !(e && std::string(e) == "0");
+  }();
+  bool done = false;
+  if (nar) {
     k_subtree_rank<ITEMS, THREADS, true><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
-  else
-    k_subtree_rank<ITEMS, THREADS, false><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+    done = true;
+  }
+  if constexpr (ITEMS == 2) {
+    if (!done && a.dim == 3 && dim3c) {
+      static bool attr3 = false;
+      if (!attr3) {
+        PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 3>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
+        attr3 = true;
+      }
+      k_subtree_rank<ITEMS, THREADS, false, 3><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+      done = true;
+    }
+  }
+  if (!done) k_subtree_rank<ITEMS, THREADS, false><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
   PKD_LAUNCH_CHECK();
 }
 
