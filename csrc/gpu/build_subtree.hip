@@ -722,6 +722,13 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   float* cellv = reinterpret_cast<float*>(tmpi + NM + 64);  // [dim][2] root cell of the segment
   const u32 lane_dummy = u32(dev::lane());
   const u32 dummy = u32(NM + 4) + lane_dummy;
+  // Item i of a thread is point kid(i): wave w owns the contiguous points [w*64*ITEMS,
+  // (w+1)*64*ITEMS), lanes consecutive within an item (conflict-free LDS reads). Waves whose
+  // whole range lies beyond n (e.g. 4 of 16 at a 1526-point segment in 2048 slots) skip
+  // the per-item phases of every level; they only join the block-wide scans and barriers.
+  const int kbase = (tid & ~63) * ITEMS + (tid & 63);
+  auto kid = [&](int i) { return kbase + i * 64; };
+  const bool wlive = int(__builtin_amdgcn_readfirstlane((tid & ~63) * ITEMS)) < n;
   stamp(a, 0);
 
   if constexpr (NARROW) {  // ids and input row indices, then the subtree levels' keys from the input rows
@@ -791,7 +798,7 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   for (int i = 0; i < ITEMS; ++i) {
     lo[i] = 0;
     sg[i] = 0;
-    nn[i] = (tid + i * THREADS) < n ? u32(n) : 0u;
+    nn[i] = kid(i) < n ? u32(n) : 0u;
   }
   __syncthreads();
   stamp(a, 1);
@@ -816,18 +823,20 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       // Branch-free (the scalar unit, shared by the CU's four SIMDs, is the bottleneck of
       // exec-mask juggling): finished points OR 0 into a private dummy word per lane.
       u32 c[ITEMS], wi[ITEMS];
-      if (ITEMS == 2) {
-        const u32 both = reinterpret_cast<const u32*>(cr)[tid];
-        c[0] = both & 0xffffu;
-        c[ITEMS - 1] = both >> 16;
-      } else {
+      if (wlive) {
+        if (ITEMS == 2) {
+          const u32 both = reinterpret_cast<const u32*>(cr)[tid];
+          c[0] = both & 0xffffu;
+          c[ITEMS - 1] = both >> 16;
+        } else {
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) c[i] = cr[tid + i * THREADS];
-      }
+          for (int i = 0; i < ITEMS; ++i) c[i] = cr[tid + i * THREADS];
+        }
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        wi[i] = nn[i] ? sg[i] * Wt + (c[i] >> 5) : dummy;
-        atomicOr(&work[wi[i]], nn[i] ? 1u << (c[i] & 31) : 0u);
+        for (int i = 0; i < ITEMS; ++i) {
+          wi[i] = nn[i] ? sg[i] * Wt + (c[i] >> 5) : dummy;
+          atomicOr(&work[wi[i]], nn[i] ? 1u << (c[i] & 31) : 0u);
+        }
       }
       __syncthreads();
       if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
@@ -844,9 +853,11 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         }
         __syncthreads();
       }
+      if (wlive) {
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i)
-        rank[i] = (Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u) + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
+        for (int i = 0; i < ITEMS; ++i)
+          rank[i] = (Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u) + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
+      }
     } else {
       // ---- exact ranks from bucket histograms (first use of the axis) ----
       // Bucket range: the block root's cell on this axis. On an axis's first use no split
@@ -867,12 +878,14 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       if (t == 0) stamp(a, 20);
       u32 ok[ITEMS];
       u32 bk[ITEMS], wi[ITEMS];
+      if (wlive) {
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {  // finished points count into a per-lane dummy word
-        const float kf = kcol[tid + i * THREADS];
-        ok[i] = orderable(kf);
-        bk[i] = nn[i] ? sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u) : dummy;
-        wi[i] = atomicAdd(&work[bk[i]], 1u);
+        for (int i = 0; i < ITEMS; ++i) {  // finished points count into a per-lane dummy word
+          const float kf = kcol[kid(i)];
+          ok[i] = orderable(kf);
+          bk[i] = nn[i] ? sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u) : dummy;
+          wi[i] = atomicAdd(&work[bk[i]], 1u);
+        }
       }
       __syncthreads();
       if (t == 0) stamp(a, 21);
@@ -880,74 +893,80 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       __syncthreads();
       if (t == 0) stamp(a, 22);
       u32 pos[ITEMS];
+      if (wlive) {
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + lane_dummy;
-        tmpk[pos[i]] = ok[i];
-        tmpi[pos[i]] = u16(tid + i * THREADS);
+        for (int i = 0; i < ITEMS; ++i) {
+          pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + lane_dummy;
+          tmpk[pos[i]] = ok[i];
+          tmpi[pos[i]] = u16(kid(i));
+        }
       }
       __syncthreads();
       if (t == 0) stamp(a, 23);
-      u32 st[ITEMS], cnt[ITEMS];
+      if (wlive) {
+        u32 st[ITEMS], cnt[ITEMS];
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const u32 bi = nn[i] ? bk[i] : 0u;
-        st[i] = work[bi];
-        const u32 en = nn[i] ? work[bi + 1] : st[i];
-        cnt[i] = en - st[i];
-        rank[i] = st[i] - work[nn[i] ? sg[i] * B : 0u];
-      }
-      // in-bucket comparisons, kU members per round: all items' reads of a round are issued
-      // together; wave-uniform trip count = largest bucket among the wave's items / kU
-      constexpr u32 kU = 2;
-      for (u32 j0 = 0;; j0 += kU) {
-        bool any = false;
+        for (int i = 0; i < ITEMS; ++i) {
+          const u32 bi = nn[i] ? bk[i] : 0u;
+          st[i] = work[bi];
+          const u32 en = nn[i] ? work[bi + 1] : st[i];
+          cnt[i] = en - st[i];
+          rank[i] = st[i] - work[nn[i] ? sg[i] * B : 0u];
+        }
+        // in-bucket comparisons, kU members per round: all items' reads of a round are issued
+        // together; wave-uniform trip count = largest bucket among the wave's items / kU
+        constexpr u32 kU = 2;
+        for (u32 j0 = 0;; j0 += kU) {
+          bool any = false;
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) any |= j0 < cnt[i];
-        if (!__ballot(any)) break;
-        u32 qk[kU][ITEMS];
+          for (int i = 0; i < ITEMS; ++i) any |= j0 < cnt[i];
+          if (!__ballot(any)) break;
+          u32 qk[kU][ITEMS];
 #pragma unroll
-        for (u32 u = 0; u < kU; ++u)
+          for (u32 u = 0; u < kU; ++u)
 #pragma unroll
-          for (int i = 0; i < ITEMS; ++i) qk[u][i] = tmpk[j0 + u < cnt[i] ? st[i] + j0 + u : 0u];
-        bool tany = false;
-#pragma unroll
-        for (u32 u = 0; u < kU; ++u)
-#pragma unroll
-          for (int i = 0; i < ITEMS; ++i) {
-            const bool act = j0 + u < cnt[i];
-            rank[i] += (act && qk[u][i] < ok[i]) ? 1u : 0u;
-            tany |= act && qk[u][i] == ok[i] && st[i] + j0 + u != pos[i];
-          }
-        if (__ballot(tany)) {  // equal keys: the id decides
+            for (int i = 0; i < ITEMS; ++i) qk[u][i] = tmpk[j0 + u < cnt[i] ? st[i] + j0 + u : 0u];
+          bool tany = false;
 #pragma unroll
           for (u32 u = 0; u < kU; ++u)
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
-              const u32 q = st[i] + j0 + u;
-              const bool tie = j0 + u < cnt[i] && qk[u][i] == ok[i] && q != pos[i];
-              rank[i] += (tie && idrow[tmpi[tie ? q : 0u]] < idrow[tid + i * THREADS]) ? 1u : 0u;
+              const bool act = j0 + u < cnt[i];
+              rank[i] += (act && qk[u][i] < ok[i]) ? 1u : 0u;
+              tany |= act && qk[u][i] == ok[i] && st[i] + j0 + u != pos[i];
             }
+          if (__ballot(tany)) {  // equal keys: the id decides
+#pragma unroll
+            for (u32 u = 0; u < kU; ++u)
+#pragma unroll
+              for (int i = 0; i < ITEMS; ++i) {
+                const u32 q = st[i] + j0 + u;
+                const bool tie = j0 + u < cnt[i] && qk[u][i] == ok[i] && q != pos[i];
+                rank[i] += (tie && idrow[tmpi[tie ? q : 0u]] < idrow[kid(i)]) ? 1u : 0u;
+              }
+          }
         }
       }
       if (t == 0) stamp(a, 24);
     }
     // ---- median / left / right (selects only; the median's slot write goes to a dummy
     // word for every other point) ----
-    u32 cn[ITEMS];
+    if (wlive) {
+      u32 cn[ITEMS];
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const u32 n0 = nn[i], mid = n0 >> 1, r = rank[i];
-      const bool is_mid = n0 != 0 && r == mid;
-      const bool right = r > mid;
-      fin[is_mid ? lo[i] + mid : u32(NM) + lane_dummy] = u32(tid + i * THREADS);
-      cn[i] = right ? r - mid - 1 : r;
-      if (keep && ITEMS != 2) cr[tid + i * THREADS] = u16(cn[i]);
-      lo[i] = right ? lo[i] + mid + 1 : lo[i];
-      sg[i] = 2 * sg[i] + (right ? 1u : 0u);
-      nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
+      for (int i = 0; i < ITEMS; ++i) {
+        const u32 n0 = nn[i], mid = n0 >> 1, r = rank[i];
+        const bool is_mid = n0 != 0 && r == mid;
+        const bool right = r > mid;
+        fin[is_mid ? lo[i] + mid : u32(NM) + lane_dummy] = u32(kid(i));
+        cn[i] = right ? r - mid - 1 : r;
+        if (keep && ITEMS != 2) cr[tid + i * THREADS] = u16(cn[i]);
+        lo[i] = right ? lo[i] + mid + 1 : lo[i];
+        sg[i] = 2 * sg[i] + (right ? 1u : 0u);
+        nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
+      }
+      if (keep && ITEMS == 2) reinterpret_cast<u32*>(cr)[tid] = (cn[0] & 0xffffu) | (cn[ITEMS - 1] << 16);
     }
-    if (keep && ITEMS == 2) reinterpret_cast<u32*>(cr)[tid] = (cn[0] & 0xffffu) | (cn[ITEMS - 1] << 16);
     __syncthreads();
     if (t < 18) stamp(a, 2 + t);
   }
