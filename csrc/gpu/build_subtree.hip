@@ -1053,6 +1053,18 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
       done = true;
     }
   }
+  if constexpr (ITEMS == 1 && THREADS == 1024) {  // d = 8 (BASELINE's high-dim config), capacity 1024
+    if (!done && a.dim == 8 && dim3c) {
+      static bool attr8 = false;
+      if (!attr8) {
+        PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 8>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
+        attr8 = true;
+      }
+      k_subtree_rank<ITEMS, THREADS, false, 8><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+      done = true;
+    }
+  }
   if (!done) k_subtree_rank<ITEMS, THREADS, false><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
   PKD_LAUNCH_CHECK();
 }
