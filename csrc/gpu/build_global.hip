@@ -896,7 +896,7 @@ __device__ __forceinline__ void add_next_hist(const LevelArgs& a, i64 s, i64 h, 
 // CAP: largest middle zone sorted in LDS (keys + indices in dynamic LDS); larger zones are
 // first narrowed by radix passes over the composite key.
 template <int CAP>
-__global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
+__device__ __forceinline__ void refine_body(LevelArgs a, i64 bid) {
   extern __shared__ __align__(16) u64 dynk[];
   u64* keys = dynk;
   u32* idx = reinterpret_cast<u32*>(dynk + CAP);
@@ -904,7 +904,7 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
   __shared__ u32 sh4[4];
   __shared__ u32 info[4];
   const int dim = a.dim;
-  const i64 s = blockIdx.x;
+  const i64 s = bid;
   const i64 h = a.heap0 + s;
   const i64 n = a.seg_n[h];
   if (n <= 0) return;
@@ -1135,9 +1135,9 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
 // other lanes with shuffles and writes the row back in place (a wave's stores issue only
 // after all of its loads returned, so in-place is safe inside the wave).
 template <int NCOL>
-__global__ __launch_bounds__(kBlock) void k_refine_small(LevelArgs a, i64 segs) {
+__device__ __forceinline__ void refine_small_body(LevelArgs a, i64 segs, i64 bid) {
   constexpr int D = NCOL - 1;
-  const i64 s = i64(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  const i64 s = bid * (kBlock / 64) + threadIdx.x / 64;
   if (s >= segs) return;
   const i64 h = a.heap0 + s;
   const i64 n = a.seg_n[h];
@@ -1363,9 +1363,9 @@ __device__ __forceinline__ void pivot_found(const LevelArgs& a, i64 h, i64 lo, i
 
 // One wave per segment whose median bucket holds <= 64 rows.
 template <int NCOL>
-__global__ __launch_bounds__(kBlock) void k_pivot_small(LevelArgs a, i64 segs) {
+__device__ __forceinline__ void pivot_small_body(LevelArgs a, i64 segs, i64 bid) {
   constexpr int D = NCOL - 1;
-  const i64 s = i64(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  const i64 s = bid * (kBlock / 64) + threadIdx.x / 64;
   if (s >= segs) return;
   const i64 h = a.heap0 + s;
   const i64 n = a.seg_n[h];
@@ -1399,12 +1399,12 @@ __global__ __launch_bounds__(kBlock) void k_pivot_small(LevelArgs a, i64 segs) {
 // One workgroup per segment with a larger median bucket: radix select (11-bit digits) of
 // the rank-t composite key, rows read in place (no staging).
 template <int NCOL>
-__global__ __launch_bounds__(kBlock) void k_pivot(LevelArgs a) {
+__device__ __forceinline__ void pivot_body(LevelArgs a, i64 bid) {
   constexpr int D = NCOL - 1;
   __shared__ u32 rh[kRadixBins];
   __shared__ u32 sh4[4];
   __shared__ u32 info[3];
-  const i64 s = blockIdx.x;
+  const i64 s = bid;
   const i64 h = a.heap0 + s;
   const i64 n = a.seg_n[h];
   if (n <= 0) return;
@@ -1476,6 +1476,27 @@ __global__ __launch_bounds__(kBlock) void k_pivot(LevelArgs a) {
     if (k == pivot) pivot_found<NCOL>(a, h, lo, n, row, k);
     else if (a.next_bins > 0) add_next_hist(a, s, h, k < pivot ? 0 : 1, nkey);
   }
+}
+
+template <int CAP>
+__global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
+  refine_body<CAP>(a, blockIdx.x);
+}
+
+// The wave-per-segment and workgroup-per-segment halves of a level's median step take
+// disjoint segments (middle zone <= 64 rows or larger), so one launch runs both: blocks
+// [0, gs) are the small path, the rest one workgroup per segment. Saves a dispatch (~5 us of
+// launch and drain) per level, which adds up over the ~20 levels of a small build.
+template <int NCOL, int CAP>
+__global__ __launch_bounds__(kBlock) void k_refine_both(LevelArgs a, i64 segs, int gs) {
+  if (int(blockIdx.x) < gs) refine_small_body<NCOL>(a, segs, blockIdx.x);
+  else refine_body<CAP>(a, i64(blockIdx.x) - gs);
+}
+
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_pivot_both(LevelArgs a, i64 segs, int gs) {
+  if (int(blockIdx.x) < gs) pivot_small_body<NCOL>(a, segs, blockIdx.x);
+  else pivot_body<NCOL>(a, i64(blockIdx.x) - gs);
 }
 
 // Second-stage histogram of level l+1 before a pair's scatter: rows are still grouped by
@@ -2180,11 +2201,11 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const int g = int((segs + 3) / 4);
       with_ncol(dim_, [&](auto nc) {
         constexpr int NC = decltype(nc)::value > 0 ? decltype(nc)::value : 9;
-        k_refine_small<NC><<<g, kBlock, 0, stream>>>(a, segs);
+        k_refine_both<NC, kRefineCap><<<g + int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a, segs, g);
       });
-      PKD_LAUNCH_CHECK();
+    } else {
+      k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
     }
-    k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
     PKD_LAUNCH_CHECK();
   };
   static const char* const kLevelNames[] = {"pkd.level0", "pkd.level1", "pkd.level2", "pkd.level3",
@@ -2222,8 +2243,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           as.bps = std::max(1, lp.bps / scan_div());
           k_scan<NC><<<int(lp.segs * as.bps), kBlock, lds_a, stream>>>(as);
           PKD_LAUNCH_CHECK();
-          k_pivot_small<NC><<<gs, kBlock, 0, stream>>>(a, lp.segs);
-          k_pivot<NC><<<int(lp.segs), kBlock, 0, stream>>>(a);
+          k_pivot_both<NC><<<gs + int(lp.segs), kBlock, 0, stream>>>(a, lp.segs, gs);
           PKD_LAUNCH_CHECK();
         }
       });
