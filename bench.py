@@ -5,15 +5,21 @@ One step = one complete exact kd-tree build of the whole point set, from the inp
 resident in HBM to the finished implicit in-order tree (ids + coordinates) in HBM.
 
 * N = 1: the level-synchronous HIP builder on one MI355X.
-* N > 1: global decomposition over RCCL (one process per GPU, torchrun env): each rank holds
-  its generation-order slice (the reference's MPI slicing, kdtree_mpi.cpp:204-224); the top
-  log2(N) levels are split with allreduced histograms, points are redistributed with one
-  all-to-all, and each GPU builds its subtree. Strong scaling: the total point count is
-  fixed, so `value` is the whole-job throughput.
+* N > 1: global decomposition over RCCL (one process per GPU): each rank holds its
+  generation-order slice (the reference's MPI slicing, kdtree_mpi.cpp:204-224); the top
+  log2(N) levels are split with allreduced histograms, points are redistributed with
+  all-to-all rounds, and each GPU builds its subtree. Strong scaling: the total point count
+  is fixed, so `value` is the whole-job throughput.
+
+Launch: under torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the env), or
+plain `python bench.py --gpus N`: without WORLD_SIZE the process becomes a launcher that never
+touches a GPU, starts N child ranks (the reference's `mpirun -np P`, Makefile:36) and exits
+with the first failing rank's status.
 
 Data: the reference generator stream (std::mt19937 + uniform_real<float>(-100,100), seed 42),
 each rank's slice generated on its own GPU by the device generator (csrc/gpu/generator.hip,
-bit-identical to the host stream; untimed).
+bit-identical to the host stream; untimed). After the timed loop (untimed) the last tree is
+checked: device error word, kd invariant on every node, ids a permutation.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -21,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,9 +38,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_MPTS = 100e6 / 924.3 / 1e6  # reference build, 100M x 3D, 924.3 s (1 core)
+METRIC = "Mpoints/sec kd-tree build, 100M x 3D float32, at 1/2/4/8 MI355X"
 
 
-def main():
+def _parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -43,83 +52,210 @@ def main():
     ap.add_argument("--data", choices=["reference", "reference-host", "device"], default="reference",
                     help="reference: the reference stream generated on the GPU (bit-identical to the host "
                          "generator); reference-host: same stream generated on the host; device: torch RNG")
-    ap.add_argument("--profile-levels", action="store_true", help="print per-phase timings to stderr")
-    args = ap.parse_args()
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: run the same control flow on host tensors over gloo (launcher / CI check; "
+                         "timings meaningless)")
+    ap.add_argument("--no-check", action="store_true", help="skip the untimed correctness check of the last tree")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(nprocs: int, argv) -> int:
+    """Start `nprocs` ranks of this script and wait for them. The launcher itself never
+    initialises a GPU (no HIP call happens before the children exist). If a rank fails, the
+    others are stopped (they would block in a collective) and its exit status is returned."""
+    port = _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.kill()
+        raise
+    for p in procs:
+        try:
+            p.wait(30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
+def _check_tree(tp, ti, depth0, id_lo, id_hi, permutation=True) -> str:
+    """'' when (tp, ti) is a valid exact kd-tree (on its device) whose ids are distinct and in
+    [id_lo, id_hi) -- all of that range when `permutation`."""
+    from parallel_kd_tree_amd import ops
+    v = int(ops.native().invariant_violations(tp.contiguous(), ti.contiguous(), depth0))
+    if v:
+        return f"{v} kd-invariant violations"
+    n = ti.numel()
+    if n == 0:
+        return "" if (not permutation or id_hi == id_lo) else "empty tree"
+    idl = ti.to(torch.int64) & 0xFFFFFFFF
+    if int(idl.min()) < id_lo or int(idl.max()) >= id_hi:
+        return "ids out of range"
+    seen = torch.zeros(id_hi - id_lo, dtype=torch.int32, device=ti.device)
+    seen.index_add_(0, idl - id_lo, torch.ones_like(idl, dtype=torch.int32))
+    if int(seen.max()) > 1:
+        return "duplicate ids"
+    if permutation and n != id_hi - id_lo:
+        return f"{n} ids for {id_hi - id_lo} points"
+    return ""
+
+
+def main(argv=None):
+    args = _parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:] if argv is None else argv))
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    share = os.environ.get("PKD_BENCH_SHARE_GPU") == "1"
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    cpu = args.device == "cpu"
     # Rehearsal knobs for a one-GPU box (never set by the driver): PKD_BENCH_SHARE_GPU=1 puts
     # every rank on cuda:0 and PKD_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks
     # on one device. The timing is then meaningless; the control flow is the real one.
-    if os.environ.get("PKD_BENCH_SHARE_GPU") == "1":
-        local_rank = 0
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        if share:
+            local_rank = 0
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
 
     from parallel_kd_tree_amd.parallel import comm
     if world > 1:
-        comm.init(backend=os.environ.get("PKD_BENCH_BACKEND", "nccl"), device=dev)
+        comm.init(backend="gloo" if cpu else os.environ.get("PKD_BENCH_BACKEND", "nccl"), device=dev)
     if rank == 0 and os.environ.get("PKD_SKIP_BUILD") != "1":
         from parallel_kd_tree_amd import _build
         _build.build()  # no-op when the in-tree extension is up to date
     if world > 1:
         comm.barrier()
+    if os.environ.get("PKD_BENCH_FAIL_RANK") == str(rank):  # launcher test: this rank dies, the rest block
+        os._exit(7)
     import parallel_kd_tree_amd as pk
 
     n, dim = args.points, args.dim
-    if world > 1:
-        from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
-        first, count = comm.forest_slice(n, world, rank)
-    else:
-        first, count = 0, n
-
-    if args.data == "reference":
+    first, count = comm.forest_slice(n, world, rank) if world > 1 else (0, n)
+    if args.data == "reference" and not cpu:
         x = pk.generate_slice(args.seed, dim, first, count, device=dev)
-    elif args.data == "reference-host":
+    elif args.data.startswith("reference"):
         x = pk.generate_slice(args.seed, dim, first, count).to(dev)
     else:
         x = pk.uniform_points(count, dim, seed=args.seed * 1000 + rank, device=dev)
-    ids = None
 
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
     if world > 1:
+        from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
         builder = GlobalTreeBuilder(n, dim, device=dev)
-        step = lambda: builder.build(x, id_base=first + 1)
+        res = {}
+
+        def step():
+            res["t"] = builder.build(x, id_base=first + 1)
+    elif cpu:
+        from parallel_kd_tree_amd import ops
+        res = {}
+
+        def step():
+            res["t"] = ops.build_cpu(x, None, "exact", 0, os.cpu_count() or 1)
     else:
         from parallel_kd_tree_amd.ops import GpuTreeBuilder
         b = GpuTreeBuilder(n, dim)
         out_pts = torch.empty_like(x)
         out_ids = torch.empty(n, dtype=torch.int32, device=dev)
-        step = lambda: b.build(x, ids, 1, out_pts, out_ids)
+
+        def step():
+            b.build(x, None, 1, out_pts, out_ids)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     if world > 1:
         dt = comm.max_float(dt)
-    # the device error word of the last build (outside the timed region)
-    err = builder.read_error() if world > 1 else b.read_error()
-    if err:
-        sys.exit(f"bench.py: rank {rank}: device build reported error flags {err}")
+
+    # ---- untimed: the last build's tree must be right --------------------------------
+    problem = ""
+    if world > 1:
+        err = builder.read_error() if not cpu else 0
+        t = res["t"]
+        if err:
+            problem = f"device build reported error flags {err}"
+        elif not args.no_check:
+            # my subtree sits at depth log2(N) and holds ids of every rank: invariant and distinct
+            # ids here; count and id sum over all ranks (plus the replicated top pivots) below
+            problem = _check_tree(t.tree_pts, t.tree_ids, (world - 1).bit_length(), 1, n + 1, permutation=False)
+            idl = t.tree_ids.to(torch.int64) & 0xFFFFFFFF
+            stats = torch.tensor([idl.numel(), int(idl.sum()) if idl.numel() else 0], dtype=torch.int64, device=dev)
+            comm.all_reduce_(stats)
+            top_ids = [int(t.top_rows[i, dim:].contiguous().view(torch.int32).item()) & 0xFFFFFFFF
+                       for i, s in enumerate(t.top_slots) if s >= 0]
+            cnt, tot = int(stats[0]) + len(top_ids), int(stats[1]) + sum(top_ids)
+            if not problem and (cnt != n or tot != n * (n + 1) // 2):
+                problem = f"the distributed tree holds {cnt} points (id sum {tot}) for ids 1..{n}"
+    elif cpu:
+        tp, ti = res["t"]
+        problem = "" if args.no_check else _check_tree(tp, ti + 1, 0, 1, n + 1)
+    else:
+        err = b.read_error()
+        if err:
+            problem = f"device build reported error flags {err} (detail {b.read_error_detail()})"
+        elif not args.no_check:
+            problem = _check_tree(out_pts, out_ids, 0, 1, n + 1)
+    if world > 1:
+        bad = torch.tensor([1 if problem else 0], dtype=torch.int64, device=dev)
+        comm.all_reduce_(bad)
+        if int(bad[0]) and not problem:
+            problem = "another rank's tree check failed"
+    if problem:
+        print(f"bench.py: rank {rank}: {problem}", file=sys.stderr, flush=True)
+        if world > 1:
+            comm.destroy()
+        sys.exit(3)
+
     ms = dt * 1e3 / args.steps
     mpts = n / (ms / 1e3) / 1e6
     if rank == 0:
         print(json.dumps({
-            "metric": "Mpoints/sec kd-tree build, 100M x 3D float32, at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(mpts, 3),
             "unit": "Mpoints/s",
             "n_gpus": world,
@@ -134,7 +270,9 @@ def main():
                     if args.data.startswith("reference") else "synthetic: on-device uniform(-100,100), reference value map",
             "config": {"model": "exact median-split kd-tree, cycling axis (implicit in-order layout)",
                        "global_batch": n, "seq_len": dim, "n_points": n, "dim": dim,
-                       "parallelism": f"global{world}" if world > 1 else "single"},
+                       "parallelism": f"global{world}" if world > 1 else "single",
+                       "device": "cpu (gloo rehearsal)" if cpu else "MI355X",
+                       "tree_checked": not args.no_check},
         }), flush=True)
     if world > 1:
         comm.destroy()

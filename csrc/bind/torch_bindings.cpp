@@ -42,11 +42,11 @@ void check_points(const torch::Tensor& pts, bool cuda) {
   TORCH_CHECK(pts.is_cuda() == cuda, cuda ? "points must be on a GPU" : "points must be on the CPU");
 }
 
-const pk::u32* opt_ids(const c10::optional<torch::Tensor>& ids, int64_t n, bool cuda) {
+const pk::u32* opt_ids(const c10::optional<torch::Tensor>& ids, int64_t n, const torch::Device& dev) {
   if (!ids.has_value() || !ids->defined()) return nullptr;
   TORCH_CHECK(ids->scalar_type() == torch::kInt32, "ids must be int32 (bits are used as uint32)");
   TORCH_CHECK(ids->is_contiguous() && ids->numel() == n, "ids must be contiguous [n]");
-  TORCH_CHECK(ids->is_cuda() == cuda, "ids on the wrong device");
+  TORCH_CHECK(ids->device() == dev, "ids must be on the points' device (", dev, "), got ", ids->device());
   return reinterpret_cast<const pk::u32*>(ids->data_ptr<int32_t>());
 }
 
@@ -72,9 +72,13 @@ struct Builder {
     torch::Tensor op = out_pts.has_value() ? *out_pts : torch::empty_like(pts);
     torch::Tensor oi = out_ids.has_value() ? *out_ids
                                            : torch::empty({b.n()}, pts.options().dtype(torch::kInt32));
-    TORCH_CHECK(op.sizes() == pts.sizes() && op.is_contiguous(), "out_pts must match points");
-    TORCH_CHECK(oi.numel() == b.n() && oi.scalar_type() == torch::kInt32, "out_ids must be int32 [n]");
-    b.build(pts.data_ptr<float>(), opt_ids(ids, b.n(), true), pk::u32(id_base), op.data_ptr<float>(),
+    TORCH_CHECK(op.sizes() == pts.sizes() && op.is_contiguous() && op.scalar_type() == torch::kFloat32,
+                "out_pts must be a contiguous float32 tensor shaped like points");
+    TORCH_CHECK(oi.numel() == b.n() && oi.scalar_type() == torch::kInt32 && oi.is_contiguous(),
+                "out_ids must be contiguous int32 [n]");
+    TORCH_CHECK(op.device() == pts.device() && oi.device() == pts.device(),
+                "out_pts / out_ids must be on the points' device");
+    b.build(pts.data_ptr<float>(), opt_ids(ids, b.n(), pts.device()), pk::u32(id_base), op.data_ptr<float>(),
             reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(), cur_stream(pts));
     return {op, oi};
   }
@@ -147,7 +151,7 @@ std::vector<torch::Tensor> build_cpu(const torch::Tensor& pts, const c10::option
   const int64_t n = pts.size(0);
   const int dim = int(pts.size(1));
   std::vector<pk::u32> perm(size_t(std::max<int64_t>(n, 1)));
-  const pk::u32* idp = opt_ids(ids, n, false);
+  const pk::u32* idp = opt_ids(ids, n, pts.device());
   if (mode == "exact") {
     pk::build_exact_cpu(pts.data_ptr<float>(), idp, n, dim, int(depth0), perm.data(), int(threads));
   } else if (mode == "reference") {
@@ -232,19 +236,21 @@ torch::Tensor nn_gpu(const torch::Tensor& pts, const c10::optional<torch::Tensor
   check_points(pts, true);
   check_points(queries, true);
   TORCH_CHECK(queries.size(1) == pts.size(1), "dimension mismatch");
+  TORCH_CHECK(queries.device() == pts.device(), "queries must be on the tree's device");
   const c10::DeviceGuard guard(pts.device());
   const int64_t nq = queries.size(0);
   hipStream_t s = cur_stream(pts);
   torch::Tensor out;
   if (into.has_value()) {
     out = *into;
-    TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == nq && out.is_cuda(), "bad `into` tensor");
+    TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == nq && out.is_contiguous() &&
+                    out.device() == pts.device(), "`into` must be a contiguous int64 [nq] tensor on the tree's device");
   } else {
     out = torch::empty({nq}, queries.options().dtype(torch::kInt64));
     pk::nn_init(reinterpret_cast<pk::u64*>(out.data_ptr<int64_t>()), nq, s);
   }
   auto* o = reinterpret_cast<pk::u64*>(out.data_ptr<int64_t>());
-  const pk::u32* idp = opt_ids(ids, pts.size(0), true);
+  const pk::u32* idp = opt_ids(ids, pts.size(0), pts.device());
   if (method == "brute") {
     pk::nn_brute(pts.data_ptr<float>(), idp, pk::u32(id_base), pts.size(0), int(pts.size(1)),
                  queries.data_ptr<float>(), nq, o, s);

@@ -199,14 +199,23 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventElapsedTime(&bld, e0, e1));
   PKD_HIP_CHECK(hipEventElapsedTime(&qry, e1, e2));
   const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
+  // the build's device error word rides along (MAX over ranks: non-zero iff any rank failed)
+  const u32 berr = local > 0 ? b->read_error(ws, s) : 0u;
   float* d_t = nullptr;
-  PKD_HIP_CHECK(hipMalloc(&d_t, 3 * sizeof(float)));
-  const float ht[3] = {gen, bld, qry};
+  PKD_HIP_CHECK(hipMalloc(&d_t, 4 * sizeof(float)));
+  const float ht[4] = {gen, bld, qry, float(berr & 0xFFFFFFu) + (berr >> 24 ? 1.0f : 0.0f)};
   PKD_HIP_CHECK(hipMemcpyAsync(d_t, ht, sizeof(ht), hipMemcpyHostToDevice, s));
-  PKD_NCCL_CHECK(ncclReduce(d_t, d_t, 3, ncclFloat32, ncclMax, 0, comm, s));
-  float mt[3];
+  PKD_NCCL_CHECK(ncclReduce(d_t, d_t, 4, ncclFloat32, ncclMax, 0, comm, s));
+  float mt[4];
   PKD_HIP_CHECK(hipMemcpyAsync(mt, d_t, sizeof(mt), hipMemcpyDeviceToHost, s));
   watchdog_wait(s, comm, timeout_s, "timing reduce");
+  if (berr) std::cerr << "kdtree_dist: rank " << rank << ": device build error word 0x" << std::hex << berr << std::dec
+                      << std::endl;
+  if (rank == 0 && mt[3] != 0.0f) {
+    std::cerr << "kdtree_dist: a rank's tree build failed; no results printed" << std::endl;
+    (void)ncclCommDestroy(comm);
+    return 3;
+  }
 
   if (rank == 0) {
     for (int q = 0; q < Q; ++q) print_result_line(N + q, std::sqrt(packed_dist(res[size_t(q)])));

@@ -76,6 +76,12 @@ int main(int argc, char** argv) {
     std::vector<u64> res(static_cast<size_t>(Q));
     PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
     PKD_HIP_CHECK(hipStreamSynchronize(s));
+    u32 detail[3] = {0, 0, 0};
+    if (const u32 err = b.read_error(ws, s, detail)) {  // after the queries: no extra sync in the build
+      std::cerr << "kdtree_gpu: device build error word 0x" << std::hex << err << std::dec << " (code " << detail[0]
+                << ", level " << detail[1] << ", value " << detail[2] << "); no results printed" << std::endl;
+      return 3;
+    }
     for (int q = 0; q < Q; ++q) print_result_line(N + q, std::sqrt(packed_dist(res[size_t(q)])));
     if (o.debug) {
       const auto tock = std::chrono::high_resolution_clock::now();

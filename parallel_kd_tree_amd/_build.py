@@ -11,6 +11,7 @@ Usage: ``python -m parallel_kd_tree_amd._build [-v] [--clean]``.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -57,20 +58,38 @@ def _ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def _hdr_mtime() -> float:
-    m = 0.0
+def _digest(*parts) -> str:
+    h = hashlib.sha256()
+    for p in parts:
+        h.update(p if isinstance(p, bytes) else str(p).encode())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _hdr_digest() -> str:
+    """Contents of every header a source may include."""
+    parts = []
     for d in (CSRC / "include", CSRC / "gpu", CSRC / "cli"):
-        for p in d.rglob("*"):
+        for p in sorted(d.rglob("*")):
             if p.suffix in (".hpp", ".h"):
-                m = max(m, p.stat().st_mtime)
-    return m
+                parts += [p.relative_to(CSRC).as_posix(), p.read_bytes()]
+    return _digest(*parts)
 
 
-def _stale(out: Path, srcs, hdr: float) -> bool:
-    if not out.exists():
-        return True
-    t = out.stat().st_mtime
-    return any(Path(s).stat().st_mtime > t for s in srcs) or hdr > t
+def _sig_path(out: Path) -> Path:
+    return out.with_name(out.name + ".sig")
+
+
+def _stale(out: Path, sig: str) -> bool:
+    """An output is stale unless it exists and was built from exactly this signature
+    (source and header contents, compiler, flags, offload arch) -- mtimes play no part, so a
+    fresh checkout or a copied tree with up-to-date outputs rebuilds nothing."""
+    sp = _sig_path(out)
+    return not (out.exists() and sp.exists() and sp.read_text().strip() == sig)
+
+
+def _mark(out: Path, sig: str) -> None:
+    _sig_path(out).write_text(sig + "\n")
 
 
 def _run(cmd, verbose):
@@ -82,70 +101,79 @@ def _run(cmd, verbose):
     return r
 
 
-def _compile(src: str, flags, verbose, hdr) -> Path:
+def _obj_sig(src: str, flags, hdr: str) -> str:
+    s = CSRC / src
+    tool = f"hipcc --offload-arch={ARCH}" if s.suffix == ".hip" else "g++ -pthread"
+    return _digest(src, s.read_bytes(), hdr, tool, *COMMON, *flags)
+
+
+def _compile(src: str, flags, verbose, sig: str) -> Path:
     s = CSRC / src
     o = OBJ / (src.replace("/", "__") + ".o")
-    if _stale(o, [s], hdr):
+    if _stale(o, sig):
         if s.suffix == ".hip":
             cmd = [ROCM / "bin" / "hipcc", f"--offload-arch={ARCH}", *COMMON, *flags, "-c", s, "-o", o]
         else:
             cmd = ["g++", *COMMON, "-pthread", *flags, "-c", s, "-o", o]
         _run(cmd, verbose)
+        _mark(o, sig)
     return o
 
 
 def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, jobs: int | None = None) -> dict:
-    """Compile every HIP/C++ source for gfx950 and link the extension + executables."""
-    OBJ.mkdir(parents=True, exist_ok=True)
-    BIN.mkdir(parents=True, exist_ok=True)
-    hdr = _hdr_mtime()
-    jobs = jobs or min(8, os.cpu_count() or 4)
+    """Compile every HIP/C++ source for gfx950 and link the extension + executables.
+
+    Every output carries a signature (``<output>.sig``) of everything it was built from; an
+    output whose signature matches is kept without looking at (or needing) its objects."""
+    hdr = _hdr_digest()
     tflags, tld = _torch_flags() if with_ext else ([], [])
-    tasks = [(s, []) for s in CORE_CPU + CORE_HIP]
+    hipflags = [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
+    flags = {s: [] for s in CORE_CPU + CORE_HIP}
     if with_ext:
-        tasks += [(s, tflags) for s in BIND]
+        flags.update({s: tflags for s in BIND})
     if with_cli:
-        hipflags = [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
-        tasks += [(s, []) for v in CLI_CPU.values() for s in v]
-        tasks += [(s, hipflags) for v in CLI_GPU.values() for s in v if (CSRC / s).exists()]
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = {src: ex.submit(_compile, src, fl, verbose, hdr) for src, fl in tasks}
-        objs = {src: f.result() for src, f in futs.items()}
-    core_cpu = [objs[s] for s in CORE_CPU]
-    core = core_cpu + [objs[s] for s in CORE_HIP]
-    out = {}
+        flags.update({s: [] for v in CLI_CPU.values() for s in v})
+        flags.update({s: hipflags for v in CLI_GPU.values() for s in v if (CSRC / s).exists()})
+    osig = {s: _obj_sig(s, fl, hdr) for s, fl in flags.items()}
+    core_cpu, core = CORE_CPU, CORE_CPU + CORE_HIP
+    # outputs: (path, object sources, link command tail)
+    outs = {}
     if with_ext:
-        so = PKG / f"_C{_ext_suffix()}"
-        srcs = core + [objs[s] for s in BIND]
-        if _stale(so, srcs, 0.0):
-            _run(["g++", "-shared", "-o", so, *srcs, *tld, "-pthread"], verbose)
-        out["extension"] = str(so)
+        outs["extension"] = (PKG / f"_C{_ext_suffix()}", core + BIND, [*tld, "-pthread"], ["-shared"])
     if with_cli:
         for name, srcs in CLI_CPU.items():
-            exe = BIN / name
-            o = [objs[s] for s in srcs]
-            if _stale(exe, o + core_cpu, 0.0):
-                _run(["g++", "-o", exe, *o, *core_cpu, "-pthread"], verbose)
-            out[name] = str(exe)
+            outs[name] = (BIN / name, srcs + core_cpu, ["-pthread"], [])
         for name, srcs in CLI_GPU.items():
-            if not all(s in objs for s in srcs):
-                continue
-            exe = BIN / name
-            o = [objs[s] for s in srcs]
-            extra = ["-lrccl"] if name == "kdtree_dist" else []
-            if _stale(exe, o + core, 0.0):
-                _run(["g++", "-o", exe, *o, *core, f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx", *extra,
-                      f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"], verbose)
-            out[name] = str(exe)
-    return out
+            if all(s in flags for s in srcs):
+                extra = ["-lrccl"] if name == "kdtree_dist" else []
+                outs[name] = (BIN / name, srcs + core, [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrocprofiler-sdk-roctx",
+                                                        *extra, f"-Wl,-rpath,{ROCM / 'lib'}", "-pthread"], [])
+    lsig = {k: _digest(*(osig[s] for s in srcs), *tail, *pre) for k, (_, srcs, tail, pre) in outs.items()}
+    todo = {k for k, (path, _, _, _) in outs.items() if _stale(path, lsig[k])}
+    result = {k: str(path) for k, (path, _, _, _) in outs.items()}
+    if not todo:
+        return result
+    OBJ.mkdir(parents=True, exist_ok=True)
+    BIN.mkdir(parents=True, exist_ok=True)
+    need = sorted({s for k in todo for s in outs[k][1]})
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        futs = {src: ex.submit(_compile, src, flags[src], verbose, osig[src]) for src in need}
+        objs = {src: f.result() for src, f in futs.items()}
+    for k in sorted(todo):
+        path, srcs, tail, pre = outs[k]
+        _run(["g++", *pre, "-o", path, *(objs[s] for s in srcs), *tail], verbose)
+        _mark(path, lsig[k])
+    return result
 
 
 def clean():
     shutil.rmtree(ROOT / "build", ignore_errors=True)
-    for p in PKG.glob("_C*.so"):
+    for p in list(PKG.glob("_C*.so")) + list(PKG.glob("_C*.so.sig")):
         p.unlink()
     for name in list(CLI_CPU) + list(CLI_GPU):
         (BIN / name).unlink(missing_ok=True)
+        (BIN / f"{name}.sig").unlink(missing_ok=True)
 
 
 if __name__ == "__main__":

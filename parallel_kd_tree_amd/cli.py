@@ -21,6 +21,17 @@ import numpy as np
 import torch
 
 
+def _all_ok(comm, err: int, device) -> None:
+    """Raise on every rank if any rank's build reported a device error (no rank prints
+    results from a corrupt tree, and none is left waiting in a collective)."""
+    flags = torch.tensor([1 if err else 0], dtype=torch.int64, device=device)
+    comm.all_reduce_(flags)
+    if err:
+        raise RuntimeError(f"rank {comm.rank()}: GPU kd-tree build reported device error word {err:#x}")
+    if int(flags[0]):
+        raise RuntimeError("another rank's GPU kd-tree build reported a device error")
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="parallel_kd_tree_amd.cli", add_help=True)
     ap.add_argument("--decomp", choices=["single", "forest", "global"], default=None)
@@ -82,20 +93,24 @@ def main(argv=None) -> int:
         tree = pk.KDTree.build(x, id_base=1, mode=a.mode, subtree_max=a.leaf_threshold)
         from .parallel.global_tree import _local_packed
         packed = _local_packed(tree, q, a.query)
+        tree.check()  # device error word, read after the queries are enqueued
         if a.save:
             tree.save(a.save)
     elif decomp == "forest":
         from .parallel.forest import ForestTree
         f = ForestTree.build(x, first, n, id_base=1, mode=a.mode)
         packed = f.query_packed(q, a.query)
+        _all_ok(comm, f.local_error(), device)
         if a.save:
             f.local.save(f"{a.save}.rank{rank}")
     else:
         if a.mode != "exact":
             raise SystemExit("--decomp global builds exact trees only")
         from .parallel.global_tree import GlobalTreeBuilder
-        t = GlobalTreeBuilder(n, dim, device=device).build(x, id_base=first + 1)
+        gb = GlobalTreeBuilder(n, dim, device=device)
+        t = gb.build(x, id_base=first + 1)
         packed = t.query_packed(q, a.query)
+        _all_ok(comm, gb.read_error() if device.type == "cuda" else 0, device)
         if a.save:
             tp, ti = t.gather_full()
             if rank == 0:

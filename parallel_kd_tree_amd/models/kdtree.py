@@ -31,19 +31,29 @@ class KDTree:
         self.depth0 = int(depth0)
         self.mode = mode
         self._host = None
+        self._builder = None  # the GPU builder whose device error word covers this tree
 
     # ------------------------------------------------------------------ construction
     @classmethod
     def build(cls, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
-              mode: str = "exact", depth0: int = 0, subtree_max: int = 0, threads: int = 1) -> "KDTree":
-        """Build from ``points`` [n, dim]. ``ids`` default to ``id_base + row``."""
+              mode: str = "exact", depth0: int = 0, subtree_max: int = 0, threads: int = 1,
+              check_ids: bool = True) -> "KDTree":
+        """Build from ``points`` [n, dim]. ``ids`` default to ``id_base + row``; explicit ids
+        must be distinct (checked unless ``check_ids=False``). A GPU build is enqueued
+        without a host sync; ``check()`` reads its device error word."""
         if points.dim() != 2:
             raise ValueError("points must be [n, dim]")
         points = points.to(torch.float32).contiguous()
         if mode not in ("exact", "reference"):
             raise ValueError("mode must be 'exact' or 'reference'")
+        if check_ids:
+            ops.check_unique_ids(ids)
         if points.is_cuda and mode == "exact":
-            tp, ti = ops.build_gpu(points, ids, id_base, depth0, subtree_max)
+            b = ops.gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
+            tp, ti = b.build(points, ids, id_base)
+            t = cls(tp, ti, depth0, mode)
+            t._builder = b
+            return t
         else:
             cpu_ids = ids
             if cpu_ids is None:
@@ -52,6 +62,16 @@ class KDTree:
             if points.is_cuda:
                 tp, ti = tp.to(points.device), ti.to(points.device)
         return cls(tp, ti, depth0, mode)
+
+    def check(self) -> "KDTree":
+        """Raise RuntimeError if the GPU build of this tree reported a device error (histogram
+        / key disagreement, subtree overflow, ...). Synchronises; a no-op for CPU trees."""
+        if self._builder is not None:
+            err, code, level, value = self._builder.read_error_detail()
+            if err:
+                raise RuntimeError(f"GPU kd-tree build failed: error word {err:#x} (code {code}, level {level}, "
+                                   f"value {value})")
+        return self
 
     # ------------------------------------------------------------------ properties
     @property

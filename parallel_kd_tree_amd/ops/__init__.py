@@ -27,7 +27,7 @@ def native_path() -> str:
     return native().__file__
 
 
-from .build import GpuTreeBuilder, build_gpu, build_cpu  # noqa: E402
+from .build import GpuTreeBuilder, build_gpu, build_cpu, check_unique_ids, gpu_builder  # noqa: E402
 from .query import nn_gpu, unpack, finalize, nn_cpu  # noqa: E402
 
-__all__ = ["native", "native_path", "GpuTreeBuilder", "build_gpu", "build_cpu", "nn_gpu", "unpack", "finalize", "nn_cpu"]
+__all__ = ["native", "native_path", "GpuTreeBuilder", "build_gpu", "build_cpu", "check_unique_ids", "gpu_builder", "nn_gpu", "unpack", "finalize", "nn_cpu"]

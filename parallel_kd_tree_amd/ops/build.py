@@ -67,19 +67,35 @@ class GpuTreeBuilder:
 _builders: dict = {}
 
 
-def build_gpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0, depth0: int = 0,
-              subtree_max: int = 0):
-    """Build the exact tree of ``points`` ([n, d] float32 on a GPU)."""
-    if not points.is_cuda:
-        raise ValueError("build_gpu needs a GPU tensor")
-    points = points.contiguous()
-    key = (points.shape[0], points.shape[1], depth0, subtree_max, points.device)
+def gpu_builder(n: int, dim: int, depth0: int = 0, subtree_max: int = 0, device=None) -> GpuTreeBuilder:
+    """A cached builder for (n, dim, depth0, subtree_max) on `device`."""
+    key = (int(n), int(dim), int(depth0), int(subtree_max), device)
     b = _builders.get(key)
     if b is None:
         if len(_builders) > 8:
             _builders.clear()
-        b = _builders[key] = GpuTreeBuilder(points.shape[0], points.shape[1], depth0, subtree_max)
+        b = _builders[key] = GpuTreeBuilder(n, dim, depth0, subtree_max)
+    return b
+
+
+def build_gpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0, depth0: int = 0,
+              subtree_max: int = 0):
+    """Build the exact tree of ``points`` ([n, d] float32 on a GPU). Explicit ``ids`` must be
+    distinct: the exact order (coordinate, id) is only total for unique ids."""
+    if not points.is_cuda:
+        raise ValueError("build_gpu needs a GPU tensor")
+    points = points.contiguous()
+    b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
     return b.build(points, ids, id_base)
+
+
+def check_unique_ids(ids: Optional[torch.Tensor]) -> None:
+    """Explicit ids must be distinct (ValueError otherwise): with two equal (key, id) pairs
+    the median rank is ambiguous and the exact builders' output is undefined."""
+    if ids is None or ids.numel() < 2:
+        return
+    if torch.unique(ids.reshape(-1)).numel() != ids.numel():
+        raise ValueError("point ids must be distinct")
 
 
 def build_cpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, mode: str = "exact", depth0: int = 0,

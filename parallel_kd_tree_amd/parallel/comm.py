@@ -162,13 +162,34 @@ def all_gather_into_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class _StagedWork:
+    """Handle of an all-to-all on host copies of device tensors (gloo): the exchange runs
+    asynchronously on gloo's thread; wait() joins it and copies the result to the device."""
+
+    def __init__(self, work, host_out: torch.Tensor, out: torch.Tensor):
+        self._work, self._host_out, self._out = work, host_out, out
+
+    def wait(self) -> bool:
+        self._work.wait()
+        self._out.copy_(self._host_out)
+        return True
+
+    def is_completed(self) -> bool:
+        return self._work.is_completed()
+
+
 def all_to_all_single_async(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
     """Starts an all-to-all and returns a handle whose wait() orders the caller's current
-    stream after it (RCCL runs it on its own stream, overlapping later compute). gloo
-    staging is synchronous; its handle is None."""
-    if not dist.is_initialized() or world() == 1 or _staged(inp):
+    stream after it (RCCL runs it on its own stream, overlapping later compute; gloo runs it
+    on its own thread, device tensors staged through host copies). With one rank there is
+    nothing to overlap: the copy is done and the handle is None."""
+    if not dist.is_initialized() or world() == 1:
         all_to_all_single_(out, inp, out_splits, in_splits)
         return None
+    if _staged(inp):
+        host_out = torch.empty(out.shape, dtype=out.dtype)
+        w = dist.all_to_all_single(host_out, inp.cpu(), out_splits, in_splits, async_op=True)
+        return _StagedWork(w, host_out, out)
     return dist.all_to_all_single(out, inp, out_splits, in_splits, async_op=True)
 
 

@@ -30,6 +30,11 @@ class ForestTree:
         t = KDTree.build(points, id_base=first_row + id_base, mode=mode, threads=threads)
         return cls(t, first_row, n_total)
 
+    def local_error(self) -> int:
+        """Device error word of this rank's build (0 = ok, also for CPU trees). Synchronises."""
+        b = self.local._builder
+        return b.read_error() if b is not None else 0
+
     def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
         """Packed (d2, global id) of the nearest point over all ranks. Reference-mode forests
         use the reference search on each rank (so results match kdtree_mpi exactly)."""

@@ -109,13 +109,17 @@ class _HostOps:
         return out
 
     @staticmethod
-    def pack(rows, dim, node, levels, pivots_u64, last_axis, P):
+    def pack(rows, dim, node, levels, pivots_u64, last_axis, P, k):
+        """Rows sorted by destination slot (round j, rank r) -> j * P + r, where rank r owns the
+        2^k leaves r * 2^k + j at depth log2(P) + k (dest_slot in csrc/gpu/dist_ops.hip)."""
         piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
         _route_cpu(rows, dim, node, piv, last_axis)
         live = (node != DONE).nonzero().flatten()
-        dest = node[live] - (P - 1)
+        leaves = P << k
+        leaf = node[live] - (leaves - 1)
+        dest = (leaf & ((1 << k) - 1)) * P + (leaf >> k)
         order = torch.sort(dest, stable=True).indices
-        return rows[live[order]].contiguous(), torch.bincount(dest, minlength=P).to(torch.int64)
+        return rows[live[order]].contiguous(), torch.bincount(dest, minlength=leaves).to(torch.int64)
 
 
 @dataclass
@@ -193,6 +197,22 @@ def _brute_packed(pts, ids, queries):
         v = (acc.view(torch.int32).to(torch.int64) << 32) | (int(ids[i]) & 0xFFFFFFFF)
         best = torch.minimum(best, v)
     return best
+
+
+def _run_rounds(R: int, issue, consume) -> None:
+    """The exchange schedule shared by the device and host paths: round j's all-to-all is
+    waited for, round j + 1's is started, and only then is round j's payload consumed (its
+    leaf subtree built), so every exchange but the first overlaps a build. ``issue(j)`` returns
+    ``(payload, handles)``; a handle is an async work object or None (already complete)."""
+    pending = issue(0)
+    for j in range(R):
+        payload, handles = pending
+        for hd in handles:
+            if hd is not None:
+                hd.wait()
+        if j + 1 < R:
+            pending = issue(j + 1)
+        consume(j, payload)
 
 
 def _all_gather_var(t: torch.Tensor) -> List[torch.Tensor]:
@@ -358,14 +378,29 @@ class GlobalTreeBuilder:
         bm = self._buf("bm", (leaves, words), torch.int32) if compact else None
         scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, leaves),), torch.uint8)
         nat.top_pack(pts, idt, id_base, node, LL, pivots, last_axis, leaves, send, bm, counts, err, scratch, k)
-        by_rank = counts.view(R, P, 4).transpose(0, 1).contiguous()  # [rank][round][4]
-        recv_counts = torch.empty_like(by_rank)
-        comm.all_to_all_single_(recv_counts, by_rank)
-        both = torch.cat([by_rank.view(-1), recv_counts.view(-1)]).cpu()  # the only host read-back of the build
+        plan = self._exchange_plan(counts, k)  # the only host read-back of the build
         self._tick(timings, "pack", t0)
-        mine, theirs = both[:4 * leaves].view(P, R, 4), both[4 * leaves:].view(P, R, 4)
+        if plan is None:
+            return None
+        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err, "R": R, "LL": LL,
+              "src_base": plan["src_base"], "src_n": plan["src_n"], "starts": plan["starts"]}
+        return send, plan["in_splits"], plan["out_splits"], top_rows, ex
+
+    def _exchange_plan(self, counts: torch.Tensor, k: int) -> Optional[dict]:
+        """Split sizes of the exchange from every rank's per-slot counts.
+
+        ``counts`` is int64 [P << k, 4] in destination-slot order (round j, rank r) -> j * P + r:
+        rows, error word, id base, local point count. The matrix is all-gathered (P * 2^k * 32 B
+        per rank), so every rank sees every rank's error bits and checks every subtree's row
+        total against the tree geometry: a failure raises on all ranks together instead of
+        leaving peers blocked inside the exchange. Returns None when a top level's middle bucket
+        overflowed its all-gather slot (the caller retries with larger slots)."""
+        P, R = self.P, 1 << k
+        full = torch.empty(P * P * R * 4, dtype=torch.int64, device=counts.device)
+        comm.all_gather_into_(full, counts.reshape(-1))
+        full = full.cpu().view(P, R, P, 4)  # [source rank][round][destination rank][field]
         errs = 0
-        for v in torch.cat([mine[:, :, 1].reshape(-1), theirs[:, :, 1].reshape(-1)]).tolist():
+        for v in full[..., 1].unique().tolist():
             errs |= int(v)
         if errs & 1:
             # a middle bucket overflowed its all-gather slot: that level's pivot (and every level
@@ -373,12 +408,19 @@ class GlobalTreeBuilder:
             return None
         if errs & 2:
             raise RuntimeError("global top levels: histogram totals disagree with the tree geometry")
-        in_splits = [mine[:, j, 0].tolist() for j in range(R)]    # rows to each rank in round j
-        out_splits = [theirs[:, j, 0].tolist() for j in range(R)]  # rows from each rank in round j
+        got = full[..., 0].sum(0)  # [round][destination rank]
+        for q in range(P):
+            for j in range(R):
+                want = segment(self.n_total, (P + q) * R - 1 + j)[1]
+                if int(got[j, q]) != want:
+                    raise RuntimeError(f"global exchange: rank {q} would receive {int(got[j, q])} points in round "
+                                       f"{j} for a subtree of {want}")
+        me = self.rank
+        in_splits = [full[me, j, :, 0].tolist() for j in range(R)]    # rows to each rank in round j
+        out_splits = [full[:, j, me, 0].tolist() for j in range(R)]   # rows from each rank in round j
         starts = np.concatenate([[0], np.cumsum([sum(v) for v in in_splits])]).astype(np.int64).tolist()
-        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err, "R": R, "LL": LL,
-              "src_base": theirs[:, 0, 2].tolist(), "src_n": theirs[:, 0, 3].tolist(), "starts": starts}
-        return send, in_splits, out_splits, top_rows, ex
+        return {"in_splits": in_splits, "out_splits": out_splits, "starts": starts,
+                "src_base": full[:, 0, 0, 2].tolist(), "src_n": full[:, 0, 0, 3].tolist()}
 
     def _inner_pivots(self, k: int):
         """(output slots, heap nodes) of the pivots inside this rank's subtree above its 2^k
@@ -421,8 +463,6 @@ class GlobalTreeBuilder:
         self._scale = scale
         send, in_splits, out_splits, top_rows, ex = res
         R, LL, rs = ex["R"], ex["LL"], ex["rs"]
-        if R == 1 and sum(out_splits[0]) != self.n_leaf:
-            raise RuntimeError(f"rank {self.rank}: received {sum(out_splits[0])} points for a subtree of {self.n_leaf}")
         src_words = [max(1, (int(v) + 31) // 32) for v in ex["src_n"]]
         bm_off = np.concatenate([[0], np.cumsum(src_words)[:-1]]).astype(np.int64).tolist()
         nat = ops.native()
@@ -437,7 +477,7 @@ class GlobalTreeBuilder:
                 recv_bm = self._buf(f"recv_bm{j}", (sum(src_words),), torch.int32)
                 handles.append(comm.all_to_all_single_async(recv_bm, ex["bm"][j * P:(j + 1) * P].reshape(-1),
                                                             src_words, [ex["words"]] * P))
-            return recv, recv_bm, handles
+            return (recv, recv_bm), handles
 
         def local_tree(recv, recv_bm, j, n_j, builder, out_pts=None, out_ids=None):
             if ex["compact"]:
@@ -456,17 +496,19 @@ class GlobalTreeBuilder:
 
         with trace_range("pkd.dist.exchange_and_build"):
             if R == 1:
-                recv, recv_bm, handles = issue(0)
-                for hd in handles:
-                    if hd is not None:
-                        hd.wait()
-                self._tick(timings, "all_to_all", t0)
-                if self.n_leaf == 0:
-                    tp = torch.empty((0, dim), dtype=torch.float32, device=self.device)
-                    ti = torch.empty((0,), dtype=torch.int32, device=self.device)
-                else:
-                    tp, ti = local_tree(recv, recv_bm, 0, self.n_leaf, self._builder)
-                    self._main_used = True
+                out = {}
+
+                def consume(j, payload):
+                    self._tick(timings, "all_to_all", t0)
+                    if self.n_leaf == 0:
+                        out["t"] = (torch.empty((0, dim), dtype=torch.float32, device=self.device),
+                                    torch.empty((0,), dtype=torch.int32, device=self.device))
+                    else:
+                        out["t"] = local_tree(payload[0], payload[1], 0, self.n_leaf, self._builder)
+                        self._main_used = True
+
+                _run_rounds(1, issue, consume)
+                tp, ti = out["t"]
             else:
                 # my subtree: node m = P - 1 + rank at depth L; its 2^k leaves at depth LL are the
                 # heap nodes first_leaf + j; the R - 1 pivots between them come from top_rows
@@ -479,22 +521,16 @@ class GlobalTreeBuilder:
                     rows = top_rows[hi]
                     tp[si] = rows[:, :dim]
                     ti[si] = rows[:, dim].contiguous().view(torch.int32)
-                pending = issue(0)
-                for j in range(R):
-                    recv, recv_bm, handles = pending
-                    for hd in handles:
-                        if hd is not None:
-                            hd.wait()
-                    if j + 1 < R:
-                        pending = issue(j + 1)  # in flight while leaf j builds
+
+                def consume(j, payload):
+                    recv, recv_bm = payload
                     lo_j, n_j = segment(self.n_total, first_leaf + j)
-                    if recv.shape[0] != n_j:
-                        raise RuntimeError(f"rank {self.rank}: round {j} received {recv.shape[0]} points for a "
-                                           f"leaf of {n_j}")
                     if n_j > 0:
                         a = lo_j - self.slot_lo
                         local_tree(recv, recv_bm, j, n_j, self._leaf_builder(n_j, self.depth0 + LL),
                                    tp[a:a + n_j], ti[a:a + n_j])
+
+                _run_rounds(R, issue, consume)
                 self._tick(timings, "all_to_all", t0)
         self._tick(timings, "local_build", t0)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
@@ -502,7 +538,13 @@ class GlobalTreeBuilder:
 
     # ---------------------------------------------------------------- host (gloo) reference path
     def _build_host(self, points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) -> DistTree:
+        """The torch reference of the device path, same schedule: top levels down to depth
+        log2(P) + k, one count exchange, 2^k all-to-all rounds (gloo async work on host
+        tensors), each leaf subtree built while the next round is in flight."""
         dim, P, L = self.dim, self.P, self.L
+        k = self.pipeline_k()
+        LL, R = L + k, 1 << k
+        leaves = P << k
         ops_h = _HostOps
         rows = _to_rows(points.to(torch.float32), ids, id_base)
         n_local = rows.shape[0]
@@ -518,10 +560,10 @@ class GlobalTreeBuilder:
         root_cell = np.stack([lo.numpy(), hi.numpy()], 1).astype(np.float32)  # [dim][2]
         cells = {0: root_cell}
         node = torch.zeros(n_local, dtype=torch.int64)
-        pivots = np.zeros(max(P - 1, 1), dtype=np.uint64)
-        top_rows = torch.zeros((max(P - 1, 1), dim + 1), dtype=torch.float32)
+        pivots = np.zeros(max(leaves - 1, 1), dtype=np.uint64)
+        top_rows = torch.zeros((max(leaves - 1, 1), dim + 1), dtype=torch.float32)
         # 2. top levels
-        for level in range(L):
+        for level in range(LL):
             nodes = 1 << level
             first = nodes - 1
             axis = (self.depth0 + level) % dim
@@ -574,23 +616,40 @@ class GlobalTreeBuilder:
                 cr[axis, 0] = pr[axis]
                 cells[2 * h + 1] = cl
                 cells[2 * h + 2] = cr
-        # 3. exchange
-        last_axis = (self.depth0 + L - 1) % dim
-        send, counts = ops_h.pack(rows, dim, node, L, pivots, last_axis, P)
-        recv_counts = torch.empty_like(counts)
-        comm.all_to_all_single_(recv_counts, counts)
-        in_splits = counts.tolist()
-        out_splits = recv_counts.tolist()
-        recv = torch.empty((sum(out_splits), dim + 1), dtype=torch.float32)
-        comm.all_to_all_single_(recv, send, out_splits, in_splits)
-        if recv.shape[0] != self.n_leaf:
-            raise RuntimeError(f"rank {self.rank}: received {recv.shape[0]} points for a subtree of {self.n_leaf}")
-        # 4. local subtree
-        if self.n_leaf == 0:
-            tp = torch.empty((0, dim), dtype=torch.float32)
-            ti = torch.empty((0,), dtype=torch.int32)
-        else:
-            tp, ti = ops.build_cpu(recv[:, :dim].contiguous(), recv[:, dim].contiguous().view(torch.int32), "exact",
-                                   self.depth0 + L, 1)
+        # 3. exchange plan: per destination slot (round j, rank r) rows, err, id base, n_local
+        last_axis = (self.depth0 + LL - 1) % dim
+        send, slot_rows = ops_h.pack(rows, dim, node, LL, pivots, last_axis, P, k)
+        counts = torch.zeros((leaves, 4), dtype=torch.int64)
+        counts[:, 0] = slot_rows
+        counts[:, 2] = int(id_base)
+        counts[:, 3] = n_local
+        plan = self._exchange_plan(counts, k)
+        in_splits, out_splits, starts = plan["in_splits"], plan["out_splits"], plan["starts"]
+        # 4. rounds: exchange leaf j + 1 while leaf j's subtree builds
+        m = P - 1 + self.rank
+        first_leaf = (m + 1) * R - 1
+        tp = torch.empty((self.n_leaf, dim), dtype=torch.float32)
+        ti = torch.empty((self.n_leaf,), dtype=torch.int32)
+        for lvl in range(k):  # pivots inside my subtree above its 2^k leaves
+            for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1):
+                if segment(self.n_total, h)[1] > 0:
+                    s_ = median_slot(self.n_total, h) - self.slot_lo
+                    tp[s_] = top_rows[h, :dim]
+                    ti[s_] = top_rows[h, dim:].contiguous().view(torch.int32)
+
+        def issue(j):
+            recv = torch.empty((sum(out_splits[j]), dim + 1), dtype=torch.float32)
+            hd = comm.all_to_all_single_async(recv, send[starts[j]:starts[j + 1]], out_splits[j], in_splits[j])
+            return recv, [hd]
+
+        def consume(j, recv):
+            lo_j, n_j = segment(self.n_total, first_leaf + j)
+            if n_j > 0:
+                a = lo_j - self.slot_lo
+                tp[a:a + n_j], ti[a:a + n_j] = ops.build_cpu(recv[:, :dim].contiguous(),
+                                                             recv[:, dim].contiguous().view(torch.int32), "exact",
+                                                             self.depth0 + LL, 1)
+
+        _run_rounds(R, issue, consume)
         return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
                         list(self.top_slots), top_rows[: P - 1], {})

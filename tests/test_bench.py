@@ -1,0 +1,62 @@
+"""bench.py driver contract on the CPU: one JSON line from rank 0, self-launch of N ranks
+without torchrun (the reference's `mpirun -np P`, Makefile:36), failure propagation."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _bench(*args, env=None, timeout=300):
+    e = dict(os.environ, PKD_SKIP_BUILD="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def _one_json(stdout):
+    lines = [l for l in stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_single_cpu():
+    r = _bench("--device", "cpu", "--points", "100000", "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr
+    j = _one_json(r.stdout)
+    assert j["n_gpus"] == 1 and j["steps"] == 2 and j["warmup"] == 1 and j["config"]["n_points"] == 100000
+    assert j["config"]["tree_checked"] and j["higher_is_better"] and j["unit"] == "Mpoints/s"
+
+
+def test_bench_self_launch_two_ranks():
+    """No WORLD_SIZE in the env: bench.py spawns its ranks itself; rank 0 alone prints."""
+    r = _bench("--gpus", "2", "--device", "cpu", "--points", "60000", "--steps", "1", "--warmup", "1")
+    assert r.returncode == 0, r.stderr
+    j = _one_json(r.stdout)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "global2" and j["config"]["tree_checked"]
+
+
+def test_bench_self_launch_four_ranks_pipelined():
+    r = _bench("--gpus", "4", "--device", "cpu", "--points", "40001", "--steps", "1", "--warmup", "0",
+               env={"PKD_PIPELINE_K": "1"})
+    assert r.returncode == 0, r.stderr
+    assert _one_json(r.stdout)["n_gpus"] == 4
+
+
+def test_bench_launcher_propagates_rank_failure():
+    """A dead rank ends the job with a non-zero status and no JSON line (the other rank,
+    blocked in a collective, is stopped by the launcher)."""
+    r = _bench("--gpus", "2", "--device", "cpu", "--points", "20000", "--steps", "1", "--warmup", "0",
+               env={"PKD_BENCH_FAIL_RANK": "1"}, timeout=200)
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "rank 1 exited with 7" in r.stderr
+
+
+def test_bench_world_mismatch_rejected():
+    r = _bench("--gpus", "2", "--device", "cpu", env={"WORLD_SIZE": "1"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -146,3 +146,57 @@ def _forest_tiny(rank, world):
 
 def test_forest_n_less_than_p():
     run(4, _forest_tiny)
+
+
+def _pipelined_case(rank, world, n, dim, k):
+    """Pipelined exchange on gloo: 2^k all-to-all rounds with real async work handles, each
+    leaf subtree built while the next round is in flight; the tree must not depend on k."""
+    import parallel_kd_tree_amd as pk
+    from parallel_kd_tree_amd import ops
+    from parallel_kd_tree_amd.parallel import comm, global_tree
+    from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
+    handles = []
+    orig = comm.all_to_all_single_async
+
+    def spy(*a, **kw):
+        h = orig(*a, **kw)
+        handles.append(h)
+        return h
+
+    global_tree.comm.all_to_all_single_async = spy
+    try:
+        first, cnt = comm.forest_slice(n, world, rank)
+        x = pk.generate_slice(13, dim, first, cnt)
+        b = GlobalTreeBuilder(n, dim, device=torch.device("cpu"))
+        assert b.pipeline_k() == k
+        t = b.build(x, id_base=first)
+    finally:
+        global_tree.comm.all_to_all_single_async = orig
+    assert len(handles) == 1 << k and all(h is not None and hasattr(h, "wait") for h in handles)
+    tp, ti = t.gather_full()
+    full = pk.generate_problem(13, dim, n)
+    cp, ci = ops.build_cpu(full, None, "exact", 0, 1)
+    assert torch.equal(ti, ci) and torch.equal(tp, cp)
+
+
+@pytest.mark.parametrize("world,k", [(2, 0), (2, 1), (2, 3), (4, 2), (8, 1)])
+def test_global_tree_pipelined_rounds(monkeypatch, world, k):
+    monkeypatch.setenv("PKD_PIPELINE_K", str(k))
+    run(world, _pipelined_case, 30_001, 3, k)
+
+
+def _plan_consistency(rank, world):
+    """A subtree total that disagrees with the tree geometry raises on EVERY rank (the count
+    matrix is all-gathered), so no rank is left waiting inside the exchange."""
+    from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
+    b = GlobalTreeBuilder(1000, 3, device=torch.device("cpu"))
+    counts = torch.zeros((world, 4), dtype=torch.int64)
+    counts[:, 0] = 1000 // (world * world)
+    if rank == 0:
+        counts[1, 0] += 1  # rank 0 claims one extra row for rank 1
+    with pytest.raises(RuntimeError, match="would receive"):
+        b._exchange_plan(counts, 0)
+
+
+def test_exchange_plan_fails_on_every_rank():
+    run(4, _plan_consistency)

@@ -1,5 +1,5 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  t 900 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/ -m gpu' \
-  q 200 'python tools/bench_query.py 2>&1 | tail -20' \
-  cli 100 'echo 42 | timeout 60 bin/kdtree_gpu --metrics-json 2>gpurun_out/cli_err.log | head -12; tail -5 gpurun_out/cli_err.log'
+  t 600 'python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/ -m gpu' \
+  b 200 'python bench.py --steps 20 --warmup 5' \
+  p 200 'cd /tmp && rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r2a -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2'
