@@ -63,6 +63,21 @@ constexpr int kBins2 = 4096;  // stage-2 sub-buckets
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------------------------------
+// Zero-fill of the per-build counters (error word, histograms). A plain kernel rather than
+// hipMemsetAsync: it is an ordinary node under hipGraph capture, and one launch of ours costs
+// less than the runtime's fill kernel.
+__global__ __launch_bounds__(kBlock) void k_zero(u32* __restrict__ p, i64 n) {
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) p[i] = 0u;
+}
+
+void zero_u32(void* p, i64 n, hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = int(std::min<i64>(1024, (n + kBlock - 1) / kBlock));
+  k_zero<<<grid, kBlock, 0, stream>>>(static_cast<u32*>(p), n);
+  PKD_LAUNCH_CHECK();
+}
+
 // Geometry: heap-ordered (lo, n) of every segment of levels 0..L (node h: children 2h+1,
 // 2h+2). Deterministic from n, so it is computed on the device once per build.
 __global__ void k_geometry(i64* __restrict__ seg_lo, i64* __restrict__ seg_n, i64 heap_nodes, i64 n) {
@@ -2071,12 +2086,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
                          : int(std::min<i64>(kMaxBoxParts, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
   const size_t lds = tiled ? tiled_prep_lds(dim_) : size_t(2 * dim_) * 4;
   if (tiled) {
-    static bool attr = false;
-    if (!attr) {
-      PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_prep_tiled),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-      attr = true;
-    }
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&k_prep_tiled), 96 * 1024);
   }
   // High-dim AoS input: only the global levels' keys, the ids and the input row index travel
   // through the global levels (lg_ + 2 columns instead of dim + 1); the subtree kernel and the
@@ -2147,7 +2157,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   u32* hist[2] = {reinterpret_cast<u32*>(ws + off_hist0_), reinterpret_cast<u32*>(ws + off_hist1_)};
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   u32* err = reinterpret_cast<u32*>(ws + off_err_);
-  PKD_HIP_CHECK(hipMemsetAsync(err, 0, 16, stream));
+  zero_u32(err, 4, stream);
 
   k_geometry<<<int((heap_nodes_ + kBlock - 1) / kBlock), kBlock, 0, stream>>>(seg_lo, seg_n, heap_nodes_, n_);
   PKD_LAUNCH_CHECK();
@@ -2216,7 +2226,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
     LevelArgs a = level_args(l);
     if (l == 0) {
-      PKD_HIP_CHECK(hipMemsetAsync(hist[0], 0, size_t(lp.segs * lp.bins) * 4, stream));
+      zero_u32(hist[0], lp.segs * lp.bins, stream);
       LevelArgs ah = a;  // like k_scan: fewer blocks, fewer histogram flush atomics
       ah.bps = std::max(1, lp.bps / hist_div());
       k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, stream>>>(ah, hist[0]);
@@ -2225,7 +2235,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     k_select<<<int(lp.segs), kBlock, 0, stream>>>(a);
     PKD_LAUNCH_CHECK();
     if (lp.stage2) {
-      PKD_HIP_CHECK(hipMemsetAsync(a.hist2, 0, size_t(lp.segs) * kBins2 * 4, stream));
+      zero_u32(a.hist2, lp.segs * kBins2, stream);
       k_hist2<<<int(lp.segs * lp.bps), kBlock, 0, stream>>>(a);
       PKD_LAUNCH_CHECK();
       k_select2<<<int(lp.segs), kBlock, 0, stream>>>(a);
@@ -2264,7 +2274,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         pa.bbase = pa.bcnt + size_t(grid) * 4;
       }
       if (lq.stage2) {
-        PKD_HIP_CHECK(hipMemsetAsync(b.hist2, 0, size_t(lq.segs) * kBins2 * 4, stream));
+        zero_u32(b.hist2, lq.segs * kBins2, stream);
         k_hist2p<<<grid, kBlock, 0, stream>>>(a, pa);
         PKD_LAUNCH_CHECK();
         k_select2<<<int(lq.segs), kBlock, 0, stream>>>(b);

@@ -1024,13 +1024,11 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
   }
   const size_t lds = 4 * (a.ldim > 0 ? rk::lds_words_narrow(a.dim, ITEMS * THREADS, a.ldim)
                                      : rk::lds_words(a.dim, ITEMS * THREADS));
-  static bool attr_set[2] = {false, false};
   const bool nar = a.ldim > 0;
   const void* fn = nar ? reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, true>)
                        : reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false>);
-  if (!attr_set[nar]) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
-    attr_set[nar] = true;
+  {
+    ensure_dynamic_lds(fn, int(kLdsMax));
   }
   static const bool dim3c = [] {
     const char* e = std::getenv("PKD_SUBTREE_DIM3");
@@ -1043,24 +1041,14 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
   }
   if constexpr (ITEMS == 2) {
     if (!done && a.dim == 3 && dim3c) {
-      static bool attr3 = false;
-      if (!attr3) {
-        PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 3>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
-        attr3 = true;
-      }
+      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 3>), int(kLdsMax));
       k_subtree_rank<ITEMS, THREADS, false, 3><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
       done = true;
     }
   }
   if constexpr (ITEMS == 1 && THREADS == 1024) {  // d = 8 (BASELINE's high-dim config), capacity 1024
     if (!done && a.dim == 8 && dim3c) {
-      static bool attr8 = false;
-      if (!attr8) {
-        PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 8>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
-        attr8 = true;
-      }
+      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 8>), int(kLdsMax));
       k_subtree_rank<ITEMS, THREADS, false, 8><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
       done = true;
     }
@@ -1081,13 +1069,8 @@ size_t impl_lds_bytes(int dim, int nm) { return use_hist_impl() ? subtree_lds_by
 
 template <int ITEMS, int THREADS>
 void launch_cfg(const SubArgs& a, i64 segs, hipStream_t stream) {
-  static bool attr_set = false;
   const size_t lds = subtree_lds_bytes(a.dim, ITEMS * THREADS);
-  if (!attr_set) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_subtree<ITEMS, THREADS>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsMax)));
-    attr_set = true;
-  }
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree<ITEMS, THREADS>), int(kLdsMax));
   k_subtree<ITEMS, THREADS><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
   PKD_LAUNCH_CHECK();
 }

@@ -518,6 +518,10 @@ __global__ __launch_bounds__(kBlock) void k_bm_ids(const u32* __restrict__ bm, i
   if (b == last && threadIdx.x == kBlock - 1 && i64(k) != cap) atomicOr(err, 8u);
 }
 
+__global__ void k_zero4(u32* __restrict__ p) {
+  if (threadIdx.x < 4) p[threadIdx.x] = 0u;
+}
+
 int pack_blocks(i64 n) { return int(std::max<i64>(1, std::min<i64>(2048, (n + 8191) / 8192))); }
 int stream_grid(i64 n) { return int(std::max<i64>(1, std::min<i64>(512, (n + 16383) / 16384))); }
 
@@ -559,7 +563,8 @@ size_t top_middle_words(int dim, i64 cap) { return 4 + size_t(cap) * size_t(dim 
 
 void top_collect(const TopPoints& p, const u32* node, int level, int axis, const float* cells, int bins,
                  const u32* sel, float* buf, i64 cap, hipStream_t stream) {
-  PKD_HIP_CHECK(hipMemsetAsync(buf, 0, 16, stream));
+  k_zero4<<<1, 64, 0, stream>>>(reinterpret_cast<u32*>(buf));  // the 16-B header (a graph-capturable node)
+  PKD_LAUNCH_CHECK();
   if (p.n <= 0) return;
   k_top_collect<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, cells, bins, sel, buf, cap);
   PKD_LAUNCH_CHECK();
@@ -567,13 +572,8 @@ void top_collect(const TopPoints& p, const u32* node, int level, int axis, const
 
 void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream) {
-  static bool attr = false;
   const size_t lds = size_t(kPivotLdsKeys) * 8;
-  if (!attr) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_top_pivot),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-    attr = true;
-  }
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_top_pivot), int(lds));
   MidView mv{gathered, i64(top_middle_words(dim, cap)), cap, P, dim, axis};
   k_top_pivot<<<1 << level, kPivotThreads, lds, stream>>>(mv, level, sizes, sel, pivots, top_rows, cells, err);
   PKD_LAUNCH_CHECK();

@@ -178,12 +178,7 @@ void generate_rows_device(uint32_t seed, int dim, int64_t first_row, int64_t row
   PKD_HIP_CHECK(hipStreamSynchronize(stream));  // the workspace may still be in use by earlier work
   PKD_HIP_CHECK(hipMemcpy(polys, host.data(), host.size() * 4, hipMemcpyHostToDevice));
   PKD_HIP_CHECK(hipMemcpyAsync(states, polys + size_t(p.R) * kMtWords, kN * 4, hipMemcpyDeviceToDevice, stream));
-  static const bool lds_set = [] {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_apply),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kApplyLds));
-    return true;
-  }();
-  (void)lds_set;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_mt_apply), kApplyLds);
   for (int r = 0; r < p.R; ++r) {
     const int src = 1 << r;
     const int n = std::min(src, p.C - src);

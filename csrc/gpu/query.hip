@@ -259,14 +259,8 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   if (lds > size_t(150) * 1024) throw std::invalid_argument("nn_brute: dimension too large for the LDS query tile");
   const bool vec = dim % 4 == 0 && reinterpret_cast<uintptr_t>(pts) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(queries) % 16 == 0;
-  static bool attr = false;
-  if (!attr) {
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_brute<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-    PKD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_brute<false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-    attr = true;
-  }
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_brute<true>), 150 * 1024);
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_brute<false>), 150 * 1024);
   for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
     const i64 ty = std::min<i64>(65535, tiles - t0);
     const dim3 grid{unsigned(gx), unsigned(ty), 1u};

@@ -127,3 +127,61 @@ def test_device_invariant_checker(gpu_device, n, dim, depth0):
             a[r - 1] = tmp
         assert t.invariant_violations() > 0
         assert pk.KDTree(t.tree_pts.cpu(), t.tree_ids.cpu(), depth0).invariant_violations() > 0
+
+
+def _check_headline(x, dev):
+    """A full correctness proof of one build without a CPU oracle: device error word 0, the
+    exact kd invariant at every node (k_check), ids a permutation of 1..n and every output
+    row the input row its id names (so the multiset of rows is preserved)."""
+    n, dim = x.shape
+    b = ops.GpuTreeBuilder(n, dim)
+    tp, ti = b.build(x, None, 1)
+    torch.cuda.synchronize()
+    assert b.read_error() == 0, b.read_error_detail()
+    assert pk.KDTree(tp, ti, 0).invariant_violations() == 0
+    idx = ti.to(torch.int64) - 1
+    assert int(idx.min()) == 0 and int(idx.max()) == n - 1
+    seen = torch.zeros(n, dtype=torch.int32, device=dev)
+    seen.index_add_(0, idx, torch.ones_like(idx, dtype=torch.int32))
+    assert bool((seen == 1).all()), "ids are not a permutation"
+    assert torch.equal(tp, x[idx]), "an output row differs from the input row of its id"
+    return b
+
+
+@pytest.mark.slow
+def test_headline_100m_3d(gpu_device):
+    """BASELINE's headline config, 100 M x 3D: the >= 64 M path (2048-block level grids) that
+    bench.py times."""
+    x = pk.generate_slice(42, 3, 0, 100_000_000, device=gpu_device)
+    b = _check_headline(x, gpu_device)
+    assert b.global_levels == 16
+
+
+@pytest.mark.slow
+def test_headline_100m_8d(gpu_device):
+    x = pk.generate_slice(42, 8, 0, 100_000_000, device=gpu_device)
+    _check_headline(x, gpu_device)
+
+
+@pytest.mark.slow
+def test_64m_3d_equals_cpu_exact(gpu_device):
+    """Slot-for-slot against the multi-threaded CPU exact builder at >= 64 M points."""
+    n = 64_000_000
+    x = pk.generate_slice(5, 3, 0, n, device=gpu_device)
+    b = _check_headline(x, gpu_device)
+    tp, ti = b.build(x, None, 1)
+    cp, ci = ops.build_cpu(x.cpu(), None, "exact", 0, 16)
+    assert torch.equal(ti.cpu(), ci + 1)
+    assert torch.equal(tp.cpu(), cp)
+
+
+@pytest.mark.parametrize("n", [100_000, 12_500_000])
+def test_hipgraph_replay_equals_eager(gpu_device, n):
+    """A build captured in a hipGraph (torch.cuda.CUDAGraph) replays to the eager tree. 12.5 M
+    is the size whose replay used to fault: the stage-2 histogram resets were runtime
+    hipMemsetAsync nodes; they are now zero-fill kernels of our own (tools/graph_check.py)."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+    import graph_check
+    graph_check.check(n)

@@ -38,3 +38,15 @@ def test_dist_cli_eval_mode_and_metrics(bin_dir):
     b = out(bin_dir / "kdtree_sequential", ["--threads", "16"], stdin="3\n")
     assert lines == b and lines[0] == "READY" and lines[-1] == "DONE"
     assert '"decomp": "forest"' in r.stderr and '"ranks": 1' in r.stderr
+
+
+@pytest.mark.parametrize("seed", [3, 42])
+@pytest.mark.parametrize("exe", ["kdtree_gpu", "kdtree_dist"])
+def test_eval_mode_matches_reference_fixture(bin_dir, exe, seed):
+    """The graded evaluation path (seed on stdin, 500k x 128) prints exactly what the real
+    reference binary printed (tests/fixtures, pinned against the compiled reference by
+    test_reference_parity.py)."""
+    from pathlib import Path
+    fix = (Path(__file__).parent / "fixtures" / f"ref_eval_seed{seed}.txt").read_text().splitlines()
+    args = ["--gpus", 1] if exe == "kdtree_dist" else []
+    assert out(bin_dir / exe, args, stdin=f"{seed}\n") == fix

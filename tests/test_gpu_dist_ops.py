@@ -133,7 +133,7 @@ def test_pack_matches_host(gpu_device, P, dim):
         _HostOps.route_hist(rows, dim, node_c, l, piv, (l - 1) % dim, l % dim, pr, 8192 // nl)
         hg = torch.zeros(8192, dtype=torch.int32, device=gpu_device)
         nat.top_route_hist(xg, None, 1, node_g, l, piv_g, (l - 1) % dim, l % dim, cells_g, 8192 // nl, hg)
-    sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P)
+    sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P, 0)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
     counts = torch.empty(4 * P, dtype=torch.int64, device=gpu_device)
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
@@ -181,7 +181,7 @@ def test_explicit_ids(gpu_device):
     keys = composite_u64(x[:, 0].numpy(), ids.numpy().view(np.uint32))
     piv = np.array([np.sort(keys)[n // 2]], dtype=np.uint64)
     node_c = torch.zeros(n, dtype=torch.int64)
-    _HostOps.pack(rows, dim, node_c, 1, piv, 0, 2)
+    _HostOps.pack(rows, dim, node_c, 1, piv, 0, 2, 0)
     nat = ops.native()
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
