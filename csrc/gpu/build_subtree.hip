@@ -22,6 +22,7 @@
 #include "device_utils.hpp"
 #include "pkdtree/hip_check.hpp"
 #include "subtree.hpp"
+#include "subtree_common.hpp"
 
 namespace pkdtree {
 
@@ -31,6 +32,7 @@ using dev::make_params;
 using dev::mbcnt;
 
 namespace {
+using namespace subtree_detail;
 
 constexpr int kSmall = 16;
 constexpr u32 kDone = 0xffffu;
@@ -44,24 +46,7 @@ size_t subtree_lds_words(int dim, int nm) {
 }
 size_t subtree_lds_bytes(int dim, int nm) { return 4 * subtree_lds_words(dim, nm); }
 
-struct SubArgs {
-  const float* cols;
-  i64 ncol;
-  int dim;
-  const i64* seg_lo;
-  const i64* seg_n;
-  const float* cells;  // heap-indexed [h][dim][2] cell of every segment root
-  i64 heap0;
-  int depth_base;
-  float* out_pts;
-  u32* out_ids;
-  u32* err;
-  unsigned long long* stamps;  // diagnostic build only (PKD_SUBTREE_STAMPS): [blocks][kStampSlots] s_memtime
-  int narrow_k;                // narrow (ldim > 0): id column; the input row index follows it
-  const float* in_rows;
-  i64 in_rs;
-  int ldim;                    // narrow: LDS key slots (slot t = key of subtree level t), 0 otherwise
-};
+
 
 __device__ __forceinline__ int pow2_floor_dev(int v) { return v <= 1 ? 1 : 1 << (31 - __clz(v)); }
 
@@ -107,31 +92,6 @@ struct Lds {
 // touches is private to the wave and LDS operations of one wave execute in order.
 //   wsub  : local sub-segment table (rel_lo << 16 | n), n0 entries (aliases sub + lo0)
 //   whist : 128 bins; wst: 128 words of per-sub-segment state; wcA/wcB: 2 x [16][dim][2]
-// Orders this wave's LDS writes before its later LDS reads (different lanes): waits for the
-// wave's outstanding LDS operations and fences the compiler.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-constexpr int kStampSlots = 32;
-constexpr int kStampBlocks = 4096;
-// slot 0 start, 1 rows loaded, 2 + t after level t (rank kernel), 30 before the store, 31 end
-__device__ __forceinline__ void stamp(const SubArgs& a, int i) {
-  if (a.stamps && threadIdx.x == 0 && blockIdx.x < kStampBlocks)
-    a.stamps[blockIdx.x * kStampSlots + i] = __builtin_amdgcn_s_memtime();
-}
-
-__device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
-  atomicOr(err, 4u);
-  if (atomicCAS(err + 1, 0u, code) == 0u) {
-    err[2] = t;
-    err[3] = v;
-  }
-}
-
 __device__ void wave_build(const Lds& L, int NM, int dim, int lo0, int n0, int depth0, u32* wsub, u32* whist,
                            u32* wst, float* wcA, float* wcB, u32* err) {
   const int ln = dev::lane();
@@ -1088,28 +1048,30 @@ std::string subtree_stamp_report() {
   std::vector<unsigned long long> h(size_t(kStampBlocks) * kStampSlots);
   PKD_HIP_CHECK(hipDeviceSynchronize());
   PKD_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-  // mean cycles between consecutive recorded slots, over blocks that recorded start and end
+  // per block, the recorded slots in time order; each slot is charged the cycles since the
+  // previous recorded one (mean over blocks that recorded start and end)
   double acc[kStampSlots] = {};
   int cnt[kStampSlots] = {};
   for (int b = 0; b < kStampBlocks; ++b) {
     const unsigned long long* s = &h[size_t(b) * kStampSlots];
     if (!s[0] || !s[31]) continue;
-    int prev = 0;
-    for (int i = 1; i < kStampSlots; ++i) {
-      if (!s[i]) continue;
-      acc[i] += double(s[i] - s[prev]);
-      ++cnt[i];
-      prev = i;
+    std::vector<std::pair<unsigned long long, int>> ev;
+    for (int i = 0; i < kStampSlots; ++i)
+      if (s[i]) ev.emplace_back(s[i], i);
+    std::sort(ev.begin(), ev.end());
+    for (size_t k = 1; k < ev.size(); ++k) {
+      acc[ev[k].second] += double(ev[k].first - ev[k - 1].first);
+      ++cnt[ev[k].second];
     }
   }
   std::ostringstream os;
-  os << "subtree stamps (mean cycles since the previous mark):";
+  os << "subtree stamps (mean cycles since the previous mark, in time order):";
   for (int i = 1; i < kStampSlots; ++i) {
     if (!cnt[i]) continue;
     os << " ";
     if (i == 1) os << "load";
     else if (i == 30) os << "levels-end";
-    else if (i >= 20 && i <= 24) os << "L0." << (i - 20);
+    else if (i >= 20 && i <= 29) os << "s" << i;
     else if (i == 31) os << "store";
     else os << "L" << (i - 2);
     os << "=" << long(acc[i] / cnt[i]);
@@ -1159,6 +1121,7 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
   if (ldim > dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
             std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
+  if (narrow_idcol < 0 && subtree_wave_enabled() && launch_subtree_wave(a, segs, nmax, stream)) return;
   if (!use_hist_impl()) {
     static const bool wide = [] {
       const char* e = std::getenv("PKD_SUBTREE_WIDE");

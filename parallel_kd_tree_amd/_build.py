@@ -28,8 +28,8 @@ ARCH = os.environ.get("PKD_OFFLOAD_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp"]
-CORE_HIP = ["gpu/build_global.hip", "gpu/build_subtree.hip", "gpu/query.hip", "gpu/dist_ops.hip",
-            "gpu/generator.hip"]
+CORE_HIP = ["gpu/build_global.hip", "gpu/build_subtree.hip", "gpu/subtree_wave.hip", "gpu/query.hip",
+            "gpu/dist_ops.hip", "gpu/generator.hip"]
 BIND = ["bind/torch_bindings.cpp", "bind/dist_bindings.cpp"]
 CLI_CPU = {"kdtree_sequential": ["cli/kdtree_sequential.cpp"]}
 CLI_GPU = {"kdtree_gpu": ["cli/kdtree_gpu.cpp"], "kdtree_dist": ["cli/kdtree_dist.cpp"]}

@@ -185,3 +185,20 @@ def test_hipgraph_replay_equals_eager(gpu_device, n):
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
     import graph_check
     graph_check.check(n)
+
+
+@pytest.mark.parametrize("dim,n,depth0,sub", [(3, 3_000_000, 0, 0), (1, 200_000, 0, 0), (2, 300_001, 0, 0),
+                                              (4, 200_000, 1, 0), (5, 150_000, 0, 0), (8, 400_000, 3, 0),
+                                              (3, 300_000, 0, 256), (3, 70, 0, 0), (8, 1000, 0, 0)])
+def test_wave_subtree_kernel(gpu_device, monkeypatch, dim, n, depth0, sub):
+    """The rank-propagation subtree kernel (csrc/gpu/subtree_wave.hip, PKD_SUBTREE_IMPL=wave)
+    builds the same unique tree as the CPU oracle: block levels, the wave hand-over at 64
+    points, every launch shape (capacities 64..2048) and dims 1..8."""
+    monkeypatch.setenv("PKD_SUBTREE_IMPL", "wave")
+    check_same(pk.generate_problem(dim * 7 + n % 5, dim, n), gpu_device, depth0=depth0, subtree_max=sub)
+
+
+def test_wave_subtree_kernel_duplicates(gpu_device, monkeypatch):
+    monkeypatch.setenv("PKD_SUBTREE_IMPL", "wave")
+    check_same(torch.randint(0, 4, (200_000, 3)).float(), gpu_device)
+    check_same(torch.zeros(30_000, 2), gpu_device)

@@ -1,5 +1,4 @@
 export TMPDIR=/tmp
 python tools/gpu_steps.py \
-  graph 200 'python tools/graph_check.py 100000 4000000 12500000 25000000 100000000' \
-  t 900 'python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/ -m gpu' \
-  b 200 'python bench.py --steps 20 --warmup 5'
+  t 600 'python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_build.py -m gpu' \
+  ab 300 'PKD_SUBTREE_STAMPS=1 python tools/bench_build.py --n 100000000 --steps 3; PKD_SUBTREE_STAMPS=1 python tools/bench_build.py --n 100000000 --dim 8 --steps 3; PKD_SUBTREE_IMPL=rank python tools/bench_build.py --n 100000000 --steps 3'
