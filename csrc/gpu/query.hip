@@ -1,7 +1,9 @@
 // Exact 1-NN kernels (see gpu_query.hpp).
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "device_utils.hpp"
 #include "pkdtree/gpu_query.hpp"
@@ -117,6 +119,235 @@ __global__ __launch_bounds__(kBlock) void k_brute(const float* __restrict__ pts,
     for (int x = 1; x < kBlock / 64; ++x) v = wmin[x][threadIdx.x] < v ? wmin[x][threadIdx.x] : v;
     if (v != kPackedInf) atomicMin((unsigned long long*)&out[q0 + threadIdx.x], (unsigned long long)v);
   }
+}
+
+// Brute force for the common high-dim shape (dim % 32 == 0, 16-B aligned rows, a tile of at
+// most 16 queries): like k_brute, but the tile size QT is a compile-time constant (10 queries
+// compute 10 sums, not 16), and every thread streams its (row, 32-coordinate chunk) sequence
+// with the NEXT chunk's eight 16-B loads issued before the current chunk's arithmetic, so loads
+// stay in flight across the multiply-add work (k_brute loads, waits, then computes). Sums run
+// over i = 0..dim-1 in order with separately rounded multiply and add, as sq_dist.
+template <int QT, int CH>
+__global__ __launch_bounds__(kBlock) void k_brute_pf(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                     u32 id_base, i64 n, int dim, const float* __restrict__ queries,
+                                                     i64 nq, u64* __restrict__ out) {
+  extern __shared__ __align__(16) float qs[];  // [QT][dim]
+  const i64 q0 = i64(blockIdx.y) * QT;
+  const int qt = int(std::min<i64>(QT, nq - q0));
+  for (int f = threadIdx.x; f < QT * dim; f += kBlock) qs[f] = f < qt * dim ? queries[q0 * dim + f] : 0.0f;
+  __syncthreads();
+  u64 best[QT];
+#pragma unroll
+  for (int k = 0; k < QT; ++k) best[k] = kPackedInf;
+  const int chunks = dim / CH;
+  const i64 stride = i64(gridDim.x) * kBlock;
+  i64 r = i64(blockIdx.x) * kBlock + threadIdx.x;
+  int c = 0;
+  float4 pv[CH / 4], pn[CH / 4];
+  auto load = [&](i64 rr, int cc, float4 (&v)[CH / 4]) {
+    const float4* src = reinterpret_cast<const float4*>(pts + rr * dim + cc * CH);
+#pragma unroll
+    for (int j = 0; j < CH / 4; ++j) v[j] = src[j];
+  };
+  if (r < n) load(r, 0, pv);
+  float acc[QT];
+#pragma unroll
+  for (int k = 0; k < QT; ++k) acc[k] = 0.0f;
+  while (r < n) {
+    // the next (row, chunk) of this thread
+    i64 rn = r;
+    int cn = c + 1;
+    if (cn == chunks) {
+      cn = 0;
+      rn = r + stride;
+    }
+    if (rn < n) load(rn, cn, pn);
+    const float* qc = qs + c * CH;
+#pragma unroll
+    for (int k = 0; k < QT; ++k) {
+      const float4* qk = reinterpret_cast<const float4*>(qc + k * dim);
+#pragma unroll
+      for (int j = 0; j < CH / 4; ++j) {
+        const float4 q4 = qk[j];
+        const float t0 = pv[j].x - q4.x, t1 = pv[j].y - q4.y, t2 = pv[j].z - q4.z, t3 = pv[j].w - q4.w;
+        const float s0 = t0 * t0, s1 = t1 * t1, s2 = t2 * t2, s3 = t3 * t3;
+        acc[k] = acc[k] + s0;
+        acc[k] = acc[k] + s1;
+        acc[k] = acc[k] + s2;
+        acc[k] = acc[k] + s3;
+      }
+    }
+    if (cn == 0) {  // row r complete
+      const u32 id = ids ? ids[r] : id_base + u32(r);
+#pragma unroll
+      for (int k = 0; k < QT; ++k) {
+        const u64 v = pack_dist_idx(acc[k], id);
+        best[k] = (k < qt && v < best[k]) ? v : best[k];
+        acc[k] = 0.0f;
+      }
+    }
+    r = rn;
+    c = cn;
+#pragma unroll
+    for (int j = 0; j < CH / 4; ++j) pv[j] = pn[j];
+  }
+  __shared__ u64 wmin[kBlock / 64][QT];
+  const int w = threadIdx.x / 64;
+#pragma unroll
+  for (int k = 0; k < QT; ++k) {
+    const u64 v = dev::wave_min_u64(best[k]);
+    if (dev::lane() == 0) wmin[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < qt) {
+    u64 v = wmin[0][threadIdx.x];
+    for (int x = 1; x < kBlock / 64; ++x) v = wmin[x][threadIdx.x] < v ? wmin[x][threadIdx.x] : v;
+    if (v != kPackedInf) atomicMin((unsigned long long*)&out[q0 + threadIdx.x], (unsigned long long)v);
+  }
+}
+
+template <int QT>
+void launch_brute_pf(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq,
+                     u64* out, hipStream_t stream) {
+  constexpr int CH = 16;  // coordinates per load round: 2 x 4 float4 in flight per lane
+  const i64 tiles = (nq + QT - 1) / QT;
+  const void* fn = reinterpret_cast<const void*>(&k_brute_pf<QT, CH>);
+  const size_t lds = size_t(QT) * dim * 4;
+  ensure_dynamic_lds(fn, int(std::max<size_t>(lds, 1)));
+  // one resident round of blocks over all tiles (no tail round); one atomic per (block, query)
+  int dev = 0, cus = 256, per_cu = 0;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  PKD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  PKD_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds));
+  const i64 want = std::max<i64>(1, i64(std::max(per_cu, 1)) * cus / std::max<i64>(1, std::min<i64>(tiles, 64)));
+  const int gx = int(std::min<i64>(want, (n + kBlock - 1) / kBlock));
+  for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
+    const i64 ty = std::min<i64>(65535, tiles - t0);
+    k_brute_pf<QT, CH><<<dim3(unsigned(gx), unsigned(ty), 1u), kBlock, lds, stream>>>(
+        pts, ids, id_base, n, dim, queries + t0 * QT * dim, nq - t0 * QT, out + t0 * QT);
+    PKD_LAUNCH_CHECK();
+  }
+}
+
+// Batched exact NN, one WAVE per query: the top of the implicit tree is walked by the whole
+// wave in lockstep (wave-uniform control flow, the median rows are broadcast loads, the stack
+// of far children lives in LDS), and every sub-tree of at most `bucket` points -- a
+// contiguous slot range of the in-order layout, medians included -- is scanned by the 64
+// lanes with coalesced row loads and a wave minimum. Same visiting rule as k_traverse (near
+// side first, far side iff its axis distance^2 <= the best distance), so the answer (minimum
+// of (d2, id)) is the same; one thread per query instead serialises the 64 different paths
+// of a wave. DC: compile-time dim (0: runtime dim, query kept in LDS).
+constexpr int kWaveStack = 48;
+template <int DC>
+__global__ __launch_bounds__(kBlock) void k_nn_wave(const float* __restrict__ P, const u32* __restrict__ ids, i64 n,
+                                                    int dim_rt, int depth0, u32 bucket,
+                                                    const float* __restrict__ queries, i64 nq,
+                                                    u64* __restrict__ out) {
+  constexpr int W = kBlock / 64;
+  __shared__ u32 st_lo[W][kWaveStack], st_n[W][kWaveStack], st_d[W][kWaveStack];
+  __shared__ float st_b[W][kWaveStack];
+  __shared__ float qsh[W][DC > 0 ? 1 : 32];
+  const int w = threadIdx.x / 64, ln = dev::lane();
+  const i64 qi = i64(blockIdx.x) * W + w;
+  if (qi >= nq || n <= 0) return;  // wave-uniform
+  const int dim = DC > 0 ? DC : dim_rt;
+  float qr[DC > 0 ? DC : 1];
+  const float* qg = queries + qi * dim;
+  if constexpr (DC > 0) {
+#pragma unroll
+    for (int c = 0; c < DC; ++c) qr[c] = qg[c];
+  } else {
+    if (ln < dim) qsh[w][ln] = qg[ln];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+  auto dist = [&](const float* p) -> float {
+    if constexpr (DC > 0) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int c = 0; c < DC; ++c) {
+        const float t = p[c] - qr[c];
+        const float sq = t * t;
+        acc = acc + sq;
+      }
+      return acc;
+    } else {
+      return sq_dist(p, &qsh[w][0], dim);
+    }
+  };
+  auto qcoord = [&](int axis) -> float {
+    if constexpr (DC > 0) {
+      float v = qr[0];
+#pragma unroll
+      for (int c = 1; c < DC; ++c) v = c == axis ? qr[c] : v;
+      return v;
+    } else {
+      return qsh[w][axis];
+    }
+  };
+  u64 best = out[qi];
+  float bd = packed_dist(best);
+  int sp = 0;
+  u32 lo = 0, cnt = u32(n);
+  int depth = 0;
+  for (;;) {
+    while (cnt > 0) {
+      if (cnt <= bucket) {  // the whole sub-tree: 64 lanes, coalesced rows
+        u64 mine = kPackedInf;
+        for (u32 j = u32(ln); j < cnt; j += 64) {
+          const u32 m = lo + j;
+          const u64 v = pack_dist_idx(dist(P + i64(m) * dim), ids[m]);
+          mine = v < mine ? v : mine;
+        }
+        mine = dev::wave_min_u64(mine);
+        if (mine < best) {
+          best = mine;
+          bd = packed_dist(best);
+        }
+        break;
+      }
+      const u32 m = lo + cnt / 2;
+      const float* p = P + i64(m) * dim;
+      const u64 v = pack_dist_idx(dist(p), ids[m]);
+      if (v < best) {
+        best = v;
+        bd = packed_dist(v);
+      }
+      const int axis = (depth0 + depth) % dim;
+      const float dax = qcoord(axis) - p[axis];
+      const float dax2 = dax * dax;
+      const u32 ln_ = cnt / 2, rn = cnt - cnt / 2 - 1;
+      u32 near_lo, near_n, far_lo, far_n;
+      if (dax < 0) {
+        near_lo = lo; near_n = ln_; far_lo = m + 1; far_n = rn;
+      } else {
+        near_lo = m + 1; near_n = rn; far_lo = lo; far_n = ln_;
+      }
+      if (far_n > 0 && dax2 <= bd && sp < kWaveStack) {
+        st_lo[w][sp] = far_lo;
+        st_n[w][sp] = far_n;
+        st_d[w][sp] = u32(depth + 1);
+        st_b[w][sp] = dax2;
+        ++sp;
+      }
+      lo = near_lo;
+      cnt = near_n;
+      ++depth;
+    }
+    bool found = false;
+    while (sp > 0) {
+      --sp;
+      if (st_b[w][sp] <= bd) {
+        lo = st_lo[w][sp];
+        cnt = st_n[w][sp];
+        depth = int(st_d[w][sp]);
+        found = true;
+        break;
+      }
+    }
+    if (!found) break;
+  }
+  if (ln == 0) out[qi] = best;
 }
 
 // One thread per query; explicit stack of far children with their lower bound.
@@ -245,6 +476,11 @@ void nn_init(u64* out, i64 nq, hipStream_t stream) {
   PKD_LAUNCH_CHECK();
 }
 
+bool brute_legacy() {
+  const char* e = std::getenv("PKD_BRUTE_LEGACY");  // A/B against k_brute
+  return e && std::string(e) == "1";
+}
+
 void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq, u64* out,
               hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
@@ -259,6 +495,16 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   if (lds > size_t(150) * 1024) throw std::invalid_argument("nn_brute: dimension too large for the LDS query tile");
   const bool vec = dim % 4 == 0 && reinterpret_cast<uintptr_t>(pts) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(queries) % 16 == 0;
+  if (vec && dim % 16 == 0 && size_t(16) * dim * 4 <= size_t(150) * 1024 && !brute_legacy()) {
+    // the prefetching kernel with the tile size that fits the queries
+    if (nq <= 1) launch_brute_pf<1>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    else if (nq <= 2) launch_brute_pf<2>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    else if (nq <= 4) launch_brute_pf<4>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    else if (nq <= 8) launch_brute_pf<8>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    else if (nq <= 10) launch_brute_pf<10>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    else launch_brute_pf<16>(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    return;
+  }
   ensure_dynamic_lds(reinterpret_cast<const void*>(&k_brute<true>), 150 * 1024);
   ensure_dynamic_lds(reinterpret_cast<const void*>(&k_brute<false>), 150 * 1024);
   for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
@@ -271,10 +517,43 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   }
 }
 
+namespace {
+template <int DC>
+void launch_nn_wave(const float* P, const u32* ids, i64 n, int dim, int depth0, u32 bucket, const float* q, i64 nq,
+                    u64* out, hipStream_t stream) {
+  constexpr int W = kBlock / 64;
+  for (i64 q0 = 0; q0 < nq; q0 += i64(W) * 1048576) {
+    const i64 m = std::min<i64>(nq - q0, i64(W) * 1048576);
+    k_nn_wave<DC><<<int((m + W - 1) / W), kBlock, 0, stream>>>(P, ids, n, dim, depth0, bucket, q + q0 * dim, m,
+                                                               out + q0);
+    PKD_LAUNCH_CHECK();
+  }
+}
+
+int traverse_mode() {  // PKD_TRAVERSE=thread: one thread per query (the older kernel)
+  const char* e = std::getenv("PKD_TRAVERSE");
+  return e && std::string(e) == "thread" ? 1 : 0;
+}
+}  // namespace
+
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries, i64 nq,
                  u64* out, hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
   TraceRange tr("pkd.nn_traverse");
+  if (dim <= 32 && traverse_mode() == 0) {
+    const u32 bucket = 512;
+    switch (dim) {
+      case 1: launch_nn_wave<1>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 2: launch_nn_wave<2>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 3: launch_nn_wave<3>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 4: launch_nn_wave<4>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 5: launch_nn_wave<5>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 6: launch_nn_wave<6>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 7: launch_nn_wave<7>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      case 8: launch_nn_wave<8>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+      default: launch_nn_wave<0>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
+    }
+  }
   k_traverse<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries, nq,
                                                                     out);
   PKD_LAUNCH_CHECK();

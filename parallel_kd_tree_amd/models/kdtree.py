@@ -100,6 +100,11 @@ class KDTree:
         return self._host
 
     def point_at(self, slot: int) -> Point:
+        """The Point of one slot. A GPU tree copies that row only (a Node walk over a 100 M
+        point tree never moves the tree to the host); CPU trees are viewed in place."""
+        if self.tree_pts.is_cuda and self._host is None:
+            row = self.tree_pts[slot].detach().cpu().numpy()
+            return Point(self.dim, int(self.tree_ids[slot].item()) & 0xFFFFFFFF, row)
         pts, ids = self._host_arrays()
         return Point(self.dim, int(ids[slot]) & 0xFFFFFFFF, pts[slot])
 
@@ -114,7 +119,7 @@ class KDTree:
             raise ValueError("query_packed needs a GPU tree; use query() on CPU trees")
         q = queries.to(self.device, torch.float32).contiguous()
         if method == "auto":
-            method = "traverse" if (self.dim <= 16 and q.shape[0] >= 64) or self.dim <= 4 else "brute"
+            method = "traverse" if self.dim <= 16 else "brute"
         return ops.nn_gpu(self.tree_pts, self.tree_ids, q, method, self.depth0, 0, into)
 
     def query(self, queries: torch.Tensor, method: str = "auto") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -137,9 +142,11 @@ class KDTree:
             return None
         q = torch.from_numpy(query.coordinates.reshape(1, -1).copy())
         if self.tree_pts.is_cuda and self.mode == "exact":
-            _, ids = self.query(q)
-            host_pts, host_ids = self._host_arrays()
-            slot = int((torch.from_numpy(host_ids).to(torch.int64) & 0xFFFFFFFF == ids[0]).nonzero()[0])
+            # the id -> slot lookup runs on the device: one comparison pass over tree_ids, and
+            # only the slot index crosses to the host (never the tree)
+            _, ids = ops.finalize(self.query_packed(q))
+            hit = (self.tree_ids == ids[0].to(torch.int32)).nonzero()
+            slot = int(hit[0, 0])
         else:
             slots, _ = ops.nn_cpu(self.tree_pts.cpu().contiguous(), q, self.depth0)
             slot = int(slots[0])

@@ -202,3 +202,44 @@ def test_wave_subtree_kernel_duplicates(gpu_device, monkeypatch):
     monkeypatch.setenv("PKD_SUBTREE_IMPL", "wave")
     check_same(torch.randint(0, 4, (200_000, 3)).float(), gpu_device)
     check_same(torch.zeros(30_000, 2), gpu_device)
+
+
+def test_nearest_neighbor_no_tree_copy(gpu_device, monkeypatch):
+    """KDTree.nearest_neighbor / Node on a 10 M GPU tree: the id -> slot lookup runs on the
+    device and a Node reads one row; the whole tree never crosses to the host (any device ->
+    host copy larger than a few rows fails the test)."""
+    from parallel_kd_tree_amd.models.node import Point
+    n = 10_000_000
+    x = pk.generate_slice(12, 3, 0, n + 1, device=gpu_device)
+    t = pk.KDTree.build(x[:n], id_base=1)
+    q = x[n:].cpu().numpy()[0]
+    orig = torch.Tensor.cpu
+    moved = []
+
+    def spy(self, *a, **kw):
+        moved.append(self.numel() * self.element_size())
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(torch.Tensor, "cpu", spy)
+    node = t.nearest_neighbor(Point(3, n + 1, q))
+    monkeypatch.setattr(torch.Tensor, "cpu", orig)
+    assert max(moved, default=0) <= 64, moved
+    d, ids = t.query(x[n:])
+    assert node.point.ID == int(ids[0].item())
+    assert t._host is None
+
+
+@pytest.mark.parametrize("n,dim,nq,depth0", [(1_000_000, 3, 3000, 0), (300_000, 8, 2000, 0), (200_000, 5, 1000, 2),
+                                             (100_000, 12, 500, 0), (1000, 3, 100, 0), (700, 2, 50, 1)])
+def test_traversal_kernels_equal_brute(gpu_device, monkeypatch, n, dim, nq, depth0):
+    """The wave-per-query traversal (bucket scans of 512-point sub-trees) and the older
+    thread-per-query traversal both return exactly the brute-force (d2, id) minimum,
+    including queries on and off the data, and trees rooted below depth 0."""
+    x = pk.generate_problem(n + dim, dim, n + nq)
+    t = pk.KDTree.build(x[:n].to(gpu_device), id_base=1, depth0=depth0)
+    q = torch.cat([x[n:], x[: nq // 4]]).to(gpu_device)  # a quarter of the queries hit a point exactly
+    pb = t.query_packed(q, "brute")
+    pw = t.query_packed(q, "traverse")
+    monkeypatch.setenv("PKD_TRAVERSE", "thread")
+    pt = t.query_packed(q, "traverse")
+    assert torch.equal(pb, pw) and torch.equal(pb, pt)

@@ -23,6 +23,8 @@ x = pk.generate_slice(42, args.dim, 0, args.n + args.queries, device=dev)
 tree = pk.KDTree.build(x[:args.n], id_base=1)
 q = x[args.n:].contiguous()
 res = {"n": args.n, "dim": args.dim, "queries": args.queries}
+from parallel_kd_tree_amd import ops  # noqa: E402
+nat = ops.native()
 out = {}
 # traversal at high dimension visits every node from one thread per query (as the reference's
 # search does at d=128): only timed where it is the right method
@@ -36,6 +38,16 @@ for method in methods:
         tree.query_packed(q, method)
     torch.cuda.synchronize()
     res[method + "_ms"] = round((time.perf_counter() - t0) * 1e3 / args.reps, 4)
+    # device time of the kernel alone (events around a pre-initialised output, no allocation)
+    into = torch.empty(q.shape[0], dtype=torch.int64, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        into.fill_(-1)
+        tree.query_packed(q, method, into)
+    e1.record()
+    torch.cuda.synchronize()
+    res[method + "_dev_ms"] = round(e0.elapsed_time(e1) / args.reps, 4)
 if "traverse" in out:
     res["same"] = bool(torch.equal(out["brute"], out["traverse"]))
 print(json.dumps(res), flush=True)
