@@ -8,6 +8,13 @@
 #include <vector>
 
 #include "pkdtree/dist_ops.hpp"
+#include "pkdtree/global_builder.hpp"
+#include "pkdtree/hip_check.hpp"
+
+#include <cstring>
+#include <exception>
+#include <thread>
+#include <tuple>
 
 namespace pkdtree {
 
@@ -152,9 +159,82 @@ void ids_from_bm(const torch::Tensor& bitmaps, const std::vector<int64_t>& off, 
   ids_from_bitmaps(cu32p(bitmaps), int(P), src, u32p(ids), scratch.data_ptr(), u32p(err), stream_of(bitmaps));
 }
 
+// The native exchange planner on host data (CPU-testable): counts [P][R * P][4].
+std::tuple<int, std::vector<std::vector<int64_t>>, std::vector<std::vector<int64_t>>, std::vector<int64_t>> plan_py(
+    const std::vector<int64_t>& counts, int64_t P, int64_t R, int64_t me, int64_t n_total) {
+  std::vector<i64> c(counts.begin(), counts.end());
+  global_plan::Plan plan;
+  const int rc = global_plan::make_plan(c, int(P), int(R), int(me), n_total, &plan);
+  std::vector<std::vector<int64_t>> in(plan.in_splits.begin(), plan.in_splits.end());
+  std::vector<std::vector<int64_t>> out(plan.out_splits.begin(), plan.out_splits.end());
+  return {rc, in, out, std::vector<int64_t>(plan.starts.begin(), plan.starts.end())};
+}
+
+// The native global builder with P ranks as threads of this process sharing the current GPU
+// (loopback communicator): rank r holds rows [first_r, first_r + local_r) of `x` (the reference's
+// MPI slicing), ids 1..N. Returns the assembled in-order tree (rank sub-trees + top pivots) on the
+// host and the OR of the ranks' error words.
+std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::Tensor& x, int64_t P, int64_t k) {
+  TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
+              "x: contiguous float32 [N, dim] host tensor");
+  const int64_t N = x.size(0);
+  const int dim = int(x.size(1));
+  int dev = 0;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  torch::Tensor tp = torch::zeros({N, dim}, torch::kFloat32);
+  torch::Tensor ti = torch::zeros({N}, torch::kInt32);
+  auto comms = make_thread_comms(int(P));
+  std::vector<std::exception_ptr> errs(static_cast<size_t>(P));
+  std::vector<u32> ew(static_cast<size_t>(P), 0u);
+  std::vector<std::thread> th;
+  for (int r = 0; r < int(P); ++r)
+    th.emplace_back([&, r] {
+      float* d = nullptr;
+      hipStream_t s = nullptr;
+      try {
+        PKD_HIP_CHECK(hipSetDevice(dev));
+        const int64_t base = N / P, first = base * r, local = base + (r == P - 1 ? N % P : 0);
+        PKD_HIP_CHECK(hipStreamCreate(&s));
+        PKD_HIP_CHECK(hipMalloc(&d, size_t(std::max<int64_t>(local, 1)) * dim * 4));
+        PKD_HIP_CHECK(hipMemcpy(d, x.data_ptr<float>() + first * dim, size_t(local) * dim * 4, hipMemcpyHostToDevice));
+        GlobalBuilder gb(*comms[size_t(r)], N, dim, int(k));
+        gb.build(d, local, u32(first + 1), s);
+        ew[size_t(r)] = gb.read_error(s);
+        PKD_HIP_CHECK(hipMemcpy(tp.data_ptr<float>() + gb.slot_lo() * dim, gb.tree_pts(), size_t(gb.n_leaf()) * dim * 4,
+                                hipMemcpyDeviceToHost));
+        PKD_HIP_CHECK(hipMemcpy(ti.data_ptr<int32_t>() + gb.slot_lo(), gb.tree_ids(), size_t(gb.n_leaf()) * 4,
+                                hipMemcpyDeviceToHost));
+        if (r == 0) {
+          const auto slots = gb.top_slots();
+          std::vector<float> rows(slots.size() * size_t(dim + 1));
+          if (!rows.empty())
+            PKD_HIP_CHECK(hipMemcpy(rows.data(), gb.top_rows(), rows.size() * 4, hipMemcpyDeviceToHost));
+          for (size_t h = 0; h < slots.size(); ++h)
+            if (slots[h] >= 0) {
+              std::memcpy(tp.data_ptr<float>() + slots[h] * dim, &rows[h * size_t(dim + 1)], size_t(dim) * 4);
+              std::memcpy(ti.data_ptr<int32_t>() + slots[h], &rows[h * size_t(dim + 1) + dim], 4);
+            }
+        }
+      } catch (...) {
+        errs[size_t(r)] = std::current_exception();
+      }
+      if (d) (void)hipFree(d);
+      if (s) (void)hipStreamDestroy(s);
+    });
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+  u32 e = 0;
+  for (u32 v : ew) e |= v;
+  return {tp, ti, int64_t(e)};
+}
+
 }  // namespace
 
 void bind_dist_ops(pybind11::module& m) {
+  m.def("global_plan", &plan_py);
+  m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("top_bbox", &bbox);
   m.def("top_root_cell", &root_cell);
   m.def("top_route_hist", &route_hist);

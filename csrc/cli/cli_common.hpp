@@ -28,6 +28,8 @@ struct Options {
   bool metrics = false;            // per-phase timings as one JSON line on stderr
   int device = 0;
   bool host_gen = false;           // generate on the host and copy (default: on the GPU)
+  std::string decomp = "forest";   // kdtree_dist: forest (kdtree_mpi.cpp) | global (one tree)
+  int pipeline_k = -1;             // kdtree_dist --decomp global: 2^k exchange rounds (-1: auto)
   std::vector<char*> positional;   // argv[0] + positionals
 };
 
@@ -43,19 +45,27 @@ inline Options parse(int argc, char** argv) {
       std::cerr << "missing value for " << name << std::endl;
       std::exit(1);
     };
+    // "--name value" or "--name=value" (exact names: --query is not a prefix of --queries)
+    auto is = [&](const char* name) { return a == name || a.rfind(std::string(name) + "=", 0) == 0; };
     if (a == "--debug") o.debug = true;
     else if (a == "--metrics-json") o.metrics = true;
-    else if (a.rfind("--mode", 0) == 0) o.mode = val("--mode");
-    else if (a.rfind("--query", 0) == 0) o.query = val("--query");
-    else if (a.rfind("--threads", 0) == 0) o.threads = std::atoi(val("--threads").c_str());
-    else if (a.rfind("--queries", 0) == 0) o.num_queries = std::atoi(val("--queries").c_str());
+    else if (is("--mode")) o.mode = val("--mode");
+    else if (is("--query")) o.query = val("--query");
+    else if (is("--threads")) o.threads = std::atoi(val("--threads").c_str());
+    else if (is("--queries")) o.num_queries = std::atoi(val("--queries").c_str());
     else if (a == "--host-gen") o.host_gen = true;
-    else if (a.rfind("--device", 0) == 0) o.device = std::atoi(val("--device").c_str());
+    else if (is("--device")) o.device = std::atoi(val("--device").c_str());
+    else if (is("--decomp")) o.decomp = val("--decomp");
+    else if (is("--pipeline-k")) o.pipeline_k = std::atoi(val("--pipeline-k").c_str());
     else o.positional.push_back(argv[i]);
   }
   const char* env = std::getenv("KDTREE_DEBUG");
   if (env && std::strcmp(env, "0") != 0) o.debug = true;
   if (o.positional.size() > 1) o.debug = true;
+  if (o.decomp != "forest" && o.decomp != "global") {
+    std::cerr << "--decomp must be forest or global" << std::endl;
+    std::exit(1);
+  }
   if (o.mode != "exact" && o.mode != "reference") {
     std::cerr << "--mode must be exact or reference" << std::endl;
     std::exit(1);

@@ -15,6 +15,10 @@
 //   * every rank answers the queries on its tree; packed (d2 << 32 | id) results are
 //     MIN-reduced to rank 0 (MPI_Reduce MIN of the distances, :253)             -> ncclReduce
 //   * rank 0 prints the protocol lines.
+// --decomp global instead builds ONE exact tree over all ranks (GlobalBuilder: top log2 P
+// levels by allreduce histograms + allgather pivot selection, one all-to-all of the points to
+// their subtree's rank, pipelined in 2^k rounds with --pipeline-k); each rank answers the
+// queries on its subtree, rank 0 also on the top pivots, and the same MIN reduce combines them.
 // Ranks with no points (N < P, the reference's segfault F7) contribute +inf.
 // Every collective is waited on with a watchdog: the stream is polled and
 // ncclCommGetAsyncError checked until a deadline (--timeout seconds, default 300); a stuck or
@@ -40,6 +44,7 @@
 
 #include "cli_common.hpp"
 #include "pkdtree/generator.hpp"
+#include "pkdtree/global_builder.hpp"
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
@@ -61,6 +66,45 @@ int g_rank = -1;
 
 struct Config {
   int seed, dim, num_points;
+};
+
+// The global builder's collectives on RCCL: allreduce / allgather as single calls, the
+// all-to-all-v as one grouped set of point-to-point sends and receives (xGMI links are
+// point-to-point; the self part is a device copy).
+class RcclComm final : public Comm {
+ public:
+  RcclComm(ncclComm_t c, int rank, int size) : c_(c), rank_(rank), size_(size) {}
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
+    PKD_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, c_, s));
+  }
+  void allreduce_min_i64(i64* buf, size_t count, hipStream_t s) override {
+    PKD_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclMin, c_, s));
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    PKD_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, c_, s));
+  }
+  void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                 const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
+    const char* sp = static_cast<const char*>(send);
+    char* rp = static_cast<char*>(recv);
+    if (send_bytes[rank_] != recv_bytes[rank_]) throw std::runtime_error("alltoallv: self size mismatch");
+    if (send_bytes[rank_])
+      PKD_HIP_CHECK(hipMemcpyAsync(rp + recv_off[rank_], sp + send_off[rank_], send_bytes[rank_],
+                                   hipMemcpyDeviceToDevice, s));
+    PKD_NCCL_CHECK(ncclGroupStart());
+    for (int p = 0; p < size_; ++p) {
+      if (p == rank_) continue;
+      if (send_bytes[p]) PKD_NCCL_CHECK(ncclSend(sp + send_off[p], send_bytes[p], ncclChar, p, c_, s));
+      if (recv_bytes[p]) PKD_NCCL_CHECK(ncclRecv(rp + recv_off[p], recv_bytes[p], ncclChar, p, c_, s));
+    }
+    PKD_NCCL_CHECK(ncclGroupEnd());
+  }
+
+ private:
+  ncclComm_t c_;
+  int rank_, size_;
 };
 
 // Waits for everything enqueued on `s` (collectives included) with a deadline, polling the
@@ -171,7 +215,17 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   u32* d_ids = nullptr;
   void* ws = nullptr;
   std::unique_ptr<GpuBuilder> b;
-  if (local > 0) {  // allocations outside the timed region
+  const bool global = o.decomp == "global";
+  std::unique_ptr<RcclComm> rcomm;
+  std::unique_ptr<GlobalBuilder> gb;
+  float* d_top = nullptr;  // rank 0, global: the top pivots as a point set [P - 1][dim] + ids
+  u32* d_top_ids = nullptr;
+  if (global) {
+    rcomm = std::make_unique<RcclComm>(comm, rank, P);
+    gb = std::make_unique<GlobalBuilder>(*rcomm, N, dim, o.pipeline_k);
+    PKD_HIP_CHECK(hipMalloc(&d_top, size_t(P) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(P) * 4));
+  } else if (local > 0) {  // allocations outside the timed region
     b = std::make_unique<GpuBuilder>(local, dim);
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(local) * 4));
@@ -179,11 +233,31 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   }
   PKD_HIP_CHECK(hipEventRecord(e0, s));
   nn_init(d_res, Q, s);
-  if (local > 0) b->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);  // global 1-based ids (kdtree_mpi.cpp:223)
+  // global 1-based ids (kdtree_mpi.cpp:223)
+  if (global) gb->build(d_x, local, u32(first + 1), s);
+  else if (local > 0) b->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);
   PKD_HIP_CHECK(hipEventRecord(e1, s));
-  if (local > 0) {
-    const float* d_q = d_x + size_t(local) * dim;
-    const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
+  const float* d_q = d_x + size_t(local) * dim;
+  const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
+  if (global) {
+    // my subtree (root at depth log2 P of the one global tree) ...
+    const i64 n = gb->n_leaf();
+    if (n > 0 && traverse) nn_traverse(gb->tree_pts(), gb->tree_ids(), n, dim, gb->top_levels(), d_q, Q, d_res, s);
+    else if (n > 0) nn_brute(gb->tree_pts(), gb->tree_ids(), 0, n, dim, d_q, Q, d_res, s);
+    // ... and on rank 0 the P - 1 replicated top pivots, split out of their [dim + 1] rows
+    if (rank == 0 && P > 1) {
+      const std::vector<i64> slots = gb->top_slots();
+      i64 nt = 0;
+      for (int h = 0; h < P - 1; ++h) {
+        if (slots[size_t(h)] < 0) continue;
+        const float* row = gb->top_rows() + size_t(h) * (dim + 1);
+        PKD_HIP_CHECK(hipMemcpyAsync(d_top + nt * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
+        PKD_HIP_CHECK(hipMemcpyAsync(d_top_ids + nt, row + dim, 4, hipMemcpyDeviceToDevice, s));
+        ++nt;
+      }
+      if (nt > 0) nn_brute(d_top, d_top_ids, 0, nt, dim, d_q, Q, d_res, s);
+    }
+  } else if (local > 0) {
     if (traverse) nn_traverse(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);
     else nn_brute(d_tree, d_ids, 0, local, dim, d_q, Q, d_res, s);
   }
@@ -200,7 +274,7 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventElapsedTime(&qry, e1, e2));
   const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
   // the build's device error word rides along (MAX over ranks: non-zero iff any rank failed)
-  const u32 berr = local > 0 ? b->read_error(ws, s) : 0u;
+  const u32 berr = global ? gb->read_error(s) : local > 0 ? b->read_error(ws, s) : 0u;
   float* d_t = nullptr;
   PKD_HIP_CHECK(hipMalloc(&d_t, 4 * sizeof(float)));
   const float ht[4] = {gen, bld, qry, float(berr & 0xFFFFFFu) + (berr >> 24 ? 1.0f : 0.0f)};
@@ -227,11 +301,16 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
     std::cout.flush();
     if (o.metrics)
       std::fprintf(stderr,
-                   "{\"ranks\": %d, \"decomp\": \"forest\", \"gen_ms\": %.3f, \"build_ms\": %.3f, "
-                   "\"query_reduce_ms\": %.3f, \"build_mpts_per_s\": %.2f, \"local_global_levels\": %d}\n",
-                   P, mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f), b ? b->global_levels() : 0);
+                   "{\"ranks\": %d, \"decomp\": \"%s\", \"gen_ms\": %.3f, \"build_ms\": %.3f, "
+                   "\"query_reduce_ms\": %.3f, \"build_mpts_per_s\": %.2f, \"local_global_levels\": %d, "
+                   "\"top_levels\": %d}\n",
+                   P, o.decomp.c_str(), mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f),
+                   b ? b->global_levels() : 0, gb ? gb->top_levels() : 0);
   }
   (void)hipFree(d_x); (void)hipFree(d_res); (void)hipFree(d_cfg); (void)hipFree(d_t);
+  if (d_top) (void)hipFree(d_top);
+  if (d_top_ids) (void)hipFree(d_top_ids);
+  gb.reset();
   if (d_tree) (void)hipFree(d_tree);
   if (d_ids) (void)hipFree(d_ids);
   if (ws) (void)hipFree(ws);
@@ -266,6 +345,10 @@ int main(int argc, char** argv) {
   cli::Options o = cli::parse(int(rest.size()), rest.data());
   if (o.mode != "exact") {
     std::cerr << "kdtree_dist builds exact trees only; use kdtree_sequential --mode reference" << std::endl;
+    return 1;
+  }
+  if (o.decomp == "global" && (P & (P - 1))) {
+    std::cerr << "--decomp global needs a power-of-two number of GPUs" << std::endl;
     return 1;
   }
   const auto tick = std::chrono::high_resolution_clock::now();

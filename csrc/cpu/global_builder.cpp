@@ -1,0 +1,434 @@
+// Native global decomposition (see pkdtree/global_builder.hpp). The orchestration mirrors
+// parallel_kd_tree_amd/parallel/global_tree.py (_top_device, _exchange_plan, _build_device);
+// the device work is the dist_ops kernels plus one GpuBuilder per leaf sub-tree.
+#include "pkdtree/global_builder.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+
+#include "pkdtree/dist_ops.hpp"
+#include "pkdtree/gpu_build.hpp"
+#include "pkdtree/hip_check.hpp"
+
+namespace pkdtree {
+
+namespace global_plan {
+
+void segment(i64 n_total, i64 h, i64* lo_out, i64* n_out) {
+  int l = 0;
+  while ((i64(1) << (l + 1)) - 1 <= h) ++l;  // level of heap node h
+  const i64 j = h + 1 - (i64(1) << l);
+  i64 lo = 0, m = n_total;
+  for (int b = l - 1; b >= 0; --b) {
+    if ((j >> b) & 1) {
+      lo = lo + m / 2 + 1;
+      m = std::max<i64>(0, m - m / 2 - 1);
+    } else {
+      m = m / 2;
+    }
+  }
+  *lo_out = lo;
+  *n_out = m;
+}
+
+i64 middle_cap(i64 n_total, int P, int level, int scale) {
+  const i64 expect = n_total * (i64(1) << level) / (i64(kTopBins) * P) + 1;
+  return std::min<i64>(std::max<i64>(2048, 3 * expect) * scale, std::max<i64>(n_total, 1));
+}
+
+int make_plan(const std::vector<i64>& counts, int P, int R, int me, i64 n_total, Plan* plan) {
+  const int S = P * R;  // destination slots per rank
+  if (counts.size() != size_t(P) * S * 4) throw std::invalid_argument("make_plan: counts must be [P][R * P][4]");
+  auto at = [&](int src, int slot, int f) { return counts[(size_t(src) * S + slot) * 4 + f]; };
+  i64 errs = 0;
+  for (int src = 0; src < P; ++src)
+    for (int slot = 0; slot < S; ++slot) errs |= at(src, slot, 1);
+  if (errs & 1) return 1;  // a middle bucket overflowed its all-gather slot: retry larger
+  if (errs & 2) throw std::runtime_error("global top levels: histogram totals disagree with the tree geometry");
+  // every rank checks every rank's receive totals: a failure raises on all ranks together
+  for (int q = 0; q < P; ++q)
+    for (int j = 0; j < R; ++j) {
+      i64 got = 0;
+      for (int src = 0; src < P; ++src) got += at(src, j * P + q, 0);
+      i64 lo, want;
+      segment(n_total, i64(P + q) * R - 1 + j, &lo, &want);
+      if (got != want)
+        throw std::runtime_error("global exchange: rank " + std::to_string(q) + " would receive " +
+                                 std::to_string(got) + " points in round " + std::to_string(j) +
+                                 " for a subtree of " + std::to_string(want));
+    }
+  plan->in_splits.assign(size_t(R), std::vector<i64>(size_t(P)));
+  plan->out_splits.assign(size_t(R), std::vector<i64>(size_t(P)));
+  plan->starts.assign(size_t(R) + 1, 0);
+  for (int j = 0; j < R; ++j) {
+    i64 tot = 0;
+    for (int p = 0; p < P; ++p) {
+      plan->in_splits[size_t(j)][size_t(p)] = at(me, j * P + p, 0);
+      plan->out_splits[size_t(j)][size_t(p)] = at(p, j * P + me, 0);
+      tot += at(me, j * P + p, 0);
+    }
+    plan->starts[size_t(j) + 1] = plan->starts[size_t(j)] + tot;
+  }
+  plan->src_base.resize(size_t(P));
+  plan->src_n.resize(size_t(P));
+  for (int p = 0; p < P; ++p) {
+    plan->src_base[size_t(p)] = at(p, 0, 2);
+    plan->src_n[size_t(p)] = at(p, 0, 3);
+  }
+  return 0;
+}
+
+}  // namespace global_plan
+
+using global_plan::segment;
+
+struct GlobalBuilder::Leaf {
+  i64 n;
+  int depth;
+  std::unique_ptr<GpuBuilder> b;
+  void* ws = nullptr;
+  ~Leaf() {
+    if (ws) (void)hipFree(ws);
+  }
+};
+
+GlobalBuilder::GlobalBuilder(Comm& comm, i64 n_total, int dim, int pipeline_k)
+    : comm_(comm), n_total_(n_total), dim_(dim), P_(comm.size()), rank_(comm.rank()) {
+  if (P_ < 1 || P_ > 64 || (P_ & (P_ - 1))) throw std::invalid_argument("global decomposition: P must be 2^k <= 64");
+  if (n_total >= (i64(1) << 32)) throw std::invalid_argument("point ids are 32-bit: at most 2^32 - 1 points");
+  if (dim < 1) throw std::invalid_argument("dim must be >= 1");
+  L_ = 0;
+  while ((1 << L_) < P_) ++L_;
+  k_ = pipeline_k >= 0 ? pipeline_k : (P_ == 2 ? 1 : 0);
+  k_ = std::max(0, std::min(k_, 6 - L_));  // at most 64 leaves (32 nodes per top level)
+  segment(n_total_, P_ - 1 + rank_, &slot_lo_, &n_leaf_);
+  PKD_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+}
+
+GlobalBuilder::~GlobalBuilder() {
+  for (auto& b : bufs_)
+    if (b.first) (void)hipFree(b.first);
+  if (tree_pts_) (void)hipFree(tree_pts_);
+  if (tree_ids_) (void)hipFree(tree_ids_);
+  if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
+}
+
+void* GlobalBuilder::buf(int slot, size_t bytes) {
+  if (bufs_.size() <= size_t(slot)) bufs_.resize(size_t(slot) + 1, {nullptr, 0});
+  auto& b = bufs_[size_t(slot)];
+  bytes = std::max<size_t>(bytes, 16);
+  if (b.second < bytes) {
+    if (b.first) PKD_HIP_CHECK(hipFree(b.first));
+    PKD_HIP_CHECK(hipMalloc(&b.first, bytes));
+    b.second = bytes;
+  }
+  return b.first;
+}
+
+GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth) {
+  for (auto& l : leaves_)
+    if (l->n == n && l->depth == depth) return *l->b;
+  auto l = std::make_unique<Leaf>();
+  l->n = n;
+  l->depth = depth;
+  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth});
+  PKD_HIP_CHECK(hipMalloc(&l->ws, std::max<size_t>(l->b->workspace_bytes(), 16)));
+  leaves_.push_back(std::move(l));
+  return *leaves_.back()->b;
+}
+
+std::vector<i64> GlobalBuilder::top_slots() const {
+  std::vector<i64> s(size_t(std::max(P_ - 1, 0)));
+  for (int h = 0; h < P_ - 1; ++h) {
+    i64 lo, n;
+    segment(n_total_, h, &lo, &n);
+    s[size_t(h)] = n > 0 ? lo + n / 2 : -1;
+  }
+  return s;
+}
+
+u32 GlobalBuilder::read_error(hipStream_t stream) const {
+  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  u32 e = 0;
+  if (bufs_.size() > 5 && bufs_[5].first) {
+    u32 w[4];
+    PKD_HIP_CHECK(hipMemcpy(w, bufs_[5].first, 16, hipMemcpyDeviceToHost));
+    e |= w[0] & 8u;
+  }
+  for (const auto& l : leaves_) e |= l->b->read_error(l->ws, stream);
+  return e;
+}
+
+void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_t s) {
+  const int dim = dim_, P = P_, LL = L_ + k_, R = 1 << k_, leaves = P << k_;
+  const TopPoints tp{pts, nullptr, n_local, dim, id_base};
+  global_plan::Plan plan;
+  float* top_rows = nullptr;
+  for (;;) {  // until no middle bucket overflows its all-gather slot
+    // 1. bounding box: one allreduce(MIN) of the encoded per-rank boxes
+    auto* box = static_cast<i64*>(buf(0, size_t(2 * dim) * 8));
+    std::vector<i64> init(size_t(2 * dim), i64(0xffffffffu));
+    PKD_HIP_CHECK(hipMemcpyAsync(box, init.data(), init.size() * 8, hipMemcpyHostToDevice, s));
+    top_bbox(tp, box, s);
+    comm_.allreduce_min_i64(box, size_t(2 * dim), s);
+    auto* cells = static_cast<float*>(buf(1, size_t(2 * leaves - 1) * dim * 2 * 4));
+    top_root_cell(box, dim, cells, s);
+    auto* node = static_cast<u32*>(buf(2, size_t(std::max<i64>(n_local, 1)) * 4));
+    auto* pivots = static_cast<u64*>(buf(3, size_t(std::max(leaves - 1, 1)) * 8));
+    PKD_HIP_CHECK(hipMemsetAsync(pivots, 0xff, size_t(std::max(leaves - 1, 1)) * 8, s));
+    top_rows = static_cast<float*>(buf(4, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4));
+    PKD_HIP_CHECK(hipMemsetAsync(top_rows, 0, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4, s));
+    auto* err = static_cast<u32*>(buf(5, 16));
+    PKD_HIP_CHECK(hipMemsetAsync(err, 0, 16, s));
+    auto* sel = static_cast<u32*>(buf(6, size_t(kTopMaxNodes) * 4 * 4));
+    auto* hist = static_cast<u32*>(buf(7, size_t(kTopBins) * 4));
+    // 2. top levels
+    for (int level = 0; level < LL; ++level) {
+      const int nodes = 1 << level, bins = kTopBins / nodes;
+      const int axis = level % dim, prev_axis = ((level - 1) % dim + dim) % dim;
+      TopSizes sizes{};
+      for (int j = 0; j < nodes; ++j) {
+        i64 lo;
+        segment(n_total_, nodes - 1 + j, &lo, &sizes.n[j]);
+      }
+      PKD_HIP_CHECK(hipMemsetAsync(hist, 0, size_t(nodes) * bins * 4, s));
+      top_route_hist(tp, node, level, pivots, prev_axis, axis, cells, bins, hist, s);
+      comm_.allreduce_sum_u32(hist, size_t(nodes) * bins, s);
+      top_select(hist, level, bins, sizes, sel, err, s);
+      const i64 cap = global_plan::middle_cap(n_total_, P, level, scale_);
+      const size_t words = top_middle_words(dim, cap);
+      auto* mid = static_cast<float*>(buf(8, words * 4));
+      top_collect(tp, node, level, axis, cells, bins, sel, mid, cap, s);
+      auto* gathered = static_cast<float*>(buf(9, size_t(P) * words * 4));
+      comm_.allgather(mid, gathered, words * 4, s);
+      top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err, s);
+    }
+    // 3. pack by destination slot (round j, rank r): 12-B rows + one bit per (row, slot)
+    const int last_axis = ((LL - 1) % dim + dim) % dim;
+    auto* send = static_cast<float*>(buf(10, size_t(std::max<i64>(n_local, 1)) * dim * 4));
+    auto* counts = static_cast<i64*>(buf(11, size_t(leaves) * 4 * 8));
+    std::vector<i64> hc(size_t(leaves) * 4, 0);
+    for (int d = 0; d < leaves; ++d) {
+      hc[size_t(d) * 4 + 2] = i64(id_base);
+      hc[size_t(d) * 4 + 3] = n_local;
+    }
+    PKD_HIP_CHECK(hipMemcpyAsync(counts, hc.data(), hc.size() * 8, hipMemcpyHostToDevice, s));
+    const i64 words = std::max<i64>(1, (n_local + 31) / 32);
+    auto* bm = static_cast<u32*>(buf(12, size_t(leaves) * words * 4));
+    void* scratch = buf(13, top_pack_scratch_bytes(n_local, leaves));
+    top_pack(tp, node, LL, pivots, last_axis, leaves, k_, send, dim, bm, words, counts, err, scratch, s);
+    // 4. the count matrix, all-gathered: the one host read-back of the build
+    auto* all = static_cast<i64*>(buf(14, size_t(P) * leaves * 4 * 8));
+    comm_.allgather(counts, all, size_t(leaves) * 4 * 8, s);
+    std::vector<i64> hall(size_t(P) * leaves * 4);
+    PKD_HIP_CHECK(hipMemcpyAsync(hall.data(), all, hall.size() * 8, hipMemcpyDeviceToHost, s));
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    if (global_plan::make_plan(hall, P, R, rank_, n_total_, &plan) == 0) break;
+    if (global_plan::middle_cap(n_total_, P, 0, scale_) >= n_total_)
+      throw std::runtime_error("global top levels: middle buckets inconsistent at full capacity");
+    scale_ *= 8;
+  }
+  top_rows_ = top_rows;  // buffer slot 4, exposed through top_rows()
+
+  // 5. my sub-tree: node P - 1 + rank at depth L; its 2^k leaves are the heap nodes
+  // first_leaf + j; the R - 1 pivots between them come from the replicated top rows
+  if (!tree_pts_) {
+    PKD_HIP_CHECK(hipMalloc(&tree_pts_, size_t(std::max<i64>(n_leaf_, 1)) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&tree_ids_, size_t(std::max<i64>(n_leaf_, 1)) * 4));
+  }
+  const i64 m = P - 1 + rank_;
+  const i64 first_leaf = (m + 1) * R - 1;
+  for (int lvl = 0; lvl < k_; ++lvl)
+    for (i64 h = (m + 1) * (i64(1) << lvl) - 1; h < (m + 2) * (i64(1) << lvl) - 1; ++h) {
+      i64 lo, n;
+      segment(n_total_, h, &lo, &n);
+      if (n <= 0) continue;
+      const i64 slot = lo + n / 2 - slot_lo_;
+      const float* row = top_rows_ + size_t(h) * (dim + 1);
+      PKD_HIP_CHECK(hipMemcpyAsync(tree_pts_ + slot * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
+      PKD_HIP_CHECK(hipMemcpyAsync(tree_ids_ + slot, row + dim, 4, hipMemcpyDeviceToDevice, s));
+    }
+  std::vector<i64> src_words(static_cast<size_t>(P)), bm_off(static_cast<size_t>(P));
+  i64 bm_total = 0;
+  for (int p = 0; p < P; ++p) {
+    src_words[size_t(p)] = std::max<i64>(1, (plan.src_n[size_t(p)] + 31) / 32);
+    bm_off[size_t(p)] = bm_total;
+    bm_total += src_words[size_t(p)];
+  }
+  const i64 send_words = std::max<i64>(1, (n_local + 31) / 32);
+  auto* send = static_cast<float*>(buf(10, 0));
+  auto* bm = static_cast<u32*>(buf(12, 0));
+  auto* err = static_cast<u32*>(buf(5, 16));
+  hipEvent_t packed, arrived[64];
+  PKD_HIP_CHECK(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
+  PKD_HIP_CHECK(hipEventRecord(packed, s));
+  PKD_HIP_CHECK(hipStreamWaitEvent(comm_stream_, packed, 0));
+  std::vector<float*> recv(static_cast<size_t>(R));
+  std::vector<u32*> recv_bm(static_cast<size_t>(R));
+  auto issue = [&](int j) {
+    i64 rows = 0;
+    for (int p = 0; p < P; ++p) rows += plan.out_splits[size_t(j)][size_t(p)];
+    recv[size_t(j)] = static_cast<float*>(buf(20 + 2 * j, size_t(std::max<i64>(rows, 1)) * dim * 4));
+    recv_bm[size_t(j)] = static_cast<u32*>(buf(21 + 2 * j, size_t(bm_total) * 4));
+    std::vector<size_t> sb(static_cast<size_t>(P)), so(sb), rb(sb), ro(sb);
+    i64 soff = plan.starts[size_t(j)], roff = 0;
+    for (int p = 0; p < P; ++p) {
+      sb[size_t(p)] = size_t(plan.in_splits[size_t(j)][size_t(p)]) * dim * 4;
+      so[size_t(p)] = size_t(soff) * dim * 4;
+      soff += plan.in_splits[size_t(j)][size_t(p)];
+      rb[size_t(p)] = size_t(plan.out_splits[size_t(j)][size_t(p)]) * dim * 4;
+      ro[size_t(p)] = size_t(roff) * dim * 4;
+      roff += plan.out_splits[size_t(j)][size_t(p)];
+    }
+    comm_.alltoallv(send, sb.data(), so.data(), recv[size_t(j)], rb.data(), ro.data(), comm_stream_);
+    for (int p = 0; p < P; ++p) {
+      sb[size_t(p)] = size_t(send_words) * 4;
+      so[size_t(p)] = size_t(i64(j) * P + p) * send_words * 4;
+      rb[size_t(p)] = size_t(src_words[size_t(p)]) * 4;
+      ro[size_t(p)] = size_t(bm_off[size_t(p)]) * 4;
+    }
+    comm_.alltoallv(bm, sb.data(), so.data(), recv_bm[size_t(j)], rb.data(), ro.data(), comm_stream_);
+    PKD_HIP_CHECK(hipEventCreateWithFlags(&arrived[j], hipEventDisableTiming));
+    PKD_HIP_CHECK(hipEventRecord(arrived[j], comm_stream_));
+  };
+  issue(0);
+  for (int j = 0; j < R; ++j) {
+    if (j + 1 < R) issue(j + 1);  // in flight while leaf j builds
+    PKD_HIP_CHECK(hipStreamWaitEvent(s, arrived[j], 0));
+    i64 lo_j, n_j;
+    segment(n_total_, first_leaf + j, &lo_j, &n_j);
+    if (n_j > 0) {
+      BmSources src{};
+      i64 off = 0;
+      for (int p = 0; p < P; ++p) {
+        src.off[p] = off;
+        src.cnt[p] = plan.out_splits[size_t(j)][size_t(p)];
+        off += src.cnt[p];
+        src.bm_off[p] = bm_off[size_t(p)];
+        src.words[p] = src_words[size_t(p)];
+        src.base[p] = u32(plan.src_base[size_t(p)]);
+      }
+      i64 max_words = 0;
+      for (int p = 0; p < P; ++p) max_words = std::max(max_words, src_words[size_t(p)]);
+      auto* lids = static_cast<u32*>(buf(15, size_t(n_j) * 4));
+      void* scr = buf(16, ids_from_bitmaps_scratch_bytes(max_words, P));
+      ids_from_bitmaps(recv_bm[size_t(j)], P, src, lids, scr, err, s);
+      GpuBuilder& b = leaf_builder(n_j, LL);
+      void* ws = nullptr;
+      for (auto& l : leaves_)
+        if (l->b.get() == &b) ws = l->ws;
+      const i64 a = lo_j - slot_lo_;
+      b.build(recv[size_t(j)], lids, 0, tree_pts_ + a * dim, tree_ids_ + a, ws, s);
+    }
+  }
+  for (int j = 0; j < R; ++j) (void)hipEventDestroy(arrived[j]);
+  (void)hipEventDestroy(packed);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Loopback communicator: ranks are threads; every collective stages through the host.
+namespace {
+
+struct Shared {
+  explicit Shared(int n) : size(n), slots(size_t(n)), sbytes(size_t(n)), soff(size_t(n)) {}
+  int size;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  long generation = 0;
+  std::vector<std::vector<char>> slots;            // each rank's staged bytes
+  std::vector<std::vector<size_t>> sbytes, soff;   // alltoallv: each rank's send layout
+
+  // A rank that fails stops arriving: the others give up after a deadline instead of hanging.
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const long gen = generation;
+    if (++arrived == size) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; })) {
+      throw std::runtime_error("loopback communicator: a rank did not reach the barrier within 120 s");
+    }
+  }
+};
+
+class ThreadComm final : public Comm {
+ public:
+  ThreadComm(std::shared_ptr<Shared> sh, int rank) : sh_(std::move(sh)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return sh_->size; }
+
+  void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
+    reduce<u32>(buf, count, s, [](u32 a, u32 b) { return a + b; });
+  }
+  void allreduce_min_i64(i64* buf, size_t count, hipStream_t s) override {
+    reduce<i64>(buf, count, s, [](i64 a, i64 b) { return std::min(a, b); });
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    stage(send, bytes, s);
+    std::vector<char> out(bytes * size_t(size()));
+    for (int r = 0; r < size(); ++r) std::memcpy(out.data() + size_t(r) * bytes, sh_->slots[size_t(r)].data(), bytes);
+    sh_->barrier();  // every rank has read every slot
+    if (bytes) PKD_HIP_CHECK(hipMemcpy(recv, out.data(), out.size(), hipMemcpyHostToDevice));
+  }
+  void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                 const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
+    size_t total = 0;
+    for (int p = 0; p < size(); ++p) total = std::max(total, send_off[p] + send_bytes[p]);
+    sh_->sbytes[size_t(rank_)].assign(send_bytes, send_bytes + size());
+    sh_->soff[size_t(rank_)].assign(send_off, send_off + size());
+    stage(send, total, s);
+    for (int p = 0; p < size(); ++p) {
+      const size_t n = sh_->sbytes[size_t(p)][size_t(rank_)];
+      if (n != recv_bytes[p]) throw std::runtime_error("loopback alltoallv: size mismatch");
+      if (n)
+        PKD_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + recv_off[p],
+                                sh_->slots[size_t(p)].data() + sh_->soff[size_t(p)][size_t(rank_)], n,
+                                hipMemcpyHostToDevice));
+    }
+    sh_->barrier();
+  }
+
+ private:
+  template <class T, class F>
+  void reduce(T* buf, size_t count, hipStream_t s, F f) {
+    stage(buf, count * sizeof(T), s);
+    std::vector<T> acc(count);
+    std::memcpy(acc.data(), sh_->slots[0].data(), count * sizeof(T));
+    for (int r = 1; r < size(); ++r) {
+      const T* v = reinterpret_cast<const T*>(sh_->slots[size_t(r)].data());
+      for (size_t i = 0; i < count; ++i) acc[i] = f(acc[i], v[i]);
+    }
+    sh_->barrier();
+    if (count) PKD_HIP_CHECK(hipMemcpy(buf, acc.data(), count * sizeof(T), hipMemcpyHostToDevice));
+  }
+  // my bytes -> my host slot; every slot is readable after the barrier
+  void stage(const void* dev, size_t bytes, hipStream_t s) {
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    auto& v = sh_->slots[size_t(rank_)];
+    v.resize(bytes);
+    if (bytes) PKD_HIP_CHECK(hipMemcpy(v.data(), dev, bytes, hipMemcpyDeviceToHost));
+    sh_->barrier();
+  }
+  std::shared_ptr<Shared> sh_;
+  int rank_;
+};
+
+}  // namespace
+
+std::vector<std::unique_ptr<Comm>> make_thread_comms(int size) {
+  auto sh = std::make_shared<Shared>(size);
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int r = 0; r < size; ++r) out.push_back(std::make_unique<ThreadComm>(sh, r));
+  return out;
+}
+
+}  // namespace pkdtree

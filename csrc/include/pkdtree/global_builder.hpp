@@ -1,0 +1,110 @@
+// Native global decomposition: ONE exact kd-tree over P ranks (one process or thread per GPU),
+// the C++ counterpart of parallel_kd_tree_amd/parallel/global_tree.py.
+//
+// The reference only splits its data into independent per-rank trees (kdtree_mpi.cpp:204-253).
+// Here the top log2(P) (+ k pipelining) levels are decided jointly: per level one
+// route+histogram pass, an allreduce(SUM) of the histogram, the median bucket per node, one
+// compaction pass, a fixed-size all-gather and a radix select of the exact pivot (the device
+// ops of dist_ops.hpp). Every point then travels to the rank that owns its top-level leaf --
+// 12-B rows plus one bit per (row, destination), ids rebuilt on the receiver -- in 2^k
+// all-to-all rounds, each on its own communication stream so round j + 1 is in flight while
+// leaf j builds. The result is slot for slot the tree one GPU builds on all points.
+//
+// Communication goes through the Comm interface: RCCL over xGMI in kdtree_dist, torch's RCCL
+// process group from Python, and an in-process loopback (threads sharing one GPU) for tests.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "pkdtree/common.hpp"
+
+namespace pkdtree {
+
+// Collectives used by the global builder. Buffers are device memory; every call is enqueued
+// on `stream` (the caller orders it after the data's producers) and completes in stream order.
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual void allreduce_sum_u32(u32* buf, size_t count, hipStream_t stream) = 0;
+  virtual void allreduce_min_i64(i64* buf, size_t count, hipStream_t stream) = 0;
+  // recv[r * bytes, (r + 1) * bytes) = send of rank r
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t stream) = 0;
+  // bytes and offsets per peer (send side: to peer r; receive side: from peer r)
+  virtual void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                         const size_t* recv_bytes, const size_t* recv_off, hipStream_t stream) = 0;
+};
+
+// Host-side geometry and planning (pure functions, unit-tested on the CPU).
+namespace global_plan {
+// (lo, n) of heap node h in the implicit tree of n_total points.
+void segment(i64 n_total, i64 h, i64* lo, i64* n);
+// Middle-bucket rows a rank may contribute at `level` (identical on every rank).
+i64 middle_cap(i64 n_total, int P, int level, int scale);
+// Exchange plan from the all-gathered per-slot counts [P][R * P][4] (rows, err, id base,
+// n_local), slots ordered (round j, rank r). Returns 0 (ok), 1 (a middle bucket overflowed:
+// retry with larger slots) or throws on inconsistent geometry. Fills per round j the rows to
+// send to / receive from every rank, and the source id bases / local sizes.
+struct Plan {
+  std::vector<std::vector<i64>> in_splits, out_splits;  // [R][P]
+  std::vector<i64> starts;                               // [R + 1] send-buffer row offsets
+  std::vector<i64> src_base, src_n;                      // [P]
+};
+int make_plan(const std::vector<i64>& counts, int P, int R, int me, i64 n_total, Plan* plan);
+}  // namespace global_plan
+
+class GpuBuilder;
+
+class GlobalBuilder {
+ public:
+  // pipeline_k < 0: 1 at P = 2, else 0 (the exchange only dominates at two ranks)
+  GlobalBuilder(Comm& comm, i64 n_total, int dim, int pipeline_k = -1);
+  ~GlobalBuilder();
+  GlobalBuilder(const GlobalBuilder&) = delete;
+  GlobalBuilder& operator=(const GlobalBuilder&) = delete;
+
+  // This rank's points [n_local][dim] (device), ids id_base + row (the reference's global
+  // 1-based ids are first_row + 1 + row). Synchronises once (the exchange plan).
+  void build(const float* pts, i64 n_local, u32 id_base, hipStream_t stream);
+
+  // This rank's share of the tree: slots [slot_lo, slot_lo + n_leaf) of the global in-order
+  // tree (device rows / ids), at depth log2(P) of the global tree.
+  i64 slot_lo() const { return slot_lo_; }
+  i64 n_leaf() const { return n_leaf_; }
+  int top_levels() const { return L_; }
+  const float* tree_pts() const { return tree_pts_; }
+  const u32* tree_ids() const { return tree_ids_; }
+  // The P - 1 replicated top pivots, heap order: rows of dim + 1 floats (coordinates, id
+  // bits) on the device, and their global slots (-1: empty node).
+  const float* top_rows() const { return top_rows_; }
+  std::vector<i64> top_slots() const;
+  // OR of the device error words of the last build (0 = ok). Synchronises `stream`.
+  u32 read_error(hipStream_t stream) const;
+
+ private:
+  void* buf(int slot, size_t bytes);
+  GpuBuilder& leaf_builder(i64 n, int depth);
+
+  Comm& comm_;
+  i64 n_total_;
+  int dim_, P_, rank_, L_, k_;
+  i64 slot_lo_ = 0, n_leaf_ = 0;
+  int scale_ = 1;
+  float* tree_pts_ = nullptr;
+  u32* tree_ids_ = nullptr;
+  float* top_rows_ = nullptr;
+  hipStream_t comm_stream_ = nullptr;
+  std::vector<std::pair<void*, size_t>> bufs_;
+  struct Leaf;
+  std::vector<std::unique_ptr<Leaf>> leaves_;
+};
+
+// In-process loopback communicator: `size` ranks are threads of one process (sharing one GPU
+// or not); collectives stage through the host and meet at a barrier. For tests of the P > 1
+// orchestration without several GPUs.
+std::vector<std::unique_ptr<Comm>> make_thread_comms(int size);
+
+}  // namespace pkdtree

@@ -30,6 +30,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp"]
 CORE_HIP = ["gpu/build_global.hip", "gpu/build_subtree.hip", "gpu/subtree_wave.hip", "gpu/query.hip",
             "gpu/dist_ops.hip", "gpu/generator.hip"]
+HOST_HIP = ["cpu/global_builder.cpp"]  # host C++ on the HIP runtime (no device code)
 BIND = ["bind/torch_bindings.cpp", "bind/dist_bindings.cpp"]
 CLI_CPU = {"kdtree_sequential": ["cli/kdtree_sequential.cpp"]}
 CLI_GPU = {"kdtree_gpu": ["cli/kdtree_gpu.cpp"], "kdtree_dist": ["cli/kdtree_dist.cpp"]}
@@ -126,16 +127,17 @@ def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, j
     Every output carries a signature (``<output>.sig``) of everything it was built from; an
     output whose signature matches is kept without looking at (or needing) its objects."""
     hdr = _hdr_digest()
-    tflags, tld = _torch_flags() if with_ext else ([], [])
     hipflags = [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
+    tflags, tld = _torch_flags() if with_ext else ([], [])
     flags = {s: [] for s in CORE_CPU + CORE_HIP}
+    flags.update({s: hipflags for s in HOST_HIP})
     if with_ext:
         flags.update({s: tflags for s in BIND})
     if with_cli:
         flags.update({s: [] for v in CLI_CPU.values() for s in v})
         flags.update({s: hipflags for v in CLI_GPU.values() for s in v if (CSRC / s).exists()})
     osig = {s: _obj_sig(s, fl, hdr) for s, fl in flags.items()}
-    core_cpu, core = CORE_CPU, CORE_CPU + CORE_HIP
+    core_cpu, core = CORE_CPU, CORE_CPU + CORE_HIP + HOST_HIP
     # outputs: (path, object sources, link command tail)
     outs = {}
     if with_ext:

@@ -83,3 +83,12 @@ def test_reference_mode_byte_parity(bin_dir, ref_binary, cfg):
     strip = lambda s: [l for l in s.splitlines() if not l.startswith("elapsed time")]
     assert strip(a.stdout) == strip(b.stdout)
     assert a.stderr == b.stderr
+
+
+@pytest.mark.parametrize("flag", [["--queries", "25"], ["--queries=25"]])
+def test_queries_option(bin_dir, flag):
+    """--queries is its own option (not read as a malformed --query)."""
+    r = run(bin_dir / "kdtree_sequential", [*flag, "--query", "brute", 4, 3, 5000])
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[1:26] == oracle_lines(4, 3, 5000, 25) and lines[26].startswith("elapsed time ")

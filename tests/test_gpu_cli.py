@@ -50,3 +50,22 @@ def test_eval_mode_matches_reference_fixture(bin_dir, exe, seed):
     fix = (Path(__file__).parent / "fixtures" / f"ref_eval_seed{seed}.txt").read_text().splitlines()
     args = ["--gpus", 1] if exe == "kdtree_dist" else []
     assert out(bin_dir / exe, args, stdin=f"{seed}\n") == fix
+
+
+@pytest.mark.parametrize("k", [0, 2])
+@pytest.mark.parametrize("cfg", [(42, 3, 1024), (3, 8, 200000), (9, 3, 1_000_003), (5, 128, 20000)])
+def test_dist_cli_global_one_rank(bin_dir, cfg, k):
+    """kdtree_dist --decomp global (native GlobalBuilder over RCCL: allreduce, allgather and
+    grouped send/recv run for real with one rank; --pipeline-k 2 exchanges in 4 rounds and
+    builds 4 leaves) prints the same lines as the CPU executable."""
+    args = ["--gpus", 1, "--decomp", "global", "--pipeline-k", k, *cfg]
+    assert out(bin_dir / "kdtree_dist", args) == out(bin_dir / "kdtree_sequential", cfg)
+
+
+def test_dist_cli_global_metrics_and_queries(bin_dir):
+    r = subprocess.run([str(bin_dir / "kdtree_dist"), "--gpus", "1", "--decomp=global", "--metrics-json",
+                        "--queries", "300", "11", "4", "100000"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if not l.startswith("elapsed time")]
+    assert lines == out(bin_dir / "kdtree_sequential", ["--queries", 300, 11, 4, 100000])
+    assert len(lines) == 301 and '"decomp": "global"' in r.stderr
