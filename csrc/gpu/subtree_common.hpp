@@ -57,5 +57,8 @@ __device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
 // this (dim, nmax); false -> the caller falls back to the per-level ranking kernel.
 bool subtree_wave_enabled();
 bool launch_subtree_wave(const subtree_detail::SubArgs& a, i64 segs, int nmax, hipStream_t stream);
+// Cross-check kernel of subtree_hist.hip (PKD_SUBTREE_IMPL=hist).
+size_t subtree_hist_lds_bytes(int dim, int nm);
+void launch_subtree_hist(const subtree_detail::SubArgs& a, i64 segs, int nmax, hipStream_t stream);
 
 }  // namespace pkdtree

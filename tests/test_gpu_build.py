@@ -204,6 +204,14 @@ def test_wave_subtree_kernel_duplicates(gpu_device, monkeypatch):
     check_same(torch.zeros(30_000, 2), gpu_device)
 
 
+@pytest.mark.parametrize("dim,n", [(3, 1_000_000), (8, 300_000), (2, 50_001), (16, 100_000)])
+def test_hist_subtree_kernel(gpu_device, monkeypatch, dim, n):
+    """The cross-check histogram-partition subtree kernel (csrc/gpu/subtree_hist.hip,
+    PKD_SUBTREE_IMPL=hist; also turns the narrow-column path off) builds the same tree."""
+    monkeypatch.setenv("PKD_SUBTREE_IMPL", "hist")
+    check_same(pk.generate_problem(dim + n % 7, dim, n), gpu_device)
+
+
 def test_nearest_neighbor_no_tree_copy(gpu_device, monkeypatch):
     """KDTree.nearest_neighbor / Node on a 10 M GPU tree: the id -> slot lookup runs on the
     device and a Node reads one row; the whole tree never crosses to the host (any device ->
