@@ -356,7 +356,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restr
   const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const u32 first = u32(P - 1);
   for (i64 i = b0 + threadIdx.x; i < b1; i += kBlock) {
-    const u32 h = route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots);
+    // levels == 0 (one rank, no pipelining): every point stays at the root's single leaf
+    const u32 h = levels > 0 ? route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots) : 0u;
     node[i] = h;
     if (h != kTopDone) atomicAdd(&cnt[dest_slot(h - first, P, pipe_k)], 1u);
   }

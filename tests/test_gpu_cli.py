@@ -68,4 +68,4 @@ def test_dist_cli_global_metrics_and_queries(bin_dir):
     assert r.returncode == 0, r.stderr
     lines = [l for l in r.stdout.splitlines() if not l.startswith("elapsed time")]
     assert lines == out(bin_dir / "kdtree_sequential", ["--queries", 300, 11, 4, 100000])
-    assert len(lines) == 301 and '"decomp": "global"' in r.stderr
+    assert len(lines) == 302 and '"decomp": "global"' in r.stderr
