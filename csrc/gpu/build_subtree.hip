@@ -77,8 +77,9 @@ size_t lds_words_narrow(int dim, int nm, int ldim) {
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
 // m <= CMAX * THREADS. Fixed-trip predicated loops and a shuffle reduction of the wave
 // totals: no per-lane loop bounds, so no exec-mask juggling on the (shared) scalar unit.
+// Branch-free per lane: out-of-range entries are read from v[0] and written to v[dummy].
 template <int THREADS, int CMAX>
-__device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
+__device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum, u32 dummy) {
   constexpr int W = THREADS / 64;
   const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
   const int C = (m + THREADS - 1) / THREADS;
@@ -86,21 +87,25 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum) {
   u32 x[CMAX], s = 0;
 #pragma unroll
   for (int j = 0; j < CMAX; ++j) {
-    const bool in = j < C && b0 + j < m;
-    x[j] = in ? v[in ? b0 + j : 0] : 0u;
+    const bool in = (j < C) & (b0 + j < m);
+    const u32 val = v[in ? b0 + j : 0];
+    x[j] = in ? val : 0u;
     s += x[j];
   }
   const u32 incl = dev::wave_incl_scan(s);
   if (ln == 63) wsum[w] = incl;
   __syncthreads();
   // prefix of the wave totals: inclusive scan of wsum over lanes, read at lane w - 1
-  const u32 pin = dev::wave_incl_scan(ln < W ? wsum[ln < W ? ln : 0] : 0u);
-  const u32 pw = w > 0 ? u32(__builtin_amdgcn_readlane(int(pin), w - 1)) : 0u;
+  const u32 ws = wsum[ln & (W - 1)];
+  const u32 pin = dev::wave_incl_scan(ln < W ? ws : 0u);
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: a scalar select, no exec juggling
+  const u32 pl = u32(__builtin_amdgcn_readlane(int(pin), wu > 0 ? wu - 1 : 0));
+  const u32 pw = wu > 0 ? pl : 0u;
   u32 run = pw + incl - s;
 #pragma unroll
   for (int j = 0; j < CMAX; ++j) {
-    const bool in = j < C && b0 + j < m;
-    if (in) v[b0 + j] = run;
+    const bool in = (j < C) & (b0 + j < m);
+    v[in ? u32(b0 + j) : dummy] = run;
     run += x[j];
   }
   if (tid == THREADS - 1) v[m] = run;
@@ -211,10 +216,15 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       }
     }
   }
+  // The per-item code of the levels is branch-free: finished or absent points compute on
+  // harmless values, loads use clamped indices and stores of such points go to per-lane dummy
+  // words. Per-item branches cost three scalar instructions each (exec save / branch /
+  // restore) on the CU's one scalar unit, which bounded the kernel (SALU = 0.76 x VALU,
+  // profiles/r2_subtree_pmc.txt).
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
     const int k = tid + i * THREADS;
-    if (k < n) fin[k] = 0xffffffffu;
+    fin[k < n ? u32(k) : u32(NM) + lane_dummy] = 0xffffffffu;
   }
   u32 lo[ITEMS], nn[ITEMS], sg[ITEMS];
 #pragma unroll
@@ -240,11 +250,13 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
     u32 rank[ITEMS];
     if (Wt > 0) {
       // ---- compressed ranks: one bitmap of Wt words per sub-segment ----
-      const int nw = S * Wt;
-      for (int w = tid; w < nw; w += THREADS) work[w] = 0;
+      const int nw = S * Wt;  // <= NM
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const int w = tid + j * THREADS;
+        work[w < nw ? u32(w) : dummy] = 0;
+      }
       __syncthreads();
-      // Branch-free (the scalar unit, shared by the CU's four SIMDs, is the bottleneck of
-      // exec-mask juggling): finished points OR 0 into a private dummy word per lane.
       u32 c[ITEMS], wi[ITEMS];
       if (wlive) {
         if (ITEMS == 2) {
@@ -257,29 +269,35 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
-          wi[i] = nn[i] ? sg[i] * Wt + (c[i] >> 5) : dummy;
-          atomicOr(&work[wi[i]], nn[i] ? 1u << (c[i] & 31) : 0u);
+          const u32 wv = sg[i] * u32(Wt) + (c[i] >> 5);
+          const u32 bit = 1u << (c[i] & 31);
+          wi[i] = nn[i] ? wv : dummy;
+          atomicOr(&work[wi[i]], nn[i] ? bit : 0u);
         }
       }
       __syncthreads();
       if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
-        const int g = dev::lane() & (Wt - 1);
+        const u32 g = lane_dummy & u32(Wt - 1);
         for (int w0 = 0; w0 < nw; w0 += THREADS) {
           const int w = w0 + tid;
-          const u32 v = w < nw ? u32(__popc(work[w])) : 0u;
+          const bool in = w < nw;
+          const u32 pc = u32(__popc(work[in ? w : 0]));
+          const u32 v = in ? pc : 0u;
           u32 incl = v;
           for (int o = 1; o < Wt; o <<= 1) {
             const u32 tt = __shfl_up(incl, o, 64);
-            if (g >= o) incl += tt;
+            incl += g >= u32(o) ? tt : 0u;
           }
-          if (w < nw) aux[w] = incl - v;
+          aux[in ? u32(w) : u32(NM) + lane_dummy] = incl - v;
         }
         __syncthreads();
       }
       if (wlive) {
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-          rank[i] = (Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u) + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
+        for (int i = 0; i < ITEMS; ++i) {
+          const u32 below = Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u;
+          rank[i] = below + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
+        }
       }
     } else {
       // ---- exact ranks from bucket histograms (first use of the axis) ----
@@ -289,12 +307,12 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       // About one point per bucket (S * B <= NM): most buckets need no comparison at all.
       const int maxsize = n >> t;
       const int B = maxsize > rk::kSmallSeg ? int(rk::pow2_ceil(u32(maxsize))) : 1;
-      const int nb = S * B;
-      u32* tmpk = aux;  // orderable keys in bucket order
+      const int nb = S * B;  // <= NM; work[nb] is the scan's total (sentinel)
+      u32* tmpk = aux;       // orderable keys in bucket order
 #pragma unroll
       for (int j = 0; j <= ITEMS; ++j) {
         const int w = tid + j * THREADS;
-        if (w <= nb) work[w] = 0;
+        work[w <= nb ? u32(w) : dummy] = 0;
       }
       const BucketParams pr = make_params(cellv[2 * axis], cellv[2 * axis + 1], B);
       __syncthreads();
@@ -306,20 +324,22 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         for (int i = 0; i < ITEMS; ++i) {  // finished points count into a per-lane dummy word
           const float kf = kcol[kid(i)];
           ok[i] = orderable(kf);
-          bk[i] = nn[i] ? sg[i] * B + (B > 1 ? bucket_of(kf, pr, B) : 0u) : dummy;
+          const u32 b = sg[i] * u32(B) + (B > 1 ? bucket_of(kf, pr, B) : 0u);
+          bk[i] = nn[i] ? b : dummy;
           wi[i] = atomicAdd(&work[bk[i]], 1u);
         }
       }
       __syncthreads();
       if (t == 0) stamp(a, 21);
-      rk::block_excl_scan<THREADS, ITEMS>(work, nb, wsum);
+      rk::block_excl_scan<THREADS, ITEMS>(work, nb, wsum, dummy);
       __syncthreads();
       if (t == 0) stamp(a, 22);
       u32 pos[ITEMS];
       if (wlive) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
-          pos[i] = nn[i] ? work[bk[i]] + wi[i] : u32(NM) + lane_dummy;
+          const u32 p = work[bk[i]] + wi[i];
+          pos[i] = nn[i] ? p : u32(NM) + lane_dummy;
           tmpk[pos[i]] = ok[i];
           tmpi[pos[i]] = u16(kid(i));
         }
@@ -331,32 +351,37 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
           const u32 bi = nn[i] ? bk[i] : 0u;
-          st[i] = work[bi];
-          const u32 en = nn[i] ? work[bi + 1] : st[i];
-          cnt[i] = en - st[i];
-          rank[i] = st[i] - work[nn[i] ? sg[i] * B : 0u];
+          const u32 sb = nn[i] ? sg[i] * u32(B) : 0u;
+          const u32 s0 = work[bi], e0 = work[bi + 1], b0 = work[sb];
+          st[i] = s0;
+          cnt[i] = e0 - s0;  // 0 for finished points (bucket 0 stands in: its count is not theirs)
+          cnt[i] = nn[i] ? cnt[i] : 0u;
+          rank[i] = s0 - b0;
         }
         // in-bucket comparisons, kU members per round: all items' reads of a round are issued
         // together; wave-uniform trip count = largest bucket among the wave's items / kU
         constexpr u32 kU = 2;
         for (u32 j0 = 0;; j0 += kU) {
-          bool any = false;
+          u32 any = 0;
 #pragma unroll
-          for (int i = 0; i < ITEMS; ++i) any |= j0 < cnt[i];
+          for (int i = 0; i < ITEMS; ++i) any |= u32(j0 < cnt[i]);
           if (!__ballot(any)) break;
           u32 qk[kU][ITEMS];
 #pragma unroll
           for (u32 u = 0; u < kU; ++u)
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i) qk[u][i] = tmpk[j0 + u < cnt[i] ? st[i] + j0 + u : 0u];
-          bool tany = false;
+            for (int i = 0; i < ITEMS; ++i) {
+              const u32 q = st[i] + j0 + u;
+              qk[u][i] = tmpk[j0 + u < cnt[i] ? q : 0u];
+            }
+          u32 tany = 0;
 #pragma unroll
           for (u32 u = 0; u < kU; ++u)
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
-              const bool act = j0 + u < cnt[i];
-              rank[i] += (act && qk[u][i] < ok[i]) ? 1u : 0u;
-              tany |= act && qk[u][i] == ok[i] && st[i] + j0 + u != pos[i];
+              const u32 act = u32(j0 + u < cnt[i]);
+              rank[i] += act & u32(qk[u][i] < ok[i]);
+              tany |= act & u32(qk[u][i] == ok[i]) & u32(st[i] + j0 + u != pos[i]);
             }
           if (__ballot(tany)) {  // equal keys: the id decides
 #pragma unroll
@@ -364,8 +389,9 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
 #pragma unroll
               for (int i = 0; i < ITEMS; ++i) {
                 const u32 q = st[i] + j0 + u;
-                const bool tie = j0 + u < cnt[i] && qk[u][i] == ok[i] && q != pos[i];
-                rank[i] += (tie && idrow[tmpi[tie ? q : 0u]] < idrow[kid(i)]) ? 1u : 0u;
+                const u32 tie = u32(j0 + u < cnt[i]) & u32(qk[u][i] == ok[i]) & u32(q != pos[i]);
+                const u32 other = idrow[tmpi[tie ? q : 0u]];
+                rank[i] += tie & u32(other < idrow[kid(i)]);
               }
           }
         }
@@ -379,14 +405,17 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 n0 = nn[i], mid = n0 >> 1, r = rank[i];
-        const bool is_mid = n0 != 0 && r == mid;
-        const bool right = r > mid;
-        fin[is_mid ? lo[i] + mid : u32(NM) + lane_dummy] = u32(kid(i));
-        cn[i] = right ? r - mid - 1 : r;
+        const u32 is_mid = u32(n0 != 0) & u32(r == mid);
+        const u32 right = u32(r > mid);
+        const u32 fslot = lo[i] + mid, rr = r - mid - 1, lr = lo[i] + mid + 1, nr = n0 - mid - 1;
+        fin[is_mid ? fslot : u32(NM) + lane_dummy] = u32(kid(i));
+        cn[i] = right ? rr : r;
         if (keep && ITEMS != 2) cr[tid + i * THREADS] = u16(cn[i]);
-        lo[i] = right ? lo[i] + mid + 1 : lo[i];
-        sg[i] = 2 * sg[i] + (right ? 1u : 0u);
-        nn[i] = (n0 == 0 || is_mid) ? 0u : (right ? n0 - mid - 1 : mid);
+        lo[i] = right ? lr : lo[i];
+        sg[i] = 2 * sg[i] + right;
+        const u32 nc = right ? nr : mid;
+        nn[i] = is_mid ? 0u : nc;  // n0 == 0 gives nc == 0 as well (mid 0, right only if r > 0 -> nr wraps)
+        nn[i] = n0 ? nn[i] : 0u;
       }
       if (keep && ITEMS == 2) reinterpret_cast<u32*>(cr)[tid] = (cn[0] & 0xffffu) | (cn[ITEMS - 1] << 16);
     }

@@ -38,8 +38,11 @@ __device__ __forceinline__ void wave_sync() {
 constexpr int kStampSlots = 32;
 constexpr int kStampBlocks = 4096;
 // slot 0 start, 1 rows loaded, 2 + t after level t (rank kernel), 30 before the store, 31 end
+// The pointer test is a kernel argument (scalar branch): with stamps off no wave touches its
+// exec mask here.
 __device__ __forceinline__ void stamp(const SubArgs& a, int i) {
-  if (a.stamps && threadIdx.x == 0 && blockIdx.x < kStampBlocks)
+  // wave 0 stores (every lane the same value to the same word): a wave-uniform condition
+  if (a.stamps != nullptr && blockIdx.x < kStampBlocks && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64)
     a.stamps[blockIdx.x * kStampSlots + i] = __builtin_amdgcn_s_memtime();
 }
 
