@@ -56,6 +56,13 @@ def _parse(argv=None):
                     help="cpu: run the same control flow on host tensors over gloo (launcher / CI check; "
                          "timings meaningless)")
     ap.add_argument("--no-check", action="store_true", help="skip the untimed correctness check of the last tree")
+    ap.add_argument("--decomp", choices=["auto", "single", "global"], default="auto",
+                    help="auto: one GPU builds alone, N > 1 GPUs build one global tree; global also at N = 1 "
+                         "(the multi-GPU code path on one rank)")
+    ap.add_argument("--impl", choices=["native", "python"], default="native",
+                    help="global decomposition: native C++ builder on its own RCCL communicator, or the Python "
+                         "orchestration over torch.distributed (host tensors always use the latter)")
+    ap.add_argument("--pipeline-k", type=int, default=-1, help="global: 2^k exchange rounds (-1: auto)")
     return ap.parse_args(argv)
 
 
@@ -173,9 +180,20 @@ def main(argv=None):
         x = pk.uniform_points(count, dim, seed=args.seed * 1000 + rank, device=dev)
 
     sync = (lambda: None) if cpu else torch.cuda.synchronize
-    if world > 1:
-        from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
-        builder = GlobalTreeBuilder(n, dim, device=dev)
+    distributed = world > 1 or args.decomp == "global"
+    if args.decomp == "single" and world > 1:
+        sys.exit("bench.py: --decomp single needs --gpus 1")
+    if world == 1 and distributed and (cpu or args.impl != "native"):
+        sys.exit("bench.py: --decomp global on one rank runs the native builder (GPU, --impl native)")
+    if distributed:
+        if args.impl == "native" and not cpu:
+            from parallel_kd_tree_amd.parallel.native_global import NativeGlobalBuilder
+            builder = NativeGlobalBuilder(n, dim, dev, pipeline_k=args.pipeline_k)
+        else:
+            from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
+            if args.pipeline_k >= 0:
+                os.environ["PKD_PIPELINE_K"] = str(args.pipeline_k)
+            builder = GlobalTreeBuilder(n, dim, device=dev)
         res = {}
 
         def step():
@@ -214,7 +232,7 @@ def main(argv=None):
 
     # ---- untimed: the last build's tree must be right --------------------------------
     problem = ""
-    if world > 1:
+    if distributed:
         err = builder.read_error() if not cpu else 0
         t = res["t"]
         if err:
@@ -225,7 +243,8 @@ def main(argv=None):
             problem = _check_tree(t.tree_pts, t.tree_ids, (world - 1).bit_length(), 1, n + 1, permutation=False)
             idl = t.tree_ids.to(torch.int64) & 0xFFFFFFFF
             stats = torch.tensor([idl.numel(), int(idl.sum()) if idl.numel() else 0], dtype=torch.int64, device=dev)
-            comm.all_reduce_(stats)
+            if world > 1:
+                comm.all_reduce_(stats)
             top_ids = [int(t.top_rows[i, dim:].contiguous().view(torch.int32).item()) & 0xFFFFFFFF
                        for i, s in enumerate(t.top_slots) if s >= 0]
             cnt, tot = int(stats[0]) + len(top_ids), int(stats[1]) + sum(top_ids)
@@ -270,7 +289,9 @@ def main(argv=None):
                     if args.data.startswith("reference") else "synthetic: on-device uniform(-100,100), reference value map",
             "config": {"model": "exact median-split kd-tree, cycling axis (implicit in-order layout)",
                        "global_batch": n, "seq_len": dim, "n_points": n, "dim": dim,
-                       "parallelism": f"global{world}" if world > 1 else "single",
+                       "parallelism": f"global{world}" if distributed else "single",
+                       "impl": ("native" if args.impl == "native" and not cpu else "python") if distributed
+                       else "native",
                        "device": "cpu (gloo rehearsal)" if cpu else "MI355X",
                        "tree_checked": not args.no_check},
         }), flush=True)

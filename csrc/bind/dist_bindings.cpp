@@ -10,6 +10,7 @@
 #include "pkdtree/dist_ops.hpp"
 #include "pkdtree/global_builder.hpp"
 #include "pkdtree/hip_check.hpp"
+#include "pkdtree/rccl_comm.hpp"
 
 #include <cstring>
 #include <exception>
@@ -229,9 +230,98 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::T
   return {tp, ti, int64_t(e)};
 }
 
+// The native global builder on its own RCCL communicator, one per process (rank). The
+// communicator's unique id comes from rank 0 (rccl_unique_id) and reaches the other ranks
+// through the Python process group; then no Python runs between the collectives of a build.
+class NativeGlobal {
+ public:
+  NativeGlobal(int64_t n_total, int64_t dim, int64_t rank, int64_t world, const std::string& uid,
+               int64_t pipeline_k, int64_t device)
+      : dim_(int(dim)), rank_(int(rank)), world_(int(world)), device_(int(device)) {
+    TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "rccl unique id: ", sizeof(ncclUniqueId), " bytes expected");
+    TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rank out of range");
+    PKD_HIP_CHECK(hipSetDevice(device_));
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    nccl_check(ncclCommInitRank(&c_, world_, id, rank_), "ncclCommInitRank", rank_);
+    comm_ = std::make_unique<RcclComm>(c_, rank_, world_);
+    gb_ = std::make_unique<GlobalBuilder>(*comm_, n_total, dim_, int(pipeline_k));
+  }
+  ~NativeGlobal() {
+    gb_.reset();
+    comm_.reset();
+    if (c_) (void)ncclCommDestroy(c_);
+  }
+  NativeGlobal(const NativeGlobal&) = delete;
+  NativeGlobal& operator=(const NativeGlobal&) = delete;
+
+  void build(const torch::Tensor& x, int64_t id_base) {
+    check_cuda(x, torch::kFloat32, "points");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == dim_, "points must be [n, dim]");
+    TORCH_CHECK(x.device().index() == device_, "points must live on the builder's device");
+    const c10::DeviceGuard g(x.device());
+    const hipStream_t s = stream_of(x);
+    const float* p = x.data_ptr<float>();
+    const int64_t n = x.size(0);
+    pybind11::gil_scoped_release nogil;  // the exchange plan blocks on the other ranks
+    gb_->build(p, n, u32(id_base), s);
+  }
+  // views of the builder's buffers (valid until the next build / the builder's end)
+  torch::Tensor tree_pts() const {
+    return torch::from_blob(const_cast<float*>(gb_->tree_pts()), {gb_->n_leaf(), dim_}, opts(torch::kFloat32));
+  }
+  torch::Tensor tree_ids() const {
+    return torch::from_blob(const_cast<u32*>(gb_->tree_ids()), {gb_->n_leaf()}, opts(torch::kInt32));
+  }
+  torch::Tensor top_rows() const {
+    return torch::from_blob(const_cast<float*>(gb_->top_rows()), {world_ - 1, dim_ + 1}, opts(torch::kFloat32));
+  }
+  std::vector<int64_t> top_slots() const {
+    const auto v = gb_->top_slots();
+    return std::vector<int64_t>(v.begin(), v.end());
+  }
+  int64_t slot_lo() const { return gb_->slot_lo(); }
+  int64_t n_leaf() const { return gb_->n_leaf(); }
+  int64_t top_levels() const { return gb_->top_levels(); }
+  int64_t read_error() const {
+    const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
+    return int64_t(gb_->read_error(c10::hip::getCurrentHIPStream(device_).stream()));
+  }
+
+ private:
+  torch::TensorOptions opts(torch::ScalarType t) const {
+    return torch::TensorOptions().dtype(t).device(torch::kCUDA, device_);
+  }
+  int dim_, rank_, world_, device_;
+  ncclComm_t c_ = nullptr;
+  std::unique_ptr<RcclComm> comm_;
+  std::unique_ptr<GlobalBuilder> gb_;
+};
+
+pybind11::bytes rccl_unique_id() {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId", 0);
+  return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
 }  // namespace
 
 void bind_dist_ops(pybind11::module& m) {
+  m.def("rccl_unique_id", &rccl_unique_id);
+  pybind11::class_<NativeGlobal>(m, "NativeGlobal")
+      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, const std::string&, int64_t, int64_t>(),
+           pybind11::arg("n_total"), pybind11::arg("dim"), pybind11::arg("rank"), pybind11::arg("world"),
+           pybind11::arg("uid"), pybind11::arg("pipeline_k") = -1, pybind11::arg("device") = 0,
+           pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("build", &NativeGlobal::build, pybind11::arg("x"), pybind11::arg("id_base"))
+      .def("tree_pts", &NativeGlobal::tree_pts)
+      .def("tree_ids", &NativeGlobal::tree_ids)
+      .def("top_rows", &NativeGlobal::top_rows)
+      .def("top_slots", &NativeGlobal::top_slots)
+      .def("slot_lo", &NativeGlobal::slot_lo)
+      .def("n_leaf", &NativeGlobal::n_leaf)
+      .def("top_levels", &NativeGlobal::top_levels)
+      .def("read_error", &NativeGlobal::read_error);
   m.def("global_plan", &plan_py);
   m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,
         pybind11::call_guard<pybind11::gil_scoped_release>());

@@ -49,6 +49,7 @@
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
 #include "pkdtree/hip_check.hpp"
+#include "pkdtree/rccl_comm.hpp"
 
 using namespace pkdtree;
 
@@ -68,44 +69,6 @@ struct Config {
   int seed, dim, num_points;
 };
 
-// The global builder's collectives on RCCL: allreduce / allgather as single calls, the
-// all-to-all-v as one grouped set of point-to-point sends and receives (xGMI links are
-// point-to-point; the self part is a device copy).
-class RcclComm final : public Comm {
- public:
-  RcclComm(ncclComm_t c, int rank, int size) : c_(c), rank_(rank), size_(size) {}
-  int rank() const override { return rank_; }
-  int size() const override { return size_; }
-  void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
-    PKD_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, c_, s));
-  }
-  void allreduce_min_i64(i64* buf, size_t count, hipStream_t s) override {
-    PKD_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclMin, c_, s));
-  }
-  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    PKD_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, c_, s));
-  }
-  void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
-                 const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
-    const char* sp = static_cast<const char*>(send);
-    char* rp = static_cast<char*>(recv);
-    if (send_bytes[rank_] != recv_bytes[rank_]) throw std::runtime_error("alltoallv: self size mismatch");
-    if (send_bytes[rank_])
-      PKD_HIP_CHECK(hipMemcpyAsync(rp + recv_off[rank_], sp + send_off[rank_], send_bytes[rank_],
-                                   hipMemcpyDeviceToDevice, s));
-    PKD_NCCL_CHECK(ncclGroupStart());
-    for (int p = 0; p < size_; ++p) {
-      if (p == rank_) continue;
-      if (send_bytes[p]) PKD_NCCL_CHECK(ncclSend(sp + send_off[p], send_bytes[p], ncclChar, p, c_, s));
-      if (recv_bytes[p]) PKD_NCCL_CHECK(ncclRecv(rp + recv_off[p], recv_bytes[p], ncclChar, p, c_, s));
-    }
-    PKD_NCCL_CHECK(ncclGroupEnd());
-  }
-
- private:
-  ncclComm_t c_;
-  int rank_, size_;
-};
 
 // Waits for everything enqueued on `s` (collectives included) with a deadline, polling the
 // communicator's asynchronous error state (the failure detector of SURVEY.md §5.3).

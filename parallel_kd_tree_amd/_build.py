@@ -50,7 +50,7 @@ def _torch_flags():
                                         "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
     libdir = Path(torch.__file__).parent / "lib"
     ldflags = [f"-L{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-               "-lamdhip64", f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
+               "-lamdhip64", "-lrccl", f"-L{ROCM / 'lib'}", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
                f"-Wl,-rpath,{ROCM / 'lib'}"]
     return cflags, ldflags
 

@@ -251,3 +251,32 @@ def test_traversal_kernels_equal_brute(gpu_device, monkeypatch, n, dim, nq, dept
     monkeypatch.setenv("PKD_TRAVERSE", "thread")
     pt = t.query_packed(q, "traverse")
     assert torch.equal(pb, pw) and torch.equal(pb, pt)
+
+
+@pytest.mark.parametrize("k", [-1, 0, 2])
+def test_native_global_builder_one_rank(gpu_device, k):
+    """parallel/native_global.py (the C++ GlobalBuilder on an RCCL communicator of one rank,
+    the multi-GPU code path of bench.py) gives the single-GPU tree slot for slot."""
+    from parallel_kd_tree_amd.parallel.native_global import NativeGlobalBuilder
+    n, dim = 300_001, 3
+    x = pk.generate_slice(5, dim, 0, n, device=gpu_device)
+    g = NativeGlobalBuilder(n, dim, gpu_device, pipeline_k=k)
+    for _ in range(2):  # buffers reused by the second build
+        t = g.build(x, id_base=1)
+    assert g.read_error() == 0 and t.slot_lo == 0 and t.tree_ids.numel() == n
+    b = ops.GpuTreeBuilder(n, dim)
+    tp, ti = b.build(x, None, 1)
+    assert torch.equal(t.tree_ids, ti) and torch.equal(t.tree_pts, tp)
+
+
+def test_bench_native_global_one_rank():
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--decomp", "global", "--points", "3000000", "--steps", "2",
+                        "--warmup", "1", "--pipeline-k", "1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["config"]["parallelism"] == "global1" and line["config"]["tree_checked"]
