@@ -118,6 +118,7 @@ GlobalBuilder::~GlobalBuilder() {
   if (tree_pts_) (void)hipFree(tree_pts_);
   if (tree_ids_) (void)hipFree(tree_ids_);
   if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
+  if (host_counts_) (void)hipHostFree(host_counts_);
 }
 
 void* GlobalBuilder::buf(int slot, size_t bytes) {
@@ -174,19 +175,18 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
   for (;;) {  // until no middle bucket overflows its all-gather slot
     // 1. bounding box: one allreduce(MIN) of the encoded per-rank boxes
     auto* box = static_cast<i64*>(buf(0, size_t(2 * dim) * 8));
-    std::vector<i64> init(size_t(2 * dim), i64(0xffffffffu));
-    PKD_HIP_CHECK(hipMemcpyAsync(box, init.data(), init.size() * 8, hipMemcpyHostToDevice, s));
+    fill_u64(box, 2 * dim, 0xffffffffull, s);
     top_bbox(tp, box, s);
     comm_.allreduce_min_i64(box, size_t(2 * dim), s);
     auto* cells = static_cast<float*>(buf(1, size_t(2 * leaves - 1) * dim * 2 * 4));
     top_root_cell(box, dim, cells, s);
     auto* node = static_cast<u32*>(buf(2, size_t(std::max<i64>(n_local, 1)) * 4));
     auto* pivots = static_cast<u64*>(buf(3, size_t(std::max(leaves - 1, 1)) * 8));
-    PKD_HIP_CHECK(hipMemsetAsync(pivots, 0xff, size_t(std::max(leaves - 1, 1)) * 8, s));
-    top_rows = static_cast<float*>(buf(4, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4));
-    PKD_HIP_CHECK(hipMemsetAsync(top_rows, 0, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4, s));
+    fill_u64(pivots, std::max(leaves - 1, 1), ~0ull, s);
+    top_rows = static_cast<float*>(buf(4, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4 + 8));  // + 8: 64-bit fill
+    fill_u64(top_rows, (i64(std::max(leaves - 1, 1)) * (dim + 1) + 1) / 2, 0ull, s);
     auto* err = static_cast<u32*>(buf(5, 16));
-    PKD_HIP_CHECK(hipMemsetAsync(err, 0, 16, s));
+    fill_u64(err, 2, 0ull, s);
     auto* sel = static_cast<u32*>(buf(6, size_t(kTopMaxNodes) * 4 * 4));
     auto* hist = static_cast<u32*>(buf(7, size_t(kTopBins) * 4));
     // 2. top levels
@@ -198,7 +198,7 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
         i64 lo;
         segment(n_total_, nodes - 1 + j, &lo, &sizes.n[j]);
       }
-      PKD_HIP_CHECK(hipMemsetAsync(hist, 0, size_t(nodes) * bins * 4, s));
+      fill_u64(hist, i64(nodes) * bins / 2, 0ull, s);
       top_route_hist(tp, node, level, pivots, prev_axis, axis, cells, bins, hist, s);
       comm_.allreduce_sum_u32(hist, size_t(nodes) * bins, s);
       top_select(hist, level, bins, sizes, sel, err, s);
@@ -214,12 +214,7 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     const int last_axis = ((LL - 1) % dim + dim) % dim;
     auto* send = static_cast<float*>(buf(10, size_t(std::max<i64>(n_local, 1)) * dim * 4));
     auto* counts = static_cast<i64*>(buf(11, size_t(leaves) * 4 * 8));
-    std::vector<i64> hc(size_t(leaves) * 4, 0);
-    for (int d = 0; d < leaves; ++d) {
-      hc[size_t(d) * 4 + 2] = i64(id_base);
-      hc[size_t(d) * 4 + 3] = n_local;
-    }
-    PKD_HIP_CHECK(hipMemcpyAsync(counts, hc.data(), hc.size() * 8, hipMemcpyHostToDevice, s));
+    top_counts_init(counts, leaves, i64(id_base), n_local, s);
     const i64 words = std::max<i64>(1, (n_local + 31) / 32);
     auto* bm = static_cast<u32*>(buf(12, size_t(leaves) * words * 4));
     void* scratch = buf(13, top_pack_scratch_bytes(n_local, leaves));
@@ -227,9 +222,20 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     // 4. the count matrix, all-gathered: the one host read-back of the build
     auto* all = static_cast<i64*>(buf(14, size_t(P) * leaves * 4 * 8));
     comm_.allgather(counts, all, size_t(leaves) * 4 * 8, s);
-    std::vector<i64> hall(size_t(P) * leaves * 4);
-    PKD_HIP_CHECK(hipMemcpyAsync(hall.data(), all, hall.size() * 8, hipMemcpyDeviceToHost, s));
-    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    // pinned staging and a polling wait: the blocking wait's wake-up cost ~0.2 ms per build
+    const size_t nall = size_t(P) * leaves * 4;
+    if (host_counts_n_ < nall) {
+      if (host_counts_) PKD_HIP_CHECK(hipHostFree(host_counts_));
+      PKD_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counts_), nall * 8, hipHostMallocDefault));
+      host_counts_n_ = nall;
+    }
+    PKD_HIP_CHECK(hipMemcpyAsync(host_counts_, all, nall * 8, hipMemcpyDeviceToHost, s));
+    for (;;) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) PKD_HIP_CHECK(q);
+    }
+    const std::vector<i64> hall(host_counts_, host_counts_ + nall);
     if (global_plan::make_plan(hall, P, R, rank_, n_total_, &plan) == 0) break;
     if (global_plan::middle_cap(n_total_, P, 0, scale_) >= n_total_)
       throw std::runtime_error("global top levels: middle buckets inconsistent at full capacity");

@@ -44,10 +44,21 @@ __global__ __launch_bounds__(kBlock) void k_top_bbox(TopPoints p, i64 T, i64* __
     const int c = int(t % dim);
     u32 lo = 0xffffffffu, nhi = 0xffffffffu;
     const i64 total = p.n * dim;
-    for (i64 f = t; f < total; f += T) {
-      const u32 k = orderable(p.pts[f]);
-      lo = min(lo, k);
-      nhi = min(nhi, ~k);
+    constexpr int U = 8;  // loads in flight per thread; past the end a thread re-reads its first value
+    const float first = p.pts[t];  // t < T <= total, same axis
+    for (i64 f0 = t; f0 < total; f0 += U * T) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const i64 f = f0 + i64(u) * T;
+        v[u] = f < total ? p.pts[f] : first;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u32 k = orderable(v[u]);
+        lo = min(lo, k);
+        nhi = min(nhi, ~k);
+      }
     }
     atomicMin(&sb[c], lo);
     atomicMin(&sb[dim + c], nhi);
@@ -365,26 +376,48 @@ __global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restr
   if (threadIdx.x < P) bcount[i64(blockIdx.x) * P + threadIdx.x] = cnt[threadIdx.x];
 }
 
-// offsets[block][d] = sum_{d' < d} total[d'] + sum_{b' < block} bcount[b'][d]
-__global__ void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P, u32* __restrict__ offsets,
-                            i64* __restrict__ counts, const u32* __restrict__ err) {
-  __shared__ u32 tot[64];
-  const int d = threadIdx.x;
-  if (d < P) {
-    u32 s = 0;
-    for (int b = 0; b < blocks; ++b) s += bcount[i64(b) * P + d];
-    tot[d] = s;
-    counts[4 * d] = i64(s);
-    counts[4 * d + 1] = i64(*err);
-  }
+// offsets[block][d] = sum_{d' < d} total[d'] + sum_{b' < block} bcount[b'][d]: one workgroup per
+// destination d, a block-wide scan of its column (blocks <= 2 * kScanThreads) plus a block-wide
+// sum of the columns before it. (One thread per destination walking all blocks took 158 us
+// at 1526 blocks: a chain of dependent loads.)
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_pack_scan(const u32* __restrict__ bcount, int blocks, int P,
+                                                            u32* __restrict__ offsets, i64* __restrict__ counts,
+                                                            const u32* __restrict__ err) {
+  constexpr int W = kScanThreads / 64;
+  __shared__ u32 wsum[W], wbef[W];
+  const int d = blockIdx.x, tid = threadIdx.x, w = tid / 64, ln = tid & 63;
+  u32 before = 0;
+  for (int b = tid; b < blocks; b += kScanThreads)
+    for (int e = 0; e < d; ++e) before += bcount[i64(b) * P + e];
+  const int C = (blocks + kScanThreads - 1) / kScanThreads;  // 1 or 2
+  const int b0 = tid * C;
+  const bool in0 = b0 < blocks, in1 = C > 1 && b0 + 1 < blocks;
+  const u32 x0 = in0 ? bcount[i64(b0) * P + d] : 0u;
+  const u32 x1 = in1 ? bcount[i64(b0 + 1) * P + d] : 0u;
+  const u32 sum = x0 + x1;
+  const u32 incl = dev::wave_incl_scan(sum);
+  u32 bw = before;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bw += __shfl_xor(bw, o, 64);
+  if (ln == 63) wsum[w] = incl;
+  if (ln == 0) wbef[w] = bw;
   __syncthreads();
-  if (d < P) {
-    u32 base = 0;
-    for (int e = 0; e < d; ++e) base += tot[e];
-    for (int b = 0; b < blocks; ++b) {
-      offsets[i64(b) * P + d] = base;
-      base += bcount[i64(b) * P + d];
-    }
+  u32 pre = 0, tot = 0, base = 0;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const u32 v = wsum[k];
+    pre += k < w ? v : 0u;
+    tot += v;
+    base += wbef[k];
+  }
+  u32 run = base + pre + incl - sum;
+  if (in0) offsets[i64(b0) * P + d] = run;
+  run += x0;
+  if (in1) offsets[i64(b0 + 1) * P + d] = run;
+  if (tid == 0) {
+    counts[4 * d] = i64(tot);
+    counts[4 * d + 1] = i64(*err);
   }
 }
 
@@ -523,15 +556,38 @@ __global__ void k_zero4(u32* __restrict__ p) {
   if (threadIdx.x < 4) p[threadIdx.x] = 0u;
 }
 
+// pattern fill of 64-bit words; words j with (j % period) == slot get `alt` instead (the count
+// matrix's id-base / n_local columns)
+__global__ void k_fill64(u64* __restrict__ p, i64 n, u64 v, int period, int slot_a, u64 alt_a, int slot_b,
+                         u64 alt_b) {
+  for (i64 j = i64(blockIdx.x) * blockDim.x + threadIdx.x; j < n; j += i64(gridDim.x) * blockDim.x) {
+    const int r = period > 0 ? int(j % period) : -1;
+    p[j] = r == slot_a ? alt_a : (r == slot_b ? alt_b : v);
+  }
+}
+
 int pack_blocks(i64 n) { return int(std::max<i64>(1, std::min<i64>(2048, (n + 8191) / 8192))); }
 int stream_grid(i64 n) { return int(std::max<i64>(1, std::min<i64>(512, (n + 16383) / 16384))); }
 
 }  // namespace
 
+void fill_u64(void* p, i64 n, u64 v, hipStream_t stream) {
+  if (n <= 0) return;
+  k_fill64<<<int(std::min<i64>(1024, (n + 255) / 256)), 256, 0, stream>>>(static_cast<u64*>(p), n, v, 0, -1, 0, -1, 0);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream_t stream) {
+  k_fill64<<<1, 256, 0, stream>>>(reinterpret_cast<u64*>(counts), i64(slots) * 4, 0, 4, 2, u64(id_base), 3,
+                                  u64(n_local));
+  PKD_LAUNCH_CHECK();
+}
+
 void top_bbox(const TopPoints& p, i64* box, hipStream_t stream) {
   if (p.n <= 0) return;
   const int dim = p.dim;
-  const i64 want = std::min<i64>(p.n * dim, i64(256) * kBlock);  // few blocks: one atomic pair each
+  // up to 2048 blocks of 8 loads in flight per thread; one LDS-reduced atomic pair per block and axis
+  const i64 want = std::min<i64>(p.n * dim, i64(2048) * kBlock);
   const i64 T = std::max<i64>(dim, (want / dim) * dim);
   const int grid = int((T + kBlock - 1) / kBlock);
   k_top_bbox<<<grid, kBlock, size_t(2) * dim * 4, stream>>>(p, T, box);
@@ -595,7 +651,8 @@ void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int 
   u32* offsets = bcount + size_t(blocks) * P;
   k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, P, pipe_k, per_block, bcount);
   PKD_LAUNCH_CHECK();
-  k_pack_scan<<<1, 64, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
+  static_assert(2 * kScanThreads >= 2048, "k_pack_scan covers at most 2 * kScanThreads blocks");
+  k_pack_scan<<<P, kScanThreads, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
   PKD_LAUNCH_CHECK();
   k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, pipe_k, per_block, offsets, out_rows, row_stride);
   PKD_LAUNCH_CHECK();

@@ -40,6 +40,11 @@ struct TopSizes {
 
 // Per-rank bounding box, encoded for ONE allreduce(MIN) over int64: box[c] = orderable(lo_c),
 // box[dim + c] = ~orderable(hi_c) (both < 2^32). The caller fills box with 0xffffffff first.
+// Device-side fills (kernels, so no host staging and graph-capturable): n 64-bit words of v;
+// the [slots][4] count matrix of top_pack with its id-base / n_local columns set.
+void fill_u64(void* p, i64 n, u64 v, hipStream_t stream);
+void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream_t stream);
+
 void top_bbox(const TopPoints& p, i64* box, hipStream_t stream);
 // cells[0] ([dim][2] lo/hi) from the reduced box.
 void top_root_cell(const i64* box, int dim, float* cells, hipStream_t stream);

@@ -97,6 +97,8 @@ class GlobalBuilder {
   u32* tree_ids_ = nullptr;
   float* top_rows_ = nullptr;
   hipStream_t comm_stream_ = nullptr;
+  i64* host_counts_ = nullptr;  // pinned copy of the all-gathered count matrix
+  size_t host_counts_n_ = 0;
   std::vector<std::pair<void*, size_t>> bufs_;
   struct Leaf;
   std::vector<std::unique_ptr<Leaf>> leaves_;
