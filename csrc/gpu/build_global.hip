@@ -1234,7 +1234,7 @@ struct PairArgs {
 
 template <int NCOL>
 __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
-  extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
+  extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins] + 64 per-lane dummy words
   constexpr int D = NCOL - 1;
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -1271,45 +1271,77 @@ __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
     bmax = 0ull;
   }
   __syncthreads();
-  constexpr int U = 8;
-  for (i64 e0 = b0; e0 < b1; e0 += kBlock * U) {
-    float k[U], nk[U];
+  // One row: its level-l zone; rows certain to go left / right add their level-(l+1) key to
+  // that child's histogram (one LDS atomic, rows of the median bucket and absent rows add 0 to
+  // a per-lane dummy word), rows of the median bucket are noted for staging. Every lane of a
+  // wave calls it together (ballots).
+  const u32 hdummy = u32(2 * nb) + u32(ln);
+  auto visit = [&](float kv, float nkv, i64 e, bool valid) {
+    const u32 z = valid ? zone_of(kv, prm, a.bins, bstar, stage2, p2, sbstar) : 3u;
+    const u32 bl = bucket_of(nkv, cp0, nb), br = u32(nb) + bucket_of(nkv, cp1, nb);
+    const u32 hb = z == 0 ? bl : br;
+    const bool side = (z == 0) | (z == 2);
+    atomicAdd(&nh[side ? hb : hdummy], 1u);
+    const u64 m = __ballot(z == 1);
+    if (m) {  // rare: note the median bucket's rows
+      const int leader = __ffsll((long long)m) - 1;
+      u32 base = 0;
+      if (ln == leader) base = atomicAdd(&mcnt, u32(__popcll(m)));
+      base = __shfl(base, leader, 64);
+      const u32 slot = base + mbcnt(m);
+      const bool direct = z == 1 && slot >= u32(kStage);
+      if (z == 1 && !direct) sidx[slot] = u32(e - b0);
+      if (__ballot(direct)) {  // staging full: reserve and copy directly
+        u64 ck = 0;
+        if (direct) {
+          const u32 g = atomicAdd(&st->cur[1], 1u);
+          if (i64(g) >= n) {
+            atomicOr(a.err, 1u);
+          } else {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock + threadIdx.x;
-      k[u] = e < b1 ? kc[e] : 0.0f;
-      nk[u] = e < b1 ? nkc[e] : 0.0f;
+            for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + g] = src_col(a, c, lo + e);
+          }
+          ck = composite_key(kv, src_id(a, lo + e));
+        }
+        wave_minmax_atomic(direct, ck, &bmin, &bmax);
+      }
+    }
+  };
+  // The 16-B aligned bulk of the block's rows is read with 16-B loads (4 rows of each key
+  // column per load); the up to 3 rows before and after it one per lane, in one extra round.
+  const i64 abs0 = lo + b0, abs1 = lo + b1;
+  const i64 A = min(abs1, (abs0 + 3) & ~i64(3));
+  const i64 nv = (abs1 - A) >> 2;
+  const i64 Bend = A + 4 * nv;
+  {
+    const int t = int(threadIdx.x);
+    const bool head = t < 3 && abs0 + t < A, tail = t >= 3 && t < 6 && Bend + (t - 3) < abs1;
+    const i64 e = head ? abs0 + t - lo : (tail ? Bend + (t - 3) - lo : 0);
+    const bool v = head | tail;
+    const float kv = v ? kc[e] : 0.0f, nkv = v ? nkc[e] : 0.0f;
+    visit(kv, nkv, e, v);
+  }
+  const float4* kc4 = reinterpret_cast<const float4*>(src + i64(a.axis) * nc + A);
+  const float4* nk4 = reinterpret_cast<const float4*>(src + i64(a.next_axis) * nc + A);
+  constexpr int U4 = 2;  // 2 x 16 B per column in flight per thread
+  for (i64 v0 = 0; v0 < nv; v0 += kBlock * U4) {
+    float4 k[U4], nk[U4];
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = v0 + i64(u) * kBlock + threadIdx.x;
+      const i64 vi = v < nv ? v : 0;
+      k[u] = kc4[vi];
+      nk[u] = nk4[vi];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock + threadIdx.x;
-      const u32 z = e < b1 ? zone_of(k[u], prm, a.bins, bstar, stage2, p2, sbstar) : 3u;
-      if (z == 0) atomicAdd(&nh[bucket_of(nk[u], cp0, nb)], 1u);
-      if (z == 2) atomicAdd(&nh[nb + bucket_of(nk[u], cp1, nb)], 1u);
-      const u64 m = __ballot(z == 1);
-      if (m) {  // rare: note the median bucket's rows
-        const int leader = __ffsll((long long)m) - 1;
-        u32 base = 0;
-        if (ln == leader) base = atomicAdd(&mcnt, u32(__popcll(m)));
-        base = __shfl(base, leader, 64);
-        const u32 slot = base + mbcnt(m);
-        const bool direct = z == 1 && slot >= u32(kStage);
-        if (z == 1 && !direct) sidx[slot] = u32(e - b0);
-        if (__ballot(direct)) {  // staging full: reserve and copy directly
-          u64 ck = 0;
-          if (direct) {
-            const u32 g = atomicAdd(&st->cur[1], 1u);
-            if (i64(g) >= n) {
-              atomicOr(a.err, 1u);
-            } else {
-#pragma unroll
-              for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + lo + g] = src_col(a, c, lo + e);
-            }
-            ck = composite_key(k[u], src_id(a, lo + e));
-          }
-          wave_minmax_atomic(direct, ck, &bmin, &bmax);
-        }
-      }
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = v0 + i64(u) * kBlock + threadIdx.x;
+      const bool in = v < nv;
+      const i64 e = A - lo + 4 * v;
+      visit(k[u].x, nk[u].x, e, in);
+      visit(k[u].y, nk[u].y, e + 1, in);
+      visit(k[u].z, nk[u].z, e + 2, in);
+      visit(k[u].w, nk[u].w, e + 3, in);
     }
   }
   __syncthreads();
@@ -2244,7 +2276,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     const int grid = int(lp.segs * lp.bps);
     if (lp.pair) {
       const LevelPlan& lq = levels_[size_t(l + 1)];
-      const size_t lds_a = size_t(2 * lp.next_bins) * 4;
+      const size_t lds_a = size_t(2 * lp.next_bins + 64) * 4;
       const int gs = int((lp.segs + 3) / 4);
       with_ncol(dim_, [&](auto nc) {
         constexpr int NC = decltype(nc)::value;
