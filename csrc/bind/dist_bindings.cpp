@@ -175,7 +175,8 @@ std::tuple<int, std::vector<std::vector<int64_t>>, std::vector<std::vector<int64
 // (loopback communicator): rank r holds rows [first_r, first_r + local_r) of `x` (the reference's
 // MPI slicing), ids 1..N. Returns the assembled in-order tree (rank sub-trees + top pivots) on the
 // host and the OR of the ranks' error words.
-std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::Tensor& x, int64_t P, int64_t k) {
+std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const torch::Tensor& x, int64_t P,
+                                                                           int64_t k) {
   TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
               "x: contiguous float32 [N, dim] host tensor");
   const int64_t N = x.size(0);
@@ -187,6 +188,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::T
   auto comms = make_thread_comms(int(P));
   std::vector<std::exception_ptr> errs(static_cast<size_t>(P));
   std::vector<u32> ew(static_cast<size_t>(P), 0u);
+  std::vector<int> scales(static_cast<size_t>(P), 0);
   std::vector<std::thread> th;
   for (int r = 0; r < int(P); ++r)
     th.emplace_back([&, r] {
@@ -201,6 +203,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::T
         GlobalBuilder gb(*comms[size_t(r)], N, dim, int(k));
         gb.build(d, local, u32(first + 1), s);
         ew[size_t(r)] = gb.read_error(s);
+        scales[size_t(r)] = gb.middle_scale();
         PKD_HIP_CHECK(hipMemcpy(tp.data_ptr<float>() + gb.slot_lo() * dim, gb.tree_pts(), size_t(gb.n_leaf()) * dim * 4,
                                 hipMemcpyDeviceToHost));
         PKD_HIP_CHECK(hipMemcpy(ti.data_ptr<int32_t>() + gb.slot_lo(), gb.tree_ids(), size_t(gb.n_leaf()) * 4,
@@ -227,7 +230,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t> global_loopback(const torch::T
     if (e) std::rethrow_exception(e);
   u32 e = 0;
   for (u32 v : ew) e |= v;
-  return {tp, ti, int64_t(e)};
+  return {tp, ti, int64_t(e), int64_t(*std::max_element(scales.begin(), scales.end()))};
 }
 
 // The native global builder on its own RCCL communicator, one per process (rank). The
@@ -283,6 +286,7 @@ class NativeGlobal {
   int64_t slot_lo() const { return gb_->slot_lo(); }
   int64_t n_leaf() const { return gb_->n_leaf(); }
   int64_t top_levels() const { return gb_->top_levels(); }
+  int64_t middle_scale() const { return gb_->middle_scale(); }
   int64_t read_error() const {
     const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
     return int64_t(gb_->read_error(c10::hip::getCurrentHIPStream(device_).stream()));
@@ -321,6 +325,7 @@ void bind_dist_ops(pybind11::module& m) {
       .def("slot_lo", &NativeGlobal::slot_lo)
       .def("n_leaf", &NativeGlobal::n_leaf)
       .def("top_levels", &NativeGlobal::top_levels)
+      .def("middle_scale", &NativeGlobal::middle_scale)
       .def("read_error", &NativeGlobal::read_error);
   m.def("global_plan", &plan_py);
   m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,

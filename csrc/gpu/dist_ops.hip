@@ -562,7 +562,7 @@ __global__ void k_fill64(u64* __restrict__ p, i64 n, u64 v, int period, int slot
                          u64 alt_b) {
   for (i64 j = i64(blockIdx.x) * blockDim.x + threadIdx.x; j < n; j += i64(gridDim.x) * blockDim.x) {
     const int r = period > 0 ? int(j % period) : -1;
-    p[j] = r == slot_a ? alt_a : (r == slot_b ? alt_b : v);
+    p[j] = (period > 0 && r == slot_a) ? alt_a : ((period > 0 && r == slot_b) ? alt_b : v);
   }
 }
 

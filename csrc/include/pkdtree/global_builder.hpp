@@ -75,6 +75,8 @@ class GlobalBuilder {
   i64 slot_lo() const { return slot_lo_; }
   i64 n_leaf() const { return n_leaf_; }
   int top_levels() const { return L_; }
+  // all-gather slot scale of the middle buckets (x 8 per overflow retry; sticky across builds)
+  int middle_scale() const { return scale_; }
   const float* tree_pts() const { return tree_pts_; }
   const u32* tree_ids() const { return tree_ids_; }
   // The P - 1 replicated top pivots, heap order: rows of dim + 1 floats (coordinates, id

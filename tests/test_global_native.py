@@ -64,8 +64,10 @@ def test_native_plan_errors(native):
                                        (2, 0, 20_000_000, 3)])
 def test_native_global_loopback(gpu_device, native, P, k, n, dim):
     x = pk.generate_problem(P + k + 3, dim, n)
-    tp, ti, err = native.global_loopback(x, P, k)
+    tp, ti, err, scale = native.global_loopback(x, P, k)
     assert err == 0
+    # the middle-bucket all-gather slots held every bucket: no overflow retry (uniform data)
+    assert scale == 1 or n < 1000
     cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
     assert torch.equal(ti, ci + 1), "native global tree differs from the exact tree"
     assert torch.equal(tp, cp)

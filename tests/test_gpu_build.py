@@ -264,6 +264,7 @@ def test_native_global_builder_one_rank(gpu_device, k):
     for _ in range(2):  # buffers reused by the second build
         t = g.build(x, id_base=1)
     assert g.read_error() == 0 and t.slot_lo == 0 and t.tree_ids.numel() == n
+    assert g._g.middle_scale() == 1, "the top levels' middle buckets overflowed their all-gather slots"
     b = ops.GpuTreeBuilder(n, dim)
     tp, ti = b.build(x, None, 1)
     assert torch.equal(t.tree_ids, ti) and torch.equal(t.tree_pts, tp)
