@@ -23,6 +23,15 @@ __device__ __forceinline__ u32 point_id(const TopPoints& p, i64 i) { return p.id
 
 // Route one point one level down below the pivot of its node (heap order). The id is only
 // read when the keys tie.
+__device__ __forceinline__ u32 route_key(u32 h, float key, const TopPoints& p, i64 i, const u64* pivots) {
+  if (h == kTopDone) return h;
+  const u32 k = orderable(key);
+  const u64 pv = pivots[h];
+  const u32 pk = u32(pv >> 32);
+  if (k != pk) return k < pk ? 2 * h + 1 : 2 * h + 2;
+  const u32 id = point_id(p, i), pid = u32(pv);
+  return id < pid ? 2 * h + 1 : (id > pid ? 2 * h + 2 : kTopDone);
+}
 __device__ __forceinline__ u32 route(u32 h, const TopPoints& p, i64 i, int axis, const u64* pivots) {
   if (h == kTopDone) return h;
   const u32 k = orderable(p.pts[i * p.dim + axis]);
@@ -99,16 +108,32 @@ __global__ __launch_bounds__(kBlock) void k_top_route_hist(TopPoints p, u32* __r
   load_params(prm, cells, int(first), nodes, p.dim, axis, bins);
   __syncthreads();
   const i64 stride = i64(gridDim.x) * kBlock;
-  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += stride) {
-    u32 h = 0;
-    if (level > 0) {
-      h = level > 1 ? node[i] : 0u;
-      h = route(h, p, i, prev_axis, pivots);
-      node[i] = h;
+  // kU rows per thread per round, every load of a round issued before its atomics
+  constexpr int kU = 4;
+  for (i64 base = i64(blockIdx.x) * kBlock + threadIdx.x; base < p.n; base += kU * stride) {
+    u32 hn[kU];
+    float kp[kU], ka[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const i64 i = base + u * stride;
+      const i64 ii = i < p.n ? i : 0;
+      hn[u] = level > 1 ? node[ii] : 0u;
+      kp[u] = p.pts[ii * p.dim + prev_axis];
+      ka[u] = p.pts[ii * p.dim + axis];
     }
-    if (h == kTopDone) continue;
-    const u32 j = h - first;
-    atomicAdd(&sh[j * bins + bucket_of(p.pts[i * p.dim + axis], prm[j], bins)], 1u);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const i64 i = base + u * stride;
+      if (i >= p.n) continue;
+      u32 h = 0;
+      if (level > 0) {
+        h = route_key(hn[u], kp[u], p, i, pivots);
+        node[i] = h;
+      }
+      if (h == kTopDone) continue;
+      const u32 j = h - first;
+      atomicAdd(&sh[j * bins + bucket_of(ka[u], prm[j], bins)], 1u);
+    }
   }
   __syncthreads();
   for (int b = threadIdx.x; b < nb_total; b += kBlock) {
@@ -178,35 +203,71 @@ __global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* 
   u32* count = reinterpret_cast<u32*>(buf);
   float* rows = buf + 4;
   const int rs = p.dim + 2;
+  // A block notes its median-bucket rows in LDS and reserves them with ONE global atomic at
+  // the end: the count word is shared by every block of every XCD, and per-wave atomics on it
+  // serialise at the memory side (~1 us each). Rows beyond the staging take the direct path.
+  constexpr int kStage = 1024;
+  __shared__ u32 sidx[kStage];
+  __shared__ u32 scount, sbase;
+  if (threadIdx.x == 0) scount = 0;
+  __syncthreads();
+  auto write_row = [&](i64 slot, i64 i, u32 h) {
+    if (slot >= cap) return;
+    float* o = rows + slot * rs;
+    const float* r = p.pts + i * p.dim;
+    for (int c = 0; c < p.dim; ++c) o[c] = r[c];
+    o[p.dim] = __uint_as_float(point_id(p, i));
+    o[p.dim + 1] = __uint_as_float(h);
+  };
   const i64 stride = i64(gridDim.x) * kBlock;
-  // the trip count is uniform across the wave (ballots below need every lane)
-  for (i64 base = i64(blockIdx.x) * kBlock; base < p.n; base += stride) {
-    const i64 i = base + threadIdx.x;
-    bool take = false;
-    u32 h = 0;
-    if (i < p.n) {
-      h = level > 0 ? node[i] : 0u;
-      if (h != kTopDone) {
+  // the trip count is uniform across the wave (ballots below need every lane); kU rows per
+  // thread per round with their loads issued together
+  constexpr int kU = 4;
+  for (i64 base0 = i64(blockIdx.x) * kBlock; base0 < p.n; base0 += kU * stride) {
+    u32 hn[kU];
+    float ka[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const i64 i = base0 + u * stride + threadIdx.x;
+      const i64 ii = i < p.n ? i : 0;
+      hn[u] = level > 0 ? node[ii] : 0u;
+      ka[u] = p.pts[ii * p.dim + axis];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const i64 i = base0 + u * stride + threadIdx.x;
+      bool take = false;
+      const u32 h = hn[u];
+      if (i < p.n && h != kTopDone) {
         const u32 j = h - first;
-        take = bucket_of(p.pts[i * p.dim + axis], prm[j], bins) == bs[j];
+        take = bucket_of(ka[u], prm[j], bins) == bs[j];
+      }
+      const u64 m = __ballot(take);
+      if (!m) continue;
+      const int leader = __ffsll((long long)m) - 1;
+      u32 lbase = 0;
+      if (dev::lane() == leader) lbase = atomicAdd(&scount, u32(__popcll(m)));
+      lbase = __shfl(lbase, leader, 64);
+      const u32 ls = lbase + mbcnt(m);
+      if (take && ls < u32(kStage)) sidx[ls] = u32(i);
+      const bool direct = take && ls >= u32(kStage);
+      if (__ballot(direct)) {  // staging full (a very skewed block): reserve per wave
+        const u64 md = __ballot(direct);
+        const int ld = __ffsll((long long)md) - 1;
+        u32 gb = 0;
+        if (dev::lane() == ld) gb = atomicAdd(count, u32(__popcll(md)));
+        gb = __shfl(gb, ld, 64);
+        if (direct) write_row(i64(gb) + mbcnt(md), i, h);
       }
     }
-    const u64 m = __ballot(take);
-    if (!m) continue;
-    const int leader = __ffsll((long long)m) - 1;
-    u32 base_slot = 0;
-    if (dev::lane() == leader) base_slot = atomicAdd(count, u32(__popcll(m)));
-    base_slot = __shfl(base_slot, leader, 64);
-    if (take) {
-      const i64 slot = i64(base_slot) + mbcnt(m);
-      if (slot < cap) {
-        float* o = rows + slot * rs;
-        const float* r = p.pts + i * p.dim;
-        for (int c = 0; c < p.dim; ++c) o[c] = r[c];
-        o[p.dim] = __uint_as_float(point_id(p, i));
-        o[p.dim + 1] = __uint_as_float(h);
-      }
-    }
+  }
+  __syncthreads();
+  const u32 staged = min(scount, u32(kStage));
+  if (threadIdx.x == 0) sbase = staged ? atomicAdd(count, staged) : 0u;
+  __syncthreads();
+  for (u32 k = threadIdx.x; k < staged; k += kBlock) {
+    const i64 i = sidx[k];
+    write_row(i64(sbase) + k, i, level > 0 ? node[i] : 0u);
   }
 }
 
