@@ -1974,6 +1974,17 @@ int pow2_floor(i64 v) {
   return p;
 }
 
+// Bins of a level whose histogram a paired pass fuses (4 grandchildren in LDS: 4 * bins words
+// per partition block). PKD_PAIR_BINS overrides (A/B of LDS occupancy vs median-bucket size).
+int pair_bins() {
+  static const int v = [] {
+    const char* e = std::getenv("PKD_PAIR_BINS");
+    const int b = e ? std::atoi(e) : kPairBins;
+    return (b >= 64 && b <= kPairBins && (b & (b - 1)) == 0) ? b : kPairBins;
+  }();
+  return v;
+}
+
 int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 24)))); }
 
 }  // namespace
@@ -2033,7 +2044,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     levels_[size_t(l)].pair = true;
     if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
       LevelPlan& g = levels_[size_t(l + 2)];
-      g.bins = std::min(g.bins, kPairBins);
+      g.bins = std::min(g.bins, pair_bins());
       levels_[size_t(l + 1)].next_bins = g.bins;
     }
     ++l;  // l+1 is the second level of the pair
