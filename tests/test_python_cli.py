@@ -62,3 +62,15 @@ def test_eval_mode_stdin_metrics():
     assert lines[0] == "READY" and lines[-1] == "DONE" and len(lines) == 12
     assert lines[1:11] == oracle_lines(3, 128, 500_000)
     assert '"build_query_ms"' in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", ["native"])
+def test_global_one_gpu_cli(impl):
+    """python -m parallel_kd_tree_amd.cli --decomp global on one GPU (native GlobalBuilder over a
+    one-rank RCCL communicator): the reference protocol lines of the exact tree."""
+    r = _run(["--decomp", "global", "--impl", impl, "--queries", "20", "11", "3", "200000"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    assert lines[0] == "READY" and lines[-1] == "DONE"
+    assert lines[1:21] == oracle_lines(11, 3, 200000, 20)
