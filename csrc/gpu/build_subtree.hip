@@ -65,9 +65,10 @@ __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(
 // 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+68 | aux nm+64 | fin nm+64 | tmpi u16 nm+64 |
 //               root cell 2*dim. The 64 dummy entries at the end of work / aux / fin / tmpi take the writes
 //               of finished points, one per lane, so those writes never share an address.
+//               + the second bitmap buffer of the compressed levels, nm/2 + 64.
 size_t lds_words(int dim, int nm) {
   return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 68 + 2 * (size_t(nm) + 64) +
-         size_t(nm) / 2 + 32 + 2 * size_t(dim);
+         size_t(nm) / 2 + 32 + 2 * size_t(dim) + size_t(nm) / 2 + 64;
 }
 // narrow mode: ldim key slots + ids + input row indices, no compressed ranks (ldim <= dim)
 size_t lds_words_narrow(int dim, int nm, int ldim) {
@@ -116,8 +117,14 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum, u32 du
 // NARROW is a template parameter so the classic (low-dim) instantiation carries none of the
 // narrow path's registers: a runtime flag cost the 100M x 3D build's subtree kernel 3.7 -> 5.65 ms.
 // DIMC > 0: the dimension as a compile-time constant (d = 3 headline shape), else a.dim.
+// Two workgroups per CU are the design point below capacity 4096 (one block's barriers hide
+// behind the other's work): the register budget is pinned to that many waves per SIMD, since one SGPR over the
+// granule halves the resident blocks (82 SGPRs: 100M x 3D subtree 3.3 -> 4.9 ms, resident
+// waves 63 -> 32 in profiles/r2_subtree_pmc.txt).
 template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0>
-__global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
+__global__ __launch_bounds__(THREADS)
+__attribute__((amdgpu_waves_per_eu((ITEMS * THREADS >= 4096 ? 1 : 2) * THREADS / 256)))  // blocks/CU x waves/SIMD
+void k_subtree_rank(SubArgs a) {
   extern __shared__ __align__(16) u32 smem[];
   __shared__ u32 wsum[THREADS / 64];
   constexpr int NM = ITEMS * THREADS;
@@ -148,6 +155,10 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   u32* fin = aux + NM + 64;           // aux / fin: NM entries + 64 per-lane dummies each
   u16* tmpi = reinterpret_cast<u16*>(fin + NM + 64);  // NM + 64 entries
   float* cellv = reinterpret_cast<float*>(tmpi + NM + 64);  // [dim][2] root cell of the segment
+  // Compressed levels alternate their bitmaps between bm1 (NM/2 words + 64 dummies; classic
+  // layout only) and work: each level zeroes the buffer of the next one after its first
+  // barrier, so a compressed level needs no zero phase of its own: 2 barriers instead of 3-4.
+  u32* bm1 = reinterpret_cast<u32*>(cellv + 2 * dim);
   const u32 lane_dummy = u32(dev::lane());
   const u32 dummy = u32(NM + 4) + lane_dummy;
   // Item i of a thread is point kid(i): wave w owns the contiguous points [w*64*ITEMS,
@@ -226,6 +237,13 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
     const int k = tid + i * THREADS;
     fin[k < n ? u32(k) : u32(NM) + lane_dummy] = 0xffffffffu;
   }
+  if constexpr (!NARROW)
+    for (int w = tid; w < NM / 2; w += THREADS) bm1[w] = 0;  // the first compressed level's bitmaps
+#pragma unroll
+  for (int j = 0; j <= ITEMS; ++j) {  // the first level's histogram (buckets + sentinel)
+    const int w = tid + j * THREADS;
+    work[w <= NM ? u32(w) : dummy] = 0;
+  }
   u32 lo[ITEMS], nn[ITEMS], sg[ITEMS];
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
@@ -236,27 +254,30 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
   __syncthreads();
   stamp(a, 1);
 
+  int cb = 1;          // bitmap buffer of the next compressed level: 1 = bm1, 0 = work
+  bool synced = true;  // false after a compressed level (it ends without a barrier)
+  bool wz = true;      // work holds zeros (a first-use level zeroes it for the next one)
+  // Wt of level t: > 0 when its ranks come from the compressed ranks of the axis's last use
+  auto words_of = [&](int t) -> int {
+    if (narrow || !keep || t < dim) return 0;
+    const u32 wbits = u32(n) >> (t - dim + 1);
+    const u32 words = rk::pow2_ceil((wbits + 31) / 32);
+    return (words <= 64 && u32(1u << t) * words <= u32(NM / 2)) ? int(words) : 0;
+  };
   for (int t = 0; t < lsub; ++t) {
     const int axis = (a.depth_base + t) % dim;
     const float* kcol = rows + (narrow ? t : axis) * NM;
     u16* cr = crank + size_t(axis) * NM;
     const int S = 1 << t;
-    int Wt = 0;
-    if (keep && t >= dim) {
-      const u32 wbits = u32(n) >> (t - dim + 1);
-      const u32 words = rk::pow2_ceil((wbits + 31) / 32);
-      if (words <= 64 && u32(S) * words <= u32(NM)) Wt = int(words);
-    }
+    const int Wt = words_of(t);
     u32 rank[ITEMS];
     if (Wt > 0) {
       // ---- compressed ranks: one bitmap of Wt words per sub-segment ----
-      const int nw = S * Wt;  // <= NM
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const int w = tid + j * THREADS;
-        work[w < nw ? u32(w) : dummy] = 0;
-      }
-      __syncthreads();
+      // (already zeroed by the previous level; its readers finished before this level's barrier)
+      u32* bmp = cb ? bm1 : work;
+      u32* nxt = cb ? work : bm1;
+      const u32 bdum = cb ? u32(NM / 2) + lane_dummy : dummy;
+      const int nw = S * Wt;  // <= NM / 2
       u32 c[ITEMS], wi[ITEMS];
       if (wlive) {
         if (ITEMS == 2) {
@@ -271,17 +292,19 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
         for (int i = 0; i < ITEMS; ++i) {
           const u32 wv = sg[i] * u32(Wt) + (c[i] >> 5);
           const u32 bit = 1u << (c[i] & 31);
-          wi[i] = nn[i] ? wv : dummy;
-          atomicOr(&work[wi[i]], nn[i] ? bit : 0u);
+          wi[i] = nn[i] ? wv : bdum;
+          atomicOr(&bmp[wi[i]], nn[i] ? bit : 0u);
         }
       }
       __syncthreads();
+      // the next compressed level's buffer: last read by the level before this one
+      for (int w = tid; w < NM / 2; w += THREADS) nxt[w] = 0;
       if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
         const u32 g = lane_dummy & u32(Wt - 1);
         for (int w0 = 0; w0 < nw; w0 += THREADS) {
           const int w = w0 + tid;
           const bool in = w < nw;
-          const u32 pc = u32(__popc(work[in ? w : 0]));
+          const u32 pc = u32(__popc(bmp[in ? w : 0]));
           const u32 v = in ? pc : 0u;
           u32 incl = v;
           for (int o = 1; o < Wt; o <<= 1) {
@@ -296,9 +319,11 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
           const u32 below = Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u;
-          rank[i] = below + u32(__popc(work[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
+          rank[i] = below + u32(__popc(bmp[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
         }
       }
+      cb ^= 1;
+      wz = false;
     } else {
       // ---- exact ranks from bucket histograms (first use of the axis) ----
       // Bucket range: the block root's cell on this axis. On an axis's first use no split
@@ -309,13 +334,16 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       const int B = maxsize > rk::kSmallSeg ? int(rk::pow2_ceil(u32(maxsize))) : 1;
       const int nb = S * B;  // <= NM; work[nb] is the scan's total (sentinel)
       u32* tmpk = aux;       // orderable keys in bucket order
-#pragma unroll
-      for (int j = 0; j <= ITEMS; ++j) {
-        const int w = tid + j * THREADS;
-        work[w <= nb ? u32(w) : dummy] = 0;
-      }
       const BucketParams pr = make_params(cellv[2 * axis], cellv[2 * axis + 1], B);
-      __syncthreads();
+      if (!wz) {  // (normally the previous level zeroed work before its closing barrier)
+        if (!synced) __syncthreads();  // the previous (compressed) level's readers of work / aux
+#pragma unroll
+        for (int j = 0; j <= ITEMS; ++j) {
+          const int w = tid + j * THREADS;
+          work[w <= nb ? u32(w) : dummy] = 0;
+        }
+        __syncthreads();
+      }
       if (t == 0) stamp(a, 20);
       u32 ok[ITEMS];
       u32 bk[ITEMS], wi[ITEMS];
@@ -334,30 +362,34 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       rk::block_excl_scan<THREADS, ITEMS>(work, nb, wsum, dummy);
       __syncthreads();
       if (t == 0) stamp(a, 22);
-      u32 pos[ITEMS];
+      // scatter into bucket order; every read of the scanned histogram happens here, so the
+      // histogram can be zeroed for the next level right after the barrier below
+      u32 pos[ITEMS], st[ITEMS], cnt[ITEMS];
       if (wlive) {
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-          const u32 p = work[bk[i]] + wi[i];
-          pos[i] = nn[i] ? p : u32(NM) + lane_dummy;
-          tmpk[pos[i]] = ok[i];
-          tmpi[pos[i]] = u16(kid(i));
-        }
-      }
-      __syncthreads();
-      if (t == 0) stamp(a, 23);
-      if (wlive) {
-        u32 st[ITEMS], cnt[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
           const u32 bi = nn[i] ? bk[i] : 0u;
           const u32 sb = nn[i] ? sg[i] * u32(B) : 0u;
           const u32 s0 = work[bi], e0 = work[bi + 1], b0 = work[sb];
+          pos[i] = nn[i] ? s0 + wi[i] : u32(NM) + lane_dummy;
+          tmpk[pos[i]] = ok[i];
+          tmpi[pos[i]] = u16(kid(i));
           st[i] = s0;
-          cnt[i] = e0 - s0;  // 0 for finished points (bucket 0 stands in: its count is not theirs)
-          cnt[i] = nn[i] ? cnt[i] : 0u;
+          cnt[i] = nn[i] ? e0 - s0 : 0u;  // 0 for finished points
           rank[i] = s0 - b0;
         }
+      }
+      __syncthreads();
+      if (t == 0) stamp(a, 23);
+      wz = t + 1 < lsub && words_of(t + 1) == 0;
+      if (wz) {  // the next level ranks by histogram too: its buckets + sentinel, zeroed now
+#pragma unroll
+        for (int j = 0; j <= ITEMS; ++j) {
+          const int w = tid + j * THREADS;
+          work[w <= NM ? u32(w) : dummy] = 0;
+        }
+      }
+      if (wlive) {
         // in-bucket comparisons, kU members per round: all items' reads of a round are issued
         // together; wave-uniform trip count = largest bucket among the wave's items / kU
         constexpr u32 kU = 2;
@@ -419,9 +451,14 @@ __global__ __launch_bounds__(THREADS) void k_subtree_rank(SubArgs a) {
       }
       if (keep && ITEMS == 2) reinterpret_cast<u32*>(cr)[tid] = (cn[0] & 0xffffu) | (cn[ITEMS - 1] << 16);
     }
-    __syncthreads();
+    // Closing barrier for first-use levels (the next level rewrites work) and for compressed
+    // levels without a prefix phase (it orders their zeroing of the next buffer before the next
+    // level's ORs); a compressed level with Wt > 1 already had its second barrier after that.
+    synced = Wt <= 1;
+    if (synced) __syncthreads();
     if (t < 18) stamp(a, 2 + t);
   }
+  if (!synced) __syncthreads();  // fin: the last level's slot writes
   stamp(a, 30);
   // in-order rows out: thread per slot, the row's dim floats (consecutive threads cover
   // consecutive 4*dim-byte runs, merged in L2)
