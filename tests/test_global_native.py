@@ -62,7 +62,7 @@ def test_native_plan_errors(native):
 @pytest.mark.parametrize("P,k,n,dim", [(1, 0, 100_000, 3), (1, 2, 200_001, 3), (2, -1, 300_000, 3), (4, 0, 250_000, 3),
                                        (4, 1, 120_000, 5), (8, 0, 400_003, 3), (8, 1, 90_000, 2), (4, 0, 7, 3),
                                        (2, 0, 20_000_000, 3), (2, 3, 300_000, 3), (8, 2, 500_000, 3),
-                                       (4, 2, 1_000_000, 8)])
+                                       (4, 2, 1_000_000, 8), (8, 0, 5, 3), (2, 1, 1, 3), (8, 1, 20, 2)])
 def test_native_global_loopback(gpu_device, native, P, k, n, dim):
     x = pk.generate_problem(P + k + 3, dim, n)
     tp, ti, err, scale = native.global_loopback(x, P, k)
