@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <sstream>
@@ -1985,12 +1986,71 @@ int pair_bins() {
   return v;
 }
 
+// Split build knobs (profiles/r2_split_build.txt): from level PKD_SPLIT_LEVEL (a pair
+// boundary) on, PKD_SPLIT_PARTS segment ranges run on PKD_SPLIT_STREAMS HIP streams, for
+// builds of at least PKD_SPLIT_MIN_N points; PKD_SPLIT=0 keeps one stream.
+struct SplitCfg {
+  bool on;
+  int level, parts, streams;
+  i64 min_n;
+};
+
+SplitCfg split_cfg() {
+  auto env_i = [](const char* k, i64 d) -> i64 {
+    const char* e = std::getenv(k);
+    return e ? std::atoll(e) : d;
+  };
+  SplitCfg c;
+  c.on = env_i("PKD_SPLIT", 1) != 0;
+  c.level = int(env_i("PKD_SPLIT_LEVEL", 2));
+  c.parts = int(env_i("PKD_SPLIT_PARTS", 4));
+  c.streams = int(env_i("PKD_SPLIT_STREAMS", 4));
+  c.min_n = env_i("PKD_SPLIT_MIN_N", i64(48) << 20);
+  return c;
+}
+
 int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 24)))); }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
 int default_subtree_max(int dim) { return subtree_capacity(dim); }
+
+struct SplitStreams {
+  std::mutex mu;
+  int device = -1;
+  std::vector<hipStream_t> side;  // streams 1..S-1 (stream 0 is the caller's)
+  hipEvent_t fork = nullptr;
+  std::vector<hipEvent_t> join;
+  ~SplitStreams() {
+    for (hipStream_t s : side) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : join) (void)hipEventDestroy(e);
+    if (fork) (void)hipEventDestroy(fork);
+  }
+};
+
+SplitStreams* GpuBuilder::split_streams_for(hipStream_t stream) const {
+  if (!split_ || split_parts_ < 2) return nullptr;
+  int dev = 0;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(split_->mu);
+  if (split_->device == dev) return split_.get();
+  if (split_->device >= 0) return nullptr;  // created for another device: build unsplit
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  PKD_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) return nullptr;  // no stream creation inside a capture
+  for (int k = 1; k < split_streams_; ++k) {
+    hipStream_t s = nullptr;
+    PKD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    split_->side.push_back(s);
+    hipEvent_t e = nullptr;
+    PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    split_->join.push_back(e);
+  }
+  PKD_HIP_CHECK(hipEventCreateWithFlags(&split_->fork, hipEventDisableTiming));
+  split_->device = dev;
+  return split_.get();
+}
 
 GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
 
@@ -2076,13 +2136,45 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   i64 max_grid = 1;
   for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
   off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
+  {
+    const SplitCfg sc = split_cfg();
+    const int L = sc.level;
+    const bool paired = lg_ >= 2 && levels_[0].pair;
+    if (sc.on && paired && !narrow_ && dim <= 8 && n_ >= sc.min_n && L >= 2 && L % 2 == 0 && L < lg_ &&
+        sc.parts >= 2 && sc.streams >= 1) {
+      const int P = std::min(pow2_floor(sc.parts), 1 << L);
+      split_level_ = L;
+      split_parts_ = P;
+      split_streams_ = std::max(1, std::min(sc.streams, P));
+      size_t hw = 1, h2w = 1, bw = 1;
+      for (int l = L; l < lg_; ++l) {  // the part's share of every per-segment array
+        const LevelPlan& lp = levels_[size_t(l)];
+        const i64 sp = lp.segs / P;
+        if (l > L) hw = std::max(hw, size_t(sp) * size_t(lp.bins));
+        if (lp.stage2) h2w = std::max(h2w, size_t(sp) * size_t(kBins2));
+        const i64 chunk = i64(kChunk);
+        const i64 pb = std::max<i64>(1, std::min<i64>(i64(lp.bps) * P / std::max(1, std::min(sc.streams, P)),
+                                                      (lp.nmax + chunk - 1) / chunk));
+        bw = std::max(bw, size_t(sp) * size_t(std::max<i64>(pb, lp.bps)) * 8);
+      }
+      split_hist_ = hw;
+      split_hist2_ = h2w;
+      split_bcnt_ = bw;
+      split_set_bytes_ = align_up(2 * hw * 4) + align_up(h2w * 4) + align_up(bw * 4);
+      off_split_ = take(split_set_bytes_ * size_t(split_streams_));
+      split_ = std::make_shared<SplitStreams>();
+    }
+  }
   ws_bytes_ = off;
 }
 
 std::string GpuBuilder::describe() const {
   std::ostringstream os;
   os << "GpuBuilder(n=" << n_ << ", dim=" << dim_ << ", global_levels=" << lg_ << ", subtree_max=" << nsub_
-     << ", workspace=" << ws_bytes_ << "B)";
+     << ", workspace=" << ws_bytes_ << "B";
+  if (split_parts_ > 1)
+    os << ", split at level " << split_level_ << " into " << split_parts_ << " parts on " << split_streams_ << " streams";
+  os << ")";
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
        << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
@@ -2208,157 +2300,223 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
   PKD_LAUNCH_CHECK();
 
+  // Levels [l0, l1) of segment range `part` of `nparts` (at level l: segments
+  // [part * segs / nparts, (part + 1) * segs / nparts)) on stream `st`. The per-segment arrays
+  // indexed by the level-relative segment (histograms, stage-2 histograms, block counts) come
+  // from `hs`; only level l0 > 0 reads its histogram from the shared arrays, where the
+  // previous (unsplit) pass wrote it.
+  struct HistSet {
+    u32* h[2];
+    u32* h2;
+    u32* bcnt;
+  };
+  auto run_range = [&](int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs, float*& src,
+                       float*& dst) {
+    auto hist_of = [&](int l) -> u32* {
+      if (l0 > 0 && l == l0)
+        return hist[l & 1] + size_t(part) * size_t(levels_[size_t(l)].segs / nparts) * size_t(levels_[size_t(l)].bins);
+      return hs.h[(l - l0) & 1];
+    };
+    // A part's kernels run next to split_streams_ - 1 others: its blocks per segment scale by
+    // parts / streams so the concurrent grids together match the unsplit level's grid.
+    auto bps_of = [&](int l) -> int {
+      const LevelPlan& lp = levels_[size_t(l)];
+      if (nparts == 1) return lp.bps;
+      const i64 chunk = dim_ <= 8 ? i64(kChunk) : i64(kBlock) * 4;
+      const i64 want = i64(lp.bps) * nparts / std::max(1, split_streams_);
+      return int(std::max<i64>(1, std::min<i64>(want, (lp.nmax + chunk - 1) / chunk)));
+    };
+    auto level_args = [&](int l) {
+      const LevelPlan& lp = levels_[size_t(l)];
+      LevelArgs a;
+      a.src = src;
+      a.dst = dst;
+      a.ncol = ncol_;
+      a.dim = dim_;
+      a.seg_lo = seg_lo;
+      a.seg_n = seg_n;
+      a.state = state;
+      a.params = params;
+      a.cells = cells;
+      a.heap0 = lp.segs - 1 + i64(part) * (lp.segs / nparts);
+      a.bps = bps_of(l);
+      a.axis = lp.axis;
+      a.next_axis = (opt_.depth0 + l + 1) % dim_;
+      a.bins = lp.bins;
+      a.next_bins = lp.next_bins;
+      a.hist = hist_of(l);
+      a.hist_next = l + 1 < lg_ ? hist_of(l + 1) : nullptr;
+      a.out_pts = out_pts;
+      a.out_ids = out_ids;
+      a.err = err;
+      a.block_reserve = (lp.segs <= 8 && lp.bps > 4) ? 1 : 0;  // only where cursor contention is high
+      a.small_done = 0;
+      a.hist2 = hs.h2;
+      a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
+      a.narrow = in_rows ? 1 : 0;
+      a.kcol = a.narrow ? l : a.axis;
+      a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
+      a.idcol = a.narrow ? narrow_k : dim_;
+      a.ncols = a.narrow ? narrow_k + 2 : dim_ + 1;
+      a.colgroup = colgroup(a.ncols - 1);
+      a.in_rows = in_rows;
+      a.in_rs = in_rs;
+      a.id_base0 = id_base;
+      return a;
+    };
+    auto refine = [&](LevelArgs& a, i64 segs) {
+      a.small_done = dim_ <= 8 ? 1 : 0;
+      if (a.small_done) {
+        const int g = int((segs + 3) / 4);
+        with_ncol(dim_, [&](auto nc) {
+          constexpr int NC = decltype(nc)::value > 0 ? decltype(nc)::value : 9;
+          k_refine_both<NC, kRefineCap><<<g + int(segs), kBlock, size_t(kRefineCap) * 12, st>>>(a, segs, g);
+        });
+      } else {
+        k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, st>>>(a);
+      }
+      PKD_LAUNCH_CHECK();
+    };
+    static const char* const kLevelNames[] = {"pkd.level0", "pkd.level1", "pkd.level2", "pkd.level3",
+                                              "pkd.level4", "pkd.level5", "pkd.level6", "pkd.level7",
+                                              "pkd.level8", "pkd.level9", "pkd.level10", "pkd.level11+"};
+    for (int l = l0; l < l1;) {
+      const LevelPlan& lp = levels_[size_t(l)];
+      const i64 segs = lp.segs / nparts;  // this part's segments at level l
+      TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
+      LevelArgs a = level_args(l);
+      if (l == 0) {
+        zero_u32(hist[0], lp.segs * lp.bins, st);
+        LevelArgs ah = a;  // like k_scan: fewer blocks, fewer histogram flush atomics
+        ah.bps = std::max(1, a.bps / hist_div());
+        k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, st>>>(ah, hist[0]);
+        PKD_LAUNCH_CHECK();
+      }
+      k_select<<<int(segs), kBlock, 0, st>>>(a);
+      PKD_LAUNCH_CHECK();
+      if (lp.stage2) {
+        zero_u32(a.hist2, segs * kBins2, st);
+        k_hist2<<<int(segs * a.bps), kBlock, 0, st>>>(a);
+        PKD_LAUNCH_CHECK();
+        k_select2<<<int(segs), kBlock, 0, st>>>(a);
+        PKD_LAUNCH_CHECK();
+      }
+      const int grid = int(segs * a.bps);
+      if (lp.pair) {
+        const LevelPlan& lq = levels_[size_t(l + 1)];
+        const i64 segs1 = lq.segs / nparts;
+        const size_t lds_a = size_t(2 * lp.next_bins + 64) * 4;
+        const int gs = int((segs + 3) / 4);
+        with_ncol(dim_, [&](auto nc) {
+          constexpr int NC = decltype(nc)::value;
+          if constexpr (NC > 0) {
+            LevelArgs as = a;  // the scan's own block split (its histogram flush scales with blocks)
+            as.bps = std::max(1, a.bps / scan_div());
+            k_scan<NC><<<int(segs * as.bps), kBlock, lds_a, st>>>(as);
+            PKD_LAUNCH_CHECK();
+            k_pivot_both<NC><<<gs + int(segs), kBlock, 0, st>>>(a, segs, gs);
+            PKD_LAUNCH_CHECK();
+          }
+        });
+        LevelArgs b = level_args(l + 1);
+        k_select<<<int(segs1), kBlock, 0, st>>>(b);
+        PKD_LAUNCH_CHECK();
+        PairArgs pa;
+        pa.stage2_1 = lq.stage2 ? 1 : 0;
+        pa.bins1 = lq.bins;
+        pa.axis2 = (opt_.depth0 + l + 2) % dim_;
+        pa.bins2 = lq.next_bins;
+        pa.hist2n = l + 2 < lg_ ? hist_of(l + 2) : hist_of(l);
+        // the second-stage pass of level l+1 reads what the block-reserve count pass would:
+        // it also counts each block's certain rows, and the scatter writes from prefix offsets
+        const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
+        if (pfx) {
+          pa.bcnt = hs.bcnt;
+          pa.bbase = pa.bcnt + size_t(grid) * 4;
+        }
+        if (lq.stage2) {
+          zero_u32(b.hist2, segs1 * kBins2, st);
+          k_hist2p<<<grid, kBlock, 0, st>>>(a, pa);
+          PKD_LAUNCH_CHECK();
+          k_select2<<<int(segs1), kBlock, 0, st>>>(b);
+          PKD_LAUNCH_CHECK();
+        }
+        if (pfx) {
+          k_block_bases<<<int(segs), kBlock, 0, st>>>(a, pa);
+          PKD_LAUNCH_CHECK();
+        }
+        const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
+        with_ncol(dim_, [&](auto nc) {
+          constexpr int NC = decltype(nc)::value;
+          if constexpr (NC > 0) {
+            constexpr int KI = NC <= 5 ? 8 : 4;
+            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
+          }
+        });
+        PKD_LAUNCH_CHECK();
+        refine(b, segs1);
+        std::swap(src, dst);
+        l += 2;
+        continue;
+      }
+      const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
+      with_ncol(dim_, [&](auto nc) {
+        constexpr int NC = decltype(nc)::value;
+        if (NC > 0 && NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, st>>>(a);
+        else if (NC > 0 && NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, st>>>(a);
+        else k_partition<NC, 4><<<grid, kBlock, lds, st>>>(a);
+      });
+      PKD_LAUNCH_CHECK();
+      refine(a, segs);
+      std::swap(src, dst);
+      l += 1;
+    }
+  };
+  auto subtree = [&](int part, int nparts, hipStream_t st, const float* src) {
+    const i64 leaves = i64(1) << lg_;
+    const i64 heap0 = leaves - 1 + i64(part) * (leaves / nparts);
+    TraceRange trs("pkd.subtree");
+    launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, leaves / nparts, opt_.depth0 + lg_, nsub_, out_pts,
+                   out_ids, err, st, in_rows ? narrow_k : -1, in_rows, in_rs);
+  };
+
   float* src = colsA;
   float* dst = colsB;
-  auto level_args = [&](int l) {
-    const LevelPlan& lp = levels_[size_t(l)];
-    LevelArgs a;
-    a.src = src;
-    a.dst = dst;
-    a.ncol = ncol_;
-    a.dim = dim_;
-    a.seg_lo = seg_lo;
-    a.seg_n = seg_n;
-    a.state = state;
-    a.params = params;
-    a.cells = cells;
-    a.heap0 = lp.segs - 1;
-    a.bps = lp.bps;
-    a.axis = lp.axis;
-    a.next_axis = (opt_.depth0 + l + 1) % dim_;
-    a.bins = lp.bins;
-    a.next_bins = lp.next_bins;
-    a.hist = hist[l & 1];
-    a.hist_next = hist[(l + 1) & 1];
-    a.out_pts = out_pts;
-    a.out_ids = out_ids;
-    a.err = err;
-    a.block_reserve = (lp.segs <= 8 && lp.bps > 4) ? 1 : 0;  // only where cursor contention is high
-    a.small_done = 0;
-    a.hist2 = reinterpret_cast<u32*>(ws + off_hist2_);
-    a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
-    a.narrow = in_rows ? 1 : 0;
-    a.kcol = a.narrow ? l : a.axis;
-    a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
-    a.idcol = a.narrow ? narrow_k : dim_;
-    a.ncols = a.narrow ? narrow_k + 2 : dim_ + 1;
-    a.colgroup = colgroup(a.ncols - 1);
-    a.in_rows = in_rows;
-    a.in_rs = in_rs;
-    a.id_base0 = id_base;
-    return a;
-  };
-  auto refine = [&](LevelArgs& a, i64 segs) {
-    a.small_done = dim_ <= 8 ? 1 : 0;
-    if (a.small_done) {
-      const int g = int((segs + 3) / 4);
-      with_ncol(dim_, [&](auto nc) {
-        constexpr int NC = decltype(nc)::value > 0 ? decltype(nc)::value : 9;
-        k_refine_both<NC, kRefineCap><<<g + int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a, segs, g);
-      });
-    } else {
-      k_refine<kRefineCap><<<int(segs), kBlock, size_t(kRefineCap) * 12, stream>>>(a);
-    }
-    PKD_LAUNCH_CHECK();
-  };
-  static const char* const kLevelNames[] = {"pkd.level0", "pkd.level1", "pkd.level2", "pkd.level3",
-                                            "pkd.level4", "pkd.level5", "pkd.level6", "pkd.level7",
-                                            "pkd.level8", "pkd.level9", "pkd.level10", "pkd.level11+"};
-  for (int l = 0; l < lg_;) {
-    const LevelPlan& lp = levels_[size_t(l)];
-    TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
-    LevelArgs a = level_args(l);
-    if (l == 0) {
-      zero_u32(hist[0], lp.segs * lp.bins, stream);
-      LevelArgs ah = a;  // like k_scan: fewer blocks, fewer histogram flush atomics
-      ah.bps = std::max(1, lp.bps / hist_div());
-      k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, stream>>>(ah, hist[0]);
-      PKD_LAUNCH_CHECK();
-    }
-    k_select<<<int(lp.segs), kBlock, 0, stream>>>(a);
-    PKD_LAUNCH_CHECK();
-    if (lp.stage2) {
-      zero_u32(a.hist2, lp.segs * kBins2, stream);
-      k_hist2<<<int(lp.segs * lp.bps), kBlock, 0, stream>>>(a);
-      PKD_LAUNCH_CHECK();
-      k_select2<<<int(lp.segs), kBlock, 0, stream>>>(a);
-      PKD_LAUNCH_CHECK();
-    }
-    const int grid = int(lp.segs * lp.bps);
-    if (lp.pair) {
-      const LevelPlan& lq = levels_[size_t(l + 1)];
-      const size_t lds_a = size_t(2 * lp.next_bins + 64) * 4;
-      const int gs = int((lp.segs + 3) / 4);
-      with_ncol(dim_, [&](auto nc) {
-        constexpr int NC = decltype(nc)::value;
-        if constexpr (NC > 0) {
-          LevelArgs as = a;  // the scan's own block split (its histogram flush scales with blocks)
-          as.bps = std::max(1, lp.bps / scan_div());
-          k_scan<NC><<<int(lp.segs * as.bps), kBlock, lds_a, stream>>>(as);
-          PKD_LAUNCH_CHECK();
-          k_pivot_both<NC><<<gs + int(lp.segs), kBlock, 0, stream>>>(a, lp.segs, gs);
-          PKD_LAUNCH_CHECK();
-        }
-      });
-      LevelArgs b = level_args(l + 1);
-      k_select<<<int(lq.segs), kBlock, 0, stream>>>(b);
-      PKD_LAUNCH_CHECK();
-      PairArgs pa;
-      pa.stage2_1 = lq.stage2 ? 1 : 0;
-      pa.bins1 = lq.bins;
-      pa.axis2 = (opt_.depth0 + l + 2) % dim_;
-      pa.bins2 = lq.next_bins;
-      pa.hist2n = hist[l & 1];
-      // the second-stage pass of level l+1 reads what the block-reserve count pass would:
-      // it also counts each block's certain rows, and the scatter writes from prefix offsets
-      const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
-      if (pfx) {
-        pa.bcnt = reinterpret_cast<u32*>(ws + off_bcnt_);
-        pa.bbase = pa.bcnt + size_t(grid) * 4;
-      }
-      if (lq.stage2) {
-        zero_u32(b.hist2, lq.segs * kBins2, stream);
-        k_hist2p<<<grid, kBlock, 0, stream>>>(a, pa);
-        PKD_LAUNCH_CHECK();
-        k_select2<<<int(lq.segs), kBlock, 0, stream>>>(b);
-        PKD_LAUNCH_CHECK();
-      }
-      if (pfx) {
-        k_block_bases<<<int(lp.segs), kBlock, 0, stream>>>(a, pa);
-        PKD_LAUNCH_CHECK();
-      }
-      const size_t lds_b = size_t(std::max(1, 4 * lq.next_bins)) * 4;
-      with_ncol(dim_, [&](auto nc) {
-        constexpr int NC = decltype(nc)::value;
-        if constexpr (NC > 0) {
-          constexpr int KI = NC <= 5 ? 8 : 4;
-          if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, stream>>>(a, pa);
-          else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, stream>>>(a, pa);
-          else k_partition2<NC, KI><<<grid, kBlock, lds_b, stream>>>(a, pa);
-        }
-      });
-      PKD_LAUNCH_CHECK();
-      refine(b, lq.segs);
-      std::swap(src, dst);
-      l += 2;
-      continue;
-    }
-    const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
-    with_ncol(dim_, [&](auto nc) {
-      constexpr int NC = decltype(nc)::value;
-      if (NC > 0 && NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, stream>>>(a);
-      else if (NC > 0 && NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, stream>>>(a);
-      else k_partition<NC, 4><<<grid, kBlock, lds, stream>>>(a);
-    });
-    PKD_LAUNCH_CHECK();
-    refine(a, lp.segs);
-    std::swap(src, dst);
-    l += 1;
+  const HistSet whole{{hist[0], hist[1]}, reinterpret_cast<u32*>(ws + off_hist2_), reinterpret_cast<u32*>(ws + off_bcnt_)};
+  SplitStreams* sp = (split_parts_ > 1 && !in_rows) ? split_streams_for(stream) : nullptr;
+  if (!sp) {
+    run_range(0, lg_, 0, 1, stream, whole, src, dst);
+    subtree(0, 1, stream, src);
+    return;
   }
-  const i64 heap0 = (i64(1) << lg_) - 1;
-  TraceRange trs("pkd.subtree");
-  launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, i64(1) << lg_, opt_.depth0 + lg_, nsub_, out_pts,
-                 out_ids, err, stream, in_rows ? narrow_k : -1, in_rows, in_rs);
+  // Split build: the top levels on `stream`, then every part's remaining levels and subtree
+  // kernel on its own stream (fork / join through events, so it also captures into a graph).
+  run_range(0, split_level_, 0, 1, stream, whole, src, dst);
+  PKD_HIP_CHECK(hipEventRecord(sp->fork, stream));
+  for (hipStream_t s2 : sp->side) PKD_HIP_CHECK(hipStreamWaitEvent(s2, sp->fork, 0));
+  float* part_src = src;
+  for (int p = 0; p < split_parts_; ++p) {
+    const int k = p % split_streams_;
+    hipStream_t st = k == 0 ? stream : sp->side[size_t(k - 1)];
+    char* set = ws + off_split_ + size_t(k) * split_set_bytes_;
+    u32* h0 = reinterpret_cast<u32*>(set);
+    u32* h1 = h0 + split_hist_;
+    u32* h2 = reinterpret_cast<u32*>(set + align_up(2 * split_hist_ * 4));
+    u32* bc = reinterpret_cast<u32*>(set + align_up(2 * split_hist_ * 4) + align_up(split_hist2_ * 4));
+    const HistSet hs{{h0, h1}, h2, bc};
+    float* s1 = src;
+    float* d1 = dst;
+    run_range(split_level_, lg_, p, split_parts_, st, hs, s1, d1);
+    subtree(p, split_parts_, st, s1);
+    part_src = s1;
+  }
+  (void)part_src;
+  for (size_t k = 0; k < sp->side.size(); ++k) {
+    PKD_HIP_CHECK(hipEventRecord(sp->join[k], sp->side[k]));
+    PKD_HIP_CHECK(hipStreamWaitEvent(stream, sp->join[k], 0));
+  }
 }
 
 }  // namespace pkdtree

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -40,6 +41,8 @@ struct LevelPlan {
   bool pair = false;    // this level and the next are moved by ONE fused partition pass
 };
 
+struct SplitStreams;  // side HIP streams + fork / join events of a split build
+
 class GpuBuilder {
  public:
   GpuBuilder(i64 n, int dim, BuildOptions opt = {});
@@ -49,6 +52,11 @@ class GpuBuilder {
   int dim() const { return dim_; }
   int global_levels() const { return lg_; }
   int subtree_max() const { return nsub_; }
+  // Split build (0 parts: off): from level split_level() on, the 2^split_level segments are
+  // built as split_parts() independent parts on split_streams() HIP streams.
+  int split_level() const { return split_level_; }
+  int split_parts() const { return split_parts_; }
+  int split_streams() const { return split_streams_; }
   const std::vector<LevelPlan>& levels() const { return levels_; }
   size_t workspace_bytes() const { return ws_bytes_; }
   std::string describe() const;
@@ -80,6 +88,9 @@ class GpuBuilder {
   // full rows are gathered from the AoS input `in_rows` (stride in_rs floats).
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
                   u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0) const;
+  // Side streams for a split build on the current device (nullptr: run unsplit, e.g. when
+  // the streams do not exist yet and `stream` is being captured into a graph).
+  SplitStreams* split_streams_for(hipStream_t stream) const;
 
   i64 n_;
   i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)
@@ -97,6 +108,14 @@ class GpuBuilder {
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,
          ws_bytes_ = 0;
+  // Split build: from level split_level_ (a pair boundary) on, segment range p of
+  // split_parts_ runs its remaining levels and its subtree kernel on stream p % split_streams_,
+  // so one part's LDS-bound subtree kernel and small select / pivot launches overlap another
+  // part's HBM-bound passes. Each stream has its own histogram set in the workspace.
+  int split_level_ = 0, split_parts_ = 0, split_streams_ = 0;
+  size_t off_split_ = 0, split_set_bytes_ = 0;
+  size_t split_hist_ = 0, split_hist2_ = 0, split_bcnt_ = 0;  // u32 words per set
+  std::shared_ptr<SplitStreams> split_;
 };
 
 // Subtree kernel capacity for a dimension (largest power of two whose LDS image fits).
