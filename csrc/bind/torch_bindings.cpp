@@ -289,6 +289,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("workspace_bytes", [](const Builder& b) { return int64_t(b.b.workspace_bytes()); })
       .def_property_readonly("global_levels", [](const Builder& b) { return b.b.global_levels(); })
       .def_property_readonly("subtree_max", [](const Builder& b) { return b.b.subtree_max(); })
+      .def_property_readonly("split_parts", [](const Builder& b) { return b.b.split_parts(); })
+      .def_property_readonly("split_level", [](const Builder& b) { return b.b.split_level(); })
+      .def_property_readonly("split_streams", [](const Builder& b) { return b.b.split_streams(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
       .def("read_error", [](Builder& b) {
         u32 d[3];

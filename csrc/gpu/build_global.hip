@@ -2041,7 +2041,9 @@ SplitStreams* GpuBuilder::split_streams_for(hipStream_t stream) const {
   if (cs != hipStreamCaptureStatusNone) return nullptr;  // no stream creation inside a capture
   for (int k = 1; k < split_streams_; ++k) {
     hipStream_t s = nullptr;
-    PKD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const char* pr = std::getenv("PKD_SPLIT_PRIO");
+    if (pr) PKD_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, std::atoi(pr)));
+    else PKD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     split_->side.push_back(s);
     hipEvent_t e = nullptr;
     PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2310,12 +2312,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     u32* h2;
     u32* bcnt;
   };
-  auto run_range = [&](int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs, float*& src,
-                       float*& dst) {
-    auto hist_of = [&](int l) -> u32* {
-      if (l0 > 0 && l == l0)
+  auto run_range = [&](int base, int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs,
+                       float*& src, float*& dst) {
+    auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
+      if (base > 0 && l == base)
         return hist[l & 1] + size_t(part) * size_t(levels_[size_t(l)].segs / nparts) * size_t(levels_[size_t(l)].bins);
-      return hs.h[(l - l0) & 1];
+      return hs.h[(l - base) & 1];
     };
     // A part's kernels run next to split_streams_ - 1 others: its blocks per segment scale by
     // parts / streams so the concurrent grids together match the unsplit level's grid.
@@ -2323,7 +2325,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const LevelPlan& lp = levels_[size_t(l)];
       if (nparts == 1) return lp.bps;
       const i64 chunk = dim_ <= 8 ? i64(kChunk) : i64(kBlock) * 4;
-      const i64 want = i64(lp.bps) * nparts / std::max(1, split_streams_);
+      const char* de = std::getenv("PKD_SPLIT_BPS_DIV");  // A/B knob, read per build
+      const i64 div = de ? std::max<i64>(1, std::atoll(de)) : i64(1);
+      const i64 want = i64(lp.bps) * nparts / (std::max(1, split_streams_) * div);
       return int(std::max<i64>(1, std::min<i64>(want, (lp.nmax + chunk - 1) / chunk)));
     };
     auto level_args = [&](int l) {
@@ -2487,32 +2491,44 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   const HistSet whole{{hist[0], hist[1]}, reinterpret_cast<u32*>(ws + off_hist2_), reinterpret_cast<u32*>(ws + off_bcnt_)};
   SplitStreams* sp = (split_parts_ > 1 && !in_rows) ? split_streams_for(stream) : nullptr;
   if (!sp) {
-    run_range(0, lg_, 0, 1, stream, whole, src, dst);
+    run_range(0, 0, lg_, 0, 1, stream, whole, src, dst);
     subtree(0, 1, stream, src);
     return;
   }
   // Split build: the top levels on `stream`, then every part's remaining levels and subtree
   // kernel on its own stream (fork / join through events, so it also captures into a graph).
-  run_range(0, split_level_, 0, 1, stream, whole, src, dst);
+  run_range(0, 0, split_level_, 0, 1, stream, whole, src, dst);
   PKD_HIP_CHECK(hipEventRecord(sp->fork, stream));
   for (hipStream_t s2 : sp->side) PKD_HIP_CHECK(hipStreamWaitEvent(s2, sp->fork, 0));
-  float* part_src = src;
-  for (int p = 0; p < split_parts_; ++p) {
+  const int P = split_parts_;
+  std::vector<hipStream_t> pst(size_t(P), stream);
+  std::vector<HistSet> phs(size_t(P), whole);
+  std::vector<float*> psrc(size_t(P), src), pdst(size_t(P), dst);
+  for (int p = 0; p < P; ++p) {
     const int k = p % split_streams_;
-    hipStream_t st = k == 0 ? stream : sp->side[size_t(k - 1)];
+    pst[size_t(p)] = k == 0 ? stream : sp->side[size_t(k - 1)];
     char* set = ws + off_split_ + size_t(k) * split_set_bytes_;
     u32* h0 = reinterpret_cast<u32*>(set);
     u32* h1 = h0 + split_hist_;
     u32* h2 = reinterpret_cast<u32*>(set + align_up(2 * split_hist_ * 4));
     u32* bc = reinterpret_cast<u32*>(set + align_up(2 * split_hist_ * 4) + align_up(split_hist2_ * 4));
-    const HistSet hs{{h0, h1}, h2, bc};
-    float* s1 = src;
-    float* d1 = dst;
-    run_range(split_level_, lg_, p, split_parts_, st, hs, s1, d1);
-    subtree(p, split_parts_, st, s1);
-    part_src = s1;
+    phs[size_t(p)] = HistSet{{h0, h1}, h2, bc};
   }
-  (void)part_src;
+  const char* order = std::getenv("PKD_SPLIT_ORDER");
+  if (order && std::string(order) == "breadth") {  // every part's level step, then the next step
+    for (int l = split_level_; l < lg_;) {
+      const int step = levels_[size_t(l)].pair ? 2 : 1;
+      for (int p = 0; p < P; ++p)
+        run_range(split_level_, l, l + step, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
+      l += step;
+    }
+    for (int p = 0; p < P; ++p) subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
+  } else {  // depth first: part p's levels and subtree, then part p + 1
+    for (int p = 0; p < P; ++p) {
+      run_range(split_level_, split_level_, lg_, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
+      subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
+    }
+  }
   for (size_t k = 0; k < sp->side.size(); ++k) {
     PKD_HIP_CHECK(hipEventRecord(sp->join[k], sp->side[k]));
     PKD_HIP_CHECK(hipStreamWaitEvent(stream, sp->join[k], 0));

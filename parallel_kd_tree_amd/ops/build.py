@@ -37,6 +37,11 @@ class GpuTreeBuilder:
     def subtree_max(self) -> int:
         return self._b.subtree_max
 
+    @property
+    def split_parts(self) -> int:
+        """Parts of a split build (0: one stream; see PKD_SPLIT* in README)."""
+        return self._b.split_parts
+
     def describe(self) -> str:
         return self._b.describe()
 

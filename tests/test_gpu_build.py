@@ -187,6 +187,60 @@ def test_hipgraph_replay_equals_eager(gpu_device, n):
     graph_check.check(n)
 
 
+@pytest.mark.parametrize("level,parts,streams", [(2, 4, 4), (2, 4, 2), (4, 16, 3), (4, 8, 1), (6, 64, 4)])
+def test_split_build_equals_cpu(gpu_device, monkeypatch, level, parts, streams):
+    """Split build (from a pair boundary on, segment ranges on several HIP streams with their own
+    histogram sets) at sizes below its default threshold: slot for slot the CPU exact tree."""
+    monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
+    monkeypatch.setenv("PKD_SPLIT_LEVEL", str(level))
+    monkeypatch.setenv("PKD_SPLIT_PARTS", str(parts))
+    monkeypatch.setenv("PKD_SPLIT_STREAMS", str(streams))
+    for seed, dim, n in ((21, 3, 3_000_001), (22, 2, 1_000_000), (23, 8, 700_000)):
+        b = ops.GpuTreeBuilder(n, dim)
+        assert b.split_parts == min(parts, 2 ** level), b.describe()
+        check_same(pk.generate_problem(seed, dim, n), gpu_device)
+
+
+@pytest.mark.parametrize("order", ["depth", "breadth"])
+def test_split_build_stage2_skewed(gpu_device, monkeypatch, order):
+    """Split build whose parts start with second-stage levels and prefix placement (18 M
+    points, split after the first pair) on skewed data, both enqueue orders."""
+    monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
+    monkeypatch.setenv("PKD_SPLIT_ORDER", order)
+    x = pk.generate_problem(6, 3, 18_000_000)
+    x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
+    check_same(x, gpu_device)
+
+
+def test_split_build_hipgraph(gpu_device, monkeypatch):
+    """A split build captured into a hipGraph (fork / join events across the side streams)
+    replays to the eager tree."""
+    monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
+    n, dim = 2_000_003, 3
+    x = pk.generate_slice(9, dim, 0, n, device=gpu_device)
+    b = ops.GpuTreeBuilder(n, dim)
+    assert b.split_parts > 1
+    ep, ei = b.build(x, None, 1)
+    torch.cuda.synchronize()
+    gp, gi = torch.empty_like(ep), torch.empty_like(ei)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.build(x, None, 1, gp, gi)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.build(x, None, 1, gp, gi)
+    gp.zero_()
+    gi.zero_()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert b.read_error() == 0
+    assert torch.equal(gi, ei) and torch.equal(gp, ep)
+
+
 @pytest.mark.parametrize("dim,n,depth0,sub", [(3, 3_000_000, 0, 0), (1, 200_000, 0, 0), (2, 300_001, 0, 0),
                                               (4, 200_000, 1, 0), (5, 150_000, 0, 0), (8, 400_000, 3, 0),
                                               (3, 300_000, 0, 256), (3, 70, 0, 0), (8, 1000, 0, 0)])

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""A/B/A/B timing of split-build variants (environment knobs read at builder construction /
+per build), each tree checked against the one-stream build. Usage:
+  split_ab.py --var unsplit:PKD_SPLIT=0 breadth:PKD_SPLIT_ORDER=breadth ... [--rounds 3]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+import parallel_kd_tree_amd as pk
+from parallel_kd_tree_amd.ops import GpuTreeBuilder
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=100_000_000)
+ap.add_argument("--dim", type=int, default=3)
+ap.add_argument("--var", nargs="+", required=True, help="name:K=V,K=V")
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--steps", type=int, default=10)
+args = ap.parse_args()
+dev = torch.device("cuda:0")
+x = pk.uniform_points(args.n, args.dim, seed=7, device=dev)
+knobs = sorted({kv.split("=")[0] for v in args.var for kv in v.split(":", 1)[1].split(",") if kv})
+
+
+def apply(spec):
+    for k in knobs:
+        os.environ.pop(k, None)
+    for kv in spec.split(","):
+        if kv:
+            k, v = kv.split("=")
+            os.environ[k] = v
+
+
+ref = None
+res = {v.split(":")[0]: [] for v in args.var}
+builders = {}
+for r in range(args.rounds):
+    for v in args.var:
+        name, spec = v.split(":", 1)
+        apply(spec)
+        if name not in builders:
+            b = GpuTreeBuilder(args.n, args.dim)
+            tp, ti = b.build(x)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = ti.clone()
+            assert b.read_error() == 0 and torch.equal(ti, ref), f"{name}: tree differs"
+            builders[name] = (b, tp, ti)
+        b, tp, ti = builders[name]
+        b.build(x, None, 0, tp, ti)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            b.build(x, None, 0, tp, ti)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        res[name].append(round(ms, 3))
+        print(json.dumps({"round": r, "var": name, "ms": round(ms, 3)}), flush=True)
+    for name, (b, tp, ti) in builders.items():
+        assert torch.equal(ti, ref), f"{name}: tree differs after timing"
+print(json.dumps({"summary": {k: {"min": min(v), "all": v} for k, v in res.items()}}), flush=True)

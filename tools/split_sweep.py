@@ -24,8 +24,38 @@ ap.add_argument("--cfg", nargs="+", default=["2,4,4", "2,4,2", "4,16,4", "4,8,4"
                 help="level,parts,streams")
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--min-n", type=int, default=None, help="PKD_SPLIT_MIN_N for the split builders")
+ap.add_argument("--graph", action="store_true", help="also time a hipGraph replay of each build")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
+
+
+def host_ms(b, x, tp, ti):
+    """Host time to enqueue one build (no synchronisation inside)."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    b.build(x, None, 0, tp, ti)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    return (t1 - t0) * 1e3
+
+
+def graph_ms(b, x, tp, ti, steps):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.build(x, None, 0, tp, ti)  # warm: side streams exist before the capture
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.build(x, None, 0, tp, ti)
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps
 
 
 def timed(b, x, tp, ti, steps):
@@ -45,7 +75,11 @@ for dim in args.dim:
         b0 = GpuTreeBuilder(n, dim)
         rp, ri = b0.build(x)
         ms0 = timed(b0, x, rp, ri, args.steps)
-        print(json.dumps({"n": n, "dim": dim, "cfg": "unsplit", "ms": round(ms0, 3), "err": b0.read_error()}), flush=True)
+        extra = {"host_ms": round(host_ms(b0, x, rp, ri), 3)}
+        if args.graph:
+            extra["graph_ms"] = round(graph_ms(b0, x, rp, ri, args.steps), 3)
+        print(json.dumps({"n": n, "dim": dim, "cfg": "unsplit", "ms": round(ms0, 3), "err": b0.read_error(), **extra}),
+              flush=True)
         del b0
         os.environ["PKD_SPLIT"] = "1"
         if args.min_n is not None:
@@ -61,10 +95,14 @@ for dim in args.dim:
             same = bool(torch.equal(ti, ri)) and bool(torch.equal(tp, rp))
             ms = timed(b, x, tp, ti, args.steps)
             same2 = bool(torch.equal(ti, ri))
+            extra = {"host_ms": round(host_ms(b, x, tp, ti), 3)}
+            if args.graph:
+                extra["graph_ms"] = round(graph_ms(b, x, tp, ti, args.steps), 3)
+                extra["same_after_graph"] = bool(torch.equal(ti, ri))
             print(json.dumps({"n": n, "dim": dim, "cfg": cfg, "ms": round(ms, 3), "vs_unsplit": round(ms / ms0, 3),
                               "err": err, "same": same, "same_after_repeat": same2,
-                              "split": "split at" in desc}), flush=True)
-            if not (same and same2 and err == 0):
+                              "split": "split at" in desc, **extra}), flush=True)
+            if not (same and same2 and err == 0 and extra.get("same_after_graph", True)):
                 print("MISMATCH", desc, flush=True)
                 sys.exit(1)
             del b, tp, ti
