@@ -1231,6 +1231,7 @@ struct PairArgs {
   // per-block write offsets bbase[block][4], so k_partition2 needs no counting pass.
   u32* bcnt = nullptr;
   u32* bbase = nullptr;
+  int exp_store = 0;     // timing experiment: coalesced in-place stores instead of the scatter
 };
 
 template <int NCOL>
@@ -1866,6 +1867,10 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
           dest = (c == 0 ? clo0 : clo1) + off;
         }
       }
+      if (pa.exp_store) {  // timing experiment only (PKD_EXP_STORE=1): rows stored in place, tree invalid
+        const i64 e = c0 + i * kBlock + threadIdx.x;
+        dest = e < b1 ? lo + e : -1;
+      }
 #pragma unroll
       for (int c = 0; c < NCOL; ++c)
         if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
@@ -2431,6 +2436,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         pa.axis2 = (opt_.depth0 + l + 2) % dim_;
         pa.bins2 = lq.next_bins;
         pa.hist2n = l + 2 < lg_ ? hist_of(l + 2) : hist_of(l);
+        pa.exp_store = std::getenv("PKD_EXP_STORE") ? 1 : 0;
         // the second-stage pass of level l+1 reads what the block-reserve count pass would:
         // it also counts each block's certain rows, and the scatter writes from prefix offsets
         const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
