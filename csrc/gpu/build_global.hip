@@ -1231,7 +1231,6 @@ struct PairArgs {
   // per-block write offsets bbase[block][4], so k_partition2 needs no counting pass.
   u32* bcnt = nullptr;
   u32* bbase = nullptr;
-  int exp_store = 0;     // timing experiment: coalesced in-place stores instead of the scatter
 };
 
 template <int NCOL>
@@ -1672,13 +1671,16 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
 // offsets; rows in a child's median bucket (their zone is decided by the second stage)
 // form 6 more pseudo-zones placed with cursor atomics.
-template <int NCOL, int KI, bool PFX = false>
+template <int NCOL, int KI, bool PFX = false, bool DB = true>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   constexpr int NZ = PFX ? 12 : 6;
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
-  __shared__ u32 gcnt[NZ][64];
+  // zone counts / bases of a chunk, double-buffered by chunk parity: chunk c + 1's counts
+  // never overwrite what chunk c's stores still read, so a chunk ends without a barrier
+  __shared__ u32 gcnt2[2][NZ][64];
+  u32(*gcnt)[64] = gcnt2[0];
   __shared__ u32 bcur[6];
   __shared__ unsigned long long bmin[2], bmax[2];  // children's middle-zone key ranges, flushed once
   if (threadIdx.x < 2) {
@@ -1792,7 +1794,9 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   }
   __syncthreads();
 
-  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+  int par = 0;
+  for (i64 c0 = b0; c0 < b1; c0 += kChunk, par ^= DB ? 1 : 0) {
+    gcnt = gcnt2[par];
     float row[kItems][NCOL];
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
@@ -1867,16 +1871,13 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
           dest = (c == 0 ? clo0 : clo1) + off;
         }
       }
-      if (pa.exp_store) {  // timing experiment only (PKD_EXP_STORE=1): rows stored in place, tree invalid
-        const i64 e = c0 + i * kBlock + threadIdx.x;
-        dest = e < b1 ? lo + e : -1;
-      }
 #pragma unroll
       for (int c = 0; c < NCOL; ++c)
         if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
     }
-    __syncthreads();
+    if (!DB) __syncthreads();
   }
+  __syncthreads();  // every wave's LDS histogram / key-range atomics before the flush
   if (threadIdx.x < 2 && bmin[threadIdx.x] != ~0ull) {
     SegState* cs = threadIdx.x == 0 ? cst0 : cst1;
     atomicMin(&cs->mid_min, bmin[threadIdx.x]);
@@ -2436,7 +2437,6 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         pa.axis2 = (opt_.depth0 + l + 2) % dim_;
         pa.bins2 = lq.next_bins;
         pa.hist2n = l + 2 < lg_ ? hist_of(l + 2) : hist_of(l);
-        pa.exp_store = std::getenv("PKD_EXP_STORE") ? 1 : 0;
         // the second-stage pass of level l+1 reads what the block-reserve count pass would:
         // it also counts each block's certain rows, and the scatter writes from prefix offsets
         const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
@@ -2460,9 +2460,13 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             constexpr int KI = NC <= 5 ? 8 : 4;
-            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            const char* dbe = std::getenv("PKD_PART_DBUF");  // A/B knob
+            const bool db = !(dbe && std::string(dbe) == "0");
+            if (pfx && db) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else if (pfx) k_partition2<NC, KI, true, false><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else if (db) k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else k_partition2<NC, KI, false, false><<<grid, kBlock, lds_b, st>>>(a, pa);
           }
         });
         PKD_LAUNCH_CHECK();
