@@ -2028,9 +2028,11 @@ struct SplitStreams {
   std::vector<hipStream_t> side;  // streams 1..S-1 (stream 0 is the caller's)
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> join;
+  std::vector<hipEvent_t> part;  // pipelined order: part p's passes done
   ~SplitStreams() {
     for (hipStream_t s : side) (void)hipStreamDestroy(s);
     for (hipEvent_t e : join) (void)hipEventDestroy(e);
+    for (hipEvent_t e : part) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
   }
 };
@@ -2056,6 +2058,11 @@ SplitStreams* GpuBuilder::split_streams_for(hipStream_t stream) const {
     split_->join.push_back(e);
   }
   PKD_HIP_CHECK(hipEventCreateWithFlags(&split_->fork, hipEventDisableTiming));
+  for (int p = 0; p < split_parts_; ++p) {
+    hipEvent_t e = nullptr;
+    PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    split_->part.push_back(e);
+  }
   split_->device = dev;
   return split_.get();
 }
@@ -2318,6 +2325,11 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     u32* h2;
     u32* bcnt;
   };
+  // Parts whose passes run at the same time (their grids share the chip): all streams, or one
+  // in the pipelined order (passes of one part at a time, subtree kernels on a second stream).
+  const char* order = std::getenv("PKD_SPLIT_ORDER");
+  const bool pipe = split_parts_ > 1 && split_streams_ >= 2 && order && std::string(order) == "pipe";
+  const int part_conc = pipe ? 1 : split_streams_;
   auto run_range = [&](int base, int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs,
                        float*& src, float*& dst) {
     auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
@@ -2333,7 +2345,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const i64 chunk = dim_ <= 8 ? i64(kChunk) : i64(kBlock) * 4;
       const char* de = std::getenv("PKD_SPLIT_BPS_DIV");  // A/B knob, read per build
       const i64 div = de ? std::max<i64>(1, std::atoll(de)) : i64(1);
-      const i64 want = i64(lp.bps) * nparts / (std::max(1, split_streams_) * div);
+      const i64 want = i64(lp.bps) * nparts / (std::max(1, part_conc) * div);
       return int(std::max<i64>(1, std::min<i64>(want, (lp.nmax + chunk - 1) / chunk)));
     };
     auto level_args = [&](int l) {
@@ -2460,8 +2472,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             constexpr int KI = NC <= 5 ? 8 : 4;
-            const char* dbe = std::getenv("PKD_PART_DBUF");  // A/B knob
-            const bool db = !(dbe && std::string(dbe) == "0");
+            // Double-buffered zone counts (no barrier at a chunk's end) pay where the pass shares
+            // the chip with other streams' kernels: split parts 12.27 -> 11.82 ms per 100M x 3D
+            // build, while a pass alone on the chip is 0.7% faster with the barrier
+            // (profiles/r2_split_build.txt). PKD_PART_DBUF=0/1 forces either.
+            const char* dbe = std::getenv("PKD_PART_DBUF");
+            const bool db = dbe ? std::string(dbe) != "0" : nparts > 1;
             if (pfx && db) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (pfx) k_partition2<NC, KI, true, false><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
@@ -2524,8 +2540,30 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     u32* bc = reinterpret_cast<u32*>(set + align_up(2 * split_hist_ * 4) + align_up(split_hist2_ * 4));
     phs[size_t(p)] = HistSet{{h0, h1}, h2, bc};
   }
-  const char* order = std::getenv("PKD_SPLIT_ORDER");
-  if (order && std::string(order) == "breadth") {  // every part's level step, then the next step
+  // PKD_SPLIT_TRACE=1 (debug, synchronises): when each part's first and last kernel ran,
+  // relative to the fork, printed to stderr
+  const bool trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
+  std::vector<hipEvent_t> tev;
+  auto tmark = [&](hipStream_t st2) {
+    if (!trace) return;
+    hipEvent_t e = nullptr;
+    PKD_HIP_CHECK(hipEventCreate(&e));
+    PKD_HIP_CHECK(hipEventRecord(e, st2));
+    tev.push_back(e);
+  };
+  tmark(stream);
+  if (pipe) {  // passes of part p on `stream`, its subtree kernel on the first side stream
+    hipStream_t sub = sp->side[0];
+    for (int p = 0; p < P; ++p) {
+      tmark(stream);
+      run_range(split_level_, split_level_, lg_, p, P, stream, phs[0], psrc[size_t(p)], pdst[size_t(p)]);
+      PKD_HIP_CHECK(hipEventRecord(sp->part[size_t(p)], stream));
+      PKD_HIP_CHECK(hipStreamWaitEvent(sub, sp->part[size_t(p)], 0));
+      tmark(sub);
+      subtree(p, P, sub, psrc[size_t(p)]);
+      tmark(sub);
+    }
+  } else if (order && std::string(order) == "breadth") {  // every part's level step, then the next step
     for (int l = split_level_; l < lg_;) {
       const int step = levels_[size_t(l)].pair ? 2 : 1;
       for (int p = 0; p < P; ++p)
@@ -2535,13 +2573,30 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     for (int p = 0; p < P; ++p) subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
   } else {  // depth first: part p's levels and subtree, then part p + 1
     for (int p = 0; p < P; ++p) {
+      tmark(pst[size_t(p)]);
       run_range(split_level_, split_level_, lg_, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
+      tmark(pst[size_t(p)]);
       subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
+      tmark(pst[size_t(p)]);
     }
   }
   for (size_t k = 0; k < sp->side.size(); ++k) {
     PKD_HIP_CHECK(hipEventRecord(sp->join[k], sp->side[k]));
     PKD_HIP_CHECK(hipStreamWaitEvent(stream, sp->join[k], 0));
+  }
+  if (trace) {
+    PKD_HIP_CHECK(hipStreamSynchronize(stream));
+    std::ostringstream os;
+    os << "split trace (ms after the fork; part: start / subtree start / end):";
+    for (size_t i = 1; i + 2 < tev.size(); i += 3) {
+      float t0 = 0, t1 = 0, t2 = 0;
+      PKD_HIP_CHECK(hipEventElapsedTime(&t0, tev[0], tev[i]));
+      PKD_HIP_CHECK(hipEventElapsedTime(&t1, tev[0], tev[i + 1]));
+      PKD_HIP_CHECK(hipEventElapsedTime(&t2, tev[0], tev[i + 2]));
+      os << " [" << (i - 1) / 3 << ": " << t0 << " / " << t1 << " / " << t2 << "]";
+    }
+    std::fprintf(stderr, "%s\n", os.str().c_str());
+    for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   }
 }
 

@@ -20,6 +20,7 @@ ap.add_argument("--dim", type=int, default=3)
 ap.add_argument("--var", nargs="+", required=True, help="name:K=V,K=V")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--fresh", action="store_true", help="a new builder per measurement, destroyed after it")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 x = pk.uniform_points(args.n, args.dim, seed=7, device=dev)
@@ -51,6 +52,8 @@ for r in range(args.rounds):
             assert b.read_error() == 0 and torch.equal(ti, ref), f"{name}: tree differs"
             builders[name] = (b, tp, ti)
         b, tp, ti = builders[name]
+        if args.fresh and r > 0:  # one builder (and its side streams) alive at a time
+            b = GpuTreeBuilder(args.n, args.dim)
         b.build(x, None, 0, tp, ti)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -59,7 +62,12 @@ for r in range(args.rounds):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
         res[name].append(round(ms, 3))
+        if args.fresh:
+            assert b.read_error() == 0 and torch.equal(ti, ref), f"{name}: tree differs"
+            builders[name] = (None, tp, ti)
+            del b
+            torch.cuda.synchronize()
         print(json.dumps({"round": r, "var": name, "ms": round(ms, 3)}), flush=True)
-    for name, (b, tp, ti) in builders.items():
+    for name, (_, tp, ti) in builders.items():
         assert torch.equal(ti, ref), f"{name}: tree differs after timing"
 print(json.dumps({"summary": {k: {"min": min(v), "all": v} for k, v in res.items()}}), flush=True)
