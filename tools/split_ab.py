@@ -21,6 +21,7 @@ ap.add_argument("--var", nargs="+", required=True, help="name:K=V,K=V")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--fresh", action="store_true", help="a new builder per measurement, destroyed after it")
+ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the build instead of eager builds")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 x = pk.uniform_points(args.n, args.dim, seed=7, device=dev)
@@ -56,10 +57,27 @@ for r in range(args.rounds):
             b = GpuTreeBuilder(args.n, args.dim)
         b.build(x, None, 0, tp, ti)
         torch.cuda.synchronize()
+        g = None
+        if args.graph:
+            cs = torch.cuda.Stream()
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                b.build(x, None, 0, tp, ti)
+            torch.cuda.current_stream().wait_stream(cs)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                b.build(x, None, 0, tp, ti)
+            g.replay()
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            b.build(x, None, 0, tp, ti)
+            if g is not None:
+                g.replay()
+            else:
+                b.build(x, None, 0, tp, ti)
         torch.cuda.synchronize()
+        del g
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
         res[name].append(round(ms, 3))
         if args.fresh:
