@@ -2472,12 +2472,10 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             constexpr int KI = NC <= 5 ? 8 : 4;
-            // Double-buffered zone counts (no barrier at a chunk's end) pay where the pass shares
-            // the chip with other streams' kernels: split parts 12.27 -> 11.82 ms per 100M x 3D
-            // build, while a pass alone on the chip is 0.7% faster with the barrier
-            // (profiles/r2_split_build.txt). PKD_PART_DBUF=0/1 forces either.
+            // Double-buffered zone counts (no barrier at a chunk's end, PKD_PART_DBUF=1) measured
+            // time-neutral to 0.7% slower, split or not (profiles/r2_split_build.txt): off.
             const char* dbe = std::getenv("PKD_PART_DBUF");
-            const bool db = dbe ? std::string(dbe) != "0" : nparts > 1;
+            const bool db = dbe && std::string(dbe) == "1";
             if (pfx && db) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (pfx) k_partition2<NC, KI, true, false><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
