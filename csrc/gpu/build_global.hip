@@ -1671,16 +1671,13 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
 // offsets; rows in a child's median bucket (their zone is decided by the second stage)
 // form 6 more pseudo-zones placed with cursor atomics.
-template <int NCOL, int KI, bool PFX = false, bool DB = true>
+template <int NCOL, int KI, bool PFX = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   constexpr int NZ = PFX ? 12 : 6;
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
-  // zone counts / bases of a chunk, double-buffered by chunk parity: chunk c + 1's counts
-  // never overwrite what chunk c's stores still read, so a chunk ends without a barrier
-  __shared__ u32 gcnt2[2][NZ][64];
-  u32(*gcnt)[64] = gcnt2[0];
+  __shared__ u32 gcnt[NZ][64];
   __shared__ u32 bcur[6];
   __shared__ unsigned long long bmin[2], bmax[2];  // children's middle-zone key ranges, flushed once
   if (threadIdx.x < 2) {
@@ -1794,9 +1791,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   }
   __syncthreads();
 
-  int par = 0;
-  for (i64 c0 = b0; c0 < b1; c0 += kChunk, par ^= DB ? 1 : 0) {
-    gcnt = gcnt2[par];
+  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
     float row[kItems][NCOL];
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
@@ -1875,9 +1870,8 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       for (int c = 0; c < NCOL; ++c)
         if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
     }
-    if (!DB) __syncthreads();
+    __syncthreads();
   }
-  __syncthreads();  // every wave's LDS histogram / key-range atomics before the flush
   if (threadIdx.x < 2 && bmin[threadIdx.x] != ~0ull) {
     SegState* cs = threadIdx.x == 0 ? cst0 : cst1;
     atomicMin(&cs->mid_min, bmin[threadIdx.x]);
@@ -2472,15 +2466,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             constexpr int KI = NC <= 5 ? 8 : 4;
-            // Double-buffered zone counts (no barrier at a chunk's end, PKD_PART_DBUF=1) measured
-            // time-neutral to 0.7% slower, split or not (profiles/r2_split_build.txt): off.
-            const char* dbe = std::getenv("PKD_PART_DBUF");
-            const bool db = dbe && std::string(dbe) == "1";
-            if (pfx && db) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else if (pfx) k_partition2<NC, KI, true, false><<<grid, kBlock, lds_b, st>>>(a, pa);
+            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else if (db) k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else k_partition2<NC, KI, false, false><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
           }
         });
         PKD_LAUNCH_CHECK();
