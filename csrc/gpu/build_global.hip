@@ -1671,7 +1671,7 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
 // offsets; rows in a child's median bucket (their zone is decided by the second stage)
 // form 6 more pseudo-zones placed with cursor atomics.
-template <int NCOL, int KI, bool PFX = false>
+template <int NCOL, int KI, bool PFX = false, bool VEC = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
@@ -1791,20 +1791,49 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   }
   __syncthreads();
 
-  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+  // VEC: each thread loads 4 consecutive rows of a column with one 16-B load (item i = 4 g + j is
+  // row 4 (g * kBlock + tid) + j of a chunk that starts on a 16-B aligned absolute row; rows
+  // outside [b0, b1) are loaded from the padded buffer and masked)
+  const i64 cstart = VEC ? (((lo + b0) & ~i64(3)) - lo) : b0;
+  for (i64 c0 = cstart; c0 < b1; c0 += kChunk) {
     float row[kItems][NCOL];
+    bool vld[kItems];
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      const i64 e = c0 + i * kBlock + threadIdx.x;
-      const i64 p = lo + (e < b1 ? e : b0);
+      for (int g = 0; g < kItems / 4; ++g) {
+        const i64 e4 = c0 + (i64(g) * kBlock + threadIdx.x) * 4;  // relative row of sub-item 0
+        const bool any = e4 < b1;
+        const i64 p4 = lo + (any ? e4 : (((lo + b0) & ~i64(3)) - lo));
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c)
-        row[i][c] = (c == D && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : src[i64(c) * nc + p];
+        for (int c = 0; c < NCOL; ++c) {
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (!(c == D && a.id_implicit)) v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
+          row[4 * g + 0][c] = v.x;
+          row[4 * g + 1][c] = v.y;
+          row[4 * g + 2][c] = v.z;
+          row[4 * g + 3][c] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const i64 e = e4 + j;
+          vld[4 * g + j] = e >= b0 && e < b1;
+          if (D >= 0 && a.id_implicit) row[4 * g + j][D] = __uint_as_float(a.id_base0 + u32(lo + e));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kItems; ++i) {
+        const i64 e = c0 + i * kBlock + threadIdx.x;
+        const i64 p = lo + (e < b1 ? e : b0);
+        vld[i] = e < b1;
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c)
+          row[i][c] = (c == D && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : src[i64(c) * nc + p];
+      }
     }
     u32 zone_pre[kItems];  // (zone index << 16) | rank-in-wave; index q, or 6 + q (PFX uncertain), 15 none
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
-      const i64 e = c0 + i * kBlock + threadIdx.x;
       float k0 = row[i][0], k1 = row[i][0], k2 = row[i][0];
 #pragma unroll
       for (int c = 1; c < D; ++c) {
@@ -1813,7 +1842,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
         k2 = c == ax2 ? row[i][c] : k2;
       }
       bool unc;
-      const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), e < b1, unc);
+      const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), vld[i], unc);
       const u32 zi = q >= 6 ? 15u : (PFX && unc ? q + 6 : q);
       u32 my = 0;
 #pragma unroll
@@ -2466,8 +2495,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             constexpr int KI = NC <= 5 ? 8 : 4;
-            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            // 16-B row loads (4 consecutive rows of a column per lane): one load instruction per
+            // 4 rows per column; the pass is bound by requests in flight per CU, not by HBM
+            // (profiles/r2_split_build.txt, CU masks). 100M x 3D 12.73 -> 12.52 ms one-stream,
+            // 12.22 -> 12.12 split. PKD_PART_VEC=0: one row per load.
+            const char* ve = std::getenv("PKD_PART_VEC");
+            const bool vec = !(ve && std::string(ve) == "0");
+            if (pfx && vec) k_partition2<NC, KI, true, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
             else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else if (vec) k_partition2<NC, KI, false, true><<<grid, kBlock, lds_b, st>>>(a, pa);
             else k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
           }
         });
