@@ -436,6 +436,49 @@ __device__ __forceinline__ void wave_minmax_atomic(bool active, u64 k, unsigned 
   }
 }
 
+// Sweep of one or two key columns over rows [lo + b0, lo + b1) with 16-B loads: the aligned
+// bulk 4 rows per lane per load (2 loads per column in flight), the up to 3 rows before and
+// after it one per lane. f(k0, k1, e) is called for every row (e relative to lo); no wave
+// operations inside f (rows are not visited by all lanes together).
+template <int NK, class F>
+__device__ __forceinline__ void sweep_keys(const float* c0, const float* c1, i64 lo, i64 b0, i64 b1, F&& f) {
+  const i64 abs0 = lo + b0, abs1 = lo + b1;
+  const i64 A = min(abs1, (abs0 + 3) & ~i64(3));
+  const i64 nv = (abs1 - A) >> 2;
+  const i64 Bend = A + 4 * nv;
+  {
+    const int t = int(threadIdx.x);
+    const bool head = t < 3 && abs0 + t < A, tail = t >= 3 && t < 6 && Bend + (t - 3) < abs1;
+    if (head | tail) {
+      const i64 p = head ? abs0 + t : Bend + (t - 3);
+      f(c0[p], NK > 1 ? c1[p] : 0.0f, p - lo);
+    }
+  }
+  const float4* v0 = reinterpret_cast<const float4*>(c0 + A);
+  const float4* v1 = reinterpret_cast<const float4*>((NK > 1 ? c1 : c0) + A);
+  constexpr int U4 = 2;
+  for (i64 w0 = 0; w0 < nv; w0 += i64(kBlock) * U4) {
+    float4 k[U4], m[U4];
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = w0 + i64(u) * kBlock + threadIdx.x;
+      const i64 vi = v < nv ? v : 0;
+      k[u] = v0[vi];
+      if (NK > 1) m[u] = v1[vi];
+    }
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = w0 + i64(u) * kBlock + threadIdx.x;
+      if (v >= nv) continue;
+      const i64 e = A - lo + 4 * v;
+      f(k[u].x, NK > 1 ? m[u].x : 0.0f, e);
+      f(k[u].y, NK > 1 ? m[u].y : 0.0f, e + 1);
+      f(k[u].z, NK > 1 ? m[u].z : 0.0f, e + 2);
+      f(k[u].w, NK > 1 ? m[u].w : 0.0f, e + 3);
+    }
+  }
+}
+
 // Histogram of a level's keys (used for the first global level only; later levels get
 // theirs from the fused partition pass).
 __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ hist) {
@@ -449,19 +492,8 @@ __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ 
   const i64 per = (n + a.bps - 1) / a.bps;
   const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
   const BucketParams p = a.params[h];
-  const float* key = a.src + i64(a.kcol) * a.ncol + lo;
-  constexpr int U = 8;
-  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
-    float k[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock;
-      k[u] = e < b1 ? key[e] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (e0 + i64(u) * kBlock < b1) atomicAdd(&sh[bucket_of(k[u], p, a.bins)], 1u);
-  }
+  const float* key = a.src + i64(a.kcol) * a.ncol;
+  sweep_keys<1>(key, key, lo, b0, b1, [&](float k, float, i64) { atomicAdd(&sh[bucket_of(k, p, a.bins)], 1u); });
   __syncthreads();
   for (int b = threadIdx.x; b < a.bins; b += kBlock) {
     const u32 v = sh[b];
@@ -586,21 +618,10 @@ __global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
   BucketParams p2;
   p2.lo = st->p2lo;
   p2.scale = st->p2scale;
-  const float* key = a.src + i64(a.kcol) * a.ncol + lo;
-  constexpr int U = 8;
-  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
-    float k[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock;
-      k[u] = e < b1 ? key[e] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock;
-      if (e < b1 && bucket_of(k[u], p, a.bins) == bstar) atomicAdd(&sh[bucket_of(k[u], p2, kBins2)], 1u);
-    }
-  }
+  const float* key = a.src + i64(a.kcol) * a.ncol;
+  sweep_keys<1>(key, key, lo, b0, b1, [&](float k, float, i64) {
+    if (bucket_of(k, p, a.bins) == bstar) atomicAdd(&sh[bucket_of(k, p2, kBins2)], 1u);
+  });
   __syncthreads();
   for (int b = threadIdx.x; b < kBins2; b += kBlock) {
     const u32 v = sh[b];
@@ -1573,41 +1594,28 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
   const BucketParams q0{c0->p2lo, c0->p2scale}, q1{c1->p2lo, c1->p2scale};
   const u32 cb0 = c0->bstar, cb1 = c1->bstar;
   const i64 nc = a.ncol;
-  const float* kc = a.src + i64(a.axis) * nc + lo;
-  const float* k1c = a.src + i64(a.next_axis) * nc + lo;
+  const float* kc = a.src + i64(a.axis) * nc;
+  const float* k1c = a.src + i64(a.next_axis) * nc;
   __shared__ u32 bc[4];
   if (threadIdx.x < 4) bc[threadIdx.x] = 0;
   u32 cnt[4] = {0, 0, 0, 0};  // certain rows: child 0 left / right, child 1 left / right
   __syncthreads();
-  constexpr int U = 8;
-  for (i64 e0 = b0 + threadIdx.x; e0 < b1; e0 += kBlock * U) {
-    float k0[U], k1[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock;
-      k0[u] = e < b1 ? kc[e] : 0.0f;
-      k1[u] = e < b1 ? k1c[e] : 0.0f;
+  sweep_keys<2>(kc, k1c, lo, b0, b1, [&](float k0, float k1, i64 e) {
+    const u32 z0 = zone_of(k0, prm, a.bins, bstar, stage2, p2, sbstar);
+    u32 c = z0 == 0 ? 0u : 1u;
+    if (z0 == 1) {
+      const u64 ck = composite_key(k0, src_id(a, lo + e));
+      if (ck == pivot) return;
+      c = ck < pivot ? 0u : 1u;
     }
+    const u32 bk = bucket_of(k1, c == 0 ? cpr0 : cpr1, pa.bins1), cb = c == 0 ? cb0 : cb1;
+    if (bk == cb) {
+      atomicAdd(&sh[c * kBins2 + bucket_of(k1, c == 0 ? q0 : q1, kBins2)], 1u);
+    } else {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const i64 e = e0 + i64(u) * kBlock;
-      if (e >= b1) continue;
-      const u32 z0 = zone_of(k0[u], prm, a.bins, bstar, stage2, p2, sbstar);
-      u32 c = z0 == 0 ? 0u : 1u;
-      if (z0 == 1) {
-        const u64 ck = composite_key(k0[u], src_id(a, lo + e));
-        if (ck == pivot) continue;
-        c = ck < pivot ? 0u : 1u;
-      }
-      const u32 b1 = bucket_of(k1[u], c == 0 ? cpr0 : cpr1, pa.bins1), cb = c == 0 ? cb0 : cb1;
-      if (b1 == cb) {
-        atomicAdd(&sh[c * kBins2 + bucket_of(k1[u], c == 0 ? q0 : q1, kBins2)], 1u);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cnt[k] += u32(k) == 2 * c + (b1 > cb ? 1u : 0u) ? 1u : 0u;
-      }
+      for (int k = 0; k < 4; ++k) cnt[k] += u32(k) == 2 * c + (bk > cb ? 1u : 0u) ? 1u : 0u;
     }
-  }
+  });
   if (pa.bcnt) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
