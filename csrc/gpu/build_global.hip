@@ -760,27 +760,51 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   }
   __syncthreads();
 
-  for (i64 c0 = b0; c0 < b1; c0 += kChunk) {
+  // Compile-time rows (NCOL > 0): 16-B loads of 4 consecutive rows of a column per lane from a
+  // 16-B aligned chunk start (as k_partition2); item i = 4 g + j, rows outside [b0, b1) masked.
+  constexpr bool VEC = NCOL > 0 && KI % 4 == 0;
+  const i64 cstart = VEC ? (((lo + b0) & ~i64(3)) - lo) : b0;
+  for (i64 c0 = cstart; c0 < b1; c0 += kChunk) {
     constexpr int NR = NCOL > 0 ? NCOL : 1;
     float row[kItems][NR];
     float kk[NCOL > 0 ? 1 : kItems], nkk[NCOL > 0 ? 1 : kItems];
+    i64 eitem[kItems];
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      const i64 e = c0 + i * kBlock + threadIdx.x;
-      const i64 p = lo + (e < b1 ? e : b0);
-      if (NCOL > 0) {
+      for (int g = 0; g < kItems / 4; ++g) {
+        const i64 e4 = c0 + (i64(g) * kBlock + threadIdx.x) * 4;
+        const i64 p4 = lo + (e4 < b1 ? e4 : cstart);
 #pragma unroll
-        for (int c = 0; c < NR; ++c) row[i][c] = src[i64(c) * nc + p];
-      } else {
-        kk[i] = src[i64(a.kcol) * nc + p];
-        nkk[i] = src[i64(a.nkcol) * nc + p];
+        for (int c = 0; c < NR; ++c) {
+          const float4 v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
+          row[4 * g + 0][c] = v.x;
+          row[4 * g + 1][c] = v.y;
+          row[4 * g + 2][c] = v.z;
+          row[4 * g + 3][c] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) eitem[4 * g + j] = e4 + j;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kItems; ++i) {
+        const i64 e = c0 + i * kBlock + threadIdx.x;
+        eitem[i] = e;
+        const i64 p = lo + (e < b1 ? e : b0);
+        if (NCOL > 0) {
+#pragma unroll
+          for (int c = 0; c < NR; ++c) row[i][c] = src[i64(c) * nc + p];
+        } else {
+          kk[i] = src[i64(a.kcol) * nc + p];
+          nkk[i] = src[i64(a.nkcol) * nc + p];
+        }
       }
     }
     u32 zone_pre[kItems];  // (zone << 16) | rank-in-wave
 #pragma unroll
     for (int i = 0; i < kItems; ++i) {
-      const i64 e = c0 + i * kBlock + threadIdx.x;
-      const bool valid = e < b1;
+      const i64 e = eitem[i];
+      const bool valid = e >= b0 && e < b1;
       // split-axis and next-axis keys: select chains over the compile-time row (no indexing)
       float key = NCOL > 0 ? row[i][0] : kk[i], nkey = NCOL > 0 ? row[i][0] : nkk[i];
       if (NCOL > 0) {
