@@ -2083,11 +2083,9 @@ struct SplitStreams {
   std::vector<hipStream_t> side;  // streams 1..S-1 (stream 0 is the caller's)
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> join;
-  std::vector<hipEvent_t> part;  // pipelined order: part p's passes done
   ~SplitStreams() {
     for (hipStream_t s : side) (void)hipStreamDestroy(s);
     for (hipEvent_t e : join) (void)hipEventDestroy(e);
-    for (hipEvent_t e : part) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
   }
 };
@@ -2104,20 +2102,13 @@ SplitStreams* GpuBuilder::split_streams_for(hipStream_t stream) const {
   if (cs != hipStreamCaptureStatusNone) return nullptr;  // no stream creation inside a capture
   for (int k = 1; k < split_streams_; ++k) {
     hipStream_t s = nullptr;
-    const char* pr = std::getenv("PKD_SPLIT_PRIO");
-    if (pr) PKD_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, std::atoi(pr)));
-    else PKD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    PKD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     split_->side.push_back(s);
     hipEvent_t e = nullptr;
     PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     split_->join.push_back(e);
   }
   PKD_HIP_CHECK(hipEventCreateWithFlags(&split_->fork, hipEventDisableTiming));
-  for (int p = 0; p < split_parts_; ++p) {
-    hipEvent_t e = nullptr;
-    PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    split_->part.push_back(e);
-  }
   split_->device = dev;
   return split_.get();
 }
@@ -2380,11 +2371,6 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     u32* h2;
     u32* bcnt;
   };
-  // Parts whose passes run at the same time (their grids share the chip): all streams, or one
-  // in the pipelined order (passes of one part at a time, subtree kernels on a second stream).
-  const char* order = std::getenv("PKD_SPLIT_ORDER");
-  const bool pipe = split_parts_ > 1 && split_streams_ >= 2 && order && std::string(order) == "pipe";
-  const int part_conc = pipe ? 1 : split_streams_;
   auto run_range = [&](int base, int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs,
                        float*& src, float*& dst) {
     auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
@@ -2398,9 +2384,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const LevelPlan& lp = levels_[size_t(l)];
       if (nparts == 1) return lp.bps;
       const i64 chunk = dim_ <= 8 ? i64(kChunk) : i64(kBlock) * 4;
-      const char* de = std::getenv("PKD_SPLIT_BPS_DIV");  // A/B knob, read per build
-      const i64 div = de ? std::max<i64>(1, std::atoll(de)) : i64(1);
-      const i64 want = i64(lp.bps) * nparts / (std::max(1, part_conc) * div);
+      const i64 want = i64(lp.bps) * nparts / std::max(1, split_streams_);
       return int(std::max<i64>(1, std::min<i64>(want, (lp.nmax + chunk - 1) / chunk)));
     };
     auto level_args = [&](int l) {
@@ -2607,33 +2591,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     tev.push_back(e);
   };
   tmark(stream);
-  if (pipe) {  // passes of part p on `stream`, its subtree kernel on the first side stream
-    hipStream_t sub = sp->side[0];
-    for (int p = 0; p < P; ++p) {
-      tmark(stream);
-      run_range(split_level_, split_level_, lg_, p, P, stream, phs[0], psrc[size_t(p)], pdst[size_t(p)]);
-      PKD_HIP_CHECK(hipEventRecord(sp->part[size_t(p)], stream));
-      PKD_HIP_CHECK(hipStreamWaitEvent(sub, sp->part[size_t(p)], 0));
-      tmark(sub);
-      subtree(p, P, sub, psrc[size_t(p)]);
-      tmark(sub);
-    }
-  } else if (order && std::string(order) == "breadth") {  // every part's level step, then the next step
-    for (int l = split_level_; l < lg_;) {
-      const int step = levels_[size_t(l)].pair ? 2 : 1;
-      for (int p = 0; p < P; ++p)
-        run_range(split_level_, l, l + step, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
-      l += step;
-    }
-    for (int p = 0; p < P; ++p) subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
-  } else {  // depth first: part p's levels and subtree, then part p + 1
-    for (int p = 0; p < P; ++p) {
-      tmark(pst[size_t(p)]);
-      run_range(split_level_, split_level_, lg_, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
-      tmark(pst[size_t(p)]);
-      subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
-      tmark(pst[size_t(p)]);
-    }
+  // Part p's remaining levels, then its subtree kernel, on stream p % split_streams_ (all parts
+  // start at the fork and run in lockstep; PKD_SPLIT_TRACE shows it)
+  for (int p = 0; p < P; ++p) {
+    tmark(pst[size_t(p)]);
+    run_range(split_level_, split_level_, lg_, p, P, pst[size_t(p)], phs[size_t(p)], psrc[size_t(p)], pdst[size_t(p)]);
+    tmark(pst[size_t(p)]);
+    subtree(p, P, pst[size_t(p)], psrc[size_t(p)]);
+    tmark(pst[size_t(p)]);
   }
   for (size_t k = 0; k < sp->side.size(); ++k) {
     PKD_HIP_CHECK(hipEventRecord(sp->join[k], sp->side[k]));

@@ -201,12 +201,10 @@ def test_split_build_equals_cpu(gpu_device, monkeypatch, level, parts, streams):
         check_same(pk.generate_problem(seed, dim, n), gpu_device)
 
 
-@pytest.mark.parametrize("order", ["depth", "breadth"])
-def test_split_build_stage2_skewed(gpu_device, monkeypatch, order):
+def test_split_build_stage2_skewed(gpu_device, monkeypatch):
     """Split build whose parts start with second-stage levels and prefix placement (18 M
-    points, split after the first pair) on skewed data, both enqueue orders."""
+    points, split after the first pair) on skewed data."""
     monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
-    monkeypatch.setenv("PKD_SPLIT_ORDER", order)
     x = pk.generate_problem(6, 3, 18_000_000)
     x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
     check_same(x, gpu_device)
