@@ -509,7 +509,11 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
       for (int v = 0; v < w; ++v) off += wcnt[v][d];
       float* o = out + i64(off + my) * rs;
       const float* r = p.pts + i * dim;
-      for (int c = 0; c < dim; ++c) o[c] = r[c];
+      if (dim == 3) {  // one 12-B load and store per row (dwordx3) instead of three dword pairs
+        *reinterpret_cast<float3*>(o) = *reinterpret_cast<const float3*>(r);
+      } else {
+        for (int c = 0; c < dim; ++c) o[c] = r[c];
+      }
       if (rs > dim) o[dim] = __uint_as_float(point_id(p, i));
     }
     __syncthreads();
