@@ -5,11 +5,14 @@ One step = one complete exact kd-tree build of the whole point set, from the inp
 resident in HBM to the finished implicit in-order tree (ids + coordinates) in HBM.
 
 * N = 1: the level-synchronous HIP builder on one MI355X.
-* N > 1: global decomposition over RCCL (one process per GPU): each rank holds its
+* N > 1: global decomposition over RCCL (one process per GPU, any N): each rank holds its
   generation-order slice (the reference's MPI slicing, kdtree_mpi.cpp:204-224); the top
-  log2(N) levels are split with allreduced histograms, points are redistributed with
-  all-to-all rounds, and each GPU builds its subtree. Strong scaling: the total point count
-  is fixed, so `value` is the whole-job throughput.
+  levels are split with allreduced histograms, points are redistributed with all-to-all
+  rounds, and each GPU builds its leaves' subtrees (csrc/cpu/global_builder.cpp). Strong
+  scaling: the total point count is fixed, so `value` is the whole-job throughput. After the
+  timed loop rank 0 prints the per-phase breakdown of one extra (untimed, profiled) build on
+  stderr -- top levels, pack, plan wait, exchange (bytes, GB/s), id rebuild, leaf builds --
+  as the MAX over ranks.
 
 Launch: under torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the env), or
 plain `python bench.py --gpus N`: without WORLD_SIZE the process becomes a launcher that never
@@ -19,7 +22,8 @@ with the first failing rank's status.
 Data: the reference generator stream (std::mt19937 + uniform_real<float>(-100,100), seed 42),
 each rank's slice generated on its own GPU by the device generator (csrc/gpu/generator.hip,
 bit-identical to the host stream; untimed). After the timed loop (untimed) the last tree is
-checked: device error word, kd invariant on every node, ids a permutation.
+checked: device error word, kd invariant on every node, ids a permutation; at N > 1 also
+every block of every rank against every top-tree pivot above it (cross-rank routing).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -39,6 +43,16 @@ sys.path.insert(0, ROOT)
 
 BASELINE_MPTS = 100e6 / 924.3 / 1e6  # reference build, 100M x 3D, 924.3 s (1 core)
 METRIC = "Mpoints/sec kd-tree build, 100M x 3D float32, at 1/2/4/8 MI355X"
+HEADLINE = (100_000_000, 3)
+
+
+def metric_name(n: int, dim: int) -> str:
+    """The BASELINE metric for the headline config; other sizes are labelled as what they are."""
+    if (n, dim) == HEADLINE:
+        return METRIC
+    size = f"{n // 1_000_000_000}B" if n % 1_000_000_000 == 0 else (
+        f"{n // 1_000_000}M" if n % 1_000_000 == 0 else str(n))
+    return f"Mpoints/sec kd-tree build, {size} x {dim}D float32 (not the headline config)"
 
 
 def _parse(argv=None):
@@ -59,10 +73,11 @@ def _parse(argv=None):
     ap.add_argument("--decomp", choices=["auto", "single", "global"], default="auto",
                     help="auto: one GPU builds alone, N > 1 GPUs build one global tree; global also at N = 1 "
                          "(the multi-GPU code path on one rank)")
-    ap.add_argument("--impl", choices=["native", "python"], default="native",
-                    help="global decomposition: native C++ builder on its own RCCL communicator, or the Python "
-                         "orchestration over torch.distributed (host tensors always use the latter)")
-    ap.add_argument("--pipeline-k", type=int, default=-1, help="global: 2^k exchange rounds (-1: auto)")
+    ap.add_argument("--pipeline-k", type=int, default=-1,
+                    help="global: extra top levels (leaves per rank = 2^k at power-of-two N; -1: auto)")
+    ap.add_argument("--timeout", type=float, default=300.0,
+                    help="global: bound of every host wait on the communicator (s); a stuck peer raises")
+    ap.add_argument("--no-profile", action="store_true", help="N > 1: skip the per-phase breakdown build")
     return ap.parse_args(argv)
 
 
@@ -135,6 +150,29 @@ def _check_tree(tp, ti, depth0, id_lo, id_hi, permutation=True) -> str:
     return ""
 
 
+def _check_share(t, n: int) -> str:
+    """'' when a rank's share of the distributed tree is valid: every block (complete subtree)
+    satisfies the kd invariant from its own root depth, ids are distinct and in 1..n, and every
+    block lies on the correct side of every top-tree pivot above it (cross-rank routing)."""
+    for off, m, depth, _ in t.blocks:
+        if m > 0:
+            p = _check_tree(t.tree_pts[off:off + m], t.tree_ids[off:off + m], t.depth0 + depth, 1, n + 1,
+                            permutation=False)
+            if p:
+                return p
+    p = _distinct_ids(t.tree_ids, n) if t.tree_ids.numel() else ""
+    return p or t.check_top_routing()
+
+
+def _distinct_ids(ids, n: int) -> str:
+    idl = ids.to(torch.int64) & 0xFFFFFFFF
+    if int(idl.min()) < 1 or int(idl.max()) > n:
+        return "ids out of range"
+    seen = torch.zeros(n + 1, dtype=torch.int32, device=ids.device)
+    seen.index_add_(0, idl, torch.ones_like(idl, dtype=torch.int32))
+    return "duplicate ids" if int(seen.max()) > 1 else ""
+
+
 def main(argv=None):
     args = _parse(argv)
     world_env = os.environ.get("WORLD_SIZE")
@@ -155,6 +193,12 @@ def main(argv=None):
     else:
         if share:
             local_rank = 0
+            # RCCL refuses two ranks on one device ("Duplicate GPU detected") unless they look
+            # like different hosts: a per-rank host id makes every rank its own "node" and the
+            # ranks talk over the loopback socket transport. The collectives, their grouping
+            # and the builder's schedule are the real ones; only the transport differs from xGMI.
+            os.environ.setdefault("NCCL_HOSTID", f"pkd-share-rank{rank}")
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
 
@@ -183,17 +227,18 @@ def main(argv=None):
     distributed = world > 1 or args.decomp == "global"
     if args.decomp == "single" and world > 1:
         sys.exit("bench.py: --decomp single needs --gpus 1")
-    if world == 1 and distributed and (cpu or args.impl != "native"):
-        sys.exit("bench.py: --decomp global on one rank runs the native builder (GPU, --impl native)")
+    if world == 1 and distributed and cpu:
+        sys.exit("bench.py: --decomp global on one rank runs the native builder (GPU)")
+    builder = None
     if distributed:
-        if args.impl == "native" and not cpu:
+        if not cpu:
             from parallel_kd_tree_amd.parallel.native_global import NativeGlobalBuilder
-            builder = NativeGlobalBuilder(n, dim, dev, pipeline_k=args.pipeline_k)
+            builder = NativeGlobalBuilder(n, dim, dev, pipeline_k=args.pipeline_k, timeout_s=args.timeout)
+            # bounded: a stuck or failed peer raises here instead of hanging the device sync
+            sync = lambda: (builder.sync(), torch.cuda.synchronize())  # noqa: E731
         else:
             from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
-            if args.pipeline_k >= 0:
-                os.environ["PKD_PIPELINE_K"] = str(args.pipeline_k)
-            builder = GlobalTreeBuilder(n, dim, device=dev)
+            builder = GlobalTreeBuilder(n, dim, device=dev, pipeline_k=args.pipeline_k)
         res = {}
 
         def step():
@@ -238,18 +283,18 @@ def main(argv=None):
         if err:
             problem = f"device build reported error flags {err}"
         elif not args.no_check:
-            # my subtree sits at depth log2(N) and holds ids of every rank: invariant and distinct
-            # ids here; count and id sum over all ranks (plus the replicated top pivots) below
-            problem = _check_tree(t.tree_pts, t.tree_ids, (world - 1).bit_length(), 1, n + 1, permutation=False)
-            idl = t.tree_ids.to(torch.int64) & 0xFFFFFFFF
-            stats = torch.tensor([idl.numel(), int(idl.sum()) if idl.numel() else 0], dtype=torch.int64, device=dev)
-            if world > 1:
-                comm.all_reduce_(stats)
-            top_ids = [int(t.top_rows[i, dim:].contiguous().view(torch.int32).item()) & 0xFFFFFFFF
-                       for i, s in enumerate(t.top_slots) if s >= 0]
-            cnt, tot = int(stats[0]) + len(top_ids), int(stats[1]) + sum(top_ids)
-            if not problem and (cnt != n or tot != n * (n + 1) // 2):
-                problem = f"the distributed tree holds {cnt} points (id sum {tot}) for ids 1..{n}"
+            problem = _check_share(t, n)
+            if not problem:
+                idl = t.tree_ids.to(torch.int64) & 0xFFFFFFFF
+                stats = torch.tensor([idl.numel(), int(idl.sum()) if idl.numel() else 0], dtype=torch.int64,
+                                     device=dev)
+                if world > 1:
+                    comm.all_reduce_(stats)
+                top_ids = [int(t.top_rows[i, dim:].contiguous().view(torch.int32).item()) & 0xFFFFFFFF
+                           for i, s in enumerate(t.top_slots) if s >= 0]
+                cnt, tot = int(stats[0]) + len(top_ids), int(stats[1]) + sum(top_ids)
+                if not problem and (cnt != n or tot != n * (n + 1) // 2):
+                    problem = f"the distributed tree holds {cnt} points (id sum {tot}) for ids 1..{n}"
     elif cpu:
         tp, ti = res["t"]
         problem = "" if args.no_check else _check_tree(tp, ti + 1, 0, 1, n + 1)
@@ -270,11 +315,31 @@ def main(argv=None):
             comm.destroy()
         sys.exit(3)
 
+    # ---- untimed: where one build's time goes (N > 1, native): one profiled build -------
+    if distributed and not cpu and not args.no_profile:
+        builder.set_profile(True)
+        step()
+        ph = builder.phases()
+        builder.set_profile(False)
+        keys = sorted(ph)
+        v = torch.tensor([ph[k] for k in keys], dtype=torch.float64, device=dev)
+        if world > 1:
+            comm.all_reduce_(v, torch.distributed.ReduceOp.MAX)
+        ph = dict(zip(keys, v.tolist()))
+        if rank == 0:
+            gbs = ph["sent_bytes"] / max(ph["exchange_ms"], 1e-9) / 1e6
+            print(json.dumps({"phases_max_over_ranks_ms": {k: round(ph[k], 4) for k in keys if k.endswith("_ms")},
+                              "exchange_sent_bytes_max": int(ph["sent_bytes"]),
+                              "exchange_max_peer_bytes": int(ph["max_peer_bytes"]),
+                              "exchange_GBps_per_rank": round(gbs, 2), "rounds": int(ph["rounds"]),
+                              "top_levels": builder.top_levels, "retries": int(ph["retries"])}),
+                  file=sys.stderr, flush=True)
+
     ms = dt * 1e3 / args.steps
     mpts = n / (ms / 1e3) / 1e6
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC,
+            "metric": metric_name(n, dim),
             "value": round(mpts, 3),
             "unit": "Mpoints/s",
             "n_gpus": world,
@@ -290,8 +355,8 @@ def main(argv=None):
             "config": {"model": "exact median-split kd-tree, cycling axis (implicit in-order layout)",
                        "global_batch": n, "seq_len": dim, "n_points": n, "dim": dim,
                        "parallelism": f"global{world}" if distributed else "single",
-                       "impl": ("native" if args.impl == "native" and not cpu else "python") if distributed
-                       else "native",
+                       "impl": "python-host (gloo)" if cpu and distributed else "native",
+                       "headline": (n, dim) == HEADLINE,
                        "device": "cpu (gloo rehearsal)" if cpu else "MI355X",
                        "tree_checked": not args.no_check},
         }), flush=True)

@@ -109,28 +109,36 @@ void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level,
             u64p(pivots), top_rows.data_ptr<float>(), cells.data_ptr<float>(), u32p(err), stream_of(gathered));
 }
 
+// out: [>= n, dim + 1] / [>= n, dim] rows, or (col_stride > 0) planes of col_stride floats
 void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base, torch::Tensor node,
-          int64_t levels, const torch::Tensor& pivots, int64_t last_axis, int64_t P, torch::Tensor out,
-          std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch,
-          int64_t pipe_k) {
+          int64_t levels, const torch::Tensor& pivots, int64_t last_axis, torch::Tensor out, int64_t col_stride,
+          std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
   const c10::DeviceGuard g(pts.device());
   TopPoints p = points_of(pts, ids, id_base);
   check_cuda(out, torch::kFloat32, "out");
-  TORCH_CHECK(out.dim() == 2 && out.size(0) >= p.n && (out.size(1) == p.dim + 1 || out.size(1) == p.dim),
-              "out must be [>= n, dim+1] or [>= n, dim]");
+  const int64_t T = int64_t(1) << levels;
+  int row_stride = p.dim;
+  if (col_stride > 0) {
+    TORCH_CHECK(out.numel() >= col_stride * p.dim && col_stride >= p.n, "out must hold dim planes of col_stride >= n");
+  } else {
+    TORCH_CHECK(out.dim() == 2 && out.size(0) >= p.n && (out.size(1) == p.dim + 1 || out.size(1) == p.dim),
+                "out must be [>= n, dim+1] or [>= n, dim]");
+    row_stride = int(out.size(1));
+  }
   check_cuda(counts, torch::kInt64, "counts");
-  TORCH_CHECK(counts.numel() == 4 * P, "counts must have 4*P entries");
-  TORCH_CHECK(size_t(scratch.numel()) >= top_pack_scratch_bytes(p.n, int(P)), "scratch too small");
+  TORCH_CHECK(counts.numel() == 4 * T, "counts must have 4 * 2^levels entries");
+  TORCH_CHECK(size_t(scratch.numel()) >= top_pack_scratch_bytes(p.n, int(T)), "scratch too small");
   u32* bm = nullptr;
   int64_t words = 0;
   if (bitmaps && bitmaps->defined()) {
     check_cuda(*bitmaps, torch::kInt32, "bitmaps");
-    TORCH_CHECK(bitmaps->dim() == 2 && bitmaps->size(0) == P && bitmaps->size(1) * 32 >= p.n, "bitmaps must be [P, >= n/32]");
+    TORCH_CHECK(bitmaps->dim() == 2 && bitmaps->size(0) == T && bitmaps->size(1) * 32 >= p.n,
+                "bitmaps must be [2^levels, >= n/32]");
     bm = u32p(*bitmaps);
     words = bitmaps->size(1);
   }
-  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), int(P), int(pipe_k), out.data_ptr<float>(),
-           int(out.size(1)), bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
+  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), out.data_ptr<float>(), row_stride, col_stride,
+           bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
 }
 
 // bitmaps: all sources' words back to back; per source (row offset, rows, word offset, words, id base)
@@ -160,21 +168,60 @@ void ids_from_bm(const torch::Tensor& bitmaps, const std::vector<int64_t>& off, 
   ids_from_bitmaps(cu32p(bitmaps), int(P), src, u32p(ids), scratch.data_ptr(), u32p(err), stream_of(bitmaps));
 }
 
-// The native exchange planner on host data (CPU-testable): counts [P][R * P][4].
-std::tuple<int, std::vector<std::vector<int64_t>>, std::vector<std::vector<int64_t>>, std::vector<int64_t>> plan_py(
-    const std::vector<int64_t>& counts, int64_t P, int64_t R, int64_t me, int64_t n_total) {
+// ---- geometry and planning (host, CPU-testable) --------------------------------------------
+pybind11::dict layout_dict(const global_plan::Layout& lay) {
+  pybind11::dict d;
+  d["P"] = lay.P;
+  d["LL"] = lay.LL;
+  d["T"] = lay.T;
+  d["R"] = lay.R;
+  d["leaf_lo"] = lay.leaf_lo;
+  d["leaf_slot"] = std::vector<int64_t>(lay.leaf_slot.begin(), lay.leaf_slot.end());
+  d["leaf_n"] = std::vector<int64_t>(lay.leaf_n.begin(), lay.leaf_n.end());
+  d["top_slot"] = std::vector<int64_t>(lay.top_slot.begin(), lay.top_slot.end());
+  d["top_owner"] = lay.top_owner;
+  d["share_lo"] = std::vector<int64_t>(lay.share_lo.begin(), lay.share_lo.end());
+  d["share_n"] = std::vector<int64_t>(lay.share_n.begin(), lay.share_n.end());
+  pybind11::list blocks, between;
+  for (int r = 0; r < lay.P; ++r) {
+    std::vector<global_plan::Block> b;
+    std::vector<i64> bw;
+    global_plan::share_blocks(lay, r, &b, &bw);
+    pybind11::list bl;
+    for (const auto& x : b) bl.append(pybind11::make_tuple(int64_t(x.off), int64_t(x.n), x.depth, int64_t(x.heap)));
+    blocks.append(bl);
+    between.append(std::vector<int64_t>(bw.begin(), bw.end()));
+  }
+  d["blocks"] = blocks;    // per rank: (offset in share, points, root depth, heap node)
+  d["between"] = between;  // per rank: heap nodes of the top rows between its blocks
+  return d;
+}
+
+pybind11::dict layout_py(int64_t n_total, int64_t P, int64_t k) {
+  return layout_dict(global_plan::make_layout(n_total, int(P), int(k)));
+}
+
+// The native exchange planner: counts [P][T][4] (rows, err, id base, n_local) flattened.
+std::tuple<int, std::vector<std::vector<int64_t>>, std::vector<std::vector<int64_t>>,
+           std::vector<std::vector<int64_t>>, std::vector<int64_t>>
+plan_py(const std::vector<int64_t>& counts, int64_t n_total, int64_t P, int64_t k, int64_t me) {
+  const auto lay = global_plan::make_layout(n_total, int(P), int(k));
   std::vector<i64> c(counts.begin(), counts.end());
   global_plan::Plan plan;
-  const int rc = global_plan::make_plan(c, int(P), int(R), int(me), n_total, &plan);
-  std::vector<std::vector<int64_t>> in(plan.in_splits.begin(), plan.in_splits.end());
-  std::vector<std::vector<int64_t>> out(plan.out_splits.begin(), plan.out_splits.end());
-  return {rc, in, out, std::vector<int64_t>(plan.starts.begin(), plan.starts.end())};
+  const int rc = global_plan::make_plan(c, lay, int(me), &plan);
+  auto cv = [](const std::vector<std::vector<i64>>& v) {
+    std::vector<std::vector<int64_t>> o;
+    for (const auto& r : v) o.emplace_back(r.begin(), r.end());
+    return o;
+  };
+  return {rc, cv(plan.send_rows), cv(plan.send_off), cv(plan.recv_rows),
+          std::vector<int64_t>(plan.leaf_start.begin(), plan.leaf_start.end())};
 }
 
 // The native global builder with P ranks as threads of this process sharing the current GPU
 // (loopback communicator): rank r holds rows [first_r, first_r + local_r) of `x` (the reference's
-// MPI slicing), ids 1..N. Returns the assembled in-order tree (rank sub-trees + top pivots) on the
-// host and the OR of the ranks' error words.
+// MPI slicing), ids 1..N. Returns the assembled in-order tree (rank shares + boundary top rows)
+// on the host, the OR of the ranks' error words and the middle-bucket scale they ended at.
 std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const torch::Tensor& x, int64_t P,
                                                                            int64_t k) {
   TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
@@ -202,6 +249,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const
         PKD_HIP_CHECK(hipMemcpy(d, x.data_ptr<float>() + first * dim, size_t(local) * dim * 4, hipMemcpyHostToDevice));
         GlobalBuilder gb(*comms[size_t(r)], N, dim, int(k));
         gb.build(d, local, u32(first + 1), s);
+        gb.wait(s);
         ew[size_t(r)] = gb.read_error(s);
         scales[size_t(r)] = gb.middle_scale();
         PKD_HIP_CHECK(hipMemcpy(tp.data_ptr<float>() + gb.slot_lo() * dim, gb.tree_pts(), size_t(gb.n_leaf()) * dim * 4,
@@ -239,7 +287,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const
 class NativeGlobal {
  public:
   NativeGlobal(int64_t n_total, int64_t dim, int64_t rank, int64_t world, const std::string& uid,
-               int64_t pipeline_k, int64_t device)
+               int64_t pipeline_k, int64_t device, double timeout_s)
       : dim_(int(dim)), rank_(int(rank)), world_(int(world)), device_(int(device)) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "rccl unique id: ", sizeof(ncclUniqueId), " bytes expected");
     TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rank out of range");
@@ -248,12 +296,14 @@ class NativeGlobal {
     std::memcpy(&id, uid.data(), sizeof(id));
     nccl_check(ncclCommInitRank(&c_, world_, id, rank_), "ncclCommInitRank", rank_);
     comm_ = std::make_unique<RcclComm>(c_, rank_, world_);
+    if (timeout_s > 0) comm_->set_timeout(timeout_s);
     gb_ = std::make_unique<GlobalBuilder>(*comm_, n_total, dim_, int(pipeline_k));
   }
   ~NativeGlobal() {
     gb_.reset();
+    const bool dead = comm_ && comm_->aborted();
     comm_.reset();
-    if (c_) (void)ncclCommDestroy(c_);
+    if (c_ && !dead) (void)ncclCommDestroy(c_);
   }
   NativeGlobal(const NativeGlobal&) = delete;
   NativeGlobal& operator=(const NativeGlobal&) = delete;
@@ -269,6 +319,13 @@ class NativeGlobal {
     pybind11::gil_scoped_release nogil;  // the exchange plan blocks on the other ranks
     gb_->build(p, n, u32(id_base), s);
   }
+  // bounded wait for the last build on the current stream (raises on a stuck / failed peer)
+  void sync() {
+    const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
+    const hipStream_t s = c10::hip::getCurrentHIPStream(device_).stream();
+    pybind11::gil_scoped_release nogil;
+    gb_->wait(s);
+  }
   // views of the builder's buffers (valid until the next build / the builder's end)
   torch::Tensor tree_pts() const {
     return torch::from_blob(const_cast<float*>(gb_->tree_pts()), {gb_->n_leaf(), dim_}, opts(torch::kFloat32));
@@ -277,12 +334,15 @@ class NativeGlobal {
     return torch::from_blob(const_cast<u32*>(gb_->tree_ids()), {gb_->n_leaf()}, opts(torch::kInt32));
   }
   torch::Tensor top_rows() const {
-    return torch::from_blob(const_cast<float*>(gb_->top_rows()), {world_ - 1, dim_ + 1}, opts(torch::kFloat32));
+    const int64_t t = std::max(gb_->layout().T - 1, 0);
+    if (t == 0) return torch::empty({0, dim_ + 1}, opts(torch::kFloat32));
+    return torch::from_blob(const_cast<float*>(gb_->top_rows()), {t, dim_ + 1}, opts(torch::kFloat32));
   }
   std::vector<int64_t> top_slots() const {
     const auto v = gb_->top_slots();
     return std::vector<int64_t>(v.begin(), v.end());
   }
+  pybind11::dict layout() const { return layout_dict(gb_->layout()); }
   int64_t slot_lo() const { return gb_->slot_lo(); }
   int64_t n_leaf() const { return gb_->n_leaf(); }
   int64_t top_levels() const { return gb_->top_levels(); }
@@ -290,6 +350,11 @@ class NativeGlobal {
   int64_t read_error() const {
     const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
     return int64_t(gb_->read_error(c10::hip::getCurrentHIPStream(device_).stream()));
+  }
+  void set_profile(bool on) { gb_->set_profile(on); }
+  std::map<std::string, double> phases() const {
+    const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
+    return gb_->phases(c10::hip::getCurrentHIPStream(device_).stream()).as_map();
   }
 
  private:
@@ -313,21 +378,27 @@ pybind11::bytes rccl_unique_id() {
 void bind_dist_ops(pybind11::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id);
   pybind11::class_<NativeGlobal>(m, "NativeGlobal")
-      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, const std::string&, int64_t, int64_t>(),
+      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, const std::string&, int64_t, int64_t, double>(),
            pybind11::arg("n_total"), pybind11::arg("dim"), pybind11::arg("rank"), pybind11::arg("world"),
            pybind11::arg("uid"), pybind11::arg("pipeline_k") = -1, pybind11::arg("device") = 0,
-           pybind11::call_guard<pybind11::gil_scoped_release>())
+           pybind11::arg("timeout_s") = 0.0, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("build", &NativeGlobal::build, pybind11::arg("x"), pybind11::arg("id_base"))
+      .def("sync", &NativeGlobal::sync)
       .def("tree_pts", &NativeGlobal::tree_pts)
       .def("tree_ids", &NativeGlobal::tree_ids)
       .def("top_rows", &NativeGlobal::top_rows)
       .def("top_slots", &NativeGlobal::top_slots)
+      .def("layout", &NativeGlobal::layout)
       .def("slot_lo", &NativeGlobal::slot_lo)
       .def("n_leaf", &NativeGlobal::n_leaf)
       .def("top_levels", &NativeGlobal::top_levels)
       .def("middle_scale", &NativeGlobal::middle_scale)
-      .def("read_error", &NativeGlobal::read_error);
-  m.def("global_plan", &plan_py);
+      .def("read_error", &NativeGlobal::read_error)
+      .def("set_profile", &NativeGlobal::set_profile)
+      .def("phases", &NativeGlobal::phases);
+  m.def("global_layout", &layout_py, pybind11::arg("n_total"), pybind11::arg("P"), pybind11::arg("k") = -1);
+  m.def("global_plan", &plan_py, pybind11::arg("counts"), pybind11::arg("n_total"), pybind11::arg("P"),
+        pybind11::arg("k"), pybind11::arg("me"));
   m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("top_bbox", &bbox);
@@ -337,11 +408,11 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("top_collect", &collect);
   m.def("top_pivot", &pivot);
   m.def("top_pack", &pack, pybind11::arg("pts"), pybind11::arg("ids"), pybind11::arg("id_base"), pybind11::arg("node"),
-        pybind11::arg("levels"), pybind11::arg("pivots"), pybind11::arg("last_axis"), pybind11::arg("P"),
-        pybind11::arg("out"), pybind11::arg("bitmaps"), pybind11::arg("counts"), pybind11::arg("err"),
-        pybind11::arg("scratch"), pybind11::arg("pipe_k") = 0);
+        pybind11::arg("levels"), pybind11::arg("pivots"), pybind11::arg("last_axis"), pybind11::arg("out"),
+        pybind11::arg("col_stride"), pybind11::arg("bitmaps"), pybind11::arg("counts"), pybind11::arg("err"),
+        pybind11::arg("scratch"));
   m.def("top_middle_words", [](int64_t dim, int64_t cap) { return int64_t(top_middle_words(int(dim), cap)); });
-  m.def("top_pack_scratch_bytes", [](int64_t n, int64_t P) { return int64_t(top_pack_scratch_bytes(n, int(P))); });
+  m.def("top_pack_scratch_bytes", [](int64_t n, int64_t T) { return int64_t(top_pack_scratch_bytes(n, int(T))); });
   m.def("ids_from_bitmaps", &ids_from_bm);
   m.def("ids_from_bitmaps_scratch_bytes",
         [](int64_t words, int64_t P) { return int64_t(ids_from_bitmaps_scratch_bytes(words, int(P))); });

@@ -15,12 +15,13 @@
 //   * every rank answers the queries on its tree; packed (d2 << 32 | id) results are
 //     MIN-reduced to rank 0 (MPI_Reduce MIN of the distances, :253)             -> ncclReduce
 //   * rank 0 prints the protocol lines.
-// --decomp global instead builds ONE exact tree over all ranks (GlobalBuilder: top log2 P
-// levels by allreduce histograms + allgather pivot selection, one all-to-all of the points to
-// their subtree's rank, pipelined in 2^k rounds with --pipeline-k); each rank answers the
-// queries on its subtree, rank 0 also on the top pivots, and the same MIN reduce combines them.
+// --decomp global instead builds ONE exact tree over all ranks, for any P (GlobalBuilder: the
+// top levels by allreduce histograms + allgather pivot selection, one all-to-all round per
+// top-level leaf of a rank, overlapped with the leaf builds; --pipeline-k adds levels); each
+// rank answers the queries on its share (complete subtrees plus the top rows between them),
+// rank 0 also on the boundary top rows, and the same MIN reduce combines them.
 // Ranks with no points (N < P, the reference's segfault F7) contribute +inf.
-// Every collective is waited on with a watchdog: the stream is polled and
+// Every collective is waited on with a watchdog (RcclComm::wait): the stream is polled and
 // ncclCommGetAsyncError checked until a deadline (--timeout seconds, default 300); a stuck or
 // failed collective aborts the communicator and the rank exits non-zero, after which the
 // launcher stops the remaining ranks and returns non-zero.
@@ -70,31 +71,6 @@ struct Config {
 };
 
 
-// Waits for everything enqueued on `s` (collectives included) with a deadline, polling the
-// communicator's asynchronous error state (the failure detector of SURVEY.md §5.3).
-void watchdog_wait(hipStream_t s, ncclComm_t comm, double timeout_s, const char* what) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t q = hipStreamQuery(s);
-    if (q == hipSuccess) return;
-    if (q != hipErrorNotReady) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(q));
-    ncclResult_t async = ncclSuccess;
-    PKD_NCCL_CHECK(ncclCommGetAsyncError(comm, &async));
-    if (async != ncclSuccess) {
-      ncclCommAbort(comm);
-      throw std::runtime_error(std::string("rank ") + std::to_string(g_rank) + ": " + what +
-                               ": asynchronous RCCL error " + ncclGetErrorString(async));
-    }
-    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (el > timeout_s) {
-      ncclCommAbort(comm);
-      throw std::runtime_error(std::string("rank ") + std::to_string(g_rank) + ": " + what + ": no progress for " +
-                               std::to_string(timeout_s) + " s (watchdog)");
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
-}
-
 void write_all(int fd, const void* p, size_t n) {
   const char* c = static_cast<const char*>(p);
   while (n) {
@@ -137,6 +113,11 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   ::close(saved_stdout);
   hipStream_t s;
   PKD_HIP_CHECK(hipStreamCreate(&s));
+  // every wait on the stream is bounded and polls the communicator's asynchronous error state
+  // (Comm::wait): a stuck or failed peer aborts the communicator and this rank exits non-zero
+  RcclComm rcomm(comm, rank, P);
+  rcomm.set_timeout(timeout_s);
+  auto watchdog_wait = [&](hipStream_t st, const char* what) { rcomm.wait(st, what); };
 
   // MPI_Bcast of the configuration (kdtree_mpi.cpp:199): rank 0's values win.
   int* d_cfg = nullptr;
@@ -146,7 +127,7 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_NCCL_CHECK(ncclBroadcast(d_cfg, d_cfg, 3, ncclInt32, 0, comm, s));
   int bcfg[3];
   PKD_HIP_CHECK(hipMemcpyAsync(bcfg, d_cfg, sizeof(bcfg), hipMemcpyDeviceToHost, s));
-  watchdog_wait(s, comm, timeout_s, "config broadcast");
+  watchdog_wait(s, "config broadcast");
   cfg = Config{bcfg[0], bcfg[1], bcfg[2]};
   const int dim = cfg.dim, Q = o.num_queries;
   const i64 N = cfg.num_points;
@@ -179,15 +160,13 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   void* ws = nullptr;
   std::unique_ptr<GpuBuilder> b;
   const bool global = o.decomp == "global";
-  std::unique_ptr<RcclComm> rcomm;
   std::unique_ptr<GlobalBuilder> gb;
-  float* d_top = nullptr;  // rank 0, global: the top pivots as a point set [P - 1][dim] + ids
+  float* d_top = nullptr;  // rank 0, global: the boundary top rows as a point set [T - 1][dim] + ids
   u32* d_top_ids = nullptr;
   if (global) {
-    rcomm = std::make_unique<RcclComm>(comm, rank, P);
-    gb = std::make_unique<GlobalBuilder>(*rcomm, N, dim, o.pipeline_k);
-    PKD_HIP_CHECK(hipMalloc(&d_top, size_t(P) * dim * 4));
-    PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(P) * 4));
+    gb = std::make_unique<GlobalBuilder>(rcomm, N, dim, o.pipeline_k);
+    PKD_HIP_CHECK(hipMalloc(&d_top, size_t(gb->layout().T) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(gb->layout().T) * 4));
   } else if (local > 0) {  // allocations outside the timed region
     b = std::make_unique<GpuBuilder>(local, dim);
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
@@ -203,17 +182,29 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   const float* d_q = d_x + size_t(local) * dim;
   const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
   if (global) {
-    // my subtree (root at depth log2 P of the one global tree) ...
-    const i64 n = gb->n_leaf();
-    if (n > 0 && traverse) nn_traverse(gb->tree_pts(), gb->tree_ids(), n, dim, gb->top_levels(), d_q, Q, d_res, s);
-    else if (n > 0) nn_brute(gb->tree_pts(), gb->tree_ids(), 0, n, dim, d_q, Q, d_res, s);
-    // ... and on rank 0 the P - 1 replicated top pivots, split out of their [dim + 1] rows
+    // my share: complete subtrees ("blocks") of the one global tree plus the top rows between
+    // them (a single subtree at depth log2 P for a power-of-two P) ...
+    std::vector<global_plan::Block> blocks;
+    std::vector<i64> between;
+    global_plan::share_blocks(gb->layout(), rank, &blocks, &between);
+    for (const auto& bl : blocks) {
+      if (bl.n <= 0) continue;
+      const float* tp = gb->tree_pts() + size_t(bl.off) * dim;
+      const u32* ti = gb->tree_ids() + bl.off;
+      if (traverse) nn_traverse(tp, ti, bl.n, dim, bl.depth, d_q, Q, d_res, s);
+      else nn_brute(tp, ti, 0, bl.n, dim, d_q, Q, d_res, s);
+    }
+    for (i64 h : between) {
+      const i64 off = gb->layout().top_slot[size_t(h)] - gb->slot_lo();
+      nn_brute(gb->tree_pts() + size_t(off) * dim, gb->tree_ids() + off, 0, 1, dim, d_q, Q, d_res, s);
+    }
+    // ... and on rank 0 the boundary top rows (outside every share), split out of their rows
     if (rank == 0 && P > 1) {
       const std::vector<i64> slots = gb->top_slots();
       i64 nt = 0;
-      for (int h = 0; h < P - 1; ++h) {
-        if (slots[size_t(h)] < 0) continue;
-        const float* row = gb->top_rows() + size_t(h) * (dim + 1);
+      for (size_t h = 0; h < slots.size(); ++h) {
+        if (slots[h] < 0) continue;
+        const float* row = gb->top_rows() + h * (dim + 1);
         PKD_HIP_CHECK(hipMemcpyAsync(d_top + nt * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
         PKD_HIP_CHECK(hipMemcpyAsync(d_top_ids + nt, row + dim, 4, hipMemcpyDeviceToDevice, s));
         ++nt;
@@ -229,7 +220,7 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventRecord(e2, s));
   std::vector<u64> res(static_cast<size_t>(Q));
   PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
-  watchdog_wait(s, comm, timeout_s, "build + queries + reduce");
+  watchdog_wait(s, "build + queries + reduce");
 
   // per-rank timings, MAX-reduced (the slowest rank bounds the job)
   float bld = 0, qry = 0;
@@ -245,7 +236,7 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_NCCL_CHECK(ncclReduce(d_t, d_t, 4, ncclFloat32, ncclMax, 0, comm, s));
   float mt[4];
   PKD_HIP_CHECK(hipMemcpyAsync(mt, d_t, sizeof(mt), hipMemcpyDeviceToHost, s));
-  watchdog_wait(s, comm, timeout_s, "timing reduce");
+  watchdog_wait(s, "timing reduce");
   if (berr) std::cerr << "kdtree_dist: rank " << rank << ": device build error word 0x" << std::hex << berr << std::dec
                       << std::endl;
   if (rank == 0 && mt[3] != 0.0f) {
@@ -308,10 +299,6 @@ int main(int argc, char** argv) {
   cli::Options o = cli::parse(int(rest.size()), rest.data());
   if (o.mode != "exact") {
     std::cerr << "kdtree_dist builds exact trees only; use kdtree_sequential --mode reference" << std::endl;
-    return 1;
-  }
-  if (o.decomp == "global" && (P & (P - 1))) {
-    std::cerr << "--decomp global needs a power-of-two number of GPUs" << std::endl;
     return 1;
   }
   const auto tick = std::chrono::high_resolution_clock::now();

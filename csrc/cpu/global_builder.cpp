@@ -1,17 +1,19 @@
-// Native global decomposition (see pkdtree/global_builder.hpp). The orchestration mirrors
-// parallel_kd_tree_amd/parallel/global_tree.py (_top_device, _exchange_plan, _build_device);
-// the device work is the dist_ops kernels plus one GpuBuilder per leaf sub-tree.
+// Native global decomposition (see pkdtree/global_builder.hpp): the geometry of who owns what,
+// the exchange planner, the build schedule and the loopback communicator. The device work is
+// the dist_ops kernels plus one GpuBuilder build per top-level leaf.
 #include "pkdtree/global_builder.hpp"
 
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "pkdtree/dist_ops.hpp"
 #include "pkdtree/gpu_build.hpp"
@@ -19,6 +21,60 @@
 
 namespace pkdtree {
 
+// ---------------------------------------------------------------------------------------------
+// Comm: bounded waits
+double Comm::default_timeout() {
+  const char* e = std::getenv("PKD_COMM_TIMEOUT");
+  return e ? std::max(0.01, std::atof(e)) : 300.0;
+}
+
+void Comm::wait(hipStream_t stream, const char* what) { poll_until_done(stream, what, {}); }
+
+void Comm::poll_until_done(hipStream_t stream, const char* what, const std::function<void()>& probe) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long it = 0;; ++it) {
+    const hipError_t q = hipStreamQuery(stream);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady)
+      throw std::runtime_error("rank " + std::to_string(rank()) + ": " + what + ": " + hipGetErrorString(q));
+    if (probe && (it & 63) == 0) probe();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > timeout_s_)
+      throw std::runtime_error("rank " + std::to_string(rank()) + ": " + what + ": not complete after " +
+                               std::to_string(timeout_s_) + " s (watchdog: a peer rank is stuck or gone)");
+    // The plan wait sits on the build's critical path: spin for the first 2 ms (the usual case
+    // ends within tens of microseconds), then yield, then sleep.
+    if (el < 2e-3) continue;
+    if (el < 20e-3) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+void Comm::alltoallv_planes(const void* send, size_t send_plane, const size_t* send_bytes, const size_t* send_off,
+                            void* recv, size_t recv_plane, const size_t* recv_bytes, const size_t* recv_off,
+                            int planes, hipStream_t stream) {
+  for (int q = 0; q < planes; ++q)
+    alltoallv(static_cast<const char*>(send) + size_t(q) * send_plane, send_bytes, send_off,
+              static_cast<char*>(recv) + size_t(q) * recv_plane, recv_bytes, recv_off, stream);
+}
+
+std::map<std::string, double> GlobalPhases::as_map() const {
+  return {{"top_ms", top_ms},
+          {"pack_ms", pack_ms},
+          {"plan_wait_ms", plan_wait_ms},
+          {"exchange_ms", exchange_ms},
+          {"exchange_span_ms", exchange_span_ms},
+          {"ids_ms", ids_ms},
+          {"leaf_ms", leaf_ms},
+          {"total_ms", total_ms},
+          {"sent_bytes", double(sent_bytes)},
+          {"recv_bytes", double(recv_bytes)},
+          {"max_peer_bytes", double(max_peer_bytes)},
+          {"rounds", double(rounds)},
+          {"retries", double(retries)}};
+}
+
+// ---------------------------------------------------------------------------------------------
 namespace global_plan {
 
 void segment(i64 n_total, i64 h, i64* lo_out, i64* n_out) {
@@ -43,38 +99,126 @@ i64 middle_cap(i64 n_total, int P, int level, int scale) {
   return std::min<i64>(std::max<i64>(2048, 3 * expect) * scale, std::max<i64>(n_total, 1));
 }
 
-int make_plan(const std::vector<i64>& counts, int P, int R, int me, i64 n_total, Plan* plan) {
-  const int S = P * R;  // destination slots per rank
-  if (counts.size() != size_t(P) * S * 4) throw std::invalid_argument("make_plan: counts must be [P][R * P][4]");
-  auto at = [&](int src, int slot, int f) { return counts[(size_t(src) * S + slot) * 4 + f]; };
+int top_levels_for(int P, int pipeline_k) {
+  if (P < 1 || P > 64) throw std::invalid_argument("global decomposition: 1 <= P <= 64 ranks");
+  int L = 0;
+  while ((1 << L) < P) ++L;
+  const bool pow2 = (P & (P - 1)) == 0;
+  const int extra = pipeline_k >= 0 ? pipeline_k : (P == 2 ? 1 : (pow2 ? 0 : 2));
+  return std::min(6, L + extra);
+}
+
+namespace {
+// heap node between leaves a and a + 1 of the T leaves at the bottom of the top tree: their
+// lowest common ancestor
+i64 gap_node(int T, int a) {
+  i64 x = T - 1 + a, y = T + a;
+  while (x != y) {
+    x = (x - 1) / 2;
+    y = (y - 1) / 2;
+  }
+  return x;
+}
+}  // namespace
+
+Layout make_layout(i64 n_total, int P, int pipeline_k) {
+  Layout lay;
+  lay.P = P;
+  lay.LL = top_levels_for(P, pipeline_k);
+  lay.T = 1 << lay.LL;
+  const int T = lay.T;
+  lay.leaf_lo.resize(size_t(P) + 1);
+  lay.R = 0;
+  for (int r = 0; r <= P; ++r) lay.leaf_lo[size_t(r)] = int(i64(r) * T / P);
+  for (int r = 0; r < P; ++r) lay.R = std::max(lay.R, lay.leaf_lo[size_t(r) + 1] - lay.leaf_lo[size_t(r)]);
+  lay.leaf_slot.assign(size_t(T), 0);
+  lay.leaf_n.assign(size_t(T), 0);
+  lay.top_slot.assign(size_t(T - 1), -1);
+  lay.top_owner.assign(size_t(T - 1), -1);
+  // in-order walk of the top tree's fringe: leaf 0, gap 0, leaf 1, ..., leaf T - 1
+  i64 pos = 0;
+  for (int t = 0; t < T; ++t) {
+    i64 lo, n;
+    segment(n_total, T - 1 + t, &lo, &n);
+    if (n > 0 && lo != pos) throw std::logic_error("global layout: leaf slot mismatch");
+    lay.leaf_slot[size_t(t)] = pos;
+    lay.leaf_n[size_t(t)] = n;
+    pos += n;
+    if (t + 1 < T) {
+      const i64 h = gap_node(T, t);
+      segment(n_total, h, &lo, &n);
+      if (n > 0) {
+        if (lo + n / 2 != pos) throw std::logic_error("global layout: top slot mismatch");
+        lay.top_slot[size_t(h)] = pos++;
+      }
+    }
+  }
+  if (pos != n_total) throw std::logic_error("global layout: slots do not cover the tree");
+  lay.share_lo.assign(size_t(P), 0);
+  lay.share_n.assign(size_t(P), 0);
+  for (int r = 0; r < P; ++r) {
+    const int a = lay.leaf_lo[size_t(r)], b = lay.leaf_lo[size_t(r) + 1];
+    for (int t = a; t + 1 < b; ++t) lay.top_owner[size_t(gap_node(T, t))] = r;
+    lay.share_lo[size_t(r)] = lay.leaf_slot[size_t(a)];
+    lay.share_n[size_t(r)] = lay.leaf_slot[size_t(b - 1)] + lay.leaf_n[size_t(b - 1)] - lay.leaf_slot[size_t(a)];
+  }
+  return lay;
+}
+
+void share_blocks(const Layout& lay, int r, std::vector<Block>* blocks, std::vector<i64>* between_heap) {
+  blocks->clear();
+  between_heap->clear();
+  const int a = lay.leaf_lo[size_t(r)], b = lay.leaf_lo[size_t(r) + 1];
+  const i64 base = lay.share_lo[size_t(r)];
+  for (int t = a; t < b;) {
+    int s = 0;  // largest aligned power-of-two run of leaves starting at t inside [t, b)
+    while (s < lay.LL && (t % (1 << (s + 1))) == 0 && t + (1 << (s + 1)) <= b) ++s;
+    const int e = t + (1 << s);  // leaves [t, e)
+    const i64 lo = lay.leaf_slot[size_t(t)];
+    const i64 hi = lay.leaf_slot[size_t(e - 1)] + lay.leaf_n[size_t(e - 1)];
+    blocks->push_back(Block{lo - base, hi - lo, lay.LL - s, ((i64(lay.T) + t) >> s) - 1});
+    if (e < b) {
+      const i64 h = gap_node(lay.T, e - 1);
+      if (lay.top_slot[size_t(h)] >= 0) between_heap->push_back(h);
+    }
+    t = e;
+  }
+}
+
+int make_plan(const std::vector<i64>& counts, const Layout& lay, int me, Plan* plan) {
+  const int P = lay.P, T = lay.T, R = lay.R;
+  if (counts.size() != size_t(P) * T * 4) throw std::invalid_argument("make_plan: counts must be [P][T][4]");
+  auto at = [&](int src, int leaf, int f) { return counts[(size_t(src) * T + leaf) * 4 + f]; };
   i64 errs = 0;
   for (int src = 0; src < P; ++src)
-    for (int slot = 0; slot < S; ++slot) errs |= at(src, slot, 1);
+    for (int t = 0; t < T; ++t) errs |= at(src, t, 1);
   if (errs & 1) return 1;  // a middle bucket overflowed its all-gather slot: retry larger
   if (errs & 2) throw std::runtime_error("global top levels: histogram totals disagree with the tree geometry");
-  // every rank checks every rank's receive totals: a failure raises on all ranks together
-  for (int q = 0; q < P; ++q)
-    for (int j = 0; j < R; ++j) {
-      i64 got = 0;
-      for (int src = 0; src < P; ++src) got += at(src, j * P + q, 0);
-      i64 lo, want;
-      segment(n_total, i64(P + q) * R - 1 + j, &lo, &want);
-      if (got != want)
-        throw std::runtime_error("global exchange: rank " + std::to_string(q) + " would receive " +
-                                 std::to_string(got) + " points in round " + std::to_string(j) +
-                                 " for a subtree of " + std::to_string(want));
-    }
-  plan->in_splits.assign(size_t(R), std::vector<i64>(size_t(P)));
-  plan->out_splits.assign(size_t(R), std::vector<i64>(size_t(P)));
-  plan->starts.assign(size_t(R) + 1, 0);
+  // every rank checks every leaf's total: a failure raises on all ranks together
+  for (int t = 0; t < T; ++t) {
+    i64 got = 0;
+    for (int src = 0; src < P; ++src) got += at(src, t, 0);
+    if (got != lay.leaf_n[size_t(t)])
+      throw std::runtime_error("global exchange: top-level leaf " + std::to_string(t) + " would receive " +
+                               std::to_string(got) + " points for a subtree of " +
+                               std::to_string(lay.leaf_n[size_t(t)]));
+  }
+  plan->leaf_start.assign(size_t(T) + 1, 0);
+  for (int t = 0; t < T; ++t) plan->leaf_start[size_t(t) + 1] = plan->leaf_start[size_t(t)] + at(me, t, 0);
+  plan->send_rows.assign(size_t(R), std::vector<i64>(size_t(P), 0));
+  plan->send_off.assign(size_t(R), std::vector<i64>(size_t(P), 0));
+  plan->recv_rows.assign(size_t(R), std::vector<i64>(size_t(P), 0));
+  const int my_a = lay.leaf_lo[size_t(me)], my_cnt = lay.leaf_lo[size_t(me) + 1] - my_a;
   for (int j = 0; j < R; ++j) {
-    i64 tot = 0;
-    for (int p = 0; p < P; ++p) {
-      plan->in_splits[size_t(j)][size_t(p)] = at(me, j * P + p, 0);
-      plan->out_splits[size_t(j)][size_t(p)] = at(p, j * P + me, 0);
-      tot += at(me, j * P + p, 0);
+    for (int q = 0; q < P; ++q) {
+      const int t = lay.leaf_lo[size_t(q)] + j;
+      if (t < lay.leaf_lo[size_t(q) + 1]) {
+        plan->send_rows[size_t(j)][size_t(q)] = at(me, t, 0);
+        plan->send_off[size_t(j)][size_t(q)] = plan->leaf_start[size_t(t)];
+      }
     }
-    plan->starts[size_t(j) + 1] = plan->starts[size_t(j)] + tot;
+    if (j < my_cnt)
+      for (int p = 0; p < P; ++p) plan->recv_rows[size_t(j)][size_t(p)] = at(p, my_a + j, 0);
   }
   plan->src_base.resize(size_t(P));
   plan->src_n.resize(size_t(P));
@@ -87,29 +231,31 @@ int make_plan(const std::vector<i64>& counts, int P, int R, int me, i64 n_total,
 
 }  // namespace global_plan
 
-using global_plan::segment;
-
+// ---------------------------------------------------------------------------------------------
 struct GlobalBuilder::Leaf {
   i64 n;
   int depth;
   std::unique_ptr<GpuBuilder> b;
-  void* ws = nullptr;
-  ~Leaf() {
-    if (ws) (void)hipFree(ws);
-  }
 };
+
+namespace {
+// timed events of a profiled build: 4 build-wide, then 5 per round
+enum { kEvStart = 0, kEvTop = 1, kEvPack = 2, kEvEnd = 3, kEvRound = 4 };
+enum { kRxBegin = 0, kRxEnd = 1, kIdsBegin = 2, kIdsEnd = 3, kLeafEnd = 4, kPerRound = 5 };
+int round_ev(int j, int which) { return kEvRound + kPerRound * j + which; }
+}  // namespace
 
 GlobalBuilder::GlobalBuilder(Comm& comm, i64 n_total, int dim, int pipeline_k)
     : comm_(comm), n_total_(n_total), dim_(dim), P_(comm.size()), rank_(comm.rank()) {
-  if (P_ < 1 || P_ > 64 || (P_ & (P_ - 1))) throw std::invalid_argument("global decomposition: P must be 2^k <= 64");
   if (n_total >= (i64(1) << 32)) throw std::invalid_argument("point ids are 32-bit: at most 2^32 - 1 points");
+  if (n_total < 0) throw std::invalid_argument("n_total must be >= 0");
   if (dim < 1) throw std::invalid_argument("dim must be >= 1");
-  L_ = 0;
-  while ((1 << L_) < P_) ++L_;
-  k_ = pipeline_k >= 0 ? pipeline_k : (P_ == 2 ? 1 : 0);
-  k_ = std::max(0, std::min(k_, 6 - L_));  // at most 64 leaves (32 nodes per top level)
-  segment(n_total_, P_ - 1 + rank_, &slot_lo_, &n_leaf_);
+  lay_ = global_plan::make_layout(n_total, P_, pipeline_k);
+  planar_ = dim <= 8;
   PKD_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  arrived_.assign(size_t(lay_.R), nullptr);
+  for (auto& e : arrived_) PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PKD_HIP_CHECK(hipEventCreateWithFlags(&packed_, hipEventDisableTiming));
 }
 
 GlobalBuilder::~GlobalBuilder() {
@@ -117,6 +263,10 @@ GlobalBuilder::~GlobalBuilder() {
     if (b.first) (void)hipFree(b.first);
   if (tree_pts_) (void)hipFree(tree_pts_);
   if (tree_ids_) (void)hipFree(tree_ids_);
+  if (leaf_ws_) (void)hipFree(leaf_ws_);
+  for (hipEvent_t e : arrived_) (void)hipEventDestroy(e);
+  for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  if (packed_) (void)hipEventDestroy(packed_);
   if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   if (host_counts_) (void)hipHostFree(host_counts_);
 }
@@ -124,7 +274,7 @@ GlobalBuilder::~GlobalBuilder() {
 void* GlobalBuilder::buf(int slot, size_t bytes) {
   if (bufs_.size() <= size_t(slot)) bufs_.resize(size_t(slot) + 1, {nullptr, 0});
   auto& b = bufs_[size_t(slot)];
-  bytes = std::max<size_t>(bytes, 16);
+  bytes = std::max<size_t>(bytes, 256);
   if (b.second < bytes) {
     if (b.first) PKD_HIP_CHECK(hipFree(b.first));
     PKD_HIP_CHECK(hipMalloc(&b.first, bytes));
@@ -139,52 +289,90 @@ GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth) {
   auto l = std::make_unique<Leaf>();
   l->n = n;
   l->depth = depth;
-  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth});
-  PKD_HIP_CHECK(hipMalloc(&l->ws, std::max<size_t>(l->b->workspace_bytes(), 16)));
+  // no split build inside a distributed build: its side streams plus the caller's and the
+  // communication stream would exceed the 4 hardware queues, and RCCL's kernels would queue
+  // behind partition passes
+  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false});
   leaves_.push_back(std::move(l));
   return *leaves_.back()->b;
 }
 
+void GlobalBuilder::ensure_leaf_workspace(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (leaf_ws_bytes_ >= bytes) return;
+  if (leaf_ws_) PKD_HIP_CHECK(hipFree(leaf_ws_));
+  PKD_HIP_CHECK(hipMalloc(&leaf_ws_, bytes));
+  leaf_ws_bytes_ = bytes;
+}
+
 std::vector<i64> GlobalBuilder::top_slots() const {
-  std::vector<i64> s(size_t(std::max(P_ - 1, 0)));
-  for (int h = 0; h < P_ - 1; ++h) {
-    i64 lo, n;
-    segment(n_total_, h, &lo, &n);
-    s[size_t(h)] = n > 0 ? lo + n / 2 : -1;
-  }
+  std::vector<i64> s(size_t(std::max(lay_.T - 1, 0)), -1);
+  for (int h = 0; h + 1 < lay_.T; ++h)
+    if (lay_.top_owner[size_t(h)] < 0) s[size_t(h)] = lay_.top_slot[size_t(h)];
   return s;
 }
 
 u32 GlobalBuilder::read_error(hipStream_t stream) const {
   PKD_HIP_CHECK(hipStreamSynchronize(stream));
-  u32 e = 0;
-  if (bufs_.size() > 5 && bufs_[5].first) {
-    u32 w[4];
-    PKD_HIP_CHECK(hipMemcpy(w, bufs_[5].first, 16, hipMemcpyDeviceToHost));
-    e |= w[0] & 8u;
+  if (bufs_.size() <= 5 || !bufs_[5].first) return 0;
+  u32 w[4];
+  PKD_HIP_CHECK(hipMemcpy(w, bufs_[5].first, 16, hipMemcpyDeviceToHost));
+  return (w[0] & 8u) | w[1];  // the compact exchange's bitmap check | the leaf builds' error words
+}
+
+void GlobalBuilder::set_profile(bool on) {
+  profile_ = on;
+  if (on && events_.empty()) {
+    events_.resize(size_t(kEvRound + kPerRound * lay_.R));
+    for (auto& e : events_) PKD_HIP_CHECK(hipEventCreate(&e));
   }
-  for (const auto& l : leaves_) e |= l->b->read_error(l->ws, stream);
-  return e;
+}
+
+GlobalPhases GlobalBuilder::phases(hipStream_t stream) const {
+  if (events_.empty()) throw std::runtime_error("GlobalBuilder::phases: no profiled build (set_profile(true))");
+  comm_.wait(stream, "global build (profile)");
+  auto el = [&](int a, int b) {
+    float ms = 0;
+    PKD_HIP_CHECK(hipEventElapsedTime(&ms, ev(a), ev(b)));
+    return double(ms);
+  };
+  GlobalPhases p = last_;
+  p.top_ms = el(kEvStart, kEvTop);
+  p.pack_ms = el(kEvTop, kEvPack);
+  p.total_ms = el(kEvStart, kEvEnd);
+  const int R = lay_.R, mine = lay_.leaf_lo[size_t(rank_) + 1] - lay_.leaf_lo[size_t(rank_)];
+  for (int j = 0; j < R; ++j) p.exchange_ms += el(round_ev(j, kRxBegin), round_ev(j, kRxEnd));
+  p.exchange_span_ms = el(round_ev(0, kRxBegin), round_ev(R - 1, kRxEnd));
+  for (int j = 0; j < mine; ++j) {
+    p.ids_ms += el(round_ev(j, kIdsBegin), round_ev(j, kIdsEnd));
+    p.leaf_ms += el(round_ev(j, kIdsEnd), round_ev(j, kLeafEnd));
+  }
+  return p;
 }
 
 void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_t s) {
-  const int dim = dim_, P = P_, LL = L_ + k_, R = 1 << k_, leaves = P << k_;
+  const int dim = dim_, P = P_, me = rank_, LL = lay_.LL, T = lay_.T, R = lay_.R;
   const TopPoints tp{pts, nullptr, n_local, dim, id_base};
   global_plan::Plan plan;
   float* top_rows = nullptr;
+  GlobalPhases info;
+  if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvStart), s));
+  // send side: planar (SoA, dim <= 8) or 12-B rows; one bitmap of send_words words per leaf
+  const i64 send_stride = planar_ ? std::max<i64>(64, (n_local + 63) / 64 * 64) : 0;
+  const i64 send_words = std::max<i64>(1, (n_local + 31) / 32);
   for (;;) {  // until no middle bucket overflows its all-gather slot
     // 1. bounding box: one allreduce(MIN) of the encoded per-rank boxes
     auto* box = static_cast<i64*>(buf(0, size_t(2 * dim) * 8));
     fill_u64(box, 2 * dim, 0xffffffffull, s);
     top_bbox(tp, box, s);
     comm_.allreduce_min_i64(box, size_t(2 * dim), s);
-    auto* cells = static_cast<float*>(buf(1, size_t(2 * leaves - 1) * dim * 2 * 4));
+    auto* cells = static_cast<float*>(buf(1, size_t(2 * T - 1) * dim * 2 * 4));
     top_root_cell(box, dim, cells, s);
     auto* node = static_cast<u32*>(buf(2, size_t(std::max<i64>(n_local, 1)) * 4));
-    auto* pivots = static_cast<u64*>(buf(3, size_t(std::max(leaves - 1, 1)) * 8));
-    fill_u64(pivots, std::max(leaves - 1, 1), ~0ull, s);
-    top_rows = static_cast<float*>(buf(4, size_t(std::max(leaves - 1, 1)) * (dim + 1) * 4 + 8));  // + 8: 64-bit fill
-    fill_u64(top_rows, (i64(std::max(leaves - 1, 1)) * (dim + 1) + 1) / 2, 0ull, s);
+    auto* pivots = static_cast<u64*>(buf(3, size_t(std::max(T - 1, 1)) * 8));
+    fill_u64(pivots, std::max(T - 1, 1), ~0ull, s);
+    top_rows = static_cast<float*>(buf(4, size_t(std::max(T - 1, 1)) * (dim + 1) * 4 + 8));  // + 8: 64-bit fill
+    fill_u64(top_rows, (i64(std::max(T - 1, 1)) * (dim + 1) + 1) / 2, 0ull, s);
     auto* err = static_cast<u32*>(buf(5, 16));
     fill_u64(err, 2, 0ull, s);
     auto* sel = static_cast<u32*>(buf(6, size_t(kTopMaxNodes) * 4 * 4));
@@ -196,7 +384,7 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
       TopSizes sizes{};
       for (int j = 0; j < nodes; ++j) {
         i64 lo;
-        segment(n_total_, nodes - 1 + j, &lo, &sizes.n[j]);
+        global_plan::segment(n_total_, nodes - 1 + j, &lo, &sizes.n[j]);
       }
       fill_u64(hist, i64(nodes) * bins / 2, 0ull, s);
       top_route_hist(tp, node, level, pivots, prev_axis, axis, cells, bins, hist, s);
@@ -210,132 +398,181 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
       comm_.allgather(mid, gathered, words * 4, s);
       top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err, s);
     }
-    // 3. pack by destination slot (round j, rank r): 12-B rows + one bit per (row, slot)
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvTop), s));
+    // 3. pack by destination leaf: coordinates (planes or rows) + one bit per (row, leaf)
     const int last_axis = ((LL - 1) % dim + dim) % dim;
-    auto* send = static_cast<float*>(buf(10, size_t(std::max<i64>(n_local, 1)) * dim * 4));
-    auto* counts = static_cast<i64*>(buf(11, size_t(leaves) * 4 * 8));
-    top_counts_init(counts, leaves, i64(id_base), n_local, s);
-    const i64 words = std::max<i64>(1, (n_local + 31) / 32);
-    auto* bm = static_cast<u32*>(buf(12, size_t(leaves) * words * 4));
-    void* scratch = buf(13, top_pack_scratch_bytes(n_local, leaves));
-    top_pack(tp, node, LL, pivots, last_axis, leaves, k_, send, dim, bm, words, counts, err, scratch, s);
-    // 4. the count matrix, all-gathered: the one host read-back of the build
-    auto* all = static_cast<i64*>(buf(14, size_t(P) * leaves * 4 * 8));
-    comm_.allgather(counts, all, size_t(leaves) * 4 * 8, s);
-    // pinned staging and a polling wait: the blocking wait's wake-up cost ~0.2 ms per build
-    const size_t nall = size_t(P) * leaves * 4;
+    auto* send = static_cast<float*>(
+        buf(10, planar_ ? size_t(dim) * send_stride * 4 : size_t(std::max<i64>(n_local, 1)) * dim * 4));
+    auto* counts = static_cast<i64*>(buf(11, size_t(T) * 4 * 8));
+    top_counts_init(counts, T, i64(id_base), n_local, s);
+    auto* bm = static_cast<u32*>(buf(12, size_t(T) * send_words * 4));
+    void* scratch = buf(13, top_pack_scratch_bytes(n_local, T));
+    top_pack(tp, node, LL, pivots, last_axis, send, dim, send_stride, bm, send_words, counts, err, scratch, s);
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvPack), s));
+    // 4. the count matrix, all-gathered: the one host read-back of the build (bounded wait)
+    auto* all = static_cast<i64*>(buf(14, size_t(P) * T * 4 * 8));
+    comm_.allgather(counts, all, size_t(T) * 4 * 8, s);
+    const size_t nall = size_t(P) * T * 4;
     if (host_counts_n_ < nall) {
       if (host_counts_) PKD_HIP_CHECK(hipHostFree(host_counts_));
       PKD_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counts_), nall * 8, hipHostMallocDefault));
       host_counts_n_ = nall;
     }
     PKD_HIP_CHECK(hipMemcpyAsync(host_counts_, all, nall * 8, hipMemcpyDeviceToHost, s));
-    for (;;) {
-      const hipError_t q = hipStreamQuery(s);
-      if (q == hipSuccess) break;
-      if (q != hipErrorNotReady) PKD_HIP_CHECK(q);
-    }
+    const auto w0 = std::chrono::steady_clock::now();
+    comm_.wait(s, "exchange plan");
+    info.plan_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     const std::vector<i64> hall(host_counts_, host_counts_ + nall);
-    if (global_plan::make_plan(hall, P, R, rank_, n_total_, &plan) == 0) break;
+    if (global_plan::make_plan(hall, lay_, me, &plan) == 0) break;
     if (global_plan::middle_cap(n_total_, P, 0, scale_) >= n_total_)
       throw std::runtime_error("global top levels: middle buckets inconsistent at full capacity");
     scale_ *= 8;
+    ++info.retries;
   }
   top_rows_ = top_rows;  // buffer slot 4, exposed through top_rows()
 
-  // 5. my sub-tree: node P - 1 + rank at depth L; its 2^k leaves are the heap nodes
-  // first_leaf + j; the R - 1 pivots between them come from the replicated top rows
-  if (!tree_pts_) {
-    PKD_HIP_CHECK(hipMalloc(&tree_pts_, size_t(std::max<i64>(n_leaf_, 1)) * dim * 4));
-    PKD_HIP_CHECK(hipMalloc(&tree_ids_, size_t(std::max<i64>(n_leaf_, 1)) * 4));
-  }
-  const i64 m = P - 1 + rank_;
-  const i64 first_leaf = (m + 1) * R - 1;
-  for (int lvl = 0; lvl < k_; ++lvl)
-    for (i64 h = (m + 1) * (i64(1) << lvl) - 1; h < (m + 2) * (i64(1) << lvl) - 1; ++h) {
-      i64 lo, n;
-      segment(n_total_, h, &lo, &n);
-      if (n <= 0) continue;
-      const i64 slot = lo + n / 2 - slot_lo_;
-      const float* row = top_rows_ + size_t(h) * (dim + 1);
-      PKD_HIP_CHECK(hipMemcpyAsync(tree_pts_ + slot * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
-      PKD_HIP_CHECK(hipMemcpyAsync(tree_ids_ + slot, row + dim, 4, hipMemcpyDeviceToDevice, s));
-    }
+  // 5. everything the rounds need, sized once from the plan: no allocation (and no implicit
+  // device synchronisation) once the first exchange is in flight
+  const int my_a = lay_.leaf_lo[size_t(me)], mine = lay_.leaf_lo[size_t(me) + 1] - my_a;
   std::vector<i64> src_words(static_cast<size_t>(P)), bm_off(static_cast<size_t>(P));
-  i64 bm_total = 0;
+  i64 bm_total = 0, max_words = 0;
   for (int p = 0; p < P; ++p) {
     src_words[size_t(p)] = std::max<i64>(1, (plan.src_n[size_t(p)] + 31) / 32);
     bm_off[size_t(p)] = bm_total;
     bm_total += src_words[size_t(p)];
+    max_words = std::max(max_words, src_words[size_t(p)]);
   }
-  const i64 send_words = std::max<i64>(1, (n_local + 31) / 32);
+  const i64 n_share = lay_.share_n[size_t(me)];
+  if (!tree_pts_) {
+    PKD_HIP_CHECK(hipMalloc(&tree_pts_, size_t(std::max<i64>(n_share, 1)) * dim * 4));
+    PKD_HIP_CHECK(hipMalloc(&tree_ids_, size_t(std::max<i64>(n_share, 1)) * 4));
+  }
+  std::vector<GpuBuilder*> lb(size_t(mine), nullptr);
+  std::vector<float*> recv(size_t(R), nullptr);
+  std::vector<u32*> recv_bm(size_t(R), nullptr), lids(size_t(R), nullptr);
+  std::vector<i64> col_stride(size_t(R), 0);
+  size_t ws_need = 0;
+  for (int j = 0; j < mine; ++j) {
+    // every source sends its bitmap for each of my leaves, empty leaves included
+    recv_bm[size_t(j)] = static_cast<u32*>(buf(21 + 3 * j, size_t(bm_total) * 4));
+    const i64 n_j = lay_.leaf_n[size_t(my_a + j)];
+    if (n_j <= 0) continue;
+    GpuBuilder& b = leaf_builder(n_j, LL);
+    lb[size_t(j)] = &b;
+    ws_need = std::max(ws_need, b.workspace_bytes());
+    if (planar_) {
+      col_stride[size_t(j)] = b.column_stride();
+      recv[size_t(j)] = static_cast<float*>(buf(20 + 3 * j, size_t(dim + 1) * b.column_stride() * 4));
+      lids[size_t(j)] = reinterpret_cast<u32*>(recv[size_t(j)] + size_t(dim) * b.column_stride());
+    } else {
+      recv[size_t(j)] = static_cast<float*>(buf(20 + 3 * j, size_t(n_j) * dim * 4));
+      lids[size_t(j)] = static_cast<u32*>(buf(22 + 3 * j, size_t(n_j) * 4));
+    }
+  }
+  ensure_leaf_workspace(ws_need);
+  void* ids_scratch = buf(16, ids_from_bitmaps_scratch_bytes(max_words, P));
   auto* send = static_cast<float*>(buf(10, 0));
   auto* bm = static_cast<u32*>(buf(12, 0));
   auto* err = static_cast<u32*>(buf(5, 16));
-  hipEvent_t packed, arrived[64];
-  PKD_HIP_CHECK(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
-  PKD_HIP_CHECK(hipEventRecord(packed, s));
-  PKD_HIP_CHECK(hipStreamWaitEvent(comm_stream_, packed, 0));
-  std::vector<float*> recv(static_cast<size_t>(R));
-  std::vector<u32*> recv_bm(static_cast<size_t>(R));
+  // the top nodes between my leaves are replicated rows: straight into my share
+  {
+    TopPlacement pl{};
+    for (int h = 0; h + 1 < T; ++h)
+      if (lay_.top_owner[size_t(h)] == me && lay_.top_slot[size_t(h)] >= 0) {
+        pl.heap[pl.count] = h;
+        pl.slot[pl.count] = lay_.top_slot[size_t(h)] - lay_.share_lo[size_t(me)];
+        ++pl.count;
+      }
+    top_place_rows(top_rows, dim, pl, tree_pts_, tree_ids_, s);
+  }
+  // exchange volume (self excluded), for the profile
+  {
+    std::vector<i64> peer(static_cast<size_t>(P), 0);
+    for (int j = 0; j < R; ++j)
+      for (int p = 0; p < P; ++p) {
+        if (p == me) continue;
+        const bool to_leaf = j < lay_.leaf_lo[size_t(p) + 1] - lay_.leaf_lo[size_t(p)];
+        const i64 sb = plan.send_rows[size_t(j)][size_t(p)] * dim * 4 + (to_leaf ? send_words * 4 : 0);
+        const i64 rb = plan.recv_rows[size_t(j)][size_t(p)] * dim * 4 + (j < mine ? src_words[size_t(p)] * 4 : 0);
+        info.sent_bytes += sb;
+        info.recv_bytes += rb;
+        peer[size_t(p)] += sb;
+      }
+    info.max_peer_bytes = *std::max_element(peer.begin(), peer.end());
+    info.rounds = R;
+  }
+  PKD_HIP_CHECK(hipEventRecord(packed_, s));
+  PKD_HIP_CHECK(hipStreamWaitEvent(comm_stream_, packed_, 0));
+  // 6. round j: leaf leaf_lo[q] + j of every rank q that has one, on the communication stream
   auto issue = [&](int j) {
-    i64 rows = 0;
-    for (int p = 0; p < P; ++p) rows += plan.out_splits[size_t(j)][size_t(p)];
-    recv[size_t(j)] = static_cast<float*>(buf(20 + 2 * j, size_t(std::max<i64>(rows, 1)) * dim * 4));
-    recv_bm[size_t(j)] = static_cast<u32*>(buf(21 + 2 * j, size_t(bm_total) * 4));
     std::vector<size_t> sb(static_cast<size_t>(P)), so(sb), rb(sb), ro(sb);
-    i64 soff = plan.starts[size_t(j)], roff = 0;
+    i64 roff = 0;
     for (int p = 0; p < P; ++p) {
-      sb[size_t(p)] = size_t(plan.in_splits[size_t(j)][size_t(p)]) * dim * 4;
-      so[size_t(p)] = size_t(soff) * dim * 4;
-      soff += plan.in_splits[size_t(j)][size_t(p)];
-      rb[size_t(p)] = size_t(plan.out_splits[size_t(j)][size_t(p)]) * dim * 4;
-      ro[size_t(p)] = size_t(roff) * dim * 4;
-      roff += plan.out_splits[size_t(j)][size_t(p)];
+      sb[size_t(p)] = size_t(plan.send_rows[size_t(j)][size_t(p)]) * 4 * (planar_ ? 1 : dim);
+      so[size_t(p)] = size_t(plan.send_off[size_t(j)][size_t(p)]) * 4 * (planar_ ? 1 : dim);
+      rb[size_t(p)] = size_t(plan.recv_rows[size_t(j)][size_t(p)]) * 4 * (planar_ ? 1 : dim);
+      ro[size_t(p)] = size_t(roff) * 4 * (planar_ ? 1 : dim);
+      roff += plan.recv_rows[size_t(j)][size_t(p)];
     }
-    comm_.alltoallv(send, sb.data(), so.data(), recv[size_t(j)], rb.data(), ro.data(), comm_stream_);
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kRxBegin)), comm_stream_));
+    comm_.group_begin();
+    if (planar_)
+      comm_.alltoallv_planes(send, size_t(send_stride) * 4, sb.data(), so.data(), recv[size_t(j)],
+                             size_t(col_stride[size_t(j)]) * 4, rb.data(), ro.data(), dim, comm_stream_);
+    else
+      comm_.alltoallv(send, sb.data(), so.data(), recv[size_t(j)], rb.data(), ro.data(), comm_stream_);
+    // id bitmaps: to every rank with a leaf in this round, from every rank if I have one
     for (int p = 0; p < P; ++p) {
-      sb[size_t(p)] = size_t(send_words) * 4;
-      so[size_t(p)] = size_t(i64(j) * P + p) * send_words * 4;
-      rb[size_t(p)] = size_t(src_words[size_t(p)]) * 4;
+      const int t = lay_.leaf_lo[size_t(p)] + j;
+      const bool has = t < lay_.leaf_lo[size_t(p) + 1];
+      sb[size_t(p)] = has ? size_t(send_words) * 4 : 0;
+      so[size_t(p)] = has ? size_t(t) * send_words * 4 : 0;
+      rb[size_t(p)] = j < mine ? size_t(src_words[size_t(p)]) * 4 : 0;
       ro[size_t(p)] = size_t(bm_off[size_t(p)]) * 4;
     }
     comm_.alltoallv(bm, sb.data(), so.data(), recv_bm[size_t(j)], rb.data(), ro.data(), comm_stream_);
-    PKD_HIP_CHECK(hipEventCreateWithFlags(&arrived[j], hipEventDisableTiming));
-    PKD_HIP_CHECK(hipEventRecord(arrived[j], comm_stream_));
+    comm_.group_end();
+    PKD_HIP_CHECK(hipEventRecord(arrived_[size_t(j)], comm_stream_));
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kRxEnd)), comm_stream_));
   };
   issue(0);
   for (int j = 0; j < R; ++j) {
     if (j + 1 < R) issue(j + 1);  // in flight while leaf j builds
-    PKD_HIP_CHECK(hipStreamWaitEvent(s, arrived[j], 0));
-    i64 lo_j, n_j;
-    segment(n_total_, first_leaf + j, &lo_j, &n_j);
+    if (j >= mine) continue;
+    PKD_HIP_CHECK(hipStreamWaitEvent(s, arrived_[size_t(j)], 0));
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kIdsBegin)), s));
+    const int t = my_a + j;
+    const i64 n_j = lay_.leaf_n[size_t(t)];
     if (n_j > 0) {
       BmSources src{};
       i64 off = 0;
       for (int p = 0; p < P; ++p) {
         src.off[p] = off;
-        src.cnt[p] = plan.out_splits[size_t(j)][size_t(p)];
+        src.cnt[p] = plan.recv_rows[size_t(j)][size_t(p)];
         off += src.cnt[p];
         src.bm_off[p] = bm_off[size_t(p)];
         src.words[p] = src_words[size_t(p)];
         src.base[p] = u32(plan.src_base[size_t(p)]);
       }
-      i64 max_words = 0;
-      for (int p = 0; p < P; ++p) max_words = std::max(max_words, src_words[size_t(p)]);
-      auto* lids = static_cast<u32*>(buf(15, size_t(n_j) * 4));
-      void* scr = buf(16, ids_from_bitmaps_scratch_bytes(max_words, P));
-      ids_from_bitmaps(recv_bm[size_t(j)], P, src, lids, scr, err, s);
-      GpuBuilder& b = leaf_builder(n_j, LL);
-      void* ws = nullptr;
-      for (auto& l : leaves_)
-        if (l->b.get() == &b) ws = l->ws;
-      const i64 a = lo_j - slot_lo_;
-      b.build(recv[size_t(j)], lids, 0, tree_pts_ + a * dim, tree_ids_ + a, ws, s);
+      ids_from_bitmaps(recv_bm[size_t(j)], P, src, lids[size_t(j)], ids_scratch, err, s);
     }
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kIdsEnd)), s));
+    if (n_j > 0) {
+      GpuBuilder& b = *lb[size_t(j)];
+      const i64 a = lay_.leaf_slot[size_t(t)] - lay_.share_lo[size_t(me)];
+      if (planar_) b.build_columns(recv[size_t(j)], tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s);
+      else b.build(recv[size_t(j)], lids[size_t(j)], 0, tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s);
+      or_error_word(b.error_word(leaf_ws_), err + 1, s);  // the leaves share one workspace
+    }
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kLeafEnd)), s));
   }
-  for (int j = 0; j < R; ++j) (void)hipEventDestroy(arrived[j]);
-  (void)hipEventDestroy(packed);
+  // the send buffers are rewritten by the next build: the caller's stream waits for the rounds
+  PKD_HIP_CHECK(hipEventRecord(packed_, comm_stream_));
+  PKD_HIP_CHECK(hipStreamWaitEvent(s, packed_, 0));
+  if (profile_) {
+    PKD_HIP_CHECK(hipEventRecord(ev(kEvEnd), s));
+    last_ = info;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

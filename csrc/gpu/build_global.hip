@@ -2201,7 +2201,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     const SplitCfg sc = split_cfg();
     const int L = sc.level;
     const bool paired = lg_ >= 2 && levels_[0].pair;
-    if (sc.on && paired && !narrow_ && dim <= 8 && n_ >= sc.min_n && L >= 2 && L % 2 == 0 && L < lg_ &&
+    if (sc.on && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.min_n && L >= 2 && L % 2 == 0 && L < lg_ &&
         sc.parts >= 2 && sc.streams >= 1) {
       const int P = std::min(pow2_floor(sc.parts), 1 << L);
       split_level_ = L;
@@ -2340,10 +2340,26 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   run_levels(out_pts, out_ids, ws, stream);
 }
 
+void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
+  if (n_ == 0) return;
+  if (narrow_) throw std::runtime_error("pkdtree: build_columns needs the full-column layout (dim <= 8)");
+  if (reinterpret_cast<uintptr_t>(cols) % 256 != 0) throw std::invalid_argument("pkdtree: columns must be 256-B aligned");
+  TraceRange tr("pkd.build");
+  char* ws = static_cast<char*>(workspace);
+  u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
+  u32* part = bbox + 2 * dim_;
+  const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
+  k_bbox_soa<<<grid, kBlock, 0, stream>>>(cols, n_, dim_, part, ncol_);
+  PKD_LAUNCH_CHECK();
+  k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, grid, dim_, bbox);
+  PKD_LAUNCH_CHECK();
+  run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, cols);
+}
+
 void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
-                            u32 id_base, const float* in_rows, i64 in_rs) const {
+                            u32 id_base, const float* in_rows, i64 in_rs, float* cols_a) const {
   const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
-  float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
+  float* colsA = cols_a ? cols_a : reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
   i64* seg_n = reinterpret_cast<i64*>(ws + off_seg_n_);

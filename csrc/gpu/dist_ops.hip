@@ -409,32 +409,25 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
   if (tid == 0 && !s_found) atomicOr(err, 1u);
 }
 
-// ---- counting sort by destination (P <= 64) -------------------------------------------
-// Destination slot of top-level leaf l. With a pipelined exchange (pipe_k > 0) rank r owns the
-// 2^pipe_k leaves r * 2^pipe_k + j, sent in round j; slots are ordered (round, rank) so each
-// round's rows are one contiguous run in rank order.
-__device__ __forceinline__ int dest_slot(u32 l, int P, int pipe_k) {
-  if (pipe_k == 0) return int(l);
-  const u32 mask = (1u << pipe_k) - 1u;
-  return int((l & mask) * u32(P >> pipe_k) + (l >> pipe_k));
-}
-
+// ---- counting sort by destination leaf (T <= 64 leaves) --------------------------------
+// Rows are grouped by top-level leaf; which rank receives a leaf in which exchange round is
+// the host planner's business (global_plan::make_plan), so the kernels never see ranks.
 __global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restrict__ node, int levels,
-                                                       const u64* __restrict__ pivots, int last_axis, int P,
-                                                       int pipe_k, i64 per_block, u32* __restrict__ bcount) {
+                                                       const u64* __restrict__ pivots, int last_axis, int T,
+                                                       i64 per_block, u32* __restrict__ bcount) {
   __shared__ u32 cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
   const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
-  const u32 first = u32(P - 1);
+  const u32 first = u32(T - 1);
   for (i64 i = b0 + threadIdx.x; i < b1; i += kBlock) {
     // levels == 0 (one rank, no pipelining): every point stays at the root's single leaf
     const u32 h = levels > 0 ? route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots) : 0u;
     node[i] = h;
-    if (h != kTopDone) atomicAdd(&cnt[dest_slot(h - first, P, pipe_k)], 1u);
+    if (h != kTopDone) atomicAdd(&cnt[h - first], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < P) bcount[i64(blockIdx.x) * P + threadIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < T) bcount[i64(blockIdx.x) * T + threadIdx.x] = cnt[threadIdx.x];
 }
 
 // offsets[block][d] = sum_{d' < d} total[d'] + sum_{b' < block} bcount[b'][d]: one workgroup per
@@ -482,13 +475,15 @@ __global__ __launch_bounds__(kScanThreads) void k_pack_scan(const u32* __restric
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int P,
-                                                         int pipe_k, i64 per_block, const u32* __restrict__ offsets,
-                                                         float* __restrict__ out, int rs) {
+// cs == 0: rows of rs floats; cs > 0: SoA planes of stride cs (ids never travel in planes: the
+// planar exchange is always the compact one)
+__global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int T,
+                                                         i64 per_block, const u32* __restrict__ offsets,
+                                                         float* __restrict__ out, int rs, i64 cs) {
   __shared__ u32 cur[64];
   __shared__ u32 wcnt[kBlock / 64][64];
-  const u32 first = u32(P - 1);
-  if (threadIdx.x < P) cur[threadIdx.x] = offsets[i64(blockIdx.x) * P + threadIdx.x];
+  const u32 first = u32(T - 1);
+  if (threadIdx.x < T) cur[threadIdx.x] = offsets[i64(blockIdx.x) * T + threadIdx.x];
   __syncthreads();
   const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const int w = threadIdx.x / 64, ln = dev::lane();
@@ -496,9 +491,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
     const i64 i = c0 + threadIdx.x;
     const u32 h = i < b1 ? node[i] : kTopDone;
-    const int d = h == kTopDone ? -1 : dest_slot(h - first, P, pipe_k);
+    const int d = h == kTopDone ? -1 : int(h - first);
     u32 my = 0;
-    for (int e = 0; e < P; ++e) {  // stable rank among same-destination points of the chunk
+    for (int e = 0; e < T; ++e) {  // stable rank among same-destination points of the chunk
       const u64 m = __ballot(d == e);
       if (ln == 0) wcnt[w][e] = __popcll(m);
       if (d == e) my = mbcnt(m);
@@ -507,17 +502,29 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
     if (d >= 0) {
       u32 off = cur[d];
       for (int v = 0; v < w; ++v) off += wcnt[v][d];
-      float* o = out + i64(off + my) * rs;
+      const i64 k = i64(off + my);
       const float* r = p.pts + i * dim;
-      if (dim == 3) {  // one 12-B load and store per row (dwordx3) instead of three dword pairs
-        *reinterpret_cast<float3*>(o) = *reinterpret_cast<const float3*>(r);
+      if (cs > 0) {
+        if (dim == 3) {  // one 12-B row load, three coalesced plane stores
+          const float3 v = *reinterpret_cast<const float3*>(r);
+          out[k] = v.x;
+          out[cs + k] = v.y;
+          out[2 * cs + k] = v.z;
+        } else {
+          for (int c = 0; c < dim; ++c) out[c * cs + k] = r[c];
+        }
       } else {
-        for (int c = 0; c < dim; ++c) o[c] = r[c];
+        float* o = out + k * rs;
+        if (dim == 3) {  // one 12-B load and store per row (dwordx3) instead of three dword pairs
+          *reinterpret_cast<float3*>(o) = *reinterpret_cast<const float3*>(r);
+        } else {
+          for (int c = 0; c < dim; ++c) o[c] = r[c];
+        }
+        if (rs > dim) o[dim] = __uint_as_float(point_id(p, i));
       }
-      if (rs > dim) o[dim] = __uint_as_float(point_id(p, i));
     }
     __syncthreads();
-    if (threadIdx.x < P) {
+    if (threadIdx.x < T) {
       u32 add = 0;
       for (int v = 0; v < kBlock / 64; ++v) add += wcnt[v][threadIdx.x];
       cur[threadIdx.x] += add;
@@ -526,18 +533,18 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   }
 }
 
-// Destination bitmaps of the compact exchange: bm[d][w] bit j = row 32w + j goes to leaf d.
-// One wave per 64 rows (two words), one ballot per destination; rows >= n give zero words,
-// so the grid covers the whole padded stride.
-__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int P, int pipe_k,
-                                                        i64 ws, u32* __restrict__ bm) {
+// Leaf bitmaps of the compact exchange: bm[d][w] bit j = row 32w + j goes to leaf d.
+// One wave per 64 rows (two words), one ballot per leaf; rows >= n give zero words, so the
+// grid covers the whole padded stride.
+__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int T, i64 ws,
+                                                        u32* __restrict__ bm) {
   const i64 wave = (i64(blockIdx.x) * kBlock + threadIdx.x) / 64;
   const int ln = dev::lane();
   const i64 row = wave * 64 + ln;
-  const u32 first = u32(P - 1);
+  const u32 first = u32(T - 1);
   const u32 h = row < n ? node[row] : kTopDone;
-  const int d = h == kTopDone ? -1 : dest_slot(h - first, P, pipe_k);
-  for (int e = 0; e < P; ++e) {
+  const int d = h == kTopDone ? -1 : int(h - first);
+  for (int e = 0; e < T; ++e) {
     const u64 m = __ballot(d == e);
     const i64 w = 2 * wave + (ln & 1);
     if (ln < 2 && w < ws) bm[i64(e) * ws + w] = ln == 0 ? u32(m) : u32(m >> 32);
@@ -701,32 +708,64 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
   PKD_LAUNCH_CHECK();
 }
 
-size_t top_pack_scratch_bytes(i64 n, int P) { return size_t(2) * pack_blocks(n) * size_t(P) * 4; }
+size_t top_pack_scratch_bytes(i64 n, int T) { return size_t(2) * pack_blocks(n) * size_t(T) * 4; }
 
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, int pipe_k,
-              float* out_rows, int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, float* out,
+              int row_stride, i64 col_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
               void* scratch, hipStream_t stream) {
-  if (P > 64 || P != (1 << levels)) throw std::invalid_argument("top_pack: P must be 2^levels <= 64");
-  if (pipe_k < 0 || pipe_k > levels) throw std::invalid_argument("top_pack: pipe_k out of range");
-  if (row_stride != p.dim && row_stride != p.dim + 1) throw std::invalid_argument("top_pack: row stride dim or dim+1");
+  if (levels < 0 || levels > 6) throw std::invalid_argument("top_pack: at most 6 top levels (64 leaves)");
+  const int T = 1 << levels;
+  if (col_stride > 0 && (col_stride < p.n || p.ids != nullptr))
+    throw std::invalid_argument("top_pack: planar output needs col_stride >= n and implicit ids");
+  if (col_stride == 0 && row_stride != p.dim && row_stride != p.dim + 1)
+    throw std::invalid_argument("top_pack: row stride dim or dim+1");
   if (bitmaps && bitmap_words * 32 < p.n) throw std::invalid_argument("top_pack: bitmap stride too small");
   const int blocks = pack_blocks(p.n);
   const i64 per_block = (std::max<i64>(p.n, 1) + blocks - 1) / blocks;
   u32* bcount = static_cast<u32*>(scratch);
-  u32* offsets = bcount + size_t(blocks) * P;
-  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, P, pipe_k, per_block, bcount);
+  u32* offsets = bcount + size_t(blocks) * T;
+  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, T, per_block, bcount);
   PKD_LAUNCH_CHECK();
   static_assert(2 * kScanThreads >= 2048, "k_pack_scan covers at most 2 * kScanThreads blocks");
-  k_pack_scan<<<P, kScanThreads, 0, stream>>>(bcount, blocks, P, offsets, counts, err);
+  k_pack_scan<<<T, kScanThreads, 0, stream>>>(bcount, blocks, T, offsets, counts, err);
   PKD_LAUNCH_CHECK();
-  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, P, pipe_k, per_block, offsets, out_rows, row_stride);
+  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, T, per_block, offsets, out, row_stride, col_stride);
   PKD_LAUNCH_CHECK();
   if (bitmaps) {
     const i64 waves = (bitmap_words + 1) / 2;
-    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, P, pipe_k, bitmap_words,
-                                                                                  bitmaps);
+    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, T, bitmap_words, bitmaps);
     PKD_LAUNCH_CHECK();
   }
+}
+
+namespace {
+__global__ void k_place_rows(const float* __restrict__ top_rows, int dim, TopPlacement pl, float* __restrict__ out_pts,
+                             u32* __restrict__ out_ids) {
+  const int i = blockIdx.x;
+  const float* r = top_rows + size_t(pl.heap[i]) * (dim + 1);
+  const i64 s = pl.slot[i];
+  for (int c = threadIdx.x; c < dim; c += blockDim.x) out_pts[s * dim + c] = r[c];
+  if (threadIdx.x == 0) out_ids[s] = __float_as_uint(r[dim]);
+}
+}  // namespace
+
+namespace {
+__global__ void k_or_word(const u32* __restrict__ src, u32* __restrict__ dst) {
+  if (threadIdx.x == 0) *dst |= *src;
+}
+}  // namespace
+
+void or_error_word(const u32* src, u32* dst, hipStream_t stream) {
+  k_or_word<<<1, 64, 0, stream>>>(src, dst);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_place_rows(const float* top_rows, int dim, const TopPlacement& pl, float* out_pts, u32* out_ids,
+                    hipStream_t stream) {
+  if (pl.count <= 0) return;
+  if (pl.count > 64) throw std::invalid_argument("top_place_rows: at most 64 rows");
+  k_place_rows<<<pl.count, 64, 0, stream>>>(top_rows, dim, pl, out_pts, out_ids);
+  PKD_LAUNCH_CHECK();
 }
 
 size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P) {

@@ -76,18 +76,32 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream);
 
 // Final routing below the last top level + counting sort of rows by destination leaf
-// (dest = node - (P - 1)): out_rows [n_kept][row_stride] grouped by destination (stable),
-// row_stride = dim + 1 (coordinates, id bits) or dim (compact: coordinates only). counts
-// [P][4] int64 = (rows for dest, err word, 2 words left to the caller). Pivot points are dropped. With
-// `bitmaps` ([P][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the destination of every
-// row is also written as one bit per (dest, row): the compact exchange sends 12-B rows plus
-// n / 8 bytes per destination instead of 16-B rows, and the receiver rebuilds the ids.
-// pipe_k > 0 (pipelined exchange): P = ranks * 2^pipe_k leaves, rank r owns leaves
-// r * 2^pipe_k + j, and destination slots (rows, counts, bitmaps) are ordered (j, r).
-size_t top_pack_scratch_bytes(i64 n, int P);
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, int P, int pipe_k,
-              float* out_rows, int row_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
+// (dest = node - (T - 1), T = 2^levels leaves <= 64). Output grouped by leaf (stable):
+//   * col_stride == 0: rows out[k][row_stride], row_stride = dim + 1 (coordinates, id bits) or
+//     dim (compact: coordinates only);
+//   * col_stride  > 0: SoA planes, coordinate c of output row k at out[c * col_stride + k]
+//     (the receiver's builder takes columns directly, no AoS -> SoA pass).
+// counts [T][4] int64 = (rows for leaf, err word, 2 words left to the caller). Pivot points are
+// dropped. With `bitmaps` ([T][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the leaf of
+// every row is also written as one bit per (leaf, row): the compact exchange sends the
+// coordinates plus n / 8 bytes per leaf instead of ids, and the receiver rebuilds the ids.
+size_t top_pack_scratch_bytes(i64 n, int T);
+void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, float* out,
+              int row_stride, i64 col_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
               void* scratch, hipStream_t stream);
+
+// Copies top-tree rows (dim + 1 floats: coordinates, id bits; heap order) into output slots:
+// out_pts[slot[i]] / out_ids[slot[i]] = top_rows[heap[i]] for i < count (<= 64).
+struct TopPlacement {
+  int count;
+  int heap[64];
+  i64 slot[64];
+};
+void top_place_rows(const float* top_rows, int dim, const TopPlacement& pl, float* out_pts, u32* out_ids,
+                    hipStream_t stream);
+
+// *dst |= *src (device words): collects the error words of builds that share a workspace.
+void or_error_word(const u32* src, u32* dst, hipStream_t stream);
 
 // Receiver of the compact exchange: rows from source s occupy [off[s], off[s] + cnt[s]) of
 // the receive buffer in increasing source-row order, so the k-th row from s has the id

@@ -1,21 +1,27 @@
-// Native global decomposition: ONE exact kd-tree over P ranks (one process or thread per GPU),
-// the C++ counterpart of parallel_kd_tree_amd/parallel/global_tree.py.
+// Native global decomposition: ONE exact kd-tree over P ranks (one process or thread per GPU).
 //
 // The reference only splits its data into independent per-rank trees (kdtree_mpi.cpp:204-253).
-// Here the top log2(P) (+ k pipelining) levels are decided jointly: per level one
+// Here the top LL levels (LL = ceil(log2 P) + k) are decided jointly: per level one
 // route+histogram pass, an allreduce(SUM) of the histogram, the median bucket per node, one
 // compaction pass, a fixed-size all-gather and a radix select of the exact pivot (the device
-// ops of dist_ops.hpp). Every point then travels to the rank that owns its top-level leaf --
-// 12-B rows plus one bit per (row, destination), ids rebuilt on the receiver -- in 2^k
-// all-to-all rounds, each on its own communication stream so round j + 1 is in flight while
-// leaf j builds. The result is slot for slot the tree one GPU builds on all points.
+// ops of dist_ops.hpp). The T = 2^LL top-level leaves are dealt to the ranks in contiguous runs
+// (rank r owns leaves [r T / P, (r + 1) T / P): any P, not only powers of two), and every point
+// travels to the rank owning its leaf -- coordinates plus one bit per (row, leaf), ids rebuilt
+// on the receiver -- in one all-to-all round per leaf of a rank, on a communication stream, so
+// round j + 1 is in flight while leaf j builds. For dim <= 8 the coordinates travel as SoA
+// planes straight into the leaf builder's input columns (no AoS -> SoA pass on the receiver).
+// The result is slot for slot the tree one GPU builds on all points.
 //
-// Communication goes through the Comm interface: RCCL over xGMI in kdtree_dist, torch's RCCL
-// process group from Python, and an in-process loopback (threads sharing one GPU) for tests.
+// Communication goes through the Comm interface: RCCL over xGMI (kdtree_dist and the Python
+// extension, one communicator per process) and an in-process loopback (threads) for tests.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
+#include <map>
 #include <memory>
+#include <string>
+#include <utility>
 #include <vector>
 
 #include "pkdtree/common.hpp"
@@ -29,6 +35,15 @@ class Comm {
   virtual ~Comm() = default;
   virtual int rank() const = 0;
   virtual int size() const = 0;
+  // Blocks until everything enqueued on `stream` (collectives included) has completed. The
+  // wait is bounded: after timeout() seconds without completion -- or as soon as the
+  // communicator reports an asynchronous error -- it throws a rank-tagged runtime_error, so a
+  // stuck or failed peer makes this rank exit non-zero instead of hanging.
+  // The base implementation polls the stream; RcclComm also polls ncclCommGetAsyncError and
+  // aborts the communicator before throwing.
+  virtual void wait(hipStream_t stream, const char* what);
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  double timeout() const { return timeout_s_; }
   virtual void allreduce_sum_u32(u32* buf, size_t count, hipStream_t stream) = 0;
   virtual void allreduce_min_i64(i64* buf, size_t count, hipStream_t stream) = 0;
   // recv[r * bytes, (r + 1) * bytes) = send of rank r
@@ -36,6 +51,25 @@ class Comm {
   // bytes and offsets per peer (send side: to peer r; receive side: from peer r)
   virtual void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                          const size_t* recv_bytes, const size_t* recv_off, hipStream_t stream) = 0;
+  // `planes` all-to-all-v's with the same per-peer layout, plane q at send + q * send_plane /
+  // recv + q * recv_plane (SoA columns). RcclComm issues them as one group.
+  virtual void alltoallv_planes(const void* send, size_t send_plane, const size_t* send_bytes, const size_t* send_off,
+                                void* recv, size_t recv_plane, const size_t* recv_bytes, const size_t* recv_off,
+                                int planes, hipStream_t stream);
+  // Collectives between group_begin() and group_end() may be fused into one launch (RCCL
+  // groups); the loopback communicator ignores them.
+  virtual void group_begin() {}
+  virtual void group_end() {}
+
+ protected:
+  // Polls `stream` until it completes or the deadline passes; `probe` (may be empty) is called
+  // between polls and throws on a communicator error. Spins briefly (the plan wait is on the
+  // build's critical path), then yields, then sleeps.
+  void poll_until_done(hipStream_t stream, const char* what, const std::function<void()>& probe);
+  double timeout_s_ = default_timeout();
+
+ private:
+  static double default_timeout();  // PKD_COMM_TIMEOUT seconds, default 300
 };
 
 // Host-side geometry and planning (pure functions, unit-tested on the CPU).
@@ -44,56 +78,101 @@ namespace global_plan {
 void segment(i64 n_total, i64 h, i64* lo, i64* n);
 // Middle-bucket rows a rank may contribute at `level` (identical on every rank).
 i64 middle_cap(i64 n_total, int P, int level, int scale);
-// Exchange plan from the all-gathered per-slot counts [P][R * P][4] (rows, err, id base,
-// n_local), slots ordered (round j, rank r). Returns 0 (ok), 1 (a middle bucket overflowed:
-// retry with larger slots) or throws on inconsistent geometry. Fills per round j the rows to
-// send to / receive from every rank, and the source id bases / local sizes.
-struct Plan {
-  std::vector<std::vector<i64>> in_splits, out_splits;  // [R][P]
-  std::vector<i64> starts;                               // [R + 1] send-buffer row offsets
-  std::vector<i64> src_base, src_n;                      // [P]
+
+// Which rank owns which part of the tree. The top LL levels have T = 2^LL leaves (heap nodes
+// T - 1 + t); rank r owns leaves [leaf_lo[r], leaf_lo[r + 1]). A rank's share of the in-order
+// tree is the contiguous slot range of its leaves plus the top nodes between them; the top
+// nodes between two ranks' leaves ("boundary" nodes, owner -1) sit outside every share.
+// LL: pipeline_k >= 0 gives ceil(log2 P) + pipeline_k; -1 picks 1 extra level at P = 2 (the
+// exchange over one xGMI link is worth overlapping), 0 at other powers of two and 2 for other
+// P (leaf runs of 4-6 keep the ranks within ~12-25% of an equal share); LL <= 6.
+struct Layout {
+  int P = 1, LL = 0, T = 1, R = 1;       // ranks, top levels, leaves, rounds (max leaves per rank)
+  std::vector<int> leaf_lo;              // [P + 1]
+  std::vector<i64> leaf_slot, leaf_n;    // [T] in-order slot range of each leaf
+  std::vector<i64> top_slot;             // [T - 1] heap order; -1: empty node
+  std::vector<int> top_owner;            // [T - 1] rank whose share holds it, -1: boundary
+  std::vector<i64> share_lo, share_n;    // [P] slot range of each rank's share
 };
-int make_plan(const std::vector<i64>& counts, int P, int R, int me, i64 n_total, Plan* plan);
+Layout make_layout(i64 n_total, int P, int pipeline_k);
+int top_levels_for(int P, int pipeline_k);
+// A rank's share as complete subtrees ("blocks": dyadic runs of its leaves) and the top nodes
+// between consecutive blocks. Block: offset in the share, points, depth of its root, heap node.
+struct Block {
+  i64 off, n;
+  int depth;
+  i64 heap;
+};
+void share_blocks(const Layout& lay, int r, std::vector<Block>* blocks, std::vector<i64>* between_heap);
+
+// Exchange plan from the all-gathered per-leaf counts [P][T][4] (rows, err, id base, n_local).
+// Returns 0 (ok), 1 (a middle bucket overflowed: retry with larger slots) or throws on
+// inconsistent geometry. Round j carries leaf leaf_lo[q] + j of every rank q that has one.
+struct Plan {
+  std::vector<std::vector<i64>> send_rows, send_off;  // [R][P] rows to peer q in round j, and where
+  std::vector<std::vector<i64>> recv_rows;             // [R][P] rows from peer p in round j
+  std::vector<i64> leaf_start;                          // [T + 1] my pack buffer's leaf offsets
+  std::vector<i64> src_base, src_n;                     // [P] id base and local rows of every rank
+};
+int make_plan(const std::vector<i64>& counts, const Layout& lay, int me, Plan* plan);
 }  // namespace global_plan
+
+// Per-phase times of one profiled build (GlobalBuilder::set_profile): hipEvent milliseconds
+// on the build's streams, plan_wait_ms on the host clock.
+struct GlobalPhases {
+  double top_ms = 0, pack_ms = 0, plan_wait_ms = 0, exchange_ms = 0, exchange_span_ms = 0, ids_ms = 0,
+         leaf_ms = 0, total_ms = 0;
+  i64 sent_bytes = 0, recv_bytes = 0, max_peer_bytes = 0;  // exchange payload, self excluded
+  int rounds = 0, retries = 0;
+  std::map<std::string, double> as_map() const;
+};
 
 class GpuBuilder;
 
 class GlobalBuilder {
  public:
-  // pipeline_k < 0: 1 at P = 2, else 0 (the exchange only dominates at two ranks)
   GlobalBuilder(Comm& comm, i64 n_total, int dim, int pipeline_k = -1);
   ~GlobalBuilder();
   GlobalBuilder(const GlobalBuilder&) = delete;
   GlobalBuilder& operator=(const GlobalBuilder&) = delete;
 
   // This rank's points [n_local][dim] (device), ids id_base + row (the reference's global
-  // 1-based ids are first_row + 1 + row). Synchronises once (the exchange plan).
+  // 1-based ids are first_row + 1 + row). Synchronises once (the exchange plan), with the
+  // communicator's deadline.
   void build(const float* pts, i64 n_local, u32 id_base, hipStream_t stream);
+  // Waits (bounded, see Comm::wait) until the last build has completed on `stream`.
+  void wait(hipStream_t stream) { comm_.wait(stream, "global build"); }
 
-  // This rank's share of the tree: slots [slot_lo, slot_lo + n_leaf) of the global in-order
-  // tree (device rows / ids), at depth log2(P) of the global tree.
-  i64 slot_lo() const { return slot_lo_; }
-  i64 n_leaf() const { return n_leaf_; }
-  int top_levels() const { return L_; }
+  const global_plan::Layout& layout() const { return lay_; }
+  // This rank's share of the tree: slots [slot_lo, slot_lo + n_leaf) of the global in-order tree.
+  i64 slot_lo() const { return lay_.share_lo[size_t(rank_)]; }
+  i64 n_leaf() const { return lay_.share_n[size_t(rank_)]; }
+  int top_levels() const { return lay_.LL; }
   // all-gather slot scale of the middle buckets (x 8 per overflow retry; sticky across builds)
   int middle_scale() const { return scale_; }
   const float* tree_pts() const { return tree_pts_; }
   const u32* tree_ids() const { return tree_ids_; }
-  // The P - 1 replicated top pivots, heap order: rows of dim + 1 floats (coordinates, id
-  // bits) on the device, and their global slots (-1: empty node).
+  // The T - 1 top-tree rows, heap order: dim + 1 floats (coordinates, id bits) on the device.
   const float* top_rows() const { return top_rows_; }
+  // Slots of the boundary top nodes (heap order, -1: empty or inside a share).
   std::vector<i64> top_slots() const;
   // OR of the device error words of the last build (0 = ok). Synchronises `stream`.
   u32 read_error(hipStream_t stream) const;
+  // Per-phase hipEvent timing of the following builds (adds event records, no host syncs).
+  void set_profile(bool on);
+  GlobalPhases phases(hipStream_t stream) const;  // of the last profiled build; synchronises
 
  private:
   void* buf(int slot, size_t bytes);
   GpuBuilder& leaf_builder(i64 n, int depth);
+  void ensure_leaf_workspace(size_t bytes);
+  hipEvent_t ev(int i) const { return events_[size_t(i)]; }
 
   Comm& comm_;
   i64 n_total_;
-  int dim_, P_, rank_, L_, k_;
-  i64 slot_lo_ = 0, n_leaf_ = 0;
+  int dim_, P_, rank_;
+  global_plan::Layout lay_;
+  bool planar_;  // dim <= 8: SoA planes into the leaf builder's columns
   int scale_ = 1;
   float* tree_pts_ = nullptr;
   u32* tree_ids_ = nullptr;
@@ -104,6 +183,13 @@ class GlobalBuilder {
   std::vector<std::pair<void*, size_t>> bufs_;
   struct Leaf;
   std::vector<std::unique_ptr<Leaf>> leaves_;
+  void* leaf_ws_ = nullptr;  // one workspace shared by the leaf builds (they run in stream order)
+  size_t leaf_ws_bytes_ = 0;
+  std::vector<hipEvent_t> arrived_;  // per round (untimed), created once
+  hipEvent_t packed_ = nullptr;
+  bool profile_ = false;
+  std::vector<hipEvent_t> events_;  // timed events of a profiled build (see set_profile)
+  GlobalPhases last_;               // host-side parts of the last profiled build
 };
 
 // In-process loopback communicator: `size` ranks are threads of one process (sharing one GPU

@@ -27,6 +27,10 @@ namespace pkdtree {
 struct BuildOptions {
   int subtree_max = 0;   // max segment handled by the LDS kernel (0 = auto from dim)
   int depth0 = 0;        // depth of the root (subtrees of a distributed tree start deeper)
+  // Split build allowed (side HIP streams for large builds). The distributed builder turns it
+  // off for its leaf builds: their streams plus its communication stream would exceed the
+  // hardware queues (GPU_MAX_HW_QUEUES = 4), and RCCL's kernels would queue behind partitions.
+  bool allow_split = true;
 };
 
 struct LevelPlan {
@@ -77,7 +81,17 @@ class GpuBuilder {
   // Sticky error word of the last build (0 = ok); synchronises the stream. Debug aid.
   // detail (optional, 3 words): first failure code, level, value.
   u32 read_error(const void* workspace, hipStream_t stream, u32* detail = nullptr) const;
+  // Device address of that error word (valid until the workspace's next build).
+  const u32* error_word(const void* workspace) const {
+    return reinterpret_cast<const u32*>(static_cast<const char*>(workspace) + off_err_);
+  }
   void build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
+  // Same, from caller-owned SoA columns (column c of row r at cols[c * column_stride() + r],
+  // column dim = ids; 256-B aligned, (dim + 1) * column_stride() floats). The columns are
+  // CLOBBERED: they serve as one of the build's two ping-pong buffers, so no AoS -> SoA pass
+  // and no copy into the workspace is needed. The distributed builder receives its exchange
+  // straight into such columns. Needs dim <= 8 (the full-column layout).
+  void build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
 
  private:
   void prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base, float* out_pts,
@@ -86,8 +100,9 @@ class GpuBuilder {
   // first pair's kernels synthesise them.
   // in_rows != nullptr: narrow columns (the lg_ global levels' keys, ids, input row index);
   // full rows are gathered from the AoS input `in_rows` (stride in_rs floats).
+  // cols_a != nullptr: replaces the workspace's first column buffer (the input of the first pass).
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
-                  u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0) const;
+                  u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0, float* cols_a = nullptr) const;
   // Side streams for a split build on the current device (nullptr: run unsplit, e.g. when
   // the streams do not exist yet and `stream` is being captured into a graph).
   SplitStreams* split_streams_for(hipStream_t stream) const;

@@ -1,7 +1,12 @@
 // The global builder's communicator on RCCL (xGMI between the GPUs of a node): allreduce and
 // allgather as single collectives, the all-to-all-v as one grouped set of point-to-point
 // sends and receives (xGMI links are point-to-point), the self part as a device copy.
-// Used by kdtree_dist --decomp global and by the Python extension (bench.py at N > 1).
+// Used by kdtree_dist (both decompositions) and by the Python extension (bench.py at N > 1).
+//
+// Failure detection: wait() polls the stream and ncclCommGetAsyncError until
+// the communicator's deadline; a stuck peer or an asynchronous RCCL error aborts the
+// communicator (so this rank's RCCL kernels stop and the process can exit) and throws a
+// rank-tagged error.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -26,6 +31,30 @@ class RcclComm final : public Comm {
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   ncclComm_t handle() const { return c_; }
+  bool aborted() const { return aborted_; }
+  // Stops the communicator's outstanding operations (idempotent); the handle is then dead and
+  // must not be destroyed with ncclCommDestroy.
+  void abort() {
+    if (!aborted_) {
+      aborted_ = true;
+      (void)ncclCommAbort(c_);
+    }
+  }
+
+  void wait(hipStream_t s, const char* what) override {
+    try {
+      poll_until_done(s, what, [&] {
+        ncclResult_t async = ncclSuccess;
+        PKD_RCCL(ncclCommGetAsyncError(c_, &async));
+        if (async != ncclSuccess)
+          throw std::runtime_error("rank " + std::to_string(rank_) + ": " + what + ": asynchronous RCCL error " +
+                                   ncclGetErrorString(async));
+      });
+    } catch (...) {
+      abort();
+      throw;
+    }
+  }
   void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
     PKD_RCCL(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, c_, s));
   }
@@ -37,24 +66,37 @@ class RcclComm final : public Comm {
   }
   void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
+    alltoallv_planes(send, 0, send_bytes, send_off, recv, 0, recv_bytes, recv_off, 1, s);
+  }
+  void alltoallv_planes(const void* send, size_t send_plane, const size_t* send_bytes, const size_t* send_off,
+                        void* recv, size_t recv_plane, const size_t* recv_bytes, const size_t* recv_off, int planes,
+                        hipStream_t s) override {
     const char* sp = static_cast<const char*>(send);
     char* rp = static_cast<char*>(recv);
     if (send_bytes[rank_] != recv_bytes[rank_]) throw std::runtime_error("alltoallv: self size mismatch");
-    if (send_bytes[rank_])
-      PKD_HIP_CHECK(hipMemcpyAsync(rp + recv_off[rank_], sp + send_off[rank_], send_bytes[rank_],
-                                   hipMemcpyDeviceToDevice, s));
-    PKD_RCCL(ncclGroupStart());
-    for (int p = 0; p < size_; ++p) {
-      if (p == rank_) continue;
-      if (send_bytes[p]) PKD_RCCL(ncclSend(sp + send_off[p], send_bytes[p], ncclChar, p, c_, s));
-      if (recv_bytes[p]) PKD_RCCL(ncclRecv(rp + recv_off[p], recv_bytes[p], ncclChar, p, c_, s));
+    if (send_bytes[rank_]) {  // the self part of every plane: one strided device copy
+      PKD_HIP_CHECK(hipMemcpy2DAsync(rp + recv_off[rank_], planes > 1 ? recv_plane : send_bytes[rank_],
+                                     sp + send_off[rank_], planes > 1 ? send_plane : send_bytes[rank_],
+                                     send_bytes[rank_], size_t(planes), hipMemcpyDeviceToDevice, s));
     }
+    PKD_RCCL(ncclGroupStart());
+    for (int q = 0; q < planes; ++q)
+      for (int p = 0; p < size_; ++p) {
+        if (p == rank_) continue;
+        if (send_bytes[p])
+          PKD_RCCL(ncclSend(sp + size_t(q) * send_plane + send_off[p], send_bytes[p], ncclChar, p, c_, s));
+        if (recv_bytes[p])
+          PKD_RCCL(ncclRecv(rp + size_t(q) * recv_plane + recv_off[p], recv_bytes[p], ncclChar, p, c_, s));
+      }
     PKD_RCCL(ncclGroupEnd());
   }
+  void group_begin() override { PKD_RCCL(ncclGroupStart()); }
+  void group_end() override { PKD_RCCL(ncclGroupEnd()); }
 
  private:
   ncclComm_t c_;
   int rank_, size_;
+  bool aborted_ = false;
 };
 
 #undef PKD_RCCL

@@ -37,9 +37,8 @@ def main(argv=None) -> int:
     ap.add_argument("--decomp", choices=["single", "forest", "global"], default=None)
     ap.add_argument("--mode", choices=["exact", "reference"], default="exact")
     ap.add_argument("--device", choices=["cuda", "cpu"], default=None)
-    ap.add_argument("--impl", choices=["native", "python"], default="native",
-                    help="--decomp global on GPUs: the C++ GlobalBuilder on its own RCCL communicator, or the "
-                         "Python orchestration over torch.distributed (host tensors always use the latter)")
+    ap.add_argument("--pipeline-k", type=int, default=-1,
+                    help="--decomp global: extra distributed top levels (more, smaller leaf builds; -1: auto)")
     ap.add_argument("--query", choices=["auto", "brute", "traverse"], default="auto")
     ap.add_argument("--queries", type=int, default=10)
     ap.add_argument("--debug", action="store_true")
@@ -109,12 +108,12 @@ def main(argv=None) -> int:
     else:
         if a.mode != "exact":
             raise SystemExit("--decomp global builds exact trees only")
-        if device.type == "cuda" and a.impl == "native":
+        if device.type == "cuda":  # the native builder on its own RCCL communicator
             from .parallel.native_global import NativeGlobalBuilder
-            gb = NativeGlobalBuilder(n, dim, device)
-        else:
+            gb = NativeGlobalBuilder(n, dim, device, pipeline_k=a.pipeline_k)
+        else:  # host tensors over gloo: the same schedule in torch
             from .parallel.global_tree import GlobalTreeBuilder
-            gb = GlobalTreeBuilder(n, dim, device=device)
+            gb = GlobalTreeBuilder(n, dim, device=device, pipeline_k=a.pipeline_k)
         t = gb.build(x, id_base=first + 1)
         packed = t.query_packed(q, a.query)
         _all_ok(comm, gb.read_error() if device.type == "cuda" else 0, device)

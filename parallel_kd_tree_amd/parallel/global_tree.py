@@ -1,27 +1,31 @@
-"""Global decomposition: ONE exact kd-tree over P ranks (P a power of two).
+"""Global decomposition: ONE exact kd-tree over P ranks (any P <= 64).
 
 North-star design (BASELINE.json): the reference's forest of independent per-rank trees
 (kdtree_mpi.cpp:204-253) becomes a single distributed tree:
 
 1. bounding box: allreduce MIN / MAX of the per-rank boxes;
-2. top log2(P) levels, level by level: every rank histograms its points (routed below the
-   pivots decided so far) into linear buckets of its node's cell, the histograms are
-   allreduced (SUM), the bucket holding each node's median is found, the few points of that
-   bucket are all-gathered and ranked under the (key, id) order -> the exact pivot point of
-   every node at that level, identical on every rank;
-3. one all-to-all: every point goes to the rank owning its top-level leaf (rank r owns heap
-   node P-1+r), pivots stay replicated;
-4. each rank builds its subtree (depth log2 P) with the single-GPU builder.
+2. top LL levels, level by level: every rank histograms its points (routed below the pivots
+   decided so far) into linear buckets of its node's cell, the histograms are allreduced (SUM),
+   the bucket holding each node's median is found, the few points of that bucket are
+   all-gathered and ranked under the (key, id) order -> the exact pivot point of every node at
+   that level, identical on every rank;
+3. the T = 2^LL top-level leaves are dealt to the ranks in contiguous runs and every point
+   travels to the rank owning its leaf, one all-to-all round per leaf of a rank;
+4. each rank builds its leaves' subtrees (depth LL).
 
 The result is slot-for-slot the tree a single GPU builds on the concatenated points.
-Communication uses torch.distributed: backend "nccl" (= RCCL over xGMI) on MI355X, "gloo" in
-CPU tests, where the per-rank device ops run as torch code with identical arithmetic.
+
+The GPU implementation is the native C++ builder (csrc/cpu/global_builder.cpp, Python handle
+:class:`~parallel_kd_tree_amd.parallel.native_global.NativeGlobalBuilder`) on RCCL. This module
+holds what both paths share -- :class:`DistTree` (a rank's share of the tree and the replicated
+top tree, with the query / gather / check helpers) -- and :class:`GlobalTreeBuilder`, the same
+schedule on host tensors over gloo (CPU tests and the CPU rehearsal of ``bench.py``): torch code
+with the kernels' arithmetic for the per-rank steps, and the native geometry and exchange
+planner (``global_layout`` / ``global_plan``) so both paths agree on who owns what.
 """
 from __future__ import annotations
 
-import math
 import os
-import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -30,12 +34,18 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
-from ..utils.trace import trace_range
 from . import comm
-from .geometry import composite_u64, make_params, median_slot, segment
+from .geometry import composite_u64, make_params, segment
 
 TOP_BINS = 8192  # nodes * bins per top level (LDS histogram in the kernel)
 DONE = 0xFFFFFFFF
+
+
+def layout(n_total: int, P: int, k: int = -1) -> dict:
+    """Who owns what (csrc/cpu/global_builder.cpp, global_plan::make_layout): LL top levels,
+    T leaves, leaf runs per rank, every rank's share (slot range, complete-subtree blocks and
+    the top rows between them), the top nodes' slots and owners (-1: boundary)."""
+    return ops.native().global_layout(int(n_total), int(P), int(k))
 
 
 def _to_rows(points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) -> torch.Tensor:
@@ -48,12 +58,17 @@ def _to_rows(points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) ->
     return rows
 
 
-def _signed_keys(rows: torch.Tensor, dim: int, axis: int) -> torch.Tensor:
-    """Composite keys as int64 with the top bit flipped, so signed order == unsigned order."""
-    kb = rows[:, axis].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+def signed_keys(pts: torch.Tensor, ids: torch.Tensor, axis: int) -> torch.Tensor:
+    """Composite (orderable(key) << 32 | id) keys as int64 with the top bit flipped, so that
+    signed order == the builder's unsigned order."""
+    kb = pts[:, axis].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     ok = torch.where((kb & 0x80000000) != 0, (~kb) & 0xFFFFFFFF, kb | 0x80000000)
-    ib = rows[:, dim].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    ib = ids.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     return ((ok ^ 0x80000000) << 32) | ib
+
+
+def _signed_keys(rows: torch.Tensor, dim: int, axis: int) -> torch.Tensor:
+    return signed_keys(rows[:, :dim], rows[:, dim], axis)
 
 
 def _u64_to_signed(v: int) -> int:
@@ -109,33 +124,49 @@ class _HostOps:
         return out
 
     @staticmethod
-    def pack(rows, dim, node, levels, pivots_u64, last_axis, P, k):
-        """Rows sorted by destination slot (round j, rank r) -> j * P + r, where rank r owns the
-        2^k leaves r * 2^k + j at depth log2(P) + k (dest_slot in csrc/gpu/dist_ops.hip)."""
-        piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
-        _route_cpu(rows, dim, node, piv, last_axis)
+    def pack(rows, dim, node, levels, pivots_u64, last_axis):
+        """Rows grouped by top-level leaf (stable) and the rows per leaf (k_pack_* kernels)."""
+        T = 1 << levels
+        if levels > 0:
+            piv = torch.tensor([_u64_to_signed(int(v)) for v in pivots_u64], dtype=torch.int64)
+            _route_cpu(rows, dim, node, piv, last_axis)
         live = (node != DONE).nonzero().flatten()
-        leaves = P << k
-        leaf = node[live] - (leaves - 1)
-        dest = (leaf & ((1 << k) - 1)) * P + (leaf >> k)
-        order = torch.sort(dest, stable=True).indices
-        return rows[live[order]].contiguous(), torch.bincount(dest, minlength=leaves).to(torch.int64)
+        leaf = node[live] - (T - 1)
+        order = torch.sort(leaf, stable=True).indices
+        return rows[live[order]].contiguous(), torch.bincount(leaf, minlength=T).to(torch.int64)
 
 
 @dataclass
 class DistTree:
-    """A rank's share of the global tree plus the replicated top tree."""
+    """A rank's share of the global tree plus the replicated top tree.
+
+    The share is the slot range [slot_lo, slot_lo + n) of the global in-order tree: complete
+    subtrees ("blocks", each a valid implicit tree with its own root depth) and the top rows
+    between them -- one block rooted at depth log2 P for a power-of-two P. ``top_rows`` holds
+    all T - 1 top-tree rows in heap order; ``top_slots[h]`` is the global slot of the boundary
+    rows (between two ranks' shares, outside every share) and -1 otherwise."""
     n_total: int
     dim: int
     depth0: int
     P: int
     rank: int
-    tree_pts: torch.Tensor           # this rank's subtree (in-order), slots [slot_lo, slot_lo + n)
+    tree_pts: torch.Tensor           # this rank's share (in-order), slots [slot_lo, slot_lo + n)
     tree_ids: torch.Tensor
     slot_lo: int
     top_slots: List[int] = field(default_factory=list)
-    top_rows: Optional[torch.Tensor] = None   # [P-1, dim+1] pivot rows, heap order
+    top_rows: Optional[torch.Tensor] = None   # [T - 1, dim + 1] top-tree rows, heap order
     timings: Dict[str, float] = field(default_factory=dict)
+    layout: Optional[dict] = None
+
+    @property
+    def blocks(self) -> List[Tuple[int, int, int, int]]:
+        """(offset in the share, points, root depth, heap node) of every complete subtree."""
+        return list(self.layout["blocks"][self.rank])
+
+    @property
+    def between(self) -> List[int]:
+        """Heap nodes of the top rows between this rank's blocks (inside its share)."""
+        return list(self.layout["between"][self.rank])
 
     def gather_full(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """Assemble the whole in-order tree on every rank (for checks and small N)."""
@@ -146,7 +177,7 @@ class DistTree:
         parts = _all_gather_var(rows)
         full = torch.empty((self.n_total, self.dim + 1), dtype=torch.float32, device=dev)
         for r, part in enumerate(parts):
-            lo, _ = segment(self.n_total, self.P - 1 + r)
+            lo = int(self.layout["share_lo"][r])
             full[lo:lo + part.shape[0]] = part
         if self.top_rows is not None:
             for i, s in enumerate(self.top_slots):
@@ -155,18 +186,55 @@ class DistTree:
         return full[:, :self.dim].contiguous(), full[:, self.dim].contiguous().view(torch.int32)
 
     def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
-        """Exact NN over the whole distributed tree: local subtree + top pivots, MIN-reduced."""
+        """Exact NN over the whole distributed tree: this rank's blocks and the top rows between
+        them, rank 0 also the boundary top rows; MIN-reduced over the ranks."""
         from ..models.kdtree import KDTree
-        local = KDTree(self.tree_pts, self.tree_ids, self.depth0 + int(math.log2(self.P)))
-        packed = _local_packed(local, queries, method)
+        dev = self.tree_pts.device
+        packed = torch.full((queries.shape[0],), ops.query.INF_PACKED, dtype=torch.int64, device=dev)
+        for off, n, depth, _ in self.blocks:
+            if n > 0:
+                t = KDTree(self.tree_pts[off:off + n], self.tree_ids[off:off + n], self.depth0 + depth)
+                packed = torch.minimum(packed, _local_packed(t, queries, method).to(dev))
+        rows = [int(self.layout["top_slot"][h]) - self.slot_lo for h in self.between]
+        if rows:
+            sel = torch.tensor(rows, dtype=torch.int64, device=dev)
+            packed = torch.minimum(packed, _brute_packed(self.tree_pts[sel], self.tree_ids[sel], queries).to(dev))
         if self.top_rows is not None and self.rank == 0:
             valid = [i for i, s in enumerate(self.top_slots) if s >= 0]
             if valid:
-                tr = self.top_rows[valid].to(packed.device)
+                tr = self.top_rows[valid].to(dev)
                 pk = _brute_packed(tr[:, :self.dim].contiguous(), tr[:, self.dim].contiguous().view(torch.int32),
-                                   queries.to(packed.device))
-                packed = torch.minimum(packed, pk)
+                                   queries.to(dev))
+                packed = torch.minimum(packed, pk.to(dev))
         return comm.min_packed_(packed)
+
+    def check_top_routing(self) -> str:
+        """'' when every block of this rank lies on the correct side of every top-tree pivot
+        above it (the cross-rank part of the tree invariant, which a per-rank invariant check
+        cannot see): for each block and each ancestor h of its root, the block's smallest /
+        largest composite key on h's axis is above / below h's pivot."""
+        if self.top_rows is None or self.top_rows.shape[0] == 0:
+            return ""
+        top = self.top_rows.to(self.tree_pts.device)
+        tkeys = {}
+        for off, n, depth, heap in self.blocks:
+            if n <= 0:
+                continue
+            pts, ids = self.tree_pts[off:off + n], self.tree_ids[off:off + n]
+            child = heap
+            while child > 0:
+                h = (child - 1) // 2
+                lvl = (h + 1).bit_length() - 1
+                axis = (self.depth0 + lvl) % self.dim
+                if h not in tkeys:
+                    tkeys[h] = int(signed_keys(top[h:h + 1, :self.dim], top[h:h + 1, self.dim], axis)[0])
+                k = signed_keys(pts, ids, axis)
+                if child == 2 * h + 1 and int(k.max()) >= tkeys[h]:
+                    return f"block at heap node {heap} reaches above the pivot of top node {h}"
+                if child == 2 * h + 2 and int(k.min()) <= tkeys[h]:
+                    return f"block at heap node {heap} reaches below the pivot of top node {h}"
+                child = h
+        return ""
 
 
 def _local_packed(tree, queries, method):
@@ -184,9 +252,9 @@ def _local_packed(tree, queries, method):
 
 
 def _brute_packed(pts, ids, queries):
-    """Packed (d2, id) minimum over a small point set (the replicated top pivots)."""
+    """Packed (d2, id) minimum over a small point set (the replicated top rows)."""
     if pts.is_cuda:
-        return ops.nn_gpu(pts, ids, queries.to(pts.device, torch.float32), "brute")
+        return ops.nn_gpu(pts.contiguous(), ids.contiguous(), queries.to(pts.device, torch.float32), "brute")
     q = queries.cpu().to(torch.float32)
     best = torch.full((q.shape[0],), ops.query.INF_PACKED, dtype=torch.int64)
     for i in range(pts.shape[0]):
@@ -200,10 +268,9 @@ def _brute_packed(pts, ids, queries):
 
 
 def _run_rounds(R: int, issue, consume) -> None:
-    """The exchange schedule shared by the device and host paths: round j's all-to-all is
-    waited for, round j + 1's is started, and only then is round j's payload consumed (its
-    leaf subtree built), so every exchange but the first overlaps a build. ``issue(j)`` returns
-    ``(payload, handles)``; a handle is an async work object or None (already complete)."""
+    """The exchange schedule of the native builder: round j + 1's all-to-all is started
+    before round j's payload is consumed (its leaf subtree built), so every exchange but the
+    first overlaps a build. ``issue(j)`` returns ``(payload, handles)``."""
     pending = issue(0)
     for j in range(R):
         payload, handles = pending
@@ -233,318 +300,56 @@ def _all_gather_var(t: torch.Tensor) -> List[torch.Tensor]:
 
 
 class GlobalTreeBuilder:
-    """Builds the global tree; reusable across builds of the same (n_total, dim).
-
-    On GPU every top-level decision is made on the device (csrc/gpu/dist_ops.hip): per level
-    one route+histogram pass, an allreduce(SUM) of the histogram, the median bucket per node,
-    one compaction pass of that bucket, a fixed-size all-gather of the compacted rows and a
-    radix select of the exact pivot. Nothing is read back until the all-to-all needs its split
-    sizes. Host tensors (gloo tests) take the torch reference path with the same arithmetic.
-    """
+    """The global decomposition on host tensors over gloo (any P <= 64): the schedule of the
+    native builder with torch code for the per-rank steps. GPU builds use
+    :class:`~parallel_kd_tree_amd.parallel.native_global.NativeGlobalBuilder`."""
 
     def __init__(self, n_total: int, dim: int, device: Optional[torch.device] = None, depth0: int = 0,
-                 timings: bool = False):
+                 pipeline_k: Optional[int] = None):
         self.P = comm.world()
         self.rank = comm.rank()
-        if self.P & (self.P - 1):
-            raise ValueError(f"global decomposition needs a power-of-two world size, got {self.P}")
+        self.device = device if device is not None else torch.device("cpu")
+        if self.device.type != "cpu":
+            raise ValueError("GlobalTreeBuilder runs on host tensors; GPU builds use NativeGlobalBuilder")
         if self.P > 64:
             raise ValueError("global decomposition supports at most 64 ranks")
-        self.L = int(math.log2(self.P))
         self.n_total, self.dim, self.depth0 = int(n_total), int(dim), int(depth0)
         if self.n_total >= 1 << 32:
             raise ValueError("point ids are 32-bit: at most 2^32 - 1 points")
-        self.device = device if device is not None else comm.device()
-        leaf = self.P - 1 + self.rank
-        self.slot_lo, self.n_leaf = segment(self.n_total, leaf)
-        self.top_slots = [median_slot(self.n_total, h) if segment(self.n_total, h)[1] > 0 else -1
-                          for h in range(self.P - 1)]
-        self.record_timings = timings
-        self._builder = None
-        self._ws: Dict[str, torch.Tensor] = {}
-        self._scale = 1
-        self._leaf_builders: Dict[tuple, object] = {}  # pipelined exchange: leaf builders, pivot slots
-        self._main_used = False  # the one-round exchange's builder has built at least once
-        if self.device.type == "cuda" and self.n_leaf > 0:
-            self._builder = ops.GpuTreeBuilder(self.n_leaf, dim, depth0 + self.L)
+        if pipeline_k is None:
+            pipeline_k = int(os.environ.get("PKD_PIPELINE_K", "-1"))
+        self.k = int(pipeline_k)
+        self.layout = layout(self.n_total, self.P, self.k)
+        self.LL = int(self.layout["LL"])
+        self.slot_lo = int(self.layout["share_lo"][self.rank])
+        self.n_leaf = int(self.layout["share_n"][self.rank])
+        self.top_slots = [int(s) if o < 0 else -1 for s, o in zip(self.layout["top_slot"], self.layout["top_owner"])]
 
     def read_error(self) -> int:
-        """Device error word of the last build (0 = ok): the local subtree build's, plus 8 if the
-        compact exchange's id bitmaps disagreed with the received row counts. Synchronises."""
-        e = self._builder.read_error() if (self._builder is not None and self._main_used) else 0
-        for b in self._leaf_builders.values():
-            if isinstance(b, ops.GpuTreeBuilder):
-                e |= b.read_error()
-        if "err" in self._ws:
-            e |= int(self._ws["err"][0].item()) & 8
-        return e
+        return 0
 
-    # ------------------------------------------------------------------------------------
-    def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
-        if self.device.type == "cuda":
-            return self._build_device(points, ids, id_base)
-        return self._build_host(points, ids, id_base)
-
-    # ---------------------------------------------------------------- device (HIP + RCCL) path
-    def _cap(self, level: int, scale: int) -> int:
-        """Middle-bucket rows a rank may contribute at `level` (uniform data: about
-        n_total * 2^level / (8192 * P)); overflow is detected and the build retried. Must be
-        the same on every rank: it sizes the all-gather."""
-        expect = self.n_total * (1 << level) // (TOP_BINS * self.P) + 1
-        return int(min(max(2048, 3 * expect) * scale, max(self.n_total, 1)))
-
-    def _buf(self, name: str, shape, dtype) -> torch.Tensor:
-        t = self._ws.get(name)
-        n = int(np.prod(shape))
-        if t is None or t.numel() < n or t.dtype != dtype:
-            t = torch.empty(n, dtype=dtype, device=self.device)
-            self._ws[name] = t
-        return t[:n].view(shape)
-
-    def _tick(self, timings: Dict[str, float], name: str, t0: List[float]) -> None:
-        if self.record_timings:
-            torch.cuda.synchronize(self.device)
-            now = time.perf_counter()
-            timings[name] = timings.get(name, 0.0) + (now - t0[0]) * 1e3
-            t0[0] = now
-
-    def pipeline_k(self) -> int:
-        """Exchange rounds 2^k per build: each rank's subtree is split k more levels down by
-        the distributed top levels, and the leaf subtrees are built one by one while the next
-        leaf's rows are in flight. The exchange only dominates at P = 2 (300 MB per direction
-        over the one xGMI link between the two GPUs, ~4-5 ms, next to a 7.2 ms local build), so
-        P = 2 takes two rounds (half the exchange hidden behind the first leaf's build, for
-        ~0.2 ms of extra top level and the slightly lower efficiency of two 25 M builds); at
-        P >= 4 the exchange is short and one round is kept. PKD_PIPELINE_K overrides."""
-        env = os.environ.get("PKD_PIPELINE_K")
-        k = int(env) if env is not None else {2: 1}.get(self.P, 0)
-        k = max(0, min(k, 6 - self.L))  # at most 64 leaves (32 nodes per top level)
-        if self.P == 1:
-            k = 0
-        return k
-
-    def _top_device(self, pts, idt, id_base, scale, timings, t0, k):
-        nat = ops.native()
-        dim, P, L = self.dim, self.P, self.L
-        LL, R = L + k, 1 << k
-        leaves = P << k
-        n_local = pts.shape[0]
-        dev = self.device
-        box = self._buf("box", (2 * dim,), torch.int64)
-        box.fill_(0xFFFFFFFF)
-        nat.top_bbox(pts, box)
-        comm.all_reduce_(box, dist.ReduceOp.MIN)
-        cells = self._buf("cells", ((2 * leaves - 1) * dim * 2,), torch.float32)
-        nat.top_root_cell(box, dim, cells)
-        node = self._buf("node", (max(n_local, 1),), torch.int32)
-        pivots = torch.full((max(leaves - 1, 1),), -1, dtype=torch.int64, device=dev)
-        top_rows = torch.zeros((max(leaves - 1, 1), dim + 1), dtype=torch.float32, device=dev)
-        err = self._buf("err", (4,), torch.int32)
-        err.zero_()
-        sel = self._buf("sel", (32 * 4,), torch.int32)
-        hist = self._buf("hist", (TOP_BINS,), torch.int32)
-        self._tick(timings, "bbox", t0)
-        for level in range(LL):
-            nodes = 1 << level
-            bins = TOP_BINS // nodes
-            axis = (self.depth0 + level) % dim
-            prev_axis = (self.depth0 + level - 1) % dim
-            sizes = [segment(self.n_total, nodes - 1 + j)[1] for j in range(nodes)]
-            h = hist[: nodes * bins]
-            h.zero_()
-            nat.top_route_hist(pts, idt, id_base, node, level, pivots, prev_axis, axis, cells, bins, h)
-            comm.all_reduce_(h, dist.ReduceOp.SUM)
-            nat.top_select(h, level, bins, sizes, sel, err)
-            cap = self._cap(level, scale)
-            words = nat.top_middle_words(dim, cap)
-            buf = self._buf("mid", (words,), torch.float32)
-            nat.top_collect(pts, idt, id_base, node, level, axis, cells, bins, sel, buf, cap)
-            gathered = self._buf("gathered", (P * words,), torch.float32)
-            comm.all_gather_into_(gathered, buf)
-            nat.top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err)
-            self._tick(timings, f"top_level{level}", t0)
-        last_axis = (self.depth0 + LL - 1) % dim
-        # Compact exchange (implicit ids): 12-B rows plus one bit per (source row, destination);
-        # the receiver rebuilds the ids from the bitmaps (csrc/gpu/dist_ops.hip, ids_from_bitmaps).
-        compact = idt is None and os.environ.get("PKD_COMPACT_EXCHANGE", "1") != "0"
-        rs = dim if compact else dim + 1
-        send = self._buf("send_c" if compact else "send", (max(n_local, 1), rs), torch.float32)
-        # per destination slot (round j, rank r): rows, err, id base, n_local
-        counts = torch.empty(4 * leaves, dtype=torch.int64, device=dev)
-        cv = counts.view(leaves, 4)
-        cv[:, 2] = int(id_base)
-        cv[:, 3] = int(n_local)
-        words = max(1, (n_local + 31) // 32)
-        bm = self._buf("bm", (leaves, words), torch.int32) if compact else None
-        scratch = self._buf("scratch", (nat.top_pack_scratch_bytes(n_local, leaves),), torch.uint8)
-        nat.top_pack(pts, idt, id_base, node, LL, pivots, last_axis, leaves, send, bm, counts, err, scratch, k)
-        plan = self._exchange_plan(counts, k)  # the only host read-back of the build
-        self._tick(timings, "pack", t0)
-        if plan is None:
-            return None
-        ex = {"compact": compact, "rs": rs, "bm": bm, "words": words, "err": err, "R": R, "LL": LL,
-              "src_base": plan["src_base"], "src_n": plan["src_n"], "starts": plan["starts"]}
-        return send, plan["in_splits"], plan["out_splits"], top_rows, ex
-
-    def _exchange_plan(self, counts: torch.Tensor, k: int) -> Optional[dict]:
-        """Split sizes of the exchange from every rank's per-slot counts.
-
-        ``counts`` is int64 [P << k, 4] in destination-slot order (round j, rank r) -> j * P + r:
-        rows, error word, id base, local point count. The matrix is all-gathered (P * 2^k * 32 B
-        per rank), so every rank sees every rank's error bits and checks every subtree's row
-        total against the tree geometry: a failure raises on all ranks together instead of
-        leaving peers blocked inside the exchange. Returns None when a top level's middle bucket
-        overflowed its all-gather slot (the caller retries with larger slots)."""
-        P, R = self.P, 1 << k
-        full = torch.empty(P * P * R * 4, dtype=torch.int64, device=counts.device)
+    def _exchange_plan(self, counts: torch.Tensor) -> dict:
+        """Split sizes of the exchange from every rank's per-leaf counts [T, 4] (rows, err, id
+        base, local points). The matrix is all-gathered, so every rank checks every leaf's
+        total against the tree geometry (global_plan::make_plan): a failure raises on all ranks
+        together instead of leaving peers blocked inside the exchange."""
+        P, T = self.P, int(self.layout["T"])
+        full = torch.empty(P * T * 4, dtype=torch.int64)
         comm.all_gather_into_(full, counts.reshape(-1))
-        full = full.cpu().view(P, R, P, 4)  # [source rank][round][destination rank][field]
-        errs = 0
-        for v in full[..., 1].unique().tolist():
-            errs |= int(v)
-        if errs & 1:
-            # a middle bucket overflowed its all-gather slot: that level's pivot (and every level
-            # routed through it, hence a possible err 2 below it) is void; retry larger
-            return None
-        if errs & 2:
-            raise RuntimeError("global top levels: histogram totals disagree with the tree geometry")
-        got = full[..., 0].sum(0)  # [round][destination rank]
-        for q in range(P):
-            for j in range(R):
-                want = segment(self.n_total, (P + q) * R - 1 + j)[1]
-                if int(got[j, q]) != want:
-                    raise RuntimeError(f"global exchange: rank {q} would receive {int(got[j, q])} points in round "
-                                       f"{j} for a subtree of {want}")
-        me = self.rank
-        in_splits = [full[me, j, :, 0].tolist() for j in range(R)]    # rows to each rank in round j
-        out_splits = [full[:, j, me, 0].tolist() for j in range(R)]   # rows from each rank in round j
-        starts = np.concatenate([[0], np.cumsum([sum(v) for v in in_splits])]).astype(np.int64).tolist()
-        return {"in_splits": in_splits, "out_splits": out_splits, "starts": starts,
-                "src_base": full[:, 0, 0, 2].tolist(), "src_n": full[:, 0, 0, 3].tolist()}
+        rc, send_rows, send_off, recv_rows, leaf_start = ops.native().global_plan(
+            full.tolist(), self.n_total, P, self.k, self.rank)
+        if rc != 0:
+            raise RuntimeError("global exchange plan: middle-bucket overflow reported by the host path")
+        fv = full.view(P, T, 4)
+        return {"send_rows": send_rows, "send_off": send_off, "recv_rows": recv_rows,
+                "src_base": fv[:, 0, 2].tolist(), "src_n": fv[:, 0, 3].tolist()}
 
-    def _inner_pivots(self, k: int):
-        """(output slots, heap nodes) of the pivots inside this rank's subtree above its 2^k
-        pipelined leaves, as device index tensors (geometry only, cached)."""
-        key = ("inner", k)
-        if key not in self._leaf_builders:
-            m = self.P - 1 + self.rank
-            inner = [h for lvl in range(k) for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1)]
-            keep = [(median_slot(self.n_total, h) - self.slot_lo, h) for h in inner if segment(self.n_total, h)[1] > 0]
-            if keep:
-                si = torch.tensor([a for a, _ in keep], dtype=torch.int64, device=self.device)
-                hi = torch.tensor([h for _, h in keep], dtype=torch.int64, device=self.device)
-                self._leaf_builders[key] = (si, hi)
-            else:
-                self._leaf_builders[key] = (None, None)
-        return self._leaf_builders[key]
-
-    def _leaf_builder(self, n: int, depth: int):
-        b = self._leaf_builders.get((n, depth))
-        if b is None:
-            b = self._leaf_builders[(n, depth)] = ops.GpuTreeBuilder(n, self.dim, depth)
-        return b
-
-    def _build_device(self, points, ids, id_base) -> DistTree:
-        dim, P, L = self.dim, self.P, self.L
-        timings: Dict[str, float] = {}
-        t0 = [time.perf_counter()]
-        pts = points.to(self.device, torch.float32).contiguous()
-        idt = None if ids is None else ids.to(self.device, torch.int32).contiguous()
-        k = self.pipeline_k()
-        scale = self._scale  # sticky: a skewed input pays its all-gather retry once, not per build
-        while True:
-            with trace_range("pkd.dist.top_levels"):
-                res = self._top_device(pts, idt, int(id_base), scale, timings, t0, k)
-            if res is not None:
-                break
-            if all(self._cap(l, scale) >= self.n_total for l in range(L + k)):
-                raise RuntimeError("global top levels: middle buckets inconsistent at full capacity")
-            scale *= 8
-        self._scale = scale
-        send, in_splits, out_splits, top_rows, ex = res
-        R, LL, rs = ex["R"], ex["LL"], ex["rs"]
-        src_words = [max(1, (int(v) + 31) // 32) for v in ex["src_n"]]
-        bm_off = np.concatenate([[0], np.cumsum(src_words)[:-1]]).astype(np.int64).tolist()
-        nat = ops.native()
-
-        def issue(j):
-            """Start round j: the rows of leaf j of every rank (+ their id bitmaps)."""
-            recv = self._buf(f"recv{j}", (sum(out_splits[j]), rs), torch.float32)
-            a, b = ex["starts"][j], ex["starts"][j + 1]
-            handles = [comm.all_to_all_single_async(recv, send[a:b], out_splits[j], in_splits[j])]
-            recv_bm = None
-            if ex["compact"]:
-                recv_bm = self._buf(f"recv_bm{j}", (sum(src_words),), torch.int32)
-                handles.append(comm.all_to_all_single_async(recv_bm, ex["bm"][j * P:(j + 1) * P].reshape(-1),
-                                                            src_words, [ex["words"]] * P))
-            return (recv, recv_bm), handles
-
-        def local_tree(recv, recv_bm, j, n_j, builder, out_pts=None, out_ids=None):
-            if ex["compact"]:
-                off = np.concatenate([[0], np.cumsum(out_splits[j])[:-1]]).astype(np.int64).tolist()
-                lids = self._buf("ids", (max(n_j, 1),), torch.int32)[:n_j]
-                scr = self._buf("bm_scratch", (nat.ids_from_bitmaps_scratch_bytes(max(src_words), P),), torch.uint8)
-                nat.ids_from_bitmaps(recv_bm, off, out_splits[j], bm_off, src_words, ex["src_base"], lids, scr,
-                                     ex["err"])
-                return builder.build(recv, lids, 0, out_pts, out_ids)
-            if out_pts is None:
-                return builder.build_rows(recv)
-            tp_, ti_ = builder.build_rows(recv)
-            out_pts.copy_(tp_)
-            out_ids.copy_(ti_)
-            return out_pts, out_ids
-
-        with trace_range("pkd.dist.exchange_and_build"):
-            if R == 1:
-                out = {}
-
-                def consume(j, payload):
-                    self._tick(timings, "all_to_all", t0)
-                    if self.n_leaf == 0:
-                        out["t"] = (torch.empty((0, dim), dtype=torch.float32, device=self.device),
-                                    torch.empty((0,), dtype=torch.int32, device=self.device))
-                    else:
-                        out["t"] = local_tree(payload[0], payload[1], 0, self.n_leaf, self._builder)
-                        self._main_used = True
-
-                _run_rounds(1, issue, consume)
-                tp, ti = out["t"]
-            else:
-                # my subtree: node m = P - 1 + rank at depth L; its 2^k leaves at depth LL are the
-                # heap nodes first_leaf + j; the R - 1 pivots between them come from top_rows
-                m = P - 1 + self.rank
-                first_leaf = (m + 1) * R - 1
-                tp = torch.empty((self.n_leaf, dim), dtype=torch.float32, device=self.device)
-                ti = torch.empty((self.n_leaf,), dtype=torch.int32, device=self.device)
-                si, hi = self._inner_pivots(k)
-                if si is not None:
-                    rows = top_rows[hi]
-                    tp[si] = rows[:, :dim]
-                    ti[si] = rows[:, dim].contiguous().view(torch.int32)
-
-                def consume(j, payload):
-                    recv, recv_bm = payload
-                    lo_j, n_j = segment(self.n_total, first_leaf + j)
-                    if n_j > 0:
-                        a = lo_j - self.slot_lo
-                        local_tree(recv, recv_bm, j, n_j, self._leaf_builder(n_j, self.depth0 + LL),
-                                   tp[a:a + n_j], ti[a:a + n_j])
-
-                _run_rounds(R, issue, consume)
-                self._tick(timings, "all_to_all", t0)
-        self._tick(timings, "local_build", t0)
-        return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
-                        list(self.top_slots), top_rows[: P - 1], timings)
-
-    # ---------------------------------------------------------------- host (gloo) reference path
-    def _build_host(self, points: torch.Tensor, ids: Optional[torch.Tensor], id_base: int) -> DistTree:
-        """The torch reference of the device path, same schedule: top levels down to depth
-        log2(P) + k, one count exchange, 2^k all-to-all rounds (gloo async work on host
-        tensors), each leaf subtree built while the next round is in flight."""
-        dim, P, L = self.dim, self.P, self.L
-        k = self.pipeline_k()
-        LL, R = L + k, 1 << k
-        leaves = P << k
+    def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0) -> DistTree:
+        """Top levels down to depth LL, one count exchange, one all-to-all round per leaf of a
+        rank (gloo async work), each leaf subtree built while the next round is in flight."""
+        dim, P = self.dim, self.P
+        lay = self.layout
+        LL, T, R = self.LL, int(lay["T"]), int(lay["R"])
         ops_h = _HostOps
         rows = _to_rows(points.to(torch.float32), ids, id_base)
         n_local = rows.shape[0]
@@ -560,8 +365,8 @@ class GlobalTreeBuilder:
         root_cell = np.stack([lo.numpy(), hi.numpy()], 1).astype(np.float32)  # [dim][2]
         cells = {0: root_cell}
         node = torch.zeros(n_local, dtype=torch.int64)
-        pivots = np.zeros(max(leaves - 1, 1), dtype=np.uint64)
-        top_rows = torch.zeros((max(leaves - 1, 1), dim + 1), dtype=torch.float32)
+        pivots = np.zeros(max(T - 1, 1), dtype=np.uint64)
+        top_rows = torch.zeros((max(T - 1, 1), dim + 1), dtype=torch.float32)
         # 2. top levels
         for level in range(LL):
             nodes = 1 << level
@@ -616,40 +421,43 @@ class GlobalTreeBuilder:
                 cr[axis, 0] = pr[axis]
                 cells[2 * h + 1] = cl
                 cells[2 * h + 2] = cr
-        # 3. exchange plan: per destination slot (round j, rank r) rows, err, id base, n_local
+        # 3. pack by leaf, exchange plan
         last_axis = (self.depth0 + LL - 1) % dim
-        send, slot_rows = ops_h.pack(rows, dim, node, LL, pivots, last_axis, P, k)
-        counts = torch.zeros((leaves, 4), dtype=torch.int64)
-        counts[:, 0] = slot_rows
+        send, leaf_rows = ops_h.pack(rows, dim, node, LL, pivots, last_axis)
+        counts = torch.zeros((T, 4), dtype=torch.int64)
+        counts[:, 0] = leaf_rows
         counts[:, 2] = int(id_base)
         counts[:, 3] = n_local
-        plan = self._exchange_plan(counts, k)
-        in_splits, out_splits, starts = plan["in_splits"], plan["out_splits"], plan["starts"]
-        # 4. rounds: exchange leaf j + 1 while leaf j's subtree builds
-        m = P - 1 + self.rank
-        first_leaf = (m + 1) * R - 1
+        plan = self._exchange_plan(counts)
+        # 4. my share: the top rows between my leaves, then one round per leaf
+        me = self.rank
+        a = int(lay["leaf_lo"][me])
+        mine = int(lay["leaf_lo"][me + 1]) - a
         tp = torch.empty((self.n_leaf, dim), dtype=torch.float32)
         ti = torch.empty((self.n_leaf,), dtype=torch.int32)
-        for lvl in range(k):  # pivots inside my subtree above its 2^k leaves
-            for h in range((m + 1) * (1 << lvl) - 1, (m + 2) * (1 << lvl) - 1):
-                if segment(self.n_total, h)[1] > 0:
-                    s_ = median_slot(self.n_total, h) - self.slot_lo
-                    tp[s_] = top_rows[h, :dim]
-                    ti[s_] = top_rows[h, dim:].contiguous().view(torch.int32)
+        for h, (s, o) in enumerate(zip(lay["top_slot"], lay["top_owner"])):
+            if o == me and s >= 0:
+                tp[s - self.slot_lo] = top_rows[h, :dim]
+                ti[s - self.slot_lo] = top_rows[h, dim:].contiguous().view(torch.int32)
 
         def issue(j):
-            recv = torch.empty((sum(out_splits[j]), dim + 1), dtype=torch.float32)
-            hd = comm.all_to_all_single_async(recv, send[starts[j]:starts[j + 1]], out_splits[j], in_splits[j])
+            parts = [send[o:o + r] for o, r in zip(plan["send_off"][j], plan["send_rows"][j])]
+            inp = torch.cat(parts, 0) if parts else send[:0]
+            recv = torch.empty((sum(plan["recv_rows"][j]), dim + 1), dtype=torch.float32)
+            hd = comm.all_to_all_single_async(recv, inp.contiguous(), plan["recv_rows"][j], plan["send_rows"][j])
             return recv, [hd]
 
         def consume(j, recv):
-            lo_j, n_j = segment(self.n_total, first_leaf + j)
+            if j >= mine:
+                return
+            t = a + j
+            n_j = int(lay["leaf_n"][t])
             if n_j > 0:
-                a = lo_j - self.slot_lo
-                tp[a:a + n_j], ti[a:a + n_j] = ops.build_cpu(recv[:, :dim].contiguous(),
+                o = int(lay["leaf_slot"][t]) - self.slot_lo
+                tp[o:o + n_j], ti[o:o + n_j] = ops.build_cpu(recv[:, :dim].contiguous(),
                                                              recv[:, dim].contiguous().view(torch.int32), "exact",
                                                              self.depth0 + LL, 1)
 
         _run_rounds(R, issue, consume)
-        return DistTree(self.n_total, dim, self.depth0, P, self.rank, tp, ti, self.slot_lo,
-                        list(self.top_slots), top_rows[: P - 1], {})
+        return DistTree(self.n_total, dim, self.depth0, P, me, tp, ti, self.slot_lo, list(self.top_slots),
+                        top_rows[: max(T - 1, 0)], {}, lay)

@@ -42,9 +42,18 @@ def test_bench_self_launch_two_ranks():
 
 def test_bench_self_launch_four_ranks_pipelined():
     r = _bench("--gpus", "4", "--device", "cpu", "--points", "40001", "--steps", "1", "--warmup", "0",
-               env={"PKD_PIPELINE_K": "1"})
+               "--pipeline-k", "1")
     assert r.returncode == 0, r.stderr
     assert _one_json(r.stdout)["n_gpus"] == 4
+
+
+def test_bench_three_ranks():
+    """A world size that is not a power of two: uneven leaf runs, same checked tree."""
+    r = _bench("--gpus", "3", "--device", "cpu", "--points", "30001", "--steps", "1", "--warmup", "0")
+    assert r.returncode == 0, r.stderr
+    j = _one_json(r.stdout)
+    assert j["n_gpus"] == 3 and j["config"]["parallelism"] == "global3" and j["config"]["tree_checked"]
+    assert j["metric"].endswith("(not the headline config)") and j["config"]["headline"] is False
 
 
 def test_bench_launcher_propagates_rank_failure():

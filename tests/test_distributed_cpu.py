@@ -79,7 +79,7 @@ def _global_case(rank, world, n, dim, seed):
 
 
 @pytest.mark.parametrize("world,n,dim", [(2, 5000, 3), (4, 20000, 3), (2, 3001, 2), (4, 1000, 5), (2, 7, 3),
-                                         (8, 3000, 3)])
+                                         (8, 3000, 3), (3, 6001, 3), (5, 4000, 2), (6, 3000, 3), (3, 4, 3)])
 def test_global_tree_equals_single(world, n, dim):
     run(world, _global_case, n, dim, 11)
 
@@ -149,8 +149,9 @@ def test_forest_n_less_than_p():
 
 
 def _pipelined_case(rank, world, n, dim, k):
-    """Pipelined exchange on gloo: 2^k all-to-all rounds with real async work handles, each
-    leaf subtree built while the next round is in flight; the tree must not depend on k."""
+    """Extra top levels on gloo: one all-to-all round per leaf of a rank, with real async work
+    handles, each leaf subtree built while the next round is in flight; the tree must not
+    depend on k."""
     import parallel_kd_tree_amd as pk
     from parallel_kd_tree_amd import ops
     from parallel_kd_tree_amd.parallel import comm, global_tree
@@ -167,36 +168,58 @@ def _pipelined_case(rank, world, n, dim, k):
     try:
         first, cnt = comm.forest_slice(n, world, rank)
         x = pk.generate_slice(13, dim, first, cnt)
-        b = GlobalTreeBuilder(n, dim, device=torch.device("cpu"))
-        assert b.pipeline_k() == k
+        b = GlobalTreeBuilder(n, dim, device=torch.device("cpu"), pipeline_k=k)
         t = b.build(x, id_base=first)
     finally:
         global_tree.comm.all_to_all_single_async = orig
-    assert len(handles) == 1 << k and all(h is not None and hasattr(h, "wait") for h in handles)
+    assert len(handles) == b.layout["R"] and all(h is not None and hasattr(h, "wait") for h in handles)
+    if world & (world - 1) == 0:
+        assert b.layout["R"] == 1 << k
+    assert t.check_top_routing() == ""
     tp, ti = t.gather_full()
     full = pk.generate_problem(13, dim, n)
     cp, ci = ops.build_cpu(full, None, "exact", 0, 1)
     assert torch.equal(ti, ci) and torch.equal(tp, cp)
 
 
-@pytest.mark.parametrize("world,k", [(2, 0), (2, 1), (2, 3), (4, 2), (8, 1)])
-def test_global_tree_pipelined_rounds(monkeypatch, world, k):
-    monkeypatch.setenv("PKD_PIPELINE_K", str(k))
+@pytest.mark.parametrize("world,k", [(2, 0), (2, 1), (2, 3), (4, 2), (8, 1), (3, 1), (6, 0)])
+def test_global_tree_pipelined_rounds(world, k):
     run(world, _pipelined_case, 30_001, 3, k)
 
 
 def _plan_consistency(rank, world):
-    """A subtree total that disagrees with the tree geometry raises on EVERY rank (the count
+    """A leaf total that disagrees with the tree geometry raises on EVERY rank (the count
     matrix is all-gathered), so no rank is left waiting inside the exchange."""
     from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
-    b = GlobalTreeBuilder(1000, 3, device=torch.device("cpu"))
-    counts = torch.zeros((world, 4), dtype=torch.int64)
-    counts[:, 0] = 1000 // (world * world)
+    b = GlobalTreeBuilder(1000, 3, device=torch.device("cpu"), pipeline_k=0)
+    T = b.layout["T"]
+    counts = torch.zeros((T, 4), dtype=torch.int64)
+    for t in range(T):  # every rank claims an equal share of every leaf ...
+        counts[t, 0] = b.layout["leaf_n"][t] // world + (1 if rank < b.layout["leaf_n"][t] % world else 0)
     if rank == 0:
-        counts[1, 0] += 1  # rank 0 claims one extra row for rank 1
+        counts[1, 0] += 1  # ... but rank 0 claims one extra row for leaf 1
     with pytest.raises(RuntimeError, match="would receive"):
-        b._exchange_plan(counts, 0)
+        b._exchange_plan(counts)
 
 
 def test_exchange_plan_fails_on_every_rank():
     run(4, _plan_consistency)
+
+
+def _routing_check_catches(rank, world):
+    """DistTree.check_top_routing sees a point on the wrong side of a top pivot (the bench's
+    cross-rank check), which no per-rank invariant check can."""
+    import parallel_kd_tree_amd as pk
+    from parallel_kd_tree_amd.parallel import comm
+    from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
+    n = 4000
+    first, cnt = comm.forest_slice(n, world, rank)
+    t = GlobalTreeBuilder(n, 3, device=torch.device("cpu")).build(pk.generate_slice(2, 3, first, cnt), id_base=1)
+    assert t.check_top_routing() == ""
+    if rank == 1:  # move rank 1's first point to the far low end of axis 0 (left of the root pivot)
+        t.tree_pts[0, 0] = -1000.0
+        assert "pivot of top node 0" in t.check_top_routing()
+
+
+def test_top_routing_check():
+    run(2, _routing_check_catches)

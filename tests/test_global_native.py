@@ -1,10 +1,12 @@
 """Native global decomposition (csrc/cpu/global_builder.cpp).
 
-CPU: the exchange planner (split sizes per round and peer, collective-consistent geometry
-checks, overflow retry signal) against the implicit-tree geometry.
+CPU: the ownership layout (leaf runs per rank for any P, shares, complete-subtree blocks,
+boundary top nodes) against the implicit-tree geometry, and the exchange planner (split sizes
+per round and peer, collective-consistent geometry checks, overflow retry signal).
 GPU: the whole native builder with P ranks as threads sharing one card through the loopback
 communicator (the P > 1 orchestration of kdtree_dist --decomp global without P GPUs): the
-assembled tree is slot for slot the single-GPU / CPU exact tree."""
+assembled tree is slot for slot the single-GPU / CPU exact tree, for uniform, duplicate-heavy
+and skewed data, powers of two and not."""
 import random
 
 import pytest
@@ -12,63 +14,144 @@ import torch
 
 import parallel_kd_tree_amd as pk
 from parallel_kd_tree_amd import ops
-from parallel_kd_tree_amd.parallel.geometry import segment
+from parallel_kd_tree_amd.parallel.geometry import median_slot, segment
 
 
-def _counts(n_total, P, R, seed):
-    """A consistent count matrix [P][R * P][4]: every leaf's rows split at random over the sources."""
+def _lay(native, n, P, k=-1):
+    return native.global_layout(n, P, k)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 64, 1000, 100_003])
+@pytest.mark.parametrize("P,k", [(1, -1), (1, 2), (2, -1), (3, -1), (4, 0), (5, -1), (6, 1), (7, -1), (8, 0),
+                                 (8, 2), (12, -1), (33, -1), (64, 0)])
+def test_layout_covers_the_tree(native, n, P, k):
+    lay = _lay(native, n, P, k)
+    T, LL = lay["T"], lay["LL"]
+    assert T == 1 << LL and LL <= 6 and T >= P
+    lo = lay["leaf_lo"]
+    assert lo[0] == 0 and lo[-1] == T and all(lo[r + 1] > lo[r] for r in range(P))
+    assert lay["R"] == max(lo[r + 1] - lo[r] for r in range(P))
+    # leaves and top nodes: slots from the implicit-tree geometry
+    for t in range(T):
+        s, m = segment(n, T - 1 + t)
+        assert lay["leaf_n"][t] == m and (m == 0 or lay["leaf_slot"][t] == s)
+    for h in range(T - 1):
+        s, m = segment(n, h)
+        assert lay["top_slot"][h] == (median_slot(n, h) if m > 0 else -1)
+    # shares, boundary rows: every slot exactly once
+    seen = torch.zeros(n, dtype=torch.int32)
+    for r in range(P):
+        a, b = lay["share_lo"][r], lay["share_lo"][r] + lay["share_n"][r]
+        seen[a:b] += 1
+        # blocks: complete subtrees of the share, and the rows between them
+        covered = 0
+        for off, m, depth, heap in lay["blocks"][r]:
+            s, mm = segment(n, heap)
+            assert mm == m and (m == 0 or s == a + off)
+            assert (heap + 1).bit_length() - 1 == depth
+            covered += m
+        covered += len(lay["between"][r])
+        assert covered == lay["share_n"][r]
+    for h in range(T - 1):
+        if lay["top_owner"][h] < 0 and lay["top_slot"][h] >= 0:
+            seen[lay["top_slot"][h]] += 1
+    assert bool((seen == 1).all())
+    if P & (P - 1) == 0 and k <= 0 and P > 1:  # power of two: one subtree at depth log2 P per rank
+        assert all(len(lay["blocks"][r]) == 1 and lay["blocks"][r][0][2] == P.bit_length() - 1 for r in range(P))
+
+
+def _counts(lay, n_total, seed):
+    """A consistent count matrix [P][T][4]: every leaf's rows split at random over the sources."""
     rng = random.Random(seed)
-    c = [[[0, 0, 7 + src, 1000 + src] for _ in range(R * P)] for src in range(P)]
-    for q in range(P):
-        for j in range(R):
-            want = segment(n_total, (P + q) * R - 1 + j)[1]
-            cuts = sorted(rng.randint(0, want) for _ in range(P - 1))
-            parts = [b - a for a, b in zip([0] + cuts, cuts + [want])]
-            for src in range(P):
-                c[src][j * P + q][0] = parts[src]
+    P, T = lay["P"], lay["T"]
+    c = [[[0, 0, 7 + src, 1000 + src] for _ in range(T)] for src in range(P)]
+    for t in range(T):
+        want = lay["leaf_n"][t]
+        cuts = sorted(rng.randint(0, want) for _ in range(P - 1))
+        parts = [b - a for a, b in zip([0] + cuts, cuts + [want])]
+        for src in range(P):
+            c[src][t][0] = parts[src]
     return c
 
 
-@pytest.mark.parametrize("P,R", [(1, 1), (1, 4), (2, 2), (4, 1), (8, 2)])
-def test_native_plan(native, P, R):
+@pytest.mark.parametrize("P,k", [(1, 0), (1, 2), (2, 1), (3, -1), (4, 0), (6, -1), (8, 1)])
+def test_native_plan(native, P, k):
     n = 100_003
-    c = _counts(n, P, R, P * 10 + R)
-    flat = [v for src in c for slot in src for v in slot]
+    lay = _lay(native, n, P, k)
+    c = _counts(lay, n, P * 10 + k)
+    flat = [v for src in c for leaf in src for v in leaf]
+    lo = lay["leaf_lo"]
     for me in range(P):
-        rc, ins, outs, starts = native.global_plan(flat, P, R, me, n)
+        rc, send_rows, send_off, recv_rows, leaf_start = native.global_plan(flat, n, P, k, me)
         assert rc == 0
-        for j in range(R):
-            assert ins[j] == [c[me][j * P + p][0] for p in range(P)]
-            assert outs[j] == [c[p][j * P + me][0] for p in range(P)]
-            assert starts[j + 1] - starts[j] == sum(ins[j])
-            assert sum(outs[j]) == segment(n, (P + me) * R - 1 + j)[1]
+        assert leaf_start[-1] == sum(c[me][t][0] for t in range(lay["T"]))
+        for j in range(lay["R"]):
+            for q in range(P):
+                t = lo[q] + j
+                if t < lo[q + 1]:
+                    assert send_rows[j][q] == c[me][t][0] and send_off[j][q] == leaf_start[t]
+                else:
+                    assert send_rows[j][q] == 0
+            mine = lo[me + 1] - lo[me]
+            if j < mine:
+                assert recv_rows[j] == [c[p][lo[me] + j][0] for p in range(P)]
+                assert sum(recv_rows[j]) == lay["leaf_n"][lo[me] + j]
+            else:
+                assert recv_rows[j] == [0] * P
 
 
 def test_native_plan_errors(native):
-    n, P, R = 5000, 4, 1
-    c = _counts(n, P, R, 1)
+    n, P, k = 5000, 4, 0
+    lay = _lay(native, n, P, k)
+    c = _counts(lay, n, 1)
     c[2][1][1] = 1  # a middle bucket overflowed on rank 2: every rank sees it and retries
-    flat = [v for src in c for slot in src for v in slot]
-    assert all(native.global_plan(flat, P, R, me, n)[0] == 1 for me in range(P))
-    c = _counts(n, P, R, 2)
-    c[0][1][0] += 1  # rank 0 claims one row too many for rank 1: every rank raises
-    flat = [v for src in c for slot in src for v in slot]
+    flat = [v for src in c for leaf in src for v in leaf]
+    assert all(native.global_plan(flat, n, P, k, me)[0] == 1 for me in range(P))
+    c = _counts(lay, n, 2)
+    c[0][1][0] += 1  # rank 0 claims one row too many for leaf 1: every rank raises
+    flat = [v for src in c for leaf in src for v in leaf]
     for me in range(P):
         with pytest.raises(RuntimeError, match="would receive"):
-            native.global_plan(flat, P, R, me, n)
+            native.global_plan(flat, n, P, k, me)
+
+
+def _loopback_equal(native, x, P, k):
+    tp, ti, err, scale = native.global_loopback(x, P, k)
+    assert err == 0
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    assert torch.equal(ti, ci + 1), "native global tree differs from the exact tree"
+    assert torch.equal(tp, cp)
+    return scale
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,k,n,dim", [(1, 0, 100_000, 3), (1, 2, 200_001, 3), (2, -1, 300_000, 3), (4, 0, 250_000, 3),
                                        (4, 1, 120_000, 5), (8, 0, 400_003, 3), (8, 1, 90_000, 2), (4, 0, 7, 3),
                                        (2, 0, 20_000_000, 3), (2, 3, 300_000, 3), (8, 2, 500_000, 3),
-                                       (4, 2, 1_000_000, 8), (8, 0, 5, 3), (2, 1, 1, 3), (8, 1, 20, 2)])
+                                       (4, 2, 1_000_000, 8), (8, 0, 5, 3), (2, 1, 1, 3), (8, 1, 20, 2),
+                                       (3, -1, 300_001, 3), (5, -1, 200_000, 3), (6, 0, 100_000, 4),
+                                       (7, -1, 77, 3), (3, 1, 50_000, 16)])
 def test_native_global_loopback(gpu_device, native, P, k, n, dim):
     x = pk.generate_problem(P + k + 3, dim, n)
-    tp, ti, err, scale = native.global_loopback(x, P, k)
-    assert err == 0
+    scale = _loopback_equal(native, x, P, k)
     # the middle-bucket all-gather slots held every bucket: no overflow retry (uniform data)
     assert scale == 1 or n < 1000
-    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
-    assert torch.equal(ti, ci + 1), "native global tree differs from the exact tree"
-    assert torch.equal(tp, cp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,k,n,kind", [(4, 0, 1_500_000, "dupes"), (2, 1, 1_200_000, "skew"),
+                                        (8, 0, 2_000_000, "skew"), (3, -1, 1_000_000, "dupes")])
+def test_native_global_loopback_hard_data(gpu_device, native, P, k, n, kind):
+    """Duplicate-heavy data (3 distinct values per axis: every median bucket is huge) and skewed
+    data (half the points in a tiny cube): the middle buckets overflow their all-gather slots,
+    the builder retries with larger slots, and the tree is still the exact one."""
+    g = torch.Generator().manual_seed(n + P)
+    if kind == "dupes":
+        x = torch.randint(0, 3, (n, 3), generator=g).float()
+    else:
+        x = torch.rand((n, 3), generator=g) * 200 - 100
+        x[: n // 2] = x[: n // 2] * 1e-4 + 3.0
+        x = x[torch.randperm(n, generator=g)].contiguous()
+    scale = _loopback_equal(native, x, P, k)
+    if kind == "dupes":
+        assert scale > 1, "duplicate-heavy data must overflow the default all-gather slots"

@@ -133,23 +133,31 @@ def test_pack_matches_host(gpu_device, P, dim):
         _HostOps.route_hist(rows, dim, node_c, l, piv, (l - 1) % dim, l % dim, pr, 8192 // nl)
         hg = torch.zeros(8192, dtype=torch.int32, device=gpu_device)
         nat.top_route_hist(xg, None, 1, node_g, l, piv_g, (l - 1) % dim, l % dim, cells_g, 8192 // nl, hg)
-    sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim, P, 0)
+    sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
     counts = torch.empty(4 * P, dtype=torch.int64, device=gpu_device)
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=gpu_device)
     node_keep = node_g.clone()
-    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, P, out, None, counts, err, scratch)
+    node_keep2 = node_g.clone()
+    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, out, 0, None, counts, err, scratch)
     cg = counts.cpu().view(P, 4)
     assert torch.equal(cc, cg[:, 0]) and int(cg[:, 1].abs().sum()) == 0
     k = int(cc.sum())
     assert torch.equal(sc.view(torch.int32), out[:k].cpu().view(torch.int32)), "pack must be stable by destination"
 
+    # planar output (SoA planes of a padded stride): the same rows, column by column
+    stride = n + 61
+    planes = torch.full((dim * stride,), -7.0, dtype=torch.float32, device=gpu_device)
+    nat.top_pack(xg, None, 1, node_keep2, L, piv_g, (L - 1) % dim, planes, stride, None, counts, err, scratch)
+    pl = planes.cpu().view(dim, stride)
+    assert torch.equal(pl[:, :k].t().contiguous(), sc[:, :dim])
+
     # compact exchange: coordinates only + destination bitmaps; ids rebuilt on the receiver side
     words = (n + 31) // 32 + 3  # any stride >= n / 32
     bm = torch.full((P, words), -1, dtype=torch.int32, device=gpu_device)
     outc = torch.empty((n, dim), dtype=torch.float32, device=gpu_device)
-    nat.top_pack(xg, None, 1, node_keep, L, piv_g, (L - 1) % dim, P, outc, bm, counts, err, scratch)
+    nat.top_pack(xg, None, 1, node_keep, L, piv_g, (L - 1) % dim, outc, 0, bm, counts, err, scratch)
     assert torch.equal(outc[:k].cpu(), sc[:, :dim])
     dest = node_keep.cpu().to(torch.int64) - (P - 1)
     bits = ((bm.cpu().to(torch.int64) & 0xFFFFFFFF)[:, :, None] >> torch.arange(32)) & 1
@@ -181,7 +189,7 @@ def test_explicit_ids(gpu_device):
     keys = composite_u64(x[:, 0].numpy(), ids.numpy().view(np.uint32))
     piv = np.array([np.sort(keys)[n // 2]], dtype=np.uint64)
     node_c = torch.zeros(n, dtype=torch.int64)
-    _HostOps.pack(rows, dim, node_c, 1, piv, 0, 2, 0)
+    _HostOps.pack(rows, dim, node_c, 1, piv, 0)
     nat = ops.native()
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
@@ -189,7 +197,7 @@ def test_explicit_ids(gpu_device):
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, 2), dtype=torch.uint8, device=gpu_device)
     nat.top_pack(x.to(gpu_device), ids.to(gpu_device), 0, node_g, 1,
-                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, 2, out, None, counts, err, scratch)
+                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, out, 0, None, counts, err, scratch)
     assert torch.equal(node_c.to(torch.int32), node_g.cpu())
     assert counts.cpu()[0::4].tolist() == [n // 2, n - n // 2 - 1]
 

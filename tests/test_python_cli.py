@@ -65,11 +65,11 @@ def test_eval_mode_stdin_metrics():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("impl", ["native"])
-def test_global_one_gpu_cli(impl):
+@pytest.mark.parametrize("k", [-1, 2])
+def test_global_one_gpu_cli(k):
     """python -m parallel_kd_tree_amd.cli --decomp global on one GPU (native GlobalBuilder over a
     one-rank RCCL communicator): the reference protocol lines of the exact tree."""
-    r = _run(["--decomp", "global", "--impl", impl, "--queries", "20", "11", "3", "200000"])
+    r = _run(["--decomp", "global", "--pipeline-k", str(k), "--queries", "20", "11", "3", "200000"])
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.splitlines()
     assert lines[0] == "READY" and lines[-1] == "DONE"
