@@ -1703,7 +1703,7 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
 // offsets; rows in a child's median bucket (their zone is decided by the second stage)
 // form 6 more pseudo-zones placed with cursor atomics.
-template <int NCOL, int KI, bool PFX = false, bool VEC = false>
+template <int NCOL, int KI, bool PFX = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
@@ -1823,44 +1823,33 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   }
   __syncthreads();
 
-  // VEC: each thread loads 4 consecutive rows of a column with one 16-B load (item i = 4 g + j is
+  // Each thread loads 4 consecutive rows of a column with one 16-B load (item i = 4 g + j is
   // row 4 (g * kBlock + tid) + j of a chunk that starts on a 16-B aligned absolute row; rows
   // outside [b0, b1) are loaded from the padded buffer and masked)
-  const i64 cstart = VEC ? (((lo + b0) & ~i64(3)) - lo) : b0;
+  static_assert(kItems % 4 == 0, "16-B row loads take 4 rows per item group");
+  const i64 cstart = ((lo + b0) & ~i64(3)) - lo;
   for (i64 c0 = cstart; c0 < b1; c0 += kChunk) {
     float row[kItems][NCOL];
     bool vld[kItems];
-    if constexpr (VEC) {
 #pragma unroll
-      for (int g = 0; g < kItems / 4; ++g) {
-        const i64 e4 = c0 + (i64(g) * kBlock + threadIdx.x) * 4;  // relative row of sub-item 0
-        const bool any = e4 < b1;
-        const i64 p4 = lo + (any ? e4 : (((lo + b0) & ~i64(3)) - lo));
+    for (int g = 0; g < kItems / 4; ++g) {
+      const i64 e4 = c0 + (i64(g) * kBlock + threadIdx.x) * 4;  // relative row of sub-item 0
+      const bool any = e4 < b1;
+      const i64 p4 = lo + (any ? e4 : (((lo + b0) & ~i64(3)) - lo));
 #pragma unroll
-        for (int c = 0; c < NCOL; ++c) {
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (!(c == D && a.id_implicit)) v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
-          row[4 * g + 0][c] = v.x;
-          row[4 * g + 1][c] = v.y;
-          row[4 * g + 2][c] = v.z;
-          row[4 * g + 3][c] = v.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const i64 e = e4 + j;
-          vld[4 * g + j] = e >= b0 && e < b1;
-          if (D >= 0 && a.id_implicit) row[4 * g + j][D] = __uint_as_float(a.id_base0 + u32(lo + e));
-        }
+      for (int c = 0; c < NCOL; ++c) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(c == D && a.id_implicit)) v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
+        row[4 * g + 0][c] = v.x;
+        row[4 * g + 1][c] = v.y;
+        row[4 * g + 2][c] = v.z;
+        row[4 * g + 3][c] = v.w;
       }
-    } else {
 #pragma unroll
-      for (int i = 0; i < kItems; ++i) {
-        const i64 e = c0 + i * kBlock + threadIdx.x;
-        const i64 p = lo + (e < b1 ? e : b0);
-        vld[i] = e < b1;
-#pragma unroll
-        for (int c = 0; c < NCOL; ++c)
-          row[i][c] = (c == D && a.id_implicit) ? __uint_as_float(a.id_base0 + u32(p)) : src[i64(c) * nc + p];
+      for (int j = 0; j < 4; ++j) {
+        const i64 e = e4 + j;
+        vld[4 * g + j] = e >= b0 && e < b1;
+        if (D >= 0 && a.id_implicit) row[4 * g + j][D] = __uint_as_float(a.id_base0 + u32(lo + e));
       }
     }
     u32 zone_pre[kItems];  // (zone index << 16) | rank-in-wave; index q, or 6 + q (PFX uncertain), 15 none
@@ -1964,68 +1953,12 @@ void with_ncol(int dim, F&& f) {
   }
 }
 
-// k_scan runs on half the scatter's blocks per segment: its per-block histogram flush (2 x
-// next_bins global atomics) halves, and the sweep stays bandwidth-bound (100M x 3D: k_scan
-// 1.57 -> 1.51 ms). PKD_SCAN_DIV overrides.
-bool implicit_ids_enabled() {
-  const char* e = std::getenv("PKD_IMPLICIT_IDS");
-  return !(e && std::string(e) == "0");
-}
-
-// First-level histogram on half the blocks (its 4096-bin flush per block is the cost beyond
-// the key read): 100M x 3D k_hist 130 -> 115 us. PKD_HIST_DIV overrides.
 // Columns per load round of the runtime-dim partition: more bytes in flight per thread for
 // wide rows (1M x 64D 2.67 -> 2.56 ms with 16, 500k x 128D 2.76 -> 2.62 ms with 32; 16D
-// keeps 8). PKD_COLGROUP overrides.
-bool narrow_enabled() {
-  const char* e = std::getenv("PKD_NARROW");
-  const char* impl = std::getenv("PKD_SUBTREE_IMPL");
-  return !(e && std::string(e) == "0") && !(impl && std::string(impl) == "hist");
-}
-
-int colgroup(int dim) {
-  const char* e = std::getenv("PKD_COLGROUP");
-  if (e) return std::atoi(e);
-  return dim >= 96 ? 32 : (dim >= 48 ? 16 : 8);
-}
-
-int hist_div() {
-  const char* e = std::getenv("PKD_HIST_DIV");
-  return e ? std::max(1, std::atoi(e)) : 2;
-}
-
-int scan_div() {
-  const char* e = std::getenv("PKD_SCAN_DIV");
-  return e ? std::max(1, std::atoi(e)) : 2;
-}
-
-bool prefix_placement() {  // read per build (tests switch it)
-  const char* e = std::getenv("PKD_PART_PREFIX");
-  return !(e && std::string(e) == "0");
-}
-
-bool items16() {
-  static const bool v = [] {
-    const char* e = std::getenv("PKD_PART_ITEMS");
-    return e && std::string(e) == "16";
-  }();
-  return v;
-}
-
-// Workgroups of a partition-type grid at the top levels: two rounds of 4 per CU for large
-// builds, one round below 64M points. Every block flushes its fused LDS histograms (up to
-// 8192 bins) with global atomics, so blocks must keep many rows each: at 12.5M points (a
-// rank's share of 100M on 8 GPUs) 1024 blocks build 7% faster than 2048, 1280 or 768
-// (profiles/r1_level_blocks_sweep.txt). PKD_LEVEL_BLOCKS overrides.
-i64 level_blocks_for(i64 n) {
-  const char* e = std::getenv("PKD_LEVEL_BLOCKS");
-  if (e) return std::max<i64>(1, std::atoll(e));
-  return n >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2;
-}
-
-i64 stage2_min() {
-  const char* e = std::getenv("PKD_STAGE2_MIN");
-  return e ? std::max<i64>(1, std::atoll(e)) : i64(kRefineCap);
+// keeps 8).
+int colgroup_for(int ncols, const Tuning& t) {
+  if (t.colgroup > 0) return t.colgroup;
+  return ncols >= 96 ? 32 : (ncols >= 48 ? 16 : 8);
 }
 
 size_t tiled_prep_lds(int dim) { return size_t(2 * dim) * 4 + size_t(dim) * (kPrepRows + 1) * 4; }
@@ -2036,45 +1969,49 @@ int pow2_floor(i64 v) {
   return p;
 }
 
-// Bins of a level whose histogram a paired pass fuses (4 grandchildren in LDS: 4 * bins words
-// per partition block). PKD_PAIR_BINS overrides (A/B of LDS occupancy vs median-bucket size).
-int pair_bins() {
-  static const int v = [] {
-    const char* e = std::getenv("PKD_PAIR_BINS");
-    const int b = e ? std::atoi(e) : kPairBins;
-    return (b >= 64 && b <= kPairBins && (b & (b - 1)) == 0) ? b : kPairBins;
-  }();
-  return v;
-}
-
-// Split build knobs (profiles/r2_split_build.txt): from level PKD_SPLIT_LEVEL (a pair
-// boundary) on, PKD_SPLIT_PARTS segment ranges run on PKD_SPLIT_STREAMS HIP streams, for
-// builds of at least PKD_SPLIT_MIN_N points; PKD_SPLIT=0 keeps one stream.
-struct SplitCfg {
-  bool on;
-  int level, parts, streams;
-  i64 min_n;
-};
-
-SplitCfg split_cfg() {
-  auto env_i = [](const char* k, i64 d) -> i64 {
-    const char* e = std::getenv(k);
-    return e ? std::atoll(e) : d;
-  };
-  SplitCfg c;
-  c.on = env_i("PKD_SPLIT", 1) != 0;
-  c.level = int(env_i("PKD_SPLIT_LEVEL", 2));
-  c.parts = int(env_i("PKD_SPLIT_PARTS", 4));
-  c.streams = int(env_i("PKD_SPLIT_STREAMS", 4));
-  c.min_n = env_i("PKD_SPLIT_MIN_N", i64(64) << 20);  // 50M: time-neutral, 25M: +3%, 12.5M: +7%
-  return c;
-}
-
 int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(std::max<i64>(1, nmax / 24)))); }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
+// Knob defaults, with their measurements:
+// * hist_div 2: the first-level histogram's 4096-bin flush per block is its cost beyond the
+//   key read; half the blocks: 100M x 3D k_hist 130 -> 115 us.
+// * scan_div 2: k_scan's per-block histogram flush (2 x next_bins global atomics) halves and
+//   the sweep stays bandwidth-bound (100M x 3D k_scan 1.57 -> 1.51 ms).
+// * level_blocks: two rounds of 4 workgroups per CU for builds >= 64 M points, one round
+//   below: at 12.5 M points (a rank's share of 100 M on 8 GPUs) 1024 blocks build 7% faster
+//   than 2048, 1280 or 768 (profiles/r1_level_blocks_sweep.txt).
+// * split: from level 2 (a pair boundary), 4 parts on 4 HIP streams for builds of >= 64 M
+//   points (50 M: time-neutral, 25 M: +3%, 12.5 M: +7%; profiles/r2_split_build.txt).
+Tuning Tuning::from_env() {
+  auto env_i = [](const char* k, i64 d) -> i64 {
+    const char* e = std::getenv(k);
+    return e ? std::atoll(e) : d;
+  };
+  Tuning t;
+  t.implicit_ids = env_i("PKD_IMPLICIT_IDS", 1) != 0;
+  const char* impl = std::getenv("PKD_SUBTREE_IMPL");
+  if (impl) throw std::invalid_argument("PKD_SUBTREE_IMPL was removed: one subtree kernel ships (k_subtree_rank)");
+  t.narrow = env_i("PKD_NARROW", 1) != 0;
+  t.pairs = env_i("PKD_PAIR", 1) != 0;
+  t.prefix = env_i("PKD_PART_PREFIX", 1) != 0;
+  t.split = env_i("PKD_SPLIT", 1) != 0;
+  t.split_trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
+  t.colgroup = int(env_i("PKD_COLGROUP", 0));
+  t.hist_div = int(std::max<i64>(1, env_i("PKD_HIST_DIV", 2)));
+  t.scan_div = int(std::max<i64>(1, env_i("PKD_SCAN_DIV", 2)));
+  const int pb = int(env_i("PKD_PAIR_BINS", kPairBins));
+  t.pair_bins = (pb >= 64 && pb <= kPairBins && (pb & (pb - 1)) == 0) ? pb : kPairBins;
+  t.level_blocks = std::max<i64>(0, env_i("PKD_LEVEL_BLOCKS", 0));
+  t.stage2_min = std::max<i64>(1, env_i("PKD_STAGE2_MIN", kRefineCap));
+  t.split_level = int(env_i("PKD_SPLIT_LEVEL", 2));
+  t.split_parts = int(env_i("PKD_SPLIT_PARTS", 4));
+  t.split_streams = int(env_i("PKD_SPLIT_STREAMS", 4));
+  t.split_min_n = env_i("PKD_SPLIT_MIN_N", i64(64) << 20);
+  return t;
+}
+
 int default_subtree_max(int dim) { return subtree_capacity(dim); }
 
 struct SplitStreams {
@@ -2113,14 +2050,15 @@ SplitStreams* GpuBuilder::split_streams_for(hipStream_t stream) const {
   return split_.get();
 }
 
-GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt_(opt) {
+GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
+    : n_(n), dim_(dim), opt_(opt), tune_(Tuning::from_env()) {
 
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   nsub_ = opt.subtree_max > 0 ? std::min(opt.subtree_max, subtree_capacity_max(dim)) : subtree_capacity(dim);
   // High dims: narrow columns (the global levels move lg + 2 columns instead of dim + 1) and the
   // key-slot subtree kernel, whose LDS holds only its own levels' keys, so segments are larger
-  if (dim > 8 && tiled_prep_lds(dim) <= size_t(96 * 1024) && narrow_enabled()) {
+  if (dim > 8 && tiled_prep_lds(dim) <= size_t(96 * 1024) && tune_.narrow) {
     const int capn = subtree_capacity_narrow(dim);
     const int cap = opt.subtree_max > 0 ? std::min(opt.subtree_max, capn) : capn;
     int lg = 0;
@@ -2135,7 +2073,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
   max_bins_ = 0;
   max_hist_ = 1;
-  const i64 level_blocks = level_blocks_for(n_);
+  const i64 level_blocks =
+      tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2);
   for (int l = 0; l < lg_; ++l) {
     LevelPlan lp;
     lp.level = l;
@@ -2151,7 +2090,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
     lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + chunk - 1) / chunk)));
     lp.axis = (opt.depth0 + l) % dim;
     // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
-    lp.stage2 = lp.nmax / lp.bins > stage2_min();
+    lp.stage2 = lp.nmax / lp.bins > tune_.stage2_min;
     if (lp.stage2) max_hist2_ = std::max<i64>(max_hist2_, lp.segs * kBins2);
     levels_.push_back(lp);
     max_bins_ = std::max(max_bins_, lp.bins);
@@ -2159,13 +2098,12 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   }
   // Pair level l with l+1 (one fused scatter pass) when rows fit the register path and
   // l+1 needs no second-stage histogram.
-  const char* pe = std::getenv("PKD_PAIR");
-  const bool pairs = dim <= 8 && !(pe && std::string(pe) == "0");
+  const bool pairs = dim <= 8 && tune_.pairs;
   for (int l = 0; pairs && l + 1 < lg_; ++l) {
     levels_[size_t(l)].pair = true;
     if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
       LevelPlan& g = levels_[size_t(l + 2)];
-      g.bins = std::min(g.bins, pair_bins());
+      g.bins = std::min(g.bins, tune_.pair_bins);
       levels_[size_t(l + 1)].next_bins = g.bins;
     }
     ++l;  // l+1 is the second level of the pair
@@ -2198,15 +2136,15 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
   for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
   off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
   {
-    const SplitCfg sc = split_cfg();
-    const int L = sc.level;
+    const Tuning& sc = tune_;
+    const int L = sc.split_level;
     const bool paired = lg_ >= 2 && levels_[0].pair;
-    if (sc.on && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.min_n && L >= 2 && L % 2 == 0 && L < lg_ &&
-        sc.parts >= 2 && sc.streams >= 1) {
-      const int P = std::min(pow2_floor(sc.parts), 1 << L);
+    if (sc.split && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.split_min_n && L >= 2 && L % 2 == 0 &&
+        L < lg_ && sc.split_parts >= 2 && sc.split_streams >= 1) {
+      const int P = std::min(pow2_floor(sc.split_parts), 1 << L);
       split_level_ = L;
       split_parts_ = P;
-      split_streams_ = std::max(1, std::min(sc.streams, P));
+      split_streams_ = std::max(1, std::min(sc.split_streams, P));
       size_t hw = 1, h2w = 1, bw = 1;
       for (int l = L; l < lg_; ++l) {  // the part's share of every per-segment array
         const LevelPlan& lp = levels_[size_t(l)];
@@ -2214,7 +2152,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt) : n_(n), dim_(dim), opt
         if (l > L) hw = std::max(hw, size_t(sp) * size_t(lp.bins));
         if (lp.stage2) h2w = std::max(h2w, size_t(sp) * size_t(kBins2));
         const i64 chunk = i64(kChunk);
-        const i64 pb = std::max<i64>(1, std::min<i64>(i64(lp.bps) * P / std::max(1, std::min(sc.streams, P)),
+        const i64 pb = std::max<i64>(1, std::min<i64>(i64(lp.bps) * P / std::max(1, std::min(sc.split_streams, P)),
                                                       (lp.nmax + chunk - 1) / chunk));
         bw = std::max(bw, size_t(sp) * size_t(std::max<i64>(pb, lp.bps)) * 8);
       }
@@ -2294,7 +2232,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
     // generated ids are synthesised by the first pair's kernels instead of written here
     // (-4 B written and -4 B read per point); the first level must be a pair for that
-    const bool implicit = ids == nullptr && lg_ >= 2 && levels_[0].pair && implicit_ids_enabled();
+    const bool implicit = ids == nullptr && lg_ >= 2 && levels_[0].pair && tune_.implicit_ids;
     k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part, implicit ? 0 : 1);
     PKD_LAUNCH_CHECK();
     k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, g, dim_, bbox);
@@ -2435,7 +2373,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
       a.idcol = a.narrow ? narrow_k : dim_;
       a.ncols = a.narrow ? narrow_k + 2 : dim_ + 1;
-      a.colgroup = colgroup(a.ncols - 1);
+      a.colgroup = colgroup_for(a.ncols - 1, tune_);
       a.in_rows = in_rows;
       a.in_rs = in_rs;
       a.id_base0 = id_base;
@@ -2465,7 +2403,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       if (l == 0) {
         zero_u32(hist[0], lp.segs * lp.bins, st);
         LevelArgs ah = a;  // like k_scan: fewer blocks, fewer histogram flush atomics
-        ah.bps = std::max(1, a.bps / hist_div());
+        ah.bps = std::max(1, a.bps / tune_.hist_div);
         k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, st>>>(ah, hist[0]);
         PKD_LAUNCH_CHECK();
       }
@@ -2488,7 +2426,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             LevelArgs as = a;  // the scan's own block split (its histogram flush scales with blocks)
-            as.bps = std::max(1, a.bps / scan_div());
+            as.bps = std::max(1, a.bps / tune_.scan_div);
             k_scan<NC><<<int(segs * as.bps), kBlock, lds_a, st>>>(as);
             PKD_LAUNCH_CHECK();
             k_pivot_both<NC><<<gs + int(segs), kBlock, 0, st>>>(a, segs, gs);
@@ -2506,7 +2444,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         pa.hist2n = l + 2 < lg_ ? hist_of(l + 2) : hist_of(l);
         // the second-stage pass of level l+1 reads what the block-reserve count pass would:
         // it also counts each block's certain rows, and the scatter writes from prefix offsets
-        const bool pfx = lq.stage2 && a.block_reserve && prefix_placement();
+        const bool pfx = lq.stage2 && a.block_reserve && tune_.prefix;
         if (pfx) {
           pa.bcnt = hs.bcnt;
           pa.bbase = pa.bcnt + size_t(grid) * 4;
@@ -2530,14 +2468,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             // 16-B row loads (4 consecutive rows of a column per lane): one load instruction per
             // 4 rows per column; the pass is bound by requests in flight per CU, not by HBM
             // (profiles/r2_split_build.txt, CU masks). 100M x 3D 12.73 -> 12.52 ms one-stream,
-            // 12.22 -> 12.12 split. PKD_PART_VEC=0: one row per load.
-            const char* ve = std::getenv("PKD_PART_VEC");
-            const bool vec = !(ve && std::string(ve) == "0");
-            if (pfx && vec) k_partition2<NC, KI, true, true><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else if (NC <= 5 && items16()) k_partition2<NC, 16><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else if (vec) k_partition2<NC, KI, false, true><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else k_partition2<NC, KI><<<grid, kBlock, lds_b, st>>>(a, pa);
+            // 12.22 -> 12.12 split.
+            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            else k_partition2<NC, KI, false><<<grid, kBlock, lds_b, st>>>(a, pa);
           }
         });
         PKD_LAUNCH_CHECK();
@@ -2549,8 +2482,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const size_t lds = size_t(std::max(1, 2 * lp.next_bins)) * 4;
       with_ncol(dim_, [&](auto nc) {
         constexpr int NC = decltype(nc)::value;
-        if (NC > 0 && NC <= 5 && items16()) k_partition<NC, 16><<<grid, kBlock, lds, st>>>(a);
-        else if (NC > 0 && NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, st>>>(a);
+        if (NC > 0 && NC <= 5) k_partition<NC, 8><<<grid, kBlock, lds, st>>>(a);
         else k_partition<NC, 4><<<grid, kBlock, lds, st>>>(a);
       });
       PKD_LAUNCH_CHECK();
@@ -2597,7 +2529,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   }
   // PKD_SPLIT_TRACE=1 (debug, synchronises): when each part's first and last kernel ran,
   // relative to the fork, printed to stderr
-  const bool trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
+  const bool trace = tune_.split_trace;
   std::vector<hipEvent_t> tev;
   auto tmark = [&](hipStream_t st2) {
     if (!trace) return;

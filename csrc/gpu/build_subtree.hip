@@ -4,9 +4,9 @@
 // inside LDS, every level computes each live point's exact (key, id) rank in its sub-segment.
 // Each segment's subtree collapses the bottom ~12 levels of build_tree_rec
 // (kdtree_sequential.cpp:30-66), where the reference spends millions of tiny sorts and
-// `new Node`s. Cross-check implementations selected by PKD_SUBTREE_IMPL live in their own
-// translation units: subtree_hist.hip (older histogram-partition kernel, "hist") and
-// subtree_wave.hip (wave-level rank kernel, "wave").
+// `new Node`s. (Alternative kernels measured against it -- a histogram-partition kernel and a
+// wave-level rank kernel -- were slower or within 1-2% and are no longer built; see
+// profiles/r2_subtree_wave_ab.txt and README "Measured dead ends".)
 #include <algorithm>
 #include <cstdlib>
 #include <sstream>
@@ -540,15 +540,7 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
   PKD_LAUNCH_CHECK();
 }
 
-// read per call (builders size their segments from it): tests switch it in-process
-bool use_hist_impl() {
-  const char* e = std::getenv("PKD_SUBTREE_IMPL");
-  return e && std::string(e) == "hist";
-}
-
-size_t impl_lds_bytes(int dim, int nm) {
-  return use_hist_impl() ? subtree_hist_lds_bytes(dim, nm) : 4 * rk::lds_words(dim, nm);
-}
+size_t impl_lds_bytes(int dim, int nm) { return 4 * rk::lds_words(dim, nm); }
 
 }  // namespace
 
@@ -605,7 +597,6 @@ int subtree_capacity(int dim) {
 }
 
 int subtree_capacity_narrow(int dim) {
-  if (use_hist_impl()) return 0;
   for (int nm = 2048; nm >= 64; nm /= 2) {
     const int ldim = rk::bitlen(u32(nm));
     if (ldim <= dim && 4 * rk::lds_words_narrow(dim, nm, ldim) <= kLdsMax / 2) return nm;
@@ -629,15 +620,13 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     PKD_HIP_CHECK(hipMemset(stamps, 0, size_t(kStampBlocks) * kStampSlots * sizeof(unsigned long long)));
   }
   subtree_stamp_buffer() = stamps;
-  if (narrow_idcol >= 0 && use_hist_impl()) throw std::runtime_error("pkdtree: narrow columns need the rank subtree kernel");
   // narrow: one key slot per subtree level (no axis repeats: the host enables narrow
   // columns only for dim >= the subtree's levels)
   const int ldim = narrow_idcol >= 0 ? rk::bitlen(u32(std::max(nmax, 1))) : 0;
   if (ldim > dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
             std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
-  if (narrow_idcol < 0 && subtree_wave_enabled() && launch_subtree_wave(a, segs, nmax, stream)) return;
-  if (!use_hist_impl()) {
+  {
     static const bool wide = [] {
       const char* e = std::getenv("PKD_SUBTREE_WIDE");
       return !(e && std::string(e) == "0");
@@ -661,9 +650,7 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     else if (nmax > 128) launch_rank_cfg<1, 256>(a, segs, stream);
     else if (nmax > 64) launch_rank_cfg<1, 128>(a, segs, stream);
     else launch_rank_cfg<1, 64>(a, segs, stream);
-    return;
   }
-  launch_subtree_hist(a, segs, nmax, stream);  // cross-check kernel (subtree_hist.hip)
 }
 
 }  // namespace pkdtree

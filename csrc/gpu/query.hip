@@ -477,16 +477,6 @@ void nn_init(u64* out, i64 nq, hipStream_t stream) {
   PKD_LAUNCH_CHECK();
 }
 
-int brute_ch() {
-  const char* e = std::getenv("PKD_BRUTE_CH");  // A/B of the load-round width
-  return e ? std::atoi(e) : 32;
-}
-
-bool brute_legacy() {
-  const char* e = std::getenv("PKD_BRUTE_LEGACY");  // A/B against k_brute
-  return e && std::string(e) == "1";
-}
-
 void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq, u64* out,
               hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
@@ -501,11 +491,11 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   if (lds > size_t(150) * 1024) throw std::invalid_argument("nn_brute: dimension too large for the LDS query tile");
   const bool vec = dim % 4 == 0 && reinterpret_cast<uintptr_t>(pts) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(queries) % 16 == 0;
-  if (vec && dim % 16 == 0 && size_t(16) * dim * 4 <= size_t(150) * 1024 && !brute_legacy()) {
+  if (vec && dim % 16 == 0 && size_t(16) * dim * 4 <= size_t(150) * 1024) {
     // the prefetching kernel with the tile size that fits the queries
     // 32 coordinates per load round where the rows allow it: 2 x 128 B in flight per lane
-    // (500k x 128D, 10 queries: 82 -> 73 us per call); PKD_BRUTE_CH=16 selects the narrower rounds
-    const bool wide = dim % 32 == 0 && brute_ch() == 32;
+    // (500k x 128D, 10 queries: 82 -> 73 us per call; 16-coordinate rounds otherwise)
+    const bool wide = dim % 32 == 0;
     if (nq <= 1) wide ? launch_brute_pf<1, 32>(pts, ids, id_base, n, dim, queries, nq, out, stream)
                       : launch_brute_pf<1>(pts, ids, id_base, n, dim, queries, nq, out, stream);
     else if (nq <= 2) wide ? launch_brute_pf<2, 32>(pts, ids, id_base, n, dim, queries, nq, out, stream)

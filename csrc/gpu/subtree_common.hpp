@@ -1,4 +1,4 @@
-// Definitions shared by the LDS subtree kernels (build_subtree.hip, subtree_wave.hip).
+// Definitions of the LDS subtree kernel (build_subtree.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -55,13 +55,5 @@ __device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
 }
 
 }  // namespace subtree_detail
-
-// The rank-propagation subtree kernel (subtree_wave.hip) for dims 1..8: launched when it takes
-// this (dim, nmax); false -> the caller falls back to the per-level ranking kernel.
-bool subtree_wave_enabled();
-bool launch_subtree_wave(const subtree_detail::SubArgs& a, i64 segs, int nmax, hipStream_t stream);
-// Cross-check kernel of subtree_hist.hip (PKD_SUBTREE_IMPL=hist).
-size_t subtree_hist_lds_bytes(int dim, int nm);
-void launch_subtree_hist(const subtree_detail::SubArgs& a, i64 segs, int nmax, hipStream_t stream);
 
 }  // namespace pkdtree

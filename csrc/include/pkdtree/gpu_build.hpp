@@ -33,6 +33,27 @@ struct BuildOptions {
   bool allow_split = true;
 };
 
+// A/B and diagnostic knobs of the builder (PKD_* environment variables, README "Tuning"),
+// read ONCE when a builder is constructed -- never while a build is being enqueued. The
+// defaults are the measured best on MI355X (profiles/ holds the sweeps).
+struct Tuning {
+  bool implicit_ids = true;   // PKD_IMPLICIT_IDS=0: the prep writes generated ids
+  bool narrow = true;         // PKD_NARROW=0: full columns at high dims
+  bool pairs = true;          // PKD_PAIR=0: one level per row-moving pass
+  bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
+  bool split = true;          // PKD_SPLIT=0: one-stream build
+  bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
+  int colgroup = 0;           // PKD_COLGROUP: columns per load round of wide rows (0: by dim)
+  int hist_div = 2;           // PKD_HIST_DIV: first-level histogram on 1/hist_div of the blocks
+  int scan_div = 2;           // PKD_SCAN_DIV: k_scan on 1/scan_div of the blocks
+  int pair_bins = 2048;       // PKD_PAIR_BINS: bins of a level a paired pass fuses
+  i64 level_blocks = 0;       // PKD_LEVEL_BLOCKS: top-level partition grid (0: by n)
+  i64 stage2_min = 2048;      // PKD_STAGE2_MIN: second-stage histogram above this median bucket
+  int split_level = 2, split_parts = 4, split_streams = 4;  // PKD_SPLIT_LEVEL / _PARTS / _STREAMS
+  i64 split_min_n = i64(64) << 20;                          // PKD_SPLIT_MIN_N
+  static Tuning from_env();
+};
+
 struct LevelPlan {
   int level;        // 0-based global level
   i64 segs;         // 2^level
@@ -111,6 +132,7 @@ class GpuBuilder {
   i64 ncol_ = 0;  // column stride of the SoA working buffers (n rounded up to 64)
   int dim_;
   BuildOptions opt_;
+  Tuning tune_;
   int lg_ = 0;      // number of global levels
   int nsub_ = 0;    // LDS subtree capacity
   std::vector<LevelPlan> levels_;

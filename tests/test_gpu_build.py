@@ -239,29 +239,11 @@ def test_split_build_hipgraph(gpu_device, monkeypatch):
     assert torch.equal(gi, ei) and torch.equal(gp, ep)
 
 
-@pytest.mark.parametrize("dim,n,depth0,sub", [(3, 3_000_000, 0, 0), (1, 200_000, 0, 0), (2, 300_001, 0, 0),
-                                              (4, 200_000, 1, 0), (5, 150_000, 0, 0), (8, 400_000, 3, 0),
-                                              (3, 300_000, 0, 256), (3, 70, 0, 0), (8, 1000, 0, 0)])
-def test_wave_subtree_kernel(gpu_device, monkeypatch, dim, n, depth0, sub):
-    """The rank-propagation subtree kernel (csrc/gpu/subtree_wave.hip, PKD_SUBTREE_IMPL=wave)
-    builds the same unique tree as the CPU oracle: block levels, the wave hand-over at 64
-    points, every launch shape (capacities 64..2048) and dims 1..8."""
+def test_removed_subtree_impl_knob_fails_loudly(gpu_device, monkeypatch):
+    """Only the shipped subtree kernel exists: the old selector is rejected, not ignored."""
     monkeypatch.setenv("PKD_SUBTREE_IMPL", "wave")
-    check_same(pk.generate_problem(dim * 7 + n % 5, dim, n), gpu_device, depth0=depth0, subtree_max=sub)
-
-
-def test_wave_subtree_kernel_duplicates(gpu_device, monkeypatch):
-    monkeypatch.setenv("PKD_SUBTREE_IMPL", "wave")
-    check_same(torch.randint(0, 4, (200_000, 3)).float(), gpu_device)
-    check_same(torch.zeros(30_000, 2), gpu_device)
-
-
-@pytest.mark.parametrize("dim,n", [(3, 1_000_000), (8, 300_000), (2, 50_001), (16, 100_000)])
-def test_hist_subtree_kernel(gpu_device, monkeypatch, dim, n):
-    """The cross-check histogram-partition subtree kernel (csrc/gpu/subtree_hist.hip,
-    PKD_SUBTREE_IMPL=hist; also turns the narrow-column path off) builds the same tree."""
-    monkeypatch.setenv("PKD_SUBTREE_IMPL", "hist")
-    check_same(pk.generate_problem(dim + n % 7, dim, n), gpu_device)
+    with pytest.raises(Exception, match="PKD_SUBTREE_IMPL was removed"):
+        ops.GpuTreeBuilder(1000, 3)
 
 
 def test_nearest_neighbor_no_tree_copy(gpu_device, monkeypatch):
