@@ -16,6 +16,7 @@
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
+#include "pkdtree/gpu_reference.hpp"
 #include "pkdtree/trace.hpp"
 
 namespace pkdtree {
@@ -111,6 +112,26 @@ struct Builder {
     torch::Tensor oi = torch::empty({b.n()}, opts.dtype(torch::kInt32));
     b.build_from_soa(op.data_ptr<float>(), reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(),
                      c10::hip::getCurrentHIPStream(dev.index()).stream());
+    return {op, oi};
+  }
+};
+
+// Reference-mode GPU builder (build_reference.hip) with a torch-allocated workspace.
+struct RefBuilder {
+  pk::ReferenceBuilder b;
+  int64_t n, dim;
+  torch::Tensor ws;
+  RefBuilder(int64_t n_, int64_t dim_, int64_t depth0) : b(n_, int(dim_), int(depth0)), n(n_), dim(dim_) {}
+  std::vector<torch::Tensor> build(const torch::Tensor& pts, const c10::optional<torch::Tensor>& ids, int64_t id_base) {
+    check_points(pts, true);
+    TORCH_CHECK(pts.size(0) == n && pts.size(1) == dim, "points shape does not match the builder");
+    const c10::DeviceGuard guard(pts.device());
+    if (!ws.defined() || ws.device() != pts.device())
+      ws = torch::empty({int64_t(b.workspace_bytes())}, pts.options().dtype(torch::kUInt8));
+    torch::Tensor op = torch::empty_like(pts);
+    torch::Tensor oi = torch::empty({n}, pts.options().dtype(torch::kInt32));
+    b.build(pts.data_ptr<float>(), opt_ids(ids, n, pts.device()), pk::u32(id_base), op.data_ptr<float>(),
+            reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()), ws.data_ptr(), cur_stream(pts));
     return {op, oi};
   }
 };
@@ -258,8 +279,12 @@ torch::Tensor nn_gpu(const torch::Tensor& pts, const c10::optional<torch::Tensor
     TORCH_CHECK(idp != nullptr, "traverse needs the tree ids");
     pk::nn_traverse(pts.data_ptr<float>(), idp, pts.size(0), int(pts.size(1)), int(depth0), queries.data_ptr<float>(),
                     nq, o, s);
+  } else if (method == "reference") {  // the reference's search procedure (reference-mode trees)
+    TORCH_CHECK(idp != nullptr, "the reference search needs the tree ids");
+    pk::nn_traverse_reference(pts.data_ptr<float>(), idp, pts.size(0), int(pts.size(1)), int(depth0),
+                              queries.data_ptr<float>(), nq, o, s);
   } else {
-    TORCH_CHECK(false, "method must be 'brute' or 'traverse'");
+    TORCH_CHECK(false, "method must be 'brute', 'traverse' or 'reference'");
   }
   return out;
 }
@@ -293,11 +318,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("split_level", [](const Builder& b) { return b.b.split_level(); })
       .def_property_readonly("split_streams", [](const Builder& b) { return b.b.split_streams(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
+      .def("error_words", [](Builder& b) {  // view of the workspace's 4 error words (int32)
+        TORCH_CHECK(b.ws.defined(), "no build yet");
+        return torch::from_blob(const_cast<pk::u32*>(b.b.error_word(b.ws.data_ptr())), {4},
+                                b.ws.options().dtype(torch::kInt32));
+      })
       .def("read_error", [](Builder& b) {
         u32 d[3];
         const u32 e = b.b.read_error(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream(), d);
         return std::vector<int64_t>{int64_t(e), int64_t(d[0]), int64_t(d[1]), int64_t(d[2])};
       });
+  py::class_<RefBuilder>(m, "ReferenceBuilder")
+      .def(py::init<int64_t, int64_t, int64_t>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0)
+      .def("build", &RefBuilder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0)
+      .def_property_readonly("sorted_levels", [](const RefBuilder& b) { return b.b.sorted_levels(); })
+      .def_property_readonly("workspace_bytes", [](const RefBuilder& b) { return int64_t(b.b.workspace_bytes()); });
   m.def("generate", &generate, py::arg("seed"), py::arg("dim"), py::arg("rows"), py::arg("first") = 0,
         py::arg("threads") = 0);
   m.def("generate_gpu", &generate_gpu, py::arg("seed"), py::arg("first"), py::arg("out"));

@@ -29,7 +29,10 @@ struct Options {
   int device = 0;
   bool host_gen = false;           // generate on the host and copy (default: on the GPU)
   std::string decomp = "forest";   // kdtree_dist: forest (kdtree_mpi.cpp) | global (one tree)
-  int pipeline_k = -1;             // kdtree_dist --decomp global: 2^k exchange rounds (-1: auto)
+  int pipeline_k = -1;             // kdtree_dist --decomp global: extra top levels (-1: auto)
+  std::string save;                // write the tree (tree_io.hpp format); forest ranks: <save>.rank<r>
+  int leaf_threshold = 0;          // largest segment of the LDS subtree kernel (0: auto from dim)
+  bool share_gpu = false;          // kdtree_dist: every rank on --device (RCCL ranks as separate hosts)
   std::vector<char*> positional;   // argv[0] + positionals
 };
 
@@ -57,6 +60,9 @@ inline Options parse(int argc, char** argv) {
     else if (is("--device")) o.device = std::atoi(val("--device").c_str());
     else if (is("--decomp")) o.decomp = val("--decomp");
     else if (is("--pipeline-k")) o.pipeline_k = std::atoi(val("--pipeline-k").c_str());
+    else if (is("--save")) o.save = val("--save");
+    else if (is("--leaf-threshold")) o.leaf_threshold = std::atoi(val("--leaf-threshold").c_str());
+    else if (a == "--share-gpu") o.share_gpu = true;
     else o.positional.push_back(argv[i]);
   }
   const char* env = std::getenv("KDTREE_DEBUG");

@@ -21,6 +21,10 @@
 // rank answers the queries on its share (complete subtrees plus the top rows between them),
 // rank 0 also on the boundary top rows, and the same MIN reduce combines them.
 // Ranks with no points (N < P, the reference's segfault F7) contribute +inf.
+// --mode reference (forest): every rank builds the reference's own quirky tree on the GPU
+// (build_reference.hip) and searches it with the reference's procedure, as kdtree_mpi does.
+// --save PATH writes the tree(s) (tree_io.hpp; forest: PATH.rank<r>), --leaf-threshold N caps
+// the LDS subtree segments, --share-gpu puts every rank on --device (one-GPU rehearsal).
 // Every collective is waited on with a watchdog (RcclComm::wait): the stream is polled and
 // ncclCommGetAsyncError checked until a deadline (--timeout seconds, default 300); a stuck or
 // failed collective aborts the communicator and the rank exits non-zero, after which the
@@ -49,8 +53,10 @@
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_generator.hpp"
 #include "pkdtree/gpu_query.hpp"
+#include "pkdtree/gpu_reference.hpp"
 #include "pkdtree/hip_check.hpp"
 #include "pkdtree/rccl_comm.hpp"
+#include "pkdtree/tree_io.hpp"
 
 using namespace pkdtree;
 
@@ -93,7 +99,14 @@ void read_all(int fd, void* p, size_t n) {
 int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vector<int>& id_pipes, double timeout_s,
              std::chrono::high_resolution_clock::time_point tick) {
   g_rank = rank;
-  PKD_HIP_CHECK(hipSetDevice(o.device + rank));
+  if (o.share_gpu) {
+    // every rank on one device (rehearsal on a one-GPU box): RCCL accepts several ranks per
+    // device only when they look like different hosts, so each rank gets its own host id and
+    // the ranks talk over the loopback socket transport
+    ::setenv("NCCL_HOSTID", ("pkd-dist-rank" + std::to_string(rank)).c_str(), 1);
+    ::setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+  }
+  PKD_HIP_CHECK(hipSetDevice(o.share_gpu ? o.device : o.device + rank));
   // RCCL prints a version banner on stdout during initialisation; stdout carries only the
   // protocol, so fd 1 points at stderr until the communicator is up.
   std::fflush(stdout);
@@ -159,6 +172,8 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   u32* d_ids = nullptr;
   void* ws = nullptr;
   std::unique_ptr<GpuBuilder> b;
+  std::unique_ptr<ReferenceBuilder> rb;  // --mode reference (forest): the reference's own tree per rank
+  const bool ref = o.mode == "reference";
   const bool global = o.decomp == "global";
   std::unique_ptr<GlobalBuilder> gb;
   float* d_top = nullptr;  // rank 0, global: the boundary top rows as a point set [T - 1][dim] + ids
@@ -168,15 +183,23 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
     PKD_HIP_CHECK(hipMalloc(&d_top, size_t(gb->layout().T) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(gb->layout().T) * 4));
   } else if (local > 0) {  // allocations outside the timed region
-    b = std::make_unique<GpuBuilder>(local, dim);
+    size_t wsb = 0;
+    if (ref) {
+      rb = std::make_unique<ReferenceBuilder>(local, dim);
+      wsb = rb->workspace_bytes();
+    } else {
+      b = std::make_unique<GpuBuilder>(local, dim, BuildOptions{o.leaf_threshold, 0});
+      wsb = b->workspace_bytes();
+    }
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(local) * 4));
-    PKD_HIP_CHECK(hipMalloc(&ws, b->workspace_bytes()));
+    PKD_HIP_CHECK(hipMalloc(&ws, std::max<size_t>(wsb, 256)));
   }
   PKD_HIP_CHECK(hipEventRecord(e0, s));
   nn_init(d_res, Q, s);
   // global 1-based ids (kdtree_mpi.cpp:223)
   if (global) gb->build(d_x, local, u32(first + 1), s);
+  else if (local > 0 && ref) rb->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);
   else if (local > 0) b->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);
   PKD_HIP_CHECK(hipEventRecord(e1, s));
   const float* d_q = d_x + size_t(local) * dim;
@@ -212,7 +235,8 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
       if (nt > 0) nn_brute(d_top, d_top_ids, 0, nt, dim, d_q, Q, d_res, s);
     }
   } else if (local > 0) {
-    if (traverse) nn_traverse(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);
+    if (ref) nn_traverse_reference(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);  // kdtree_mpi.cpp:234-243
+    else if (traverse) nn_traverse(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);
     else nn_brute(d_tree, d_ids, 0, local, dim, d_q, Q, d_res, s);
   }
   // MPI_Reduce(MIN) to rank 0 (kdtree_mpi.cpp:253), the id riding along in the low bits
@@ -228,7 +252,7 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventElapsedTime(&qry, e1, e2));
   const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
   // the build's device error word rides along (MAX over ranks: non-zero iff any rank failed)
-  const u32 berr = global ? gb->read_error(s) : local > 0 ? b->read_error(ws, s) : 0u;
+  const u32 berr = global ? gb->read_error(s) : (local > 0 && b) ? b->read_error(ws, s) : 0u;
   float* d_t = nullptr;
   PKD_HIP_CHECK(hipMalloc(&d_t, 4 * sizeof(float)));
   const float ht[4] = {gen, bld, qry, float(berr & 0xFFFFFFu) + (berr >> 24 ? 1.0f : 0.0f)};
@@ -260,6 +284,35 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
                    "\"top_levels\": %d}\n",
                    P, o.decomp.c_str(), mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f),
                    b ? b->global_levels() : 0, gb ? gb->top_levels() : 0);
+  }
+  // --save: forest ranks write their own trees (<path>.rank<r>, like kdtree_mpi's independent
+  // trees); the global tree is one file, every rank writing its share into its slot range
+  if (!o.save.empty()) {
+    const int mode = ref ? kTreeModeReference : kTreeModeExact;
+    if (!global) {
+      const std::string path = o.save + ".rank" + std::to_string(rank);
+      tree_file_create(path, local, dim, 0, mode);
+      if (local > 0) tree_file_write_device(path, local, dim, 0, local, d_tree, d_ids, s);
+    } else {
+      if (rank == 0) tree_file_create(o.save, N, dim, 0, mode);
+      PKD_NCCL_CHECK(ncclAllReduce(d_t, d_t, 1, ncclFloat32, ncclMax, comm, s));  // barrier: the file exists
+      watchdog_wait(s, "save barrier");
+      tree_file_write_device(o.save, N, dim, gb->slot_lo(), gb->n_leaf(), gb->tree_pts(), gb->tree_ids(), s);
+      if (rank == 0) {
+        const std::vector<i64> slots = gb->top_slots();
+        std::vector<float> rows(slots.size() * size_t(dim + 1));
+        if (!rows.empty())
+          PKD_HIP_CHECK(hipMemcpy(rows.data(), gb->top_rows(), rows.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t h = 0; h < slots.size(); ++h) {
+          if (slots[h] < 0) continue;
+          u32 id;
+          std::memcpy(&id, &rows[h * size_t(dim + 1) + dim], 4);
+          tree_file_write(o.save, N, dim, slots[h], 1, &rows[h * size_t(dim + 1)], &id);
+        }
+      }
+      PKD_NCCL_CHECK(ncclAllReduce(d_t, d_t, 1, ncclFloat32, ncclMax, comm, s));  // every share written
+      watchdog_wait(s, "save barrier");
+    }
   }
   (void)hipFree(d_x); (void)hipFree(d_res); (void)hipFree(d_cfg); (void)hipFree(d_t);
   if (d_top) (void)hipFree(d_top);
@@ -297,8 +350,10 @@ int main(int argc, char** argv) {
     return 1;
   }
   cli::Options o = cli::parse(int(rest.size()), rest.data());
-  if (o.mode != "exact") {
-    std::cerr << "kdtree_dist builds exact trees only; use kdtree_sequential --mode reference" << std::endl;
+  if (o.mode != "exact" && o.decomp == "global") {
+    std::cerr << "kdtree_dist --decomp global builds exact trees only (the reference's quirky tree depends on "
+                 "array positions, which the redistribution does not keep); use --decomp forest"
+              << std::endl;
     return 1;
   }
   const auto tick = std::chrono::high_resolution_clock::now();

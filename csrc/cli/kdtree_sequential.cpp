@@ -1,6 +1,7 @@
 // kdtree_sequential — CPU executable with the reference's protocol
 // (kdtree_sequential.cpp:140-208). Options: --mode exact|reference, --threads T
-// (threaded exact build: the reference's missing OMP variant, Makefile:23-27).
+// (threaded exact build: the reference's missing OMP variant, Makefile:23-27), --save PATH
+// (the tree in the tree_io.hpp format; ids are the reference's 1-based point ids).
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -9,6 +10,7 @@
 #include "cli_common.hpp"
 #include "pkdtree/cpu_tree.hpp"
 #include "pkdtree/generator.hpp"
+#include "pkdtree/tree_io.hpp"
 
 using namespace pkdtree;
 
@@ -27,6 +29,12 @@ int main(int argc, char** argv) {
   }
   std::vector<float> tree(static_cast<size_t>(N) * static_cast<size_t>(p.dim));
   gather_rows(x.data(), nullptr, perm.data(), N, p.dim, tree.data(), nullptr);
+  if (!o.save.empty()) {
+    std::vector<u32> ids(static_cast<size_t>(N));
+    for (i64 i = 0; i < N; ++i) ids[size_t(i)] = perm[size_t(i)] + 1;  // reference ids 1..N
+    tree_file_create(o.save, N, p.dim, 0, o.mode == "reference" ? kTreeModeReference : kTreeModeExact);
+    tree_file_write(o.save, N, p.dim, 0, N, tree.data(), ids.data());
+  }
   for (int q = 0; q < Q; ++q) {
     const float* qp = x.data() + size_t(N + q) * size_t(p.dim);
     const NNResult r = nn_search_cpu(tree.data(), N, p.dim, 0, qp);

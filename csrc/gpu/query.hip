@@ -352,6 +352,12 @@ __global__ __launch_bounds__(kBlock) void k_nn_wave(const float* __restrict__ P,
 }
 
 // One thread per query; explicit stack of far children with their lower bound.
+// REF: the reference's search procedure (nearest, kdtree_sequential.cpp:75-130) on a tree that
+// may violate the kd invariant (reference mode): near side first, the far side only if its
+// axis distance^2 is STRICTLY below the best distance (checked once the near side is done,
+// i.e. when popped), the best replaced only on a strictly smaller distance. The search then
+// visits exactly the reference's nodes and returns its distance, including its misses.
+template <bool REF>
 __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P, const u32* __restrict__ ids, i64 n,
                                                      int dim, int depth0, const float* __restrict__ queries, i64 nq,
                                                      u64* __restrict__ out) {
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P
       const float* p = P + i64(m) * dim;
       const float d2 = sq_dist(p, q, dim);
       const u64 v = pack_dist_idx(d2, ids[m]);
-      if (v < best) {
+      if (REF ? d2 < bd : v < best) {
         best = v;
         bd = d2;
       }
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P
       } else {
         near_lo = m + 1; near_n = rn; far_lo = lo; far_n = ln_;
       }
-      if (far_n > 0 && dax2 <= bd && sp < kStack) {
+      if (far_n > 0 && (REF ? dax2 < bd : dax2 <= bd) && sp < kStack) {
         st_lo[sp] = far_lo;
         st_n[sp] = far_n;
         st_d[sp] = (unsigned char)(depth + 1);
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P
     bool found = false;
     while (sp > 0) {
       --sp;
-      if (st_b[sp] <= bd) {
+      if (REF ? st_b[sp] < bd : st_b[sp] <= bd) {
         lo = st_lo[sp];
         cnt = st_n[sp];
         depth = st_d[sp];
@@ -558,8 +564,17 @@ void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int
       default: launch_nn_wave<0>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, nq, out, stream); return;
     }
   }
-  k_traverse<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries, nq,
-                                                                    out);
+  k_traverse<false><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries,
+                                                                           nq, out);
+  PKD_LAUNCH_CHECK();
+}
+
+void nn_traverse_reference(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0,
+                           const float* queries, i64 nq, u64* out, hipStream_t stream) {
+  if (nq <= 0 || n <= 0) return;
+  TraceRange tr("pkd.nn_traverse_reference");
+  k_traverse<true><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries,
+                                                                          nq, out);
   PKD_LAUNCH_CHECK();
 }
 

@@ -28,6 +28,13 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
                  i64 nq, u64* out, hipStream_t stream);
 
+// The reference's search procedure (kdtree_sequential.cpp:75-130: near side first, far side
+// iff axis distance^2 < best, strict improvements only) for reference-mode trees: the same
+// visited nodes and the same (possibly non-nearest) answer as the reference. `out` should
+// start at kPackedInf (nn_init): the reference starts every search afresh from the root.
+void nn_traverse_reference(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0,
+                           const float* queries, i64 nq, u64* out, hipStream_t stream);
+
 // Exact-mode invariant checked on the device (a semantic race detector for the partition
 // scatters): every slot k walks down from the root of its tree; at each
 // ancestor m it must sit on the side its slot says (k < m -> (key, id) below m's, k > m ->

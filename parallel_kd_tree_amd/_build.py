@@ -27,9 +27,10 @@ BIN = ROOT / "bin"
 ARCH = os.environ.get("PKD_OFFLOAD_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
-CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp"]
-CORE_HIP = ["gpu/build_global.hip", "gpu/build_subtree.hip", "gpu/query.hip", "gpu/dist_ops.hip", "gpu/generator.hip"]
-HOST_HIP = ["cpu/global_builder.cpp"]  # host C++ on the HIP runtime (no device code)
+CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp", "cpu/tree_io.cpp"]
+CORE_HIP = ["gpu/build_global.hip", "gpu/build_subtree.hip", "gpu/build_reference.hip", "gpu/query.hip",
+            "gpu/dist_ops.hip", "gpu/generator.hip"]
+HOST_HIP = ["cpu/global_builder.cpp", "cpu/tree_io_device.cpp"]  # host C++ on the HIP runtime (no device code)
 BIND = ["bind/torch_bindings.cpp", "bind/dist_bindings.cpp"]
 CLI_CPU = {"kdtree_sequential": ["cli/kdtree_sequential.cpp"]}
 CLI_GPU = {"kdtree_gpu": ["cli/kdtree_gpu.cpp"], "kdtree_dist": ["cli/kdtree_dist.cpp"]}

@@ -9,7 +9,11 @@ Modes
   exact      median under the total order (coordinate, id): unique tree, exact NN, identical
              for any number of GPUs (default).
   reference  the reference's quirky tree (sorts only the first n-1 points of every segment,
-             kdtree_sequential.cpp:46-48): CPU only, byte-identical outputs to the reference.
+             kdtree_sequential.cpp:46-48) and its search procedure (:75-130), which can miss
+             the true NN. On the CPU byte-identical to the reference binaries; on the GPU
+             (csrc/gpu/build_reference.hip: one segmented radix sort per level) identical
+             whenever no two points of a segment tie on its axis -- std::sort is unstable, so
+             the order of ties is the C++ library's business.
 """
 from __future__ import annotations
 
@@ -31,7 +35,7 @@ class KDTree:
         self.depth0 = int(depth0)
         self.mode = mode
         self._host = None
-        self._builder = None  # the GPU builder whose device error word covers this tree
+        self._err = None  # device copy of the GPU build's error words (exact mode)
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -52,8 +56,12 @@ class KDTree:
             b = ops.gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
             tp, ti = b.build(points, ids, id_base)
             t = cls(tp, ti, depth0, mode)
-            t._builder = b
+            t._err = b.error_words()  # this build's error words (device copy, stream-ordered)
             return t
+        if points.is_cuda:  # reference mode on the GPU
+            b = ops.reference_builder(points.shape[0], points.shape[1], depth0, points.device)
+            tp, ti = b.build(points, ids, id_base)
+            return cls(tp, ti, depth0, mode)
         else:
             cpu_ids = ids
             if cpu_ids is None:
@@ -66,8 +74,8 @@ class KDTree:
     def check(self) -> "KDTree":
         """Raise RuntimeError if the GPU build of this tree reported a device error (histogram
         / key disagreement, subtree overflow, ...). Synchronises; a no-op for CPU trees."""
-        if self._builder is not None:
-            err, code, level, value = self._builder.read_error_detail()
+        if self._err is not None:
+            err, code, level, value = (int(v) & 0xFFFFFFFF for v in self._err.tolist())
             if err:
                 raise RuntimeError(f"GPU kd-tree build failed: error word {err:#x} (code {code}, level {level}, "
                                    f"value {value})")
@@ -114,11 +122,14 @@ class KDTree:
     # ------------------------------------------------------------------ queries
     def query_packed(self, queries: torch.Tensor, method: str = "auto",
                      into: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Packed (d2, id) int64 per query (GPU). ``method``: auto | brute | traverse."""
+        """Packed (d2, id) int64 per query (GPU). ``method``: auto | brute | traverse. A
+        reference-mode tree always answers with the reference's search procedure."""
         if not self.tree_pts.is_cuda:
             raise ValueError("query_packed needs a GPU tree; use query() on CPU trees")
         q = queries.to(self.device, torch.float32).contiguous()
-        if method == "auto":
+        if self.mode == "reference":
+            method = "reference"
+        elif method == "auto":
             method = "traverse" if self.dim <= 16 else "brute"
         return ops.nn_gpu(self.tree_pts, self.tree_ids, q, method, self.depth0, 0, into)
 
@@ -126,9 +137,9 @@ class KDTree:
         """Exact nearest neighbour: (distance float32, id int64) per query row.
 
         Exact-mode trees return the true NN (ties -> smallest id). Reference-mode trees
-        on the CPU reproduce the reference search (which can miss the NN).
+        reproduce the reference search (which can miss the NN).
         """
-        if self.tree_pts.is_cuda and self.mode == "exact":
+        if self.tree_pts.is_cuda:
             return ops.finalize(self.query_packed(queries, method))
         q = queries.detach().cpu().to(torch.float32).contiguous()
         slots, d2 = ops.nn_cpu(self.tree_pts.cpu().contiguous(), q, self.depth0, brute=(method == "brute"))
@@ -141,7 +152,7 @@ class KDTree:
         if self.n == 0:
             return None
         q = torch.from_numpy(query.coordinates.reshape(1, -1).copy())
-        if self.tree_pts.is_cuda and self.mode == "exact":
+        if self.tree_pts.is_cuda:
             # the id -> slot lookup runs on the device: one comparison pass over tree_ids, and
             # only the slot index crosses to the host (never the tree)
             _, ids = ops.finalize(self.query_packed(q))

@@ -49,6 +49,11 @@ class GpuTreeBuilder:
         """Sticky device error word of the last build (0 = ok). Synchronises."""
         return int(self._b.read_error()[0])
 
+    def error_words(self) -> torch.Tensor:
+        """A device copy (int32 [4]: error word, first failure code, level, value) of the last
+        build's error words, ordered after it on the current stream: no host sync."""
+        return self._b.error_words().clone()
+
     def read_error_detail(self):
         """(error word, first failure code, level, value). Synchronises."""
         return tuple(int(v) for v in self._b.read_error())
@@ -69,7 +74,29 @@ class GpuTreeBuilder:
         return tuple(self._b.build_from_soa(torch.device(device)))
 
 
+class ReferenceTreeBuilder:
+    """Reference-mode builder on the GPU (csrc/gpu/build_reference.hip): the reference's own
+    tree (first n - 1 points sorted per segment), one segmented radix sort per level."""
+
+    def __init__(self, n: int, dim: int, depth0: int = 0):
+        self._b = native().ReferenceBuilder(int(n), int(dim), int(depth0))
+        self.n, self.dim, self.depth0 = int(n), int(dim), int(depth0)
+
+    def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0):
+        return tuple(self._b.build(points.contiguous(), ids, int(id_base)))
+
+
 _builders: dict = {}
+
+
+def reference_builder(n: int, dim: int, depth0: int = 0, device=None) -> ReferenceTreeBuilder:
+    key = ("reference", int(n), int(dim), int(depth0), device)
+    b = _builders.get(key)
+    if b is None:
+        if len(_builders) > 8:
+            _builders.clear()
+        b = _builders[key] = ReferenceTreeBuilder(n, dim, depth0)
+    return b
 
 
 def gpu_builder(n: int, dim: int, depth0: int = 0, subtree_max: int = 0, device=None) -> GpuTreeBuilder:

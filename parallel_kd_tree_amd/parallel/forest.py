@@ -32,8 +32,8 @@ class ForestTree:
 
     def local_error(self) -> int:
         """Device error word of this rank's build (0 = ok, also for CPU trees). Synchronises."""
-        b = self.local._builder
-        return b.read_error() if b is not None else 0
+        e = self.local._err
+        return int(e[0].item()) & 0xFFFFFFFF if e is not None else 0
 
     def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
         """Packed (d2, global id) of the nearest point over all ranks. Reference-mode forests

@@ -92,3 +92,18 @@ def test_queries_option(bin_dir, flag):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.splitlines()
     assert lines[1:26] == oracle_lines(4, 3, 5000, 25) and lines[26].startswith("elapsed time ")
+
+
+@pytest.mark.parametrize("mode", ["exact", "reference"])
+def test_save_tree_file(bin_dir, tmp_path, mode):
+    """--save writes the tree (utils/io.py format, reference 1-based ids) that KDTree.load reads:
+    the same tree the Python API builds, in either mode."""
+    import torch
+    f = tmp_path / "t.pkd"
+    r = run(bin_dir / "kdtree_sequential", ["--mode", mode, "--save", f, 7, 3, 5000])
+    assert r.returncode == 0, r.stderr
+    t = pk.KDTree.load(f)
+    x = pk.generate_problem(7, 3, 5000)
+    ref = pk.KDTree.build(x, id_base=1, mode=mode)
+    assert t.mode == mode and t.n == 5000
+    assert torch.equal(t.tree_ids, ref.tree_ids) and torch.equal(t.tree_pts, ref.tree_pts)

@@ -1,0 +1,122 @@
+"""GPU reference mode: the reference's own quirky tree (kdtree_sequential.cpp:46-48 sorts only the
+first n - 1 points of every segment) and its search procedure (:75-130), on the GPU
+(csrc/gpu/build_reference.hip, nn_traverse_reference in csrc/gpu/query.hip).
+
+Oracle: the CPU reference-mode builder and search (csrc/cpu/cpu_tree.cpp), which the parity
+tests pin to the compiled reference binary. std::sort is unstable, so the tree is only
+defined up to ties: the builder tests use tie-free data (a random permutation of distinct
+values per axis); the CLI tests use the reference generator at sizes where its
+~22.5 M distinct values per axis (F5) leave the reference's segments tie-free."""
+import subprocess
+from pathlib import Path
+
+import pytest
+import torch
+
+import parallel_kd_tree_amd as pk
+from parallel_kd_tree_amd import ops
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+BIN = ROOT / "bin"
+
+
+def tie_free(n, dim, seed):
+    g = torch.Generator().manual_seed(seed)
+    cols = [(torch.randperm(n, generator=g).float() + 0.5) / max(n, 1) * 200 - 100 for _ in range(dim)]
+    return torch.stack(cols, 1).contiguous() if n else torch.empty((0, dim))
+
+
+@pytest.mark.parametrize("n,dim", [(1, 3), (2, 3), (3, 2), (5, 1), (100, 3), (1023, 3), (1024, 3), (4097, 2),
+                                   (100_000, 3), (30_000, 8), (20_000, 16)])
+def test_reference_tree_equals_cpu(gpu_device, n, dim):
+    x = tie_free(n, dim, n + dim)
+    tp, ti = ops.ReferenceTreeBuilder(n, dim).build(x.to(gpu_device), None, 1)
+    cp, ci = ops.build_cpu(x, (torch.arange(n) + 1).to(torch.int32), "reference", 0, 1)
+    assert torch.equal(ti.cpu(), ci), "GPU reference tree differs from the CPU reference tree"
+    assert torch.equal(tp.cpu(), cp)
+
+
+def test_reference_tree_is_not_exact(gpu_device):
+    """The reference tree violates the kd invariant: the mode is not a relabel
+    of the exact tree."""
+    x = tie_free(50_000, 3, 4)
+    t = pk.KDTree.build(x.to(gpu_device), id_base=1, mode="reference")
+    assert t.mode == "reference" and t.invariant_violations() > 0
+
+
+@pytest.mark.parametrize("n,dim", [(20_000, 3), (5_000, 8), (2_000, 64)])
+def test_reference_search_equals_cpu(gpu_device, n, dim):
+    """KDTree(mode='reference') on the GPU answers exactly what the CPU reference search answers
+    -- including the queries where the quirky tree makes it miss the true nearest neighbour."""
+    x = tie_free(n + 400, dim, dim)
+    pts, q = x[:n], x[n:]
+    tg = pk.KDTree.build(pts.to(gpu_device), id_base=1, mode="reference")
+    tc = pk.KDTree.build(pts, id_base=1, mode="reference")
+    dg, _ = tg.query(q.to(gpu_device))
+    dc, _ = tc.query(q)
+    assert torch.equal(dg.cpu(), dc)
+    if dim <= 3:  # the reference search really is approximate here (F1): some answers are not the NN
+        brute = ((pts[None].double() - q[:, None].double()) ** 2).sum(-1).min(1).values.sqrt().float()
+        assert bool((dc > brute).any())
+
+
+def _run(args, **kw):
+    return subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=300, **kw)
+
+
+@pytest.mark.parametrize("seed,dim,n", [(42, 3, 1024), (7, 2, 5000), (3, 128, 2000)])
+def test_kdtree_gpu_reference_mode_cli(seed, dim, n):
+    """bin/kdtree_gpu --mode reference prints what kdtree_sequential --mode reference (the
+    reference binary's output, tests/test_reference_parity.py) prints."""
+    g = _run([BIN / "kdtree_gpu", "--mode", "reference", seed, dim, n])
+    c = _run([BIN / "kdtree_sequential", "--mode", "reference", seed, dim, n])
+    assert g.returncode == 0 and c.returncode == 0, g.stderr + c.stderr
+    strip = lambda out: [l for l in out.splitlines() if not l.startswith("elapsed time")]  # noqa: E731
+    assert strip(g.stdout) == strip(c.stdout)
+
+
+def test_kdtree_dist_reference_forest_share_gpu():
+    """kdtree_dist --mode reference: per-rank reference trees + the reference search + MIN reduce,
+    i.e. the reference MPI program (kdtree_mpi.cpp); three ranks over RCCL on one card."""
+    g = _run([BIN / "kdtree_dist", "--gpus", "3", "--share-gpu", "--mode", "reference", 5, 3, 4000])
+    assert g.returncode == 0, g.stderr[-2000:]
+    lines = [l for l in g.stdout.splitlines() if l.startswith("ID:")]
+    x = pk.generate_problem(5, 3, 4010)
+    q = x[4000:]
+    best = None
+    for r in range(3):
+        first, cnt = 1333 * r, 1333 + (1 if r == 2 else 0)
+        t = pk.KDTree.build(x[first:first + cnt], id_base=first + 1, mode="reference")
+        d, _ = t.query(q)
+        best = d if best is None else torch.minimum(best, d)
+    from parallel_kd_tree_amd.utils import protocol
+    assert lines == [protocol.result_line(4000 + i, float(best[i])) for i in range(10)]
+
+
+def test_cli_save_and_leaf_threshold(tmp_path):
+    """--save writes the tree file (utils/io.py format) and --leaf-threshold only changes how it
+    is built, never the tree."""
+    a, b = tmp_path / "a.pkd", tmp_path / "b.pkd"
+    r1 = _run([BIN / "kdtree_gpu", "--save", a, 9, 3, 300_000])
+    r2 = _run([BIN / "kdtree_gpu", "--save", b, "--leaf-threshold", "256", 9, 3, 300_000])
+    assert r1.returncode == 0 and r2.returncode == 0, r1.stderr + r2.stderr
+    assert r1.stdout == r2.stdout
+    ta, tb = pk.KDTree.load(a), pk.KDTree.load(b)
+    x = pk.generate_problem(9, 3, 300_000)
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    assert torch.equal(ta.tree_ids, ci + 1) and torch.equal(ta.tree_pts, cp)
+    assert torch.equal(tb.tree_ids, ta.tree_ids) and torch.equal(tb.tree_pts, ta.tree_pts)
+
+
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_kdtree_dist_global_save_share_gpu(tmp_path, gpus):
+    """kdtree_dist --decomp global --save: every rank writes its share into one file, rank 0 the
+    boundary top rows; the file is the single-GPU exact tree (any rank count)."""
+    f = tmp_path / "g.pkd"
+    r = _run([BIN / "kdtree_dist", "--gpus", gpus, "--share-gpu", "--decomp", "global", "--save", f, 13, 3, 250_001])
+    assert r.returncode == 0, r.stderr[-2000:]
+    t = pk.KDTree.load(f)
+    x = pk.generate_problem(13, 3, 250_001)
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    assert torch.equal(t.tree_ids, ci + 1) and torch.equal(t.tree_pts, cp)
