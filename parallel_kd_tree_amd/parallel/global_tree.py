@@ -185,28 +185,132 @@ class DistTree:
                     full[s] = self.top_rows[i].to(dev)
         return full[:, :self.dim].contiguous(), full[:, self.dim].contiguous().view(torch.int32)
 
-    def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
-        """Exact NN over the whole distributed tree: this rank's blocks and the top rows between
-        them, rank 0 also the boundary top rows; MIN-reduced over the ranks."""
-        from ..models.kdtree import KDTree
+    def query_packed(self, queries: torch.Tensor, method: str = "auto", routed: bool = True) -> torch.Tensor:
+        """Exact NN over the whole distributed tree, packed (d2 << 32 | id), on every rank.
+
+        routed (default): queries are replicated on every rank (as in kdtree_mpi.cpp:234-243),
+        but each is searched where it can matter:
+          1. every query descends the replicated top tree to its home leaf; only the rank
+             owning that leaf searches it (in the block holding the leaf) -> ~Q / P searches
+             per rank; one MIN all-reduce gives every query a candidate radius;
+          2. a rank searches a query in one of its other blocks (or, for the home block, never
+             again) only if the query's best ball reaches that block's cell (the box cut out by
+             the top pivots above it), starting from the candidate radius; a second MIN
+             all-reduce gives the answer.
+        The top rows between blocks and the boundary rows are brute-forced (<= 63 rows).
+        routed=False: every rank searches every query in all its blocks (one MIN all-reduce).
+        ``self.last_query_work`` holds this rank's (query, block) searches of the last call."""
         dev = self.tree_pts.device
-        packed = torch.full((queries.shape[0],), ops.query.INF_PACKED, dtype=torch.int64, device=dev)
-        for off, n, depth, _ in self.blocks:
-            if n > 0:
-                t = KDTree(self.tree_pts[off:off + n], self.tree_ids[off:off + n], self.depth0 + depth)
-                packed = torch.minimum(packed, _local_packed(t, queries, method).to(dev))
+        q = queries.to(dev, torch.float32).contiguous()
+        Q = q.shape[0]
+        packed = torch.full((Q,), ops.query.INF_PACKED, dtype=torch.int64, device=dev)
+        blocks = [b for b in self.blocks if b[1] > 0]
+        work = 0
+        if not routed:
+            for b in blocks:
+                packed = torch.minimum(packed, self._search_block(b, q, method, None))
+                work += Q
+        else:
+            home_blk = self._home_blocks(q)  # [Q]: index into `blocks` of this rank, -1 elsewhere
+            for i, b in enumerate(blocks):
+                sel = (home_blk == i).nonzero().flatten()
+                if sel.numel():
+                    packed[sel] = self._search_block(b, q[sel], method, None)
+                    work += int(sel.numel())
+        packed = self._brute_top(packed, q)
+        packed = comm.min_packed_(packed)
+        if routed:
+            d2 = ops.unpack(packed)[0].to(torch.float64)
+            for i, b in enumerate(blocks):
+                lo, hi = self._block_box(b)
+                gap = torch.clamp(lo[None, :] - q.double(), min=0) + torch.clamp(q.double() - hi[None, :], min=0)
+                bd2 = (gap * gap).sum(1)
+                # conservative: the box bound is exact math, point distances are fp32 sums
+                reach = (bd2 <= d2 * (1 + 1e-5) + 1e-30) & (home_blk != i)
+                sel = reach.nonzero().flatten()
+                if sel.numel():
+                    packed[sel] = self._search_block(b, q[sel], method, packed[sel].clone())
+                    work += int(sel.numel())
+            packed = comm.min_packed_(packed)
+        self.last_query_work = work
+        return packed
+
+    # ---- routed-query helpers ----------------------------------------------------------
+    def _search_block(self, b, q, method, into):
+        """Packed NN of queries q in block b (MIN-combined with / pruned by `into`)."""
+        from ..models.kdtree import KDTree
+        off, n, depth, _ = b
+        t = KDTree(self.tree_pts[off:off + n], self.tree_ids[off:off + n], self.depth0 + depth)
+        if t.tree_pts.is_cuda:
+            return t.query_packed(q, method, into=into)
+        r = _local_packed(t, q, method).to(q.device)
+        return r if into is None else torch.minimum(r, into)
+
+    def _brute_top(self, packed, q):
+        """MIN with the top rows between this rank's blocks and (rank 0) the boundary rows."""
+        dev = packed.device
         rows = [int(self.layout["top_slot"][h]) - self.slot_lo for h in self.between]
         if rows:
             sel = torch.tensor(rows, dtype=torch.int64, device=dev)
-            packed = torch.minimum(packed, _brute_packed(self.tree_pts[sel], self.tree_ids[sel], queries).to(dev))
+            packed = torch.minimum(packed, _brute_packed(self.tree_pts[sel], self.tree_ids[sel], q).to(dev))
         if self.top_rows is not None and self.rank == 0:
             valid = [i for i, s in enumerate(self.top_slots) if s >= 0]
             if valid:
                 tr = self.top_rows[valid].to(dev)
-                pk = _brute_packed(tr[:, :self.dim].contiguous(), tr[:, self.dim].contiguous().view(torch.int32),
-                                   queries.to(dev))
+                pk = _brute_packed(tr[:, :self.dim].contiguous(), tr[:, self.dim].contiguous().view(torch.int32), q)
                 packed = torch.minimum(packed, pk.to(dev))
-        return comm.min_packed_(packed)
+        return packed
+
+    def _pivot_keys(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(axis, split coordinate) of every top node (heap order), on the tree's device."""
+        T1 = 0 if self.top_rows is None else int(self.top_rows.shape[0])
+        axes = torch.tensor([(self.depth0 + (h + 1).bit_length() - 1) % self.dim for h in range(T1)],
+                            dtype=torch.int64)
+        keys = self.top_rows[torch.arange(T1), axes].float() if T1 else torch.empty(0)
+        return axes.to(self.tree_pts.device), keys.to(self.tree_pts.device)
+
+    def _home_blocks(self, q: torch.Tensor) -> torch.Tensor:
+        """Index of the block (of this rank's blocks with points) holding each query's home leaf:
+        the leaf reached by descending the top tree (coordinate < pivot -> left, else right,
+        the search's own near side); -1 when the home leaf belongs to another rank."""
+        LL, T = int(self.layout["LL"]), int(self.layout["T"])
+        axes, keys = self._pivot_keys()
+        h = torch.zeros(q.shape[0], dtype=torch.int64, device=q.device)
+        for _ in range(LL):
+            go_right = q.gather(1, axes[h][:, None])[:, 0] >= keys[h]
+            h = 2 * h + 1 + go_right.to(torch.int64)
+        leaf = h - (T - 1)
+        out = torch.full_like(leaf, -1)
+        blocks = [b for b in self.blocks if b[1] > 0]
+        for i, (_, _, depth, heap) in enumerate(blocks):
+            s = LL - depth  # levels between the block root and the top-level leaves
+            first = ((heap + 1) << s) - T  # first leaf of the block
+            out = torch.where((leaf >= first) & (leaf < first + (1 << s)), torch.full_like(out, i), out)
+        return out
+
+    def _block_box(self, b) -> Tuple[torch.Tensor, torch.Tensor]:
+        """The cell of a block: [lo, hi] per axis cut out by the top pivots above its root
+        (closed: points equal to a pivot's coordinate may sit on either side)."""
+        if not hasattr(self, "_boxes"):
+            self._boxes = {}
+        heap = b[3]
+        if heap not in self._boxes:
+            lo = torch.full((self.dim,), float("-inf"), dtype=torch.float64)
+            hi = torch.full((self.dim,), float("inf"), dtype=torch.float64)
+            top = self.top_rows.detach().cpu() if self.top_rows is not None else None
+            child = heap
+            while child > 0:
+                h = (child - 1) // 2
+                a = (self.depth0 + (h + 1).bit_length() - 1) % self.dim
+                v = float(top[h, a])
+                if child == 2 * h + 1:
+                    hi[a] = min(hi[a], v)
+                else:
+                    lo[a] = max(lo[a], v)
+                child = h
+            dev = self.tree_pts.device
+            self._boxes[heap] = (lo.to(dev), hi.to(dev))
+        return self._boxes[heap]
 
     def check_top_routing(self) -> str:
         """'' when every block of this rank lies on the correct side of every top-tree pivot

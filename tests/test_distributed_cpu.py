@@ -223,3 +223,31 @@ def _routing_check_catches(rank, world):
 
 def test_top_routing_check():
     run(2, _routing_check_catches)
+
+
+def _routed_queries(rank, world, n, dim, nq):
+    """Routed queries (home leaf first, then only the blocks the best ball reaches) give the
+    brute-force distances with ~1/P of the (query, block) searches per rank."""
+    import parallel_kd_tree_amd as pk
+    from parallel_kd_tree_amd import ops
+    from parallel_kd_tree_amd.parallel import comm
+    from parallel_kd_tree_amd.parallel.global_tree import GlobalTreeBuilder
+    first, cnt = comm.forest_slice(n, world, rank)
+    x = pk.generate_slice(17, dim, first, cnt)
+    t = GlobalTreeBuilder(n, dim, device=torch.device("cpu")).build(x, id_base=first + 1)
+    full = pk.generate_problem(17, dim, n + nq)
+    q = full[n:]
+    d2, _ = ops.unpack(t.query_packed(q))
+    work = t.last_query_work
+    d2a, _ = ops.unpack(t.query_packed(q, routed=False))
+    ref = ((full[:n][None].double() - q[:, None].double()) ** 2).sum(-1).min(1).values
+    assert torch.equal(d2.double(), ref.float().double()) or torch.allclose(d2.double(), ref, rtol=1e-6)
+    assert torch.equal(d2, d2a)
+    tot = torch.tensor([work], dtype=torch.int64)
+    comm.all_reduce_(tot)
+    assert int(tot) < 1.5 * nq, f"routed queries searched {int(tot)} (query, block) pairs for {nq} queries"
+
+
+@pytest.mark.parametrize("world,dim", [(4, 3), (3, 2)])
+def test_routed_queries(world, dim):
+    run(world, _routed_queries, 20_000, dim, 300)

@@ -152,3 +152,34 @@ def test_bench_rccl_share_gpu(gpus):
     assert line["config"]["tree_checked"] and not line["config"]["headline"]
     phases = [json.loads(s) for s in r.stderr.splitlines() if s.startswith('{"phases_max_over_ranks_ms"')]
     assert len(phases) == 1 and phases[0]["phases_max_over_ranks_ms"]["leaf_ms"] > 0
+
+
+def _routed(rank, world, n, dim, nq):
+    """10 000 queries on the distributed tree: each is searched on its home rank, then only where
+    its best ball reaches -- brute-force answers with ~1/P of the per-rank query work."""
+    import parallel_kd_tree_amd as pk
+    from parallel_kd_tree_amd import ops
+    from parallel_kd_tree_amd.parallel import comm
+    from parallel_kd_tree_amd.parallel.native_global import NativeGlobalBuilder
+    dev = torch.device("cuda", 0)
+    first, cnt = comm.forest_slice(n, world, rank)
+    full = pk.generate_problem(31, dim, n + nq)
+    b = NativeGlobalBuilder(n, dim, dev, timeout_s=60)
+    t = b.build(full[first:first + cnt].to(dev), id_base=first + 1)
+    q = full[n:].to(dev)
+    d2, ids = ops.unpack(t.query_packed(q))
+    work = t.last_query_work
+    d2a, _ = ops.unpack(t.query_packed(q, routed=False))
+    assert torch.equal(d2, d2a)
+    pts = full[:n].to(dev).double()
+    ref = torch.cat([torch.cdist(q[i:i + 500].double(), pts).pow(2).min(1).values for i in range(0, nq, 500)])
+    got = ((pts[ids.to(dev) - 1] - q.double()) ** 2).sum(-1)
+    assert torch.allclose(got, ref, rtol=0, atol=1e-9)
+    tot = torch.tensor([work], dtype=torch.int64, device=dev)
+    comm.all_reduce_(tot)
+    assert int(tot) < 1.3 * nq, f"{int(tot)} (query, block) searches over {world} ranks for {nq} queries"
+
+
+@pytest.mark.parametrize("world,dim", [(4, 3), (3, 4)])
+def test_routed_queries_rccl(world, dim):
+    run_rccl(world, _routed, 400_000, dim, 10_000)

@@ -101,7 +101,8 @@ def test_cli_save_and_leaf_threshold(tmp_path):
     r1 = _run([BIN / "kdtree_gpu", "--save", a, 9, 3, 300_000])
     r2 = _run([BIN / "kdtree_gpu", "--save", b, "--leaf-threshold", "256", 9, 3, 300_000])
     assert r1.returncode == 0 and r2.returncode == 0, r1.stderr + r2.stderr
-    assert r1.stdout == r2.stdout
+    strip = lambda out: [l for l in out.splitlines() if not l.startswith("elapsed time")]  # noqa: E731
+    assert strip(r1.stdout) == strip(r2.stdout)
     ta, tb = pk.KDTree.load(a), pk.KDTree.load(b)
     x = pk.generate_problem(9, 3, 300_000)
     cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
