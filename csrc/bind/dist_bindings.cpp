@@ -83,20 +83,39 @@ void route_hist(const torch::Tensor& pts, const std::optional<torch::Tensor>& id
 }
 
 void select(const torch::Tensor& hist, int64_t level, int64_t bins, const std::vector<int64_t>& sizes,
-            torch::Tensor sel, torch::Tensor err) {
+            torch::Tensor sel, torch::Tensor err, std::optional<torch::Tensor> zero_hist,
+            std::optional<torch::Tensor> zero_hdr) {
   const c10::DeviceGuard g(hist.device());
   TORCH_CHECK(int64_t(sizes.size()) == (int64_t(1) << level), "one size per node");
-  top_select(cu32p(hist), int(level), int(bins), sizes_of(sizes), u32p(sel), u32p(err), stream_of(hist));
+  u32* zh = nullptr;
+  if (zero_hist && zero_hist->defined()) {
+    TORCH_CHECK(zero_hist->numel() >= kTopBins, "zero_hist must hold kTopBins words");
+    zh = u32p(*zero_hist);
+  }
+  u32* zd = zero_hdr && zero_hdr->defined() ? reinterpret_cast<u32*>(zero_hdr->data_ptr()) : nullptr;
+  top_select(cu32p(hist), int(level), int(bins), sizes_of(sizes), u32p(sel), u32p(err), zh, zd, stream_of(hist));
 }
 
-void collect(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base,
-             const torch::Tensor& node, int64_t level, int64_t axis, const torch::Tensor& cells, int64_t bins,
-             const torch::Tensor& sel, torch::Tensor buf, int64_t cap) {
+void collect_route(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base,
+                   torch::Tensor node, int64_t level, int64_t axis, int64_t next_axis, const torch::Tensor& cells,
+                   int64_t bins, int64_t next_bins, const torch::Tensor& sel, torch::Tensor buf, int64_t cap,
+                   std::optional<torch::Tensor> hist_next) {
   const c10::DeviceGuard g(pts.device());
   TopPoints p = points_of(pts, ids, id_base);
   TORCH_CHECK(size_t(buf.numel()) >= top_middle_words(p.dim, cap), "middle buffer too small");
-  top_collect(p, cu32p(node), int(level), int(axis), cells.data_ptr<float>(), int(bins), cu32p(sel),
-              buf.data_ptr<float>(), cap, stream_of(pts));
+  TORCH_CHECK(node.numel() >= p.n, "node array too small");
+  u32* hn = hist_next && hist_next->defined() ? u32p(*hist_next) : nullptr;
+  top_collect_route(p, u32p(node), int(level), int(axis), int(next_axis), cells.data_ptr<float>(), int(bins),
+                    int(next_bins), cu32p(sel), buf.data_ptr<float>(), cap, hn, stream_of(pts));
+}
+
+void fixup(const torch::Tensor& buf, int64_t cap, int64_t dim, int64_t level, int64_t axis, int64_t next_axis,
+           const torch::Tensor& pivots, const torch::Tensor& cells, int64_t next_bins, torch::Tensor node,
+           std::optional<torch::Tensor> hist_next) {
+  const c10::DeviceGuard g(buf.device());
+  u32* hn = hist_next && hist_next->defined() ? u32p(*hist_next) : nullptr;
+  top_fixup(buf.data_ptr<float>(), cap, int(dim), int(level), int(axis), int(next_axis), cu64p(pivots),
+            cells.data_ptr<float>(), int(next_bins), u32p(node), hn, stream_of(buf));
 }
 
 void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level, int64_t axis, int64_t dim,
@@ -109,9 +128,10 @@ void pivot(const torch::Tensor& gathered, int64_t P, int64_t cap, int64_t level,
             u64p(pivots), top_rows.data_ptr<float>(), cells.data_ptr<float>(), u32p(err), stream_of(gathered));
 }
 
-// out: [>= n, dim + 1] / [>= n, dim] rows, or (col_stride > 0) planes of col_stride floats
-void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base, torch::Tensor node,
-          int64_t levels, const torch::Tensor& pivots, int64_t last_axis, torch::Tensor out, int64_t col_stride,
+// out: [>= n, dim + 1] / [>= n, dim] rows, or (col_stride > 0) planes of col_stride floats.
+// node: as the top levels left it (leaf heap nodes, kTopDone for pivots).
+void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int64_t id_base,
+          const torch::Tensor& node, int64_t levels, torch::Tensor out, int64_t col_stride,
           std::optional<torch::Tensor> bitmaps, torch::Tensor counts, const torch::Tensor& err, torch::Tensor scratch) {
   const c10::DeviceGuard g(pts.device());
   TopPoints p = points_of(pts, ids, id_base);
@@ -137,8 +157,8 @@ void pack(const torch::Tensor& pts, const std::optional<torch::Tensor>& ids, int
     bm = u32p(*bitmaps);
     words = bitmaps->size(1);
   }
-  top_pack(p, u32p(node), int(levels), cu64p(pivots), int(last_axis), out.data_ptr<float>(), row_stride, col_stride,
-           bm, words, counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
+  top_pack(p, cu32p(node), int(levels), out.data_ptr<float>(), row_stride, col_stride, bm, words,
+           counts.data_ptr<int64_t>(), cu32p(err), scratch.data_ptr(), stream_of(pts));
 }
 
 // bitmaps: all sources' words back to back; per source (row offset, rows, word offset, words, id base)
@@ -404,13 +424,15 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("top_bbox", &bbox);
   m.def("top_root_cell", &root_cell);
   m.def("top_route_hist", &route_hist);
-  m.def("top_select", &select);
-  m.def("top_collect", &collect);
+  m.def("top_select", &select, pybind11::arg("hist"), pybind11::arg("level"), pybind11::arg("bins"),
+        pybind11::arg("sizes"), pybind11::arg("sel"), pybind11::arg("err"), pybind11::arg("zero_hist") = std::nullopt,
+        pybind11::arg("zero_hdr") = std::nullopt);
+  m.def("top_collect_route", &collect_route);
+  m.def("top_fixup", &fixup);
   m.def("top_pivot", &pivot);
   m.def("top_pack", &pack, pybind11::arg("pts"), pybind11::arg("ids"), pybind11::arg("id_base"), pybind11::arg("node"),
-        pybind11::arg("levels"), pybind11::arg("pivots"), pybind11::arg("last_axis"), pybind11::arg("out"),
-        pybind11::arg("col_stride"), pybind11::arg("bitmaps"), pybind11::arg("counts"), pybind11::arg("err"),
-        pybind11::arg("scratch"));
+        pybind11::arg("levels"), pybind11::arg("out"), pybind11::arg("col_stride"), pybind11::arg("bitmaps"),
+        pybind11::arg("counts"), pybind11::arg("err"), pybind11::arg("scratch"));
   m.def("top_middle_words", [](int64_t dim, int64_t cap) { return int64_t(top_middle_words(int(dim), cap)); });
   m.def("top_pack_scratch_bytes", [](int64_t n, int64_t T) { return int64_t(top_pack_scratch_bytes(n, int(T))); });
   m.def("ids_from_bitmaps", &ids_from_bm);

@@ -376,38 +376,42 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     auto* err = static_cast<u32*>(buf(5, 16));
     fill_u64(err, 2, 0ull, s);
     auto* sel = static_cast<u32*>(buf(6, size_t(kTopMaxNodes) * 4 * 4));
-    auto* hist = static_cast<u32*>(buf(7, size_t(kTopBins) * 4));
-    // 2. top levels
+    u32* hist[2] = {static_cast<u32*>(buf(7, size_t(kTopBins) * 4)), static_cast<u32*>(buf(17, size_t(kTopBins) * 4))};
+    if (LL > 0) fill_u64(hist[0], kTopBins / 2, 0ull, s);
+    // 2. top levels: level 0's histogram, then per level one fused pass (median-bucket rows
+    // staged, every other row routed to its child and counted into the next level's histogram)
+    // and, after the pivot, the fix-up of the staged rows
     for (int level = 0; level < LL; ++level) {
-      const int nodes = 1 << level, bins = kTopBins / nodes;
-      const int axis = level % dim, prev_axis = ((level - 1) % dim + dim) % dim;
+      const int nodes = 1 << level, bins = kTopBins / nodes, next_bins = kTopBins / (2 * nodes);
+      const int axis = level % dim, next_axis = (level + 1) % dim;
+      u32* hcur = hist[level & 1];
+      u32* hnext = level + 1 < LL ? hist[(level + 1) & 1] : nullptr;
       TopSizes sizes{};
       for (int j = 0; j < nodes; ++j) {
         i64 lo;
         global_plan::segment(n_total_, nodes - 1 + j, &lo, &sizes.n[j]);
       }
-      fill_u64(hist, i64(nodes) * bins / 2, 0ull, s);
-      top_route_hist(tp, node, level, pivots, prev_axis, axis, cells, bins, hist, s);
-      comm_.allreduce_sum_u32(hist, size_t(nodes) * bins, s);
-      top_select(hist, level, bins, sizes, sel, err, s);
+      if (level == 0) top_route_hist(tp, node, 0, pivots, 0, axis, cells, bins, hcur, s);
+      comm_.allreduce_sum_u32(hcur, size_t(nodes) * bins, s);
       const i64 cap = global_plan::middle_cap(n_total_, P, level, scale_);
       const size_t words = top_middle_words(dim, cap);
       auto* mid = static_cast<float*>(buf(8, words * 4));
-      top_collect(tp, node, level, axis, cells, bins, sel, mid, cap, s);
+      top_select(hcur, level, bins, sizes, sel, err, hnext, reinterpret_cast<u32*>(mid), s);
+      top_collect_route(tp, node, level, axis, next_axis, cells, bins, next_bins, sel, mid, cap, hnext, s);
       auto* gathered = static_cast<float*>(buf(9, size_t(P) * words * 4));
       comm_.allgather(mid, gathered, words * 4, s);
       top_pivot(gathered, P, cap, level, axis, dim, sizes, sel, pivots, top_rows, cells, err, s);
+      top_fixup(mid, cap, dim, level, axis, next_axis, pivots, cells, next_bins, node, hnext, s);
     }
     if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvTop), s));
     // 3. pack by destination leaf: coordinates (planes or rows) + one bit per (row, leaf)
-    const int last_axis = ((LL - 1) % dim + dim) % dim;
     auto* send = static_cast<float*>(
         buf(10, planar_ ? size_t(dim) * send_stride * 4 : size_t(std::max<i64>(n_local, 1)) * dim * 4));
     auto* counts = static_cast<i64*>(buf(11, size_t(T) * 4 * 8));
     top_counts_init(counts, T, i64(id_base), n_local, s);
     auto* bm = static_cast<u32*>(buf(12, size_t(T) * send_words * 4));
     void* scratch = buf(13, top_pack_scratch_bytes(n_local, T));
-    top_pack(tp, node, LL, pivots, last_axis, send, dim, send_stride, bm, send_words, counts, err, scratch, s);
+    top_pack(tp, node, LL, send, dim, send_stride, bm, send_words, counts, err, scratch, s);
     if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvPack), s));
     // 4. the count matrix, all-gathered: the one host read-back of the build (bounded wait)
     auto* all = static_cast<i64*>(buf(14, size_t(P) * T * 4 * 8));

@@ -144,9 +144,17 @@ __global__ __launch_bounds__(kBlock) void k_top_route_hist(TopPoints p, u32* __r
 
 // ---- median bucket per node ----------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_top_select(const u32* __restrict__ hist, int level, int bins,
-                                                       TopSizes sizes, u32* __restrict__ sel, u32* __restrict__ err) {
+                                                       TopSizes sizes, u32* __restrict__ sel, u32* __restrict__ err,
+                                                       u32* __restrict__ zero_hist, u32* __restrict__ zero_hdr) {
   __shared__ u32 part[kBlock];
   const int j = blockIdx.x;
+  // the next level's histogram (kTopBins words, one slice per block) and the staging header:
+  // zeroed here instead of by separate fill launches
+  if (zero_hist) {
+    const int per = kTopBins >> level;
+    for (int b = threadIdx.x; b < per; b += kBlock) zero_hist[j * per + b] = 0u;
+  }
+  if (zero_hdr && j == 0 && threadIdx.x < 4) zero_hdr[threadIdx.x] = 0u;
   const u32* hs = hist + size_t(j) * bins;
   const i64 size = sizes.n[j];
   const int per = (bins + kBlock - 1) / kBlock;
@@ -188,21 +196,41 @@ __global__ __launch_bounds__(kBlock) void k_top_select(const u32* __restrict__ h
   }
 }
 
-// ---- middle-bucket compaction --------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* __restrict__ node, int level,
-                                                        int axis, const float* __restrict__ cells, int bins,
-                                                        const u32* __restrict__ sel, float* __restrict__ buf,
-                                                        i64 cap) {
-  __shared__ BucketParams prm[kTopMaxNodes];
+// ---- middle-bucket compaction fused with the next level's routing and histogram ----------
+// Per point of a level-l node h: its bucket b on the level's axis against the node's median
+// bucket b*. b != b*: the side is already certain -> node[i] = child and (l + 1 < levels) the
+// point counts into the child's histogram of the next axis, bucketed over h's cell (so a
+// node's histogram is always bucketed over its PARENT's cell: the only cell known before the
+// parent's pivot; for dim >= 2 it equals the node's own cell on that axis). b == b*: the row
+// is staged for the exact pivot; top_fixup routes it once the pivot is known. One pass per
+// level instead of a collect pass plus a route+histogram pass.
+// Staged row: coordinates, id bits, node h, input row index (dim + 3 words).
+__global__ __launch_bounds__(kBlock) void k_top_collect_route(TopPoints p, u32* __restrict__ node, int level,
+                                                              int axis, int next_axis, const float* __restrict__ cells,
+                                                              int bins, int next_bins, const u32* __restrict__ sel,
+                                                              float* __restrict__ buf, i64 cap,
+                                                              u32* __restrict__ hist_next) {
+  extern __shared__ __align__(16) u32 nh[];  // next level's histogram (2 * nodes * next_bins words)
+  __shared__ BucketParams prm[kTopMaxNodes], nprm[kTopMaxNodes];
   __shared__ u32 bs[kTopMaxNodes];
   const int nodes = 1 << level;
   const u32 first = u32(nodes - 1);
-  load_params(prm, cells, int(first), nodes, p.dim, axis, bins);
+  const bool has_next = hist_next != nullptr;
+  const int nb_next = has_next ? 2 * nodes * next_bins : 0;
+  for (int b = threadIdx.x; b < nb_next; b += kBlock) nh[b] = 0;
+  // level-l bucket ranges: the parent's cell (see k_top_select's histograms: at level l >= 1
+  // they are built by the previous level's pass, which knows only the parent's cell)
+  for (int j = threadIdx.x; j < nodes; j += kBlock) {
+    const int hc = level == 0 ? 0 : (int(first) + j - 1) / 2;
+    const float* c = cells + (size_t(hc) * p.dim + axis) * 2;
+    prm[j] = make_params(c[0], c[1], bins);
+  }
+  if (has_next) load_params(nprm, cells, int(first), nodes, p.dim, next_axis, next_bins);
   for (int j = threadIdx.x; j < nodes; j += kBlock) bs[j] = sel[4 * j];
   __syncthreads();
   u32* count = reinterpret_cast<u32*>(buf);
   float* rows = buf + 4;
-  const int rs = p.dim + 2;
+  const int rs = p.dim + 3;
   // A block notes its median-bucket rows in LDS and reserves them with ONE global atomic at
   // the end: the count word is shared by every block of every XCD, and per-wave atomics on it
   // serialise at the memory side (~1 us each). Rows beyond the staging take the direct path.
@@ -212,12 +240,19 @@ __global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* 
   if (threadIdx.x == 0) scount = 0;
   __syncthreads();
   auto write_row = [&](i64 slot, i64 i, u32 h) {
-    if (slot >= cap) return;
+    if (slot >= cap) {
+      // the median bucket overflowed its staging slots: the pivot kernel flags it and the
+      // whole top-level pass is retried with larger slots; until then the row still gets a
+      // valid child, so every later kernel indexes in range
+      node[i] = 2 * h + 1;
+      return;
+    }
     float* o = rows + slot * rs;
     const float* r = p.pts + i * p.dim;
     for (int c = 0; c < p.dim; ++c) o[c] = r[c];
     o[p.dim] = __uint_as_float(point_id(p, i));
     o[p.dim + 1] = __uint_as_float(h);
+    o[p.dim + 2] = __uint_as_float(u32(i));
   };
   const i64 stride = i64(gridDim.x) * kBlock;
   // the trip count is uniform across the wave (ballots below need every lane); kU rows per
@@ -225,22 +260,29 @@ __global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* 
   constexpr int kU = 4;
   for (i64 base0 = i64(blockIdx.x) * kBlock; base0 < p.n; base0 += kU * stride) {
     u32 hn[kU];
-    float ka[kU];
+    float ka[kU], kn[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const i64 i = base0 + u * stride + threadIdx.x;
       const i64 ii = i < p.n ? i : 0;
       hn[u] = level > 0 ? node[ii] : 0u;
       ka[u] = p.pts[ii * p.dim + axis];
+      kn[u] = p.pts[ii * p.dim + next_axis];
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const i64 i = base0 + u * stride + threadIdx.x;
       bool take = false;
       const u32 h = hn[u];
-      if (i < p.n && h != kTopDone) {
+      if (i < p.n && h != kTopDone && h - first < u32(nodes)) {
         const u32 j = h - first;
-        take = bucket_of(ka[u], prm[j], bins) == bs[j];
+        const u32 b = bucket_of(ka[u], prm[j], bins), bst = bs[j];
+        take = b == bst;
+        if (!take) {
+          const u32 c = b < bst ? 0u : 1u;
+          node[i] = 2 * h + 1 + c;
+          if (has_next) atomicAdd(&nh[(2 * j + c) * next_bins + bucket_of(kn[u], nprm[j], next_bins)], 1u);
+        }
       }
       const u64 m = __ballot(take);
       if (!m) continue;
@@ -269,6 +311,37 @@ __global__ __launch_bounds__(kBlock) void k_top_collect(TopPoints p, const u32* 
     const i64 i = sidx[k];
     write_row(i64(sbase) + k, i, level > 0 ? node[i] : 0u);
   }
+  for (int b = threadIdx.x; b < nb_next; b += kBlock) {
+    const u32 v = nh[b];
+    if (v) atomicAdd(&hist_next[b], v);
+  }
+}
+
+// The staged (median-bucket) rows of this rank, once the level's pivots are known: route each
+// below its node's pivot (the pivot itself -> kTopDone) and count it into the next histogram.
+__global__ __launch_bounds__(kBlock) void k_top_fixup(const float* __restrict__ buf, i64 cap, int dim, int level,
+                                                      int axis, int next_axis, const u64* __restrict__ pivots,
+                                                      const float* __restrict__ cells, int next_bins,
+                                                      u32* __restrict__ node, u32* __restrict__ hist_next) {
+  const u32 cnt = min(u32(cap), reinterpret_cast<const u32*>(buf)[0]);
+  const float* rows = buf + 4;
+  const u32 first = u32((1 << level) - 1);
+  for (u32 k = blockIdx.x * kBlock + threadIdx.x; k < cnt; k += gridDim.x * kBlock) {
+    const float* r = rows + i64(k) * (dim + 3);
+    const u32 h = __float_as_uint(r[dim + 1]);
+    if (h - first >= u32(1 << level)) continue;  // never: staged rows carry their level's node
+    const u64 ck = composite_key(r[axis], __float_as_uint(r[dim]));
+    const u64 pv = pivots[h];
+    const u32 child = ck < pv ? 2 * h + 1 : (ck > pv ? 2 * h + 2 : kTopDone);
+    node[__float_as_uint(r[dim + 2])] = child;
+    if (hist_next != nullptr && child != kTopDone) {
+      const u32 j = h - first;
+      const float* c = cells + (size_t(h) * dim + next_axis) * 2;
+      const BucketParams np = make_params(c[0], c[1], next_bins);
+      atomicAdd(&hist_next[(child - 2 * first - 1) * next_bins + bucket_of(r[next_axis], np, next_bins)], 1u);
+      (void)j;
+    }
+  }
 }
 
 // ---- exact pivot per node (radix select over the gathered middles) ---------------------
@@ -278,7 +351,7 @@ struct MidView {
   i64 cap;
   int P, dim, axis;
   __device__ u32 count(int r) const { return min(u32(cap), reinterpret_cast<const u32*>(g + r * stride)[0]); }
-  __device__ const float* row(int r, u32 k) const { return g + r * stride + 4 + i64(k) * (dim + 2); }
+  __device__ const float* row(int r, u32 k) const { return g + r * stride + 4 + i64(k) * (dim + 3); }
   __device__ u64 key(const float* row) const {
     return composite_key(row[axis], __float_as_uint(row[dim]));
   }
@@ -412,19 +485,20 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
 // ---- counting sort by destination leaf (T <= 64 leaves) --------------------------------
 // Rows are grouped by top-level leaf; which rank receives a leaf in which exchange round is
 // the host planner's business (global_plan::make_plan), so the kernels never see ranks.
-__global__ __launch_bounds__(kBlock) void k_pack_count(TopPoints p, u32* __restrict__ node, int levels,
-                                                       const u64* __restrict__ pivots, int last_axis, int T,
+__global__ __launch_bounds__(kBlock) void k_pack_count(const u32* __restrict__ node, i64 n, int levels, int T,
                                                        i64 per_block, u32* __restrict__ bcount) {
   __shared__ u32 cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
+  const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(n, b0 + per_block);
   const u32 first = u32(T - 1);
   for (i64 i = b0 + threadIdx.x; i < b1; i += kBlock) {
-    // levels == 0 (one rank, no pipelining): every point stays at the root's single leaf
-    const u32 h = levels > 0 ? route(levels > 1 ? node[i] : 0u, p, i, last_axis, pivots) : 0u;
-    node[i] = h;
-    if (h != kTopDone) atomicAdd(&cnt[h - first], 1u);
+    // the top levels left every point at its leaf (or kTopDone for pivots); no top levels:
+    // every point is at the root's single leaf and `node` was never written
+    const u32 h = levels > 0 ? node[i] : 0u;
+    // out-of-range nodes (a bug) are dropped: the leaf totals then fail the plan's geometry
+    // check on every rank instead of indexing out of bounds here
+    if (h != kTopDone && h - first < u32(T)) atomicAdd(&cnt[h - first], 1u);
   }
   __syncthreads();
   if (threadIdx.x < T) bcount[i64(blockIdx.x) * T + threadIdx.x] = cnt[threadIdx.x];
@@ -476,10 +550,13 @@ __global__ __launch_bounds__(kScanThreads) void k_pack_scan(const u32* __restric
 }
 
 // cs == 0: rows of rs floats; cs > 0: SoA planes of stride cs (ids never travel in planes: the
-// planar exchange is always the compact one)
-__global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int T,
+// planar exchange is always the compact one). bm != nullptr: the leaf bitmaps of the compact
+// exchange come from the same ballots (a block's rows start on a multiple of 256, so wave w's
+// 64 rows of a chunk are exactly bitmap words 2 k and 2 k + 1 of every leaf).
+__global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int levels, int T,
                                                          i64 per_block, const u32* __restrict__ offsets,
-                                                         float* __restrict__ out, int rs, i64 cs) {
+                                                         float* __restrict__ out, int rs, i64 cs, u32* __restrict__ bm,
+                                                         i64 bm_words) {
   __shared__ u32 cur[64];
   __shared__ u32 wcnt[kBlock / 64][64];
   const u32 first = u32(T - 1);
@@ -490,13 +567,15 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   const int dim = p.dim;
   for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
     const i64 i = c0 + threadIdx.x;
-    const u32 h = i < b1 ? node[i] : kTopDone;
-    const int d = h == kTopDone ? -1 : int(h - first);
+    const u32 h = i < b1 ? (levels > 0 ? node[i] : 0u) : kTopDone;
+    const int d = (h == kTopDone || h - first >= u32(T)) ? -1 : int(h - first);
     u32 my = 0;
+    const i64 word = (c0 + 64 * w) / 32;  // this wave's first bitmap word
     for (int e = 0; e < T; ++e) {  // stable rank among same-destination points of the chunk
       const u64 m = __ballot(d == e);
       if (ln == 0) wcnt[w][e] = __popcll(m);
       if (d == e) my = mbcnt(m);
+      if (bm && ln < 2 && word + ln < bm_words) bm[i64(e) * bm_words + word + ln] = ln == 0 ? u32(m) : u32(m >> 32);
     }
     __syncthreads();
     if (d >= 0) {
@@ -530,24 +609,6 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
       cur[threadIdx.x] += add;
     }
     __syncthreads();
-  }
-}
-
-// Leaf bitmaps of the compact exchange: bm[d][w] bit j = row 32w + j goes to leaf d.
-// One wave per 64 rows (two words), one ballot per leaf; rows >= n give zero words, so the
-// grid covers the whole padded stride.
-__global__ __launch_bounds__(kBlock) void k_pack_bitmap(const u32* __restrict__ node, i64 n, int T, i64 ws,
-                                                        u32* __restrict__ bm) {
-  const i64 wave = (i64(blockIdx.x) * kBlock + threadIdx.x) / 64;
-  const int ln = dev::lane();
-  const i64 row = wave * 64 + ln;
-  const u32 first = u32(T - 1);
-  const u32 h = row < n ? node[row] : kTopDone;
-  const int d = h == kTopDone ? -1 : int(h - first);
-  for (int e = 0; e < T; ++e) {
-    const u64 m = __ballot(d == e);
-    const i64 w = 2 * wave + (ln & 1);
-    if (ln < 2 && w < ws) bm[i64(e) * ws + w] = ln == 0 ? u32(m) : u32(m >> 32);
   }
 }
 
@@ -624,10 +685,6 @@ __global__ __launch_bounds__(kBlock) void k_bm_ids(const u32* __restrict__ bm, i
   if (b == last && threadIdx.x == kBlock - 1 && i64(k) != cap) atomicOr(err, 8u);
 }
 
-__global__ void k_zero4(u32* __restrict__ p) {
-  if (threadIdx.x < 4) p[threadIdx.x] = 0u;
-}
-
 // pattern fill of 64-bit words; words j with (j % period) == slot get `alt` instead (the count
 // matrix's id-base / n_local columns)
 __global__ void k_fill64(u64* __restrict__ p, i64 n, u64 v, int period, int slot_a, u64 alt_a, int slot_b,
@@ -682,20 +739,33 @@ void top_route_hist(const TopPoints& p, u32* node, int level, const u64* pivots,
   PKD_LAUNCH_CHECK();
 }
 
-void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err,
-                hipStream_t stream) {
-  k_top_select<<<1 << level, kBlock, 0, stream>>>(hist, level, bins, sizes, sel, err);
+void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err, u32* zero_hist,
+                u32* zero_hdr, hipStream_t stream) {
+  k_top_select<<<1 << level, kBlock, 0, stream>>>(hist, level, bins, sizes, sel, err, zero_hist, zero_hdr);
   PKD_LAUNCH_CHECK();
 }
 
-size_t top_middle_words(int dim, i64 cap) { return 4 + size_t(cap) * size_t(dim + 2); }
+size_t top_middle_words(int dim, i64 cap) { return 4 + size_t(cap) * size_t(dim + 3); }
 
-void top_collect(const TopPoints& p, const u32* node, int level, int axis, const float* cells, int bins,
-                 const u32* sel, float* buf, i64 cap, hipStream_t stream) {
-  k_zero4<<<1, 64, 0, stream>>>(reinterpret_cast<u32*>(buf));  // the 16-B header (a graph-capturable node)
-  PKD_LAUNCH_CHECK();
+void top_collect_route(const TopPoints& p, u32* node, int level, int axis, int next_axis, const float* cells,
+                       int bins, int next_bins, const u32* sel, float* buf, i64 cap, u32* hist_next,
+                       hipStream_t stream) {
+  if ((1 << level) > kTopMaxNodes) throw std::invalid_argument("top_collect_route: too many nodes");
+  if (hist_next && 2 * (1 << level) * next_bins > kTopBins)
+    throw std::invalid_argument("top_collect_route: next level's nodes * bins exceeds 8192");
   if (p.n <= 0) return;
-  k_top_collect<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, cells, bins, sel, buf, cap);
+  const size_t lds = hist_next ? size_t(2) * (1 << level) * next_bins * 4 : 0;
+  k_top_collect_route<<<stream_grid(p.n), kBlock, lds, stream>>>(p, node, level, axis, next_axis, cells, bins,
+                                                                  next_bins, sel, buf, cap, hist_next);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_fixup(const float* buf, i64 cap, int dim, int level, int axis, int next_axis, const u64* pivots,
+               const float* cells, int next_bins, u32* node, u32* hist_next, hipStream_t stream) {
+  // the staged rows: at most cap, usually a few thousand; one small grid
+  const int grid = int(std::max<i64>(1, std::min<i64>(256, (cap + kBlock - 1) / kBlock)));
+  k_top_fixup<<<grid, kBlock, 0, stream>>>(buf, cap, dim, level, axis, next_axis, pivots, cells, next_bins, node,
+                                           hist_next);
   PKD_LAUNCH_CHECK();
 }
 
@@ -710,9 +780,8 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
 
 size_t top_pack_scratch_bytes(i64 n, int T) { return size_t(2) * pack_blocks(n) * size_t(T) * 4; }
 
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, float* out,
-              int row_stride, i64 col_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
-              void* scratch, hipStream_t stream) {
+void top_pack(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
+              u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch, hipStream_t stream) {
   if (levels < 0 || levels > 6) throw std::invalid_argument("top_pack: at most 6 top levels (64 leaves)");
   const int T = 1 << levels;
   if (col_stride > 0 && (col_stride < p.n || p.ids != nullptr))
@@ -721,21 +790,18 @@ void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int 
     throw std::invalid_argument("top_pack: row stride dim or dim+1");
   if (bitmaps && bitmap_words * 32 < p.n) throw std::invalid_argument("top_pack: bitmap stride too small");
   const int blocks = pack_blocks(p.n);
-  const i64 per_block = (std::max<i64>(p.n, 1) + blocks - 1) / blocks;
+  // rows per block a multiple of 256: every wave's 64 rows of a chunk are two whole bitmap words
+  const i64 per_block = ((std::max<i64>(p.n, 1) + blocks - 1) / blocks + 255) / 256 * 256;
   u32* bcount = static_cast<u32*>(scratch);
   u32* offsets = bcount + size_t(blocks) * T;
-  k_pack_count<<<blocks, kBlock, 0, stream>>>(p, node, levels, pivots, last_axis, T, per_block, bcount);
+  k_pack_count<<<blocks, kBlock, 0, stream>>>(node, p.n, levels, T, per_block, bcount);
   PKD_LAUNCH_CHECK();
   static_assert(2 * kScanThreads >= 2048, "k_pack_scan covers at most 2 * kScanThreads blocks");
   k_pack_scan<<<T, kScanThreads, 0, stream>>>(bcount, blocks, T, offsets, counts, err);
   PKD_LAUNCH_CHECK();
-  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, T, per_block, offsets, out, row_stride, col_stride);
+  k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, levels, T, per_block, offsets, out, row_stride, col_stride,
+                                                bitmaps, bitmap_words);
   PKD_LAUNCH_CHECK();
-  if (bitmaps) {
-    const i64 waves = (bitmap_words + 1) / 2;
-    k_pack_bitmap<<<int((waves * 64 + kBlock - 1) / kBlock), kBlock, 0, stream>>>(node, p.n, T, bitmap_words, bitmaps);
-    PKD_LAUNCH_CHECK();
-  }
 }
 
 namespace {

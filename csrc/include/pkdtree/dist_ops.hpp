@@ -59,14 +59,25 @@ void top_route_hist(const TopPoints& p, u32* node, int level, const u64* pivots,
 
 // Per node of the level: the bucket b* holding the element of rank size/2 and the counts
 // below / inside it. sel[j] = {b*, count_less, count_mid, 0}. err |= 2 on inconsistent sums.
-void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err,
-                hipStream_t stream);
+// Also zeroes zero_hist (the next level's histogram, kTopBins words; may be null) and the
+// 16-B header of the level's staging buffer (may be null).
+void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32* sel, u32* err, u32* zero_hist,
+                u32* zero_hdr, hipStream_t stream);
 
-// Middle-bucket compaction: buf = [4 header words: count, 0, 0, 0][cap][dim + 2] floats
-// (coordinates, id bits, node); count may exceed cap (the pivot kernel flags it).
+// Median-bucket staging fused with the next level's routing and histogram (one pass per top
+// level): points outside their node's median bucket go to their child now (node[i]) and count
+// into hist_next (nullptr at the last top level); points inside it are staged in buf =
+// [4 header words: count, 0, 0, 0][cap][dim + 3] floats (coordinates, id bits, node, input
+// row); count may exceed cap (the pivot kernel flags it). A node's histogram is bucketed over
+// its parent's cell (the root's own at level 0), which top_route_hist at level 0 matches.
 size_t top_middle_words(int dim, i64 cap);
-void top_collect(const TopPoints& p, const u32* node, int level, int axis, const float* cells, int bins,
-                 const u32* sel, float* buf, i64 cap, hipStream_t stream);
+void top_collect_route(const TopPoints& p, u32* node, int level, int axis, int next_axis, const float* cells,
+                       int bins, int next_bins, const u32* sel, float* buf, i64 cap, u32* hist_next,
+                       hipStream_t stream);
+// After the level's pivots: routes this rank's staged rows (buf from top_collect_route) below
+// their node's pivot and counts them into hist_next (may be null).
+void top_fixup(const float* buf, i64 cap, int dim, int level, int axis, int next_axis, const u64* pivots,
+               const float* cells, int next_bins, u32* node, u32* hist_next, hipStream_t stream);
 
 // Exact pivots of one level from the all-gathered middle buffers (P consecutive buffers of
 // top_middle_words(dim, cap) words): per node, the element of rank size/2 - count_less among
@@ -75,20 +86,20 @@ void top_collect(const TopPoints& p, const u32* node, int level, int axis, const
 void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream);
 
-// Final routing below the last top level + counting sort of rows by destination leaf
-// (dest = node - (T - 1), T = 2^levels leaves <= 64). Output grouped by leaf (stable):
+// Counting sort of rows by top-level leaf (dest = node - (T - 1), T = 2^levels leaves <= 64;
+// node[] as the top levels left it, kTopDone rows -- the pivots -- dropped; levels == 0: every
+// row at leaf 0 and node[] unread). Output grouped by leaf (stable):
 //   * col_stride == 0: rows out[k][row_stride], row_stride = dim + 1 (coordinates, id bits) or
 //     dim (compact: coordinates only);
 //   * col_stride  > 0: SoA planes, coordinate c of output row k at out[c * col_stride + k]
 //     (the receiver's builder takes columns directly, no AoS -> SoA pass).
-// counts [T][4] int64 = (rows for leaf, err word, 2 words left to the caller). Pivot points are
-// dropped. With `bitmaps` ([T][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the leaf of
-// every row is also written as one bit per (leaf, row): the compact exchange sends the
+// counts [T][4] int64 = (rows for leaf, err word, 2 words left to the caller). With `bitmaps`
+// ([T][bitmap_words] u32, bitmap_words >= ceil(n / 32)) the leaf of every row is also written
+// as one bit per (leaf, row) -- from the scatter's own ballots: the compact exchange sends the
 // coordinates plus n / 8 bytes per leaf instead of ids, and the receiver rebuilds the ids.
 size_t top_pack_scratch_bytes(i64 n, int T);
-void top_pack(const TopPoints& p, u32* node, int levels, const u64* pivots, int last_axis, float* out,
-              int row_stride, i64 col_stride, u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err,
-              void* scratch, hipStream_t stream);
+void top_pack(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
+              u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch, hipStream_t stream);
 
 // Copies top-tree rows (dim + 1 floats: coordinates, id bits; heap order) into output slots:
 // out_pts[slot[i]] / out_ids[slot[i]] = top_rows[heap[i]] for i < count (<= 64).

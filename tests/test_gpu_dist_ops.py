@@ -26,10 +26,19 @@ def _pivots(x, n, dim, levels, seed):
 
 
 def _cells(nodes_total, dim, seed):
+    """Random cells [h][dim][2] shaped like the builder's: a child's cell is its parent's except
+    on the parent's split axis (so a node's histogram may be bucketed over its parent's cell)."""
     rng = np.random.default_rng(seed)
-    lo = rng.uniform(-120, -20, size=(nodes_total, dim)).astype(np.float32)
-    hi = rng.uniform(20, 120, size=(nodes_total, dim)).astype(np.float32)
-    return np.stack([lo, hi], -1).astype(np.float32)  # [h][dim][2]
+    c = np.zeros((nodes_total, dim, 2), dtype=np.float32)
+    c[0, :, 0] = rng.uniform(-120, -20, size=dim)
+    c[0, :, 1] = rng.uniform(20, 120, size=dim)
+    for h in range(1, nodes_total):
+        p = (h - 1) // 2
+        a = ((p + 1).bit_length() - 1) % dim
+        c[h] = c[p]
+        c[h, a, 0] = rng.uniform(-120, -20)
+        c[h, a, 1] = rng.uniform(20, 120)
+    return c
 
 
 def test_bbox(gpu_device):
@@ -85,17 +94,25 @@ def test_route_hist_select_collect_pivot(gpu_device, level, dim):
         b = int(np.searchsorted(cum, sizes[j] // 2, side="right"))
         assert s[j, 0] == b and s[j, 1] == (cum[b - 1] if b else 0) and s[j, 2] == hh[j, b]
     assert int(err[0]) == 0
-    # collect + pivot (one rank: the gathered buffer is the local one)
-    axis = level % dim
+    # fused collect + route + next histogram, pivot, fix-up (one rank: the gathered buffer is the
+    # local one); select zeroes the next histogram and the staging header
+    axis, next_axis = level % dim, (level + 1) % dim
+    next_bins = 8192 // (2 * nl)
     cap = 8192
     words = nat.top_middle_words(dim, cap)
-    buf = torch.empty(words, dtype=torch.float32, device=gpu_device)
-    nat.top_collect(xg, None, 1, node_g, level, axis, cells_g, bins, sel, buf, cap)
+    buf = torch.full((words,), 7.0, dtype=torch.float32, device=gpu_device)
+    hn = torch.full((8192,), 5, dtype=torch.int32, device=gpu_device)
+    nat.top_select(hg, level, bins, sizes, sel, err, hn, buf)
+    node_f = node_g.clone()
+    nat.top_collect_route(xg, None, 1, node_f, level, axis, next_axis, cells_g, bins, next_bins, sel, buf, cap, hn)
+    staged = int(buf[:1].view(torch.int32).item())
+    assert staged == int(sel.cpu().view(32, 4)[:nl, 2].sum()), "staged rows differ from the median buckets' counts"
     pivots = torch.full((2 * nl,), -1, dtype=torch.int64, device=gpu_device)
     top_rows = torch.zeros((2 * nl, dim + 1), dtype=torch.float32, device=gpu_device)
     cg = cells_g.clone()
     nat.top_pivot(buf, 1, cap, level, axis, dim, sizes, sel, pivots, top_rows, cg, err)
     assert int(err[0]) == 0
+    nat.top_fixup(buf, cap, dim, level, axis, next_axis, pivots, cg, next_bins, node_f, hn)
     pv = pivots.cpu().numpy().view(np.uint64)
     ids = np.arange(1, n + 1, dtype=np.uint32)
     nodes_np = node_c.numpy()
@@ -112,6 +129,13 @@ def test_route_hist_select_collect_pivot(gpu_device, level, dim):
         assert torch.equal(tr[:dim], x[i]) and int(tr[dim].view(torch.int32)) == i + 1
         c = cg.cpu().view(-1, dim, 2)
         assert float(c[2 * h + 1, axis, 1]) == float(x[i, axis]) and float(c[2 * h + 2, axis, 0]) == float(x[i, axis])
+    # every point routed below its pivot, and the next level's histogram, as the host path does it
+    nl2 = 2 * nl
+    params2 = np.stack([np.array(make_params(cells[nl2 - 1 + j, next_axis, 0], cells[nl2 - 1 + j, next_axis, 1],
+                                             next_bins)) for j in range(nl2)]).astype(np.float32)
+    hc2 = _HostOps.route_hist(rows, dim, node_c, level + 1, pv, axis, next_axis, params2, next_bins)
+    assert torch.equal(node_c.to(torch.int32), node_f.cpu()), "fused routing differs from the host routing"
+    assert torch.equal(hc2, hn.cpu()[: nl2 * next_bins]), "fused next-level histogram differs"
 
 
 @pytest.mark.parametrize("P,dim", [(2, 3), (4, 3), (8, 3), (8, 5)])
@@ -134,13 +158,15 @@ def test_pack_matches_host(gpu_device, P, dim):
         hg = torch.zeros(8192, dtype=torch.int32, device=gpu_device)
         nat.top_route_hist(xg, None, 1, node_g, l, piv_g, (l - 1) % dim, l % dim, cells_g, 8192 // nl, hg)
     sc, cc = _HostOps.pack(rows, dim, node_c, L, piv, (L - 1) % dim)
+    # top_pack takes the nodes as the (fused) top levels leave them: routed to the leaves
+    node_g = node_c.to(torch.int32).to(gpu_device)
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
     counts = torch.empty(4 * P, dtype=torch.int64, device=gpu_device)
     err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, P), dtype=torch.uint8, device=gpu_device)
     node_keep = node_g.clone()
     node_keep2 = node_g.clone()
-    nat.top_pack(xg, None, 1, node_g, L, piv_g, (L - 1) % dim, out, 0, None, counts, err, scratch)
+    nat.top_pack(xg, None, 1, node_g, L, out, 0, None, counts, err, scratch)
     cg = counts.cpu().view(P, 4)
     assert torch.equal(cc, cg[:, 0]) and int(cg[:, 1].abs().sum()) == 0
     k = int(cc.sum())
@@ -149,15 +175,15 @@ def test_pack_matches_host(gpu_device, P, dim):
     # planar output (SoA planes of a padded stride): the same rows, column by column
     stride = n + 61
     planes = torch.full((dim * stride,), -7.0, dtype=torch.float32, device=gpu_device)
-    nat.top_pack(xg, None, 1, node_keep2, L, piv_g, (L - 1) % dim, planes, stride, None, counts, err, scratch)
+    nat.top_pack(xg, None, 1, node_keep2, L, planes, stride, None, counts, err, scratch)
     pl = planes.cpu().view(dim, stride)
     assert torch.equal(pl[:, :k].t().contiguous(), sc[:, :dim])
 
     # compact exchange: coordinates only + destination bitmaps; ids rebuilt on the receiver side
-    words = (n + 31) // 32 + 3  # any stride >= n / 32
+    words = (n + 31) // 32
     bm = torch.full((P, words), -1, dtype=torch.int32, device=gpu_device)
     outc = torch.empty((n, dim), dtype=torch.float32, device=gpu_device)
-    nat.top_pack(xg, None, 1, node_keep, L, piv_g, (L - 1) % dim, outc, 0, bm, counts, err, scratch)
+    nat.top_pack(xg, None, 1, node_keep, L, outc, 0, bm, counts, err, scratch)
     assert torch.equal(outc[:k].cpu(), sc[:, :dim])
     dest = node_keep.cpu().to(torch.int64) - (P - 1)
     bits = ((bm.cpu().to(torch.int64) & 0xFFFFFFFF)[:, :, None] >> torch.arange(32)) & 1
@@ -180,7 +206,8 @@ def test_pack_matches_host(gpu_device, P, dim):
 
 
 def test_explicit_ids(gpu_device):
-    """Explicit id arrays route ties by id exactly like implicit ones."""
+    """Explicit id arrays route ties by id exactly like implicit ones (level 0 of the fused top
+    levels: histogram, select, staging, pivot, fix-up), and the pack counts the two leaves."""
     n, dim = 20_000, 2
     g = torch.Generator().manual_seed(5)
     x = torch.randint(0, 4, (n, dim), generator=g).float()  # massive ties
@@ -191,14 +218,28 @@ def test_explicit_ids(gpu_device):
     node_c = torch.zeros(n, dtype=torch.int64)
     _HostOps.pack(rows, dim, node_c, 1, piv, 0)
     nat = ops.native()
+    xg, ig = x.to(gpu_device), ids.to(gpu_device)
     node_g = torch.zeros(n, dtype=torch.int32, device=gpu_device)
+    cells = torch.tensor([-1.0, 5.0, -1.0, 5.0] * 3, dtype=torch.float32, device=gpu_device)
+    hist = torch.zeros(8192, dtype=torch.int32, device=gpu_device)
+    nat.top_route_hist(xg, ig, 0, node_g, 0, torch.zeros(1, dtype=torch.int64, device=gpu_device), 0, 0, cells, 8192,
+                       hist)
+    sel = torch.zeros(128, dtype=torch.int32, device=gpu_device)
+    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
+    cap = n
+    buf = torch.empty(nat.top_middle_words(dim, cap), dtype=torch.float32, device=gpu_device)
+    nat.top_select(hist, 0, 8192, [n], sel, err, None, buf)
+    nat.top_collect_route(xg, ig, 0, node_g, 0, 0, 1, cells, 8192, 4096, sel, buf, cap, None)
+    pivots = torch.full((2,), -1, dtype=torch.int64, device=gpu_device)
+    top_rows = torch.zeros((2, dim + 1), dtype=torch.float32, device=gpu_device)
+    nat.top_pivot(buf, 1, cap, 0, 0, dim, [n], sel, pivots, top_rows, cells, err)
+    nat.top_fixup(buf, cap, dim, 0, 0, 1, pivots, cells, 4096, node_g, None)
+    assert int(err[0]) == 0 and int(pivots[0]) == int(piv.view(np.int64)[0])
+    assert torch.equal(node_c.to(torch.int32), node_g.cpu())
     out = torch.empty((n, dim + 1), dtype=torch.float32, device=gpu_device)
     counts = torch.empty(8, dtype=torch.int64, device=gpu_device)
-    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
     scratch = torch.empty(nat.top_pack_scratch_bytes(n, 2), dtype=torch.uint8, device=gpu_device)
-    nat.top_pack(x.to(gpu_device), ids.to(gpu_device), 0, node_g, 1,
-                 torch.from_numpy(piv.view(np.int64).copy()).to(gpu_device), 0, out, 0, None, counts, err, scratch)
-    assert torch.equal(node_c.to(torch.int32), node_g.cpu())
+    nat.top_pack(xg, ig, 0, node_g, 1, out, 0, None, counts, err, scratch)
     assert counts.cpu()[0::4].tolist() == [n // 2, n - n // 2 - 1]
 
 
