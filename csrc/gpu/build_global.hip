@@ -43,6 +43,7 @@ constexpr int kRefineCap = 2048;            // middle zone handled in LDS by one
 constexpr int kRadixBits = 11;
 constexpr i64 kLevelBlocks = 2048;          // partition-type grids of the top levels (large builds)
 constexpr int kPairBins = 2048;             // bins of a level whose histogram a paired pass fuses (4 children)
+constexpr int kTripleBins = 1024;           // bins of a level whose histogram a triple's scatter fuses (8 children)
 constexpr int kRadixBins = 1 << kRadixBits;
 
 struct SegState {
@@ -1703,13 +1704,18 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // PFX: prefix placement (pa.bbase): rows of certain zones are written from per-block
 // offsets; rows in a child's median bucket (their zone is decided by the second stage)
 // form 6 more pseudo-zones placed with cursor atomics.
-template <int NCOL, int KI, bool PFX = false>
+template <int NCOL, int KI, bool PFX = false, bool ATOM = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   constexpr int NZ = PFX ? 12 : 6;
+  constexpr int W = kBlock / 64;
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2]
   __shared__ u32 gcnt[NZ][64];
+  // ATOM: zone ranks from one LDS atomic per row on its wave's zone counter (see k_partition3)
+  __shared__ u32 wcnt[ATOM ? W : 1][16];
+  __shared__ u32 wbase[ATOM ? W : 1][16];
+  if (ATOM && threadIdx.x < W * 16) (&wcnt[0][0])[threadIdx.x] = 0;
   __shared__ u32 bcur[6];
   __shared__ unsigned long long bmin[2], bmax[2];  // children's middle-zone key ranges, flushed once
   if (threadIdx.x < 2) {
@@ -1865,14 +1871,18 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       bool unc;
       const u32 q = classify(k0, k1, __float_as_uint(row[i][D]), vld[i], unc);
       const u32 zi = q >= 6 ? 15u : (PFX && unc ? q + 6 : q);
-      u32 my = 0;
+      if constexpr (ATOM) {
+        zone_pre[i] = (zi << 16) | atomicAdd(&wcnt[w][zi], 1u);
+      } else {
+        u32 my = 0;
 #pragma unroll
-      for (int z = 0; z < NZ; ++z) {
-        const u64 m = __ballot(zi == u32(z));
-        if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
-        if (zi == u32(z)) my = mbcnt(m);
+        for (int z = 0; z < NZ; ++z) {
+          const u64 m = __ballot(zi == u32(z));
+          if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
+          if (zi == u32(z)) my = mbcnt(m);
+        }
+        zone_pre[i] = (zi << 16) | my;
       }
-      zone_pre[i] = (zi << 16) | my;
       if (fuse && q < 6 && q != 1 && q != 4) {
         const u32 g = (q / 3) * 2 + (q % 3 == 2 ? 1u : 0u);
         atomicAdd(&nh[g * nb2 + bucket_of(k2, sgp[g], nb2)], 1u);
@@ -1884,6 +1894,33 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       }
     }
     __syncthreads();
+    if constexpr (ATOM) {
+      if (threadIdx.x < NZ) {  // thread z: zone z's waves, scanned and reserved at once
+        const int z = int(threadIdx.x);
+        u32 c[W], tot = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          c[k] = wcnt[k][z];
+          tot += c[k];
+        }
+        u32 base = 0;
+        if (PFX && z >= 6) {
+          base = tot ? atomicAdd(&(z < 9 ? cst0 : cst1)->cur[(z - 6) % 3], tot) : 0u;
+        } else if (PFX || a.block_reserve) {
+          base = bcur[z];
+          bcur[z] = base + tot;
+        } else {
+          base = tot ? atomicAdd(&(z < 3 ? cst0 : cst1)->cur[z % 3], tot) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          wbase[k][z] = base;
+          base += c[k];
+          wcnt[k][z] = 0;
+        }
+      }
+      if (threadIdx.x >= NZ && threadIdx.x < NZ + W) wcnt[threadIdx.x - NZ][15] = 0;
+    } else
     for (int z = w; z < NZ; z += kBlock / 64) {  // wave w scans zones w, w+4 (, w+8)
       const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
       const u32 incl = dev::wave_incl_scan(v);
@@ -1908,7 +1945,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       i64 dest = -1;
       if (zi < u32(NZ)) {
         const u32 c = (zi % 6) / 3;
-        const u32 off = gcnt[zi][i * 4 + w] + (zone_pre[i] & 0xffffu);
+        const u32 off = (ATOM ? wbase[w][zi] : gcnt[zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
         const i64 cn = c == 0 ? n / 2 : n - n / 2 - 1;
         if (i64(off) >= cn) {
           atomicOr(a.err, 1u);
@@ -1930,6 +1967,415 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   if (fuse) {
     u32* hn = pa.hist2n + (4 * s) * nb2;
     for (int b = threadIdx.x; b < 4 * nb2; b += kBlock) {
+      const u32 v = nh[b];
+      if (v) atomicAdd(&hn[b], v);
+    }
+  }
+}
+
+// =====================================================================================
+// Triple global levels: levels l, l+1 and l+2 are moved by ONE scatter pass.
+//   k_scan       as for a pair: level l's median bucket staged, level l+1's histograms;
+//   k_pivot*     level l's exact pivot;  k_select  level l+1;
+//   k_scan2      keys of l, l+1, l+2 (12 B / row): every row is routed to its child by level
+//                l's exact pivot; rows of the child's median bucket of level l+1 are staged in
+//                the child's middle-zone area of dst (scratch), every other row adds its
+//                level-(l+2) key to its grandchild's histogram (fused, LDS);
+//   k_pivot*     level l+1's exact pivots (the staged rows; their level-(l+2) keys complete the
+//                grandchildren's histograms);  k_select  level l+2;
+//   k_partition3 one read + one write of every row: grandchild (exact pivots of l and l+1) and
+//                zone inside it (level l+2's median bucket) give 12 destination zones; the
+//                level-(l+3) histograms of the 8 great-grandchildren are fused in;
+//   k_refine*    level l+2's middle zones.
+// Traffic per three levels: 8 + 12 + 32 B / row instead of 1.5 pairs' 60 B.
+struct TripleArgs {
+  int bins1;    // level l+1 bins
+  int axis2;    // level l+2 axis
+  int bins2;    // level l+2 bins
+  u32* hist2;   // level l+2 histograms [4 * segs][bins2] (k_scan2)
+  int axis3;    // level l+3 axis
+  int bins3;    // level l+3 bins (0: l+3 is the subtree level)
+  u32* hist3;   // level l+3 histograms [8 * segs][bins3] (k_partition3)
+};
+
+template <int NCOL>
+__global__ __launch_bounds__(kBlock) void k_scan2(LevelArgs a, TripleArgs ta) {
+  extern __shared__ __align__(16) u32 nh[];  // [4 * bins2] + 64 per-lane dummy words
+  constexpr int D = NCOL - 1;
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const int nb = ta.bins2;
+  for (int b = threadIdx.x; b < 4 * nb + 64; b += kBlock) nh[b] = 0;
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
+  const SegState* st = a.state + h;
+  const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
+  const u64 pivot = st->pivot;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const BucketParams prm = a.params[h];
+  SegState* const cst0 = a.state + 2 * h + 1;
+  SegState* const cst1 = a.state + 2 * h + 2;
+  const BucketParams cp0 = a.params[2 * h + 1], cp1 = a.params[2 * h + 2];
+  const u32 cb0 = cst0->bstar, cb1 = cst1->bstar;
+  const i64 clo0 = a.seg_lo[2 * h + 1], clo1 = a.seg_lo[2 * h + 2];
+  const i64 cn0 = a.seg_n[2 * h + 1], cn1 = a.seg_n[2 * h + 2];
+  __shared__ BucketParams gp[4];  // grandchildren's level-(l+2) bucketing
+  constexpr int kStage = 512;
+  __shared__ u32 sidx[2][kStage];
+  __shared__ u32 mcnt[2], mbase[2];
+  __shared__ unsigned long long bmin[2], bmax[2];
+  if (threadIdx.x < 4) gp[threadIdx.x] = a.params[2 * (2 * h + 1 + threadIdx.x / 2) + 1 + (threadIdx.x & 1)];
+  if (threadIdx.x < 2) {
+    mcnt[threadIdx.x] = 0;
+    bmin[threadIdx.x] = ~0ull;
+    bmax[threadIdx.x] = 0ull;
+  }
+  __syncthreads();
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  const i64 nc = a.ncol;
+  const int ln = dev::lane();
+  const u32 hdummy = u32(4 * nb) + u32(ln);
+  // One row (all lanes of a wave together: ballots): child by level l's exact pivot; the
+  // child's median bucket of level l+1 -> staged, else the grandchild's level-(l+2) histogram.
+  auto visit = [&](float k0, float k1, float k2, i64 e, bool valid) {
+    const u32 z = valid ? zone_of(k0, prm, a.bins, bstar, stage2, p2, sbstar) : 3u;
+    bool live = valid;
+    u32 c = z == 0 ? 0u : 1u;
+    if (z == 1) {
+      const u64 ck = composite_key(k0, src_id(a, lo + e));
+      live = ck != pivot;  // level l's median: already written out
+      c = ck < pivot ? 0u : 1u;
+    }
+    const u32 b1 = bucket_of(k1, c == 0 ? cp0 : cp1, ta.bins1), cb = c == 0 ? cb0 : cb1;
+    const bool mid = live && b1 == cb;
+    const u32 g = 2 * c + (b1 > cb ? 1u : 0u);
+    atomicAdd(&nh[(live && !mid) ? g * u32(nb) + bucket_of(k2, gp[g], nb) : hdummy], 1u);
+    if (__ballot(mid)) {  // rare: note the child's median-bucket rows (per child list)
+#pragma unroll
+      for (u32 cc = 0; cc < 2; ++cc) {
+        const bool me = mid && c == cc;
+        const u64 m = __ballot(me);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        u32 base = 0;
+        if (ln == leader) base = atomicAdd(&mcnt[cc], u32(__popcll(m)));
+        base = __shfl(base, leader, 64);
+        const u32 slot = base + mbcnt(m);
+        const bool direct = me && slot >= u32(kStage);
+        if (me && !direct) sidx[cc][slot] = u32(e - b0);
+        if (__ballot(direct)) {  // staging list full: reserve and copy directly
+          u64 ck = 0;
+          if (direct) {
+            const u32 q = atomicAdd(&(cc == 0 ? cst0 : cst1)->cur[1], 1u);
+            if (i64(q) >= (cc == 0 ? cn0 : cn1)) {
+              atomicOr(a.err, 1u);
+            } else {
+#pragma unroll
+              for (int col = 0; col < NCOL; ++col) dst[i64(col) * nc + (cc == 0 ? clo0 : clo1) + q] = src_col(a, col, lo + e);
+            }
+            ck = composite_key(k1, src_id(a, lo + e));
+          }
+          wave_minmax_atomic(direct, ck, &bmin[cc], &bmax[cc]);
+        }
+      }
+    }
+  };
+  const i64 abs0 = lo + b0, abs1 = lo + b1;
+  const i64 A = min(abs1, (abs0 + 3) & ~i64(3));
+  const i64 nv = (abs1 - A) >> 2;
+  const i64 Bend = A + 4 * nv;
+  const float* kc = src + i64(a.axis) * nc;
+  const float* k1c = src + i64(a.next_axis) * nc;
+  const float* k2c = src + i64(ta.axis2) * nc;
+  {
+    const int t = int(threadIdx.x);
+    const bool head = t < 3 && abs0 + t < A, tail = t >= 3 && t < 6 && Bend + (t - 3) < abs1;
+    const i64 p = head ? abs0 + t : (tail ? Bend + (t - 3) : lo);
+    const bool v = head | tail;
+    visit(v ? kc[p] : 0.0f, v ? k1c[p] : 0.0f, v ? k2c[p] : 0.0f, p - lo, v);
+  }
+  const float4* k04 = reinterpret_cast<const float4*>(kc + A);
+  const float4* k14 = reinterpret_cast<const float4*>(k1c + A);
+  const float4* k24 = reinterpret_cast<const float4*>(k2c + A);
+  constexpr int U4 = 2;
+  for (i64 v0 = 0; v0 < nv; v0 += kBlock * U4) {
+    float4 x0[U4], x1[U4], x2[U4];
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = v0 + i64(u) * kBlock + threadIdx.x;
+      const i64 vi = v < nv ? v : 0;
+      x0[u] = k04[vi];
+      x1[u] = k14[vi];
+      x2[u] = k24[vi];
+    }
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const i64 v = v0 + i64(u) * kBlock + threadIdx.x;
+      const bool in = v < nv;
+      const i64 e = A - lo + 4 * v;
+      visit(x0[u].x, x1[u].x, x2[u].x, e, in);
+      visit(x0[u].y, x1[u].y, x2[u].y, e + 1, in);
+      visit(x0[u].z, x1[u].z, x2[u].z, e + 2, in);
+      visit(x0[u].w, x1[u].w, x2[u].w, e + 3, in);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const u32 staged = min(mcnt[threadIdx.x], u32(kStage));
+    mbase[threadIdx.x] = staged ? atomicAdd(&(threadIdx.x == 0 ? cst0 : cst1)->cur[1], staged) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (u32 cc = 0; cc < 2; ++cc) {
+    const u32 staged = min(mcnt[cc], u32(kStage));
+    const i64 clo = cc == 0 ? clo0 : clo1, cn = cc == 0 ? cn0 : cn1;
+    for (u32 r0 = 0; r0 < staged; r0 += kBlock) {  // uniform trip count: every lane reaches the wave ops
+      const u32 k2 = r0 + threadIdx.x;
+      const bool act = k2 < staged;
+      const i64 q = i64(mbase[cc]) + k2;
+      u64 ck = 0;
+      if (act) {
+        const i64 e = b0 + sidx[cc][k2];
+        float row[NCOL];
+#pragma unroll
+        for (int col = 0; col < NCOL; ++col) row[col] = src_col(a, col, lo + e);
+        if (q >= cn) {
+          atomicOr(a.err, 1u);
+        } else {
+#pragma unroll
+          for (int col = 0; col < NCOL; ++col) dst[i64(col) * nc + clo + q] = row[col];
+        }
+        float key = row[0];
+#pragma unroll
+        for (int col = 1; col < D; ++col) key = col == a.next_axis ? row[col] : key;
+        ck = composite_key(key, __float_as_uint(row[D]));
+      }
+      wave_minmax_atomic(act, ck, &bmin[cc], &bmax[cc]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && bmin[threadIdx.x] != ~0ull) {
+    SegState* cs = threadIdx.x == 0 ? cst0 : cst1;
+    atomicMin(&cs->mid_min, bmin[threadIdx.x]);
+    atomicMax(&cs->mid_max, bmax[threadIdx.x]);
+  }
+  u32* hn = ta.hist2 + (4 * s) * nb;
+  for (int b = threadIdx.x; b < 4 * nb; b += kBlock) {
+    const u32 v = nh[b];
+    if (v) atomicAdd(&hn[b], v);
+  }
+}
+
+// Pass of a triple: a = level l (src -> dst); grandchildren (heap 4h + 3 + g) receive the rows.
+template <int NCOL, int KI, bool ATOM = true>
+__global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs ta) {
+  constexpr int kItems = KI;
+  constexpr int kChunk = kBlock * KI;
+  constexpr int NZ = 12;  // 4 grandchildren x (left of / inside / right of the level-(l+2) median bucket)
+  constexpr int D = NCOL - 1;
+  static_assert(kItems % 4 == 0, "16-B row loads take 4 rows per item group");
+  constexpr int W = kBlock / 64;
+  extern __shared__ __align__(16) u32 nh[];  // [8 * bins3]
+  // Zone ranks: every row takes its rank inside (wave, zone) from one LDS atomic on the wave's
+  // counter of its zone (16 counters per wave, the last one for rows that stay behind); after
+  // a barrier the waves' counts are scanned per zone and reserved in the grandchild's zone.
+  // One atomic per row instead of 12 ballots and 12 count stores per row.
+  __shared__ u32 wcnt[W][16];
+  __shared__ u32 wbase[W][16];
+  __shared__ u32 gcnt[ATOM ? 1 : NZ][64];
+  __shared__ unsigned long long bmin[4], bmax[4];  // grandchildren's middle-zone key ranges, flushed once
+  __shared__ BucketParams gpar[4], ggp[8];
+  __shared__ u32 gbs[4];
+  __shared__ i64 glo[4], gn[4];
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const int nb3 = ta.bins3;
+  const bool fuse = nb3 > 0;
+  if (fuse)
+    for (int b = threadIdx.x; b < 8 * nb3; b += kBlock) nh[b] = 0;
+  const i64 g0 = 4 * h + 3;  // heap index of the first grandchild
+  if (threadIdx.x < W * 16) (&wcnt[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x < 4) {
+    const int t = int(threadIdx.x);
+    bmin[t] = ~0ull;
+    bmax[t] = 0ull;
+    gpar[t] = a.params[g0 + t];
+    gbs[t] = a.state[g0 + t].bstar;
+    glo[t] = a.seg_lo[g0 + t];
+    gn[t] = a.seg_n[g0 + t];
+  }
+  if (fuse && threadIdx.x < 8) ggp[threadIdx.x] = a.params[2 * g0 + 1 + threadIdx.x];
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
+  const SegState* st = a.state + h;
+  const u32 bstar = st->bstar, stage2 = st->stage2, sbstar = st->sbstar;
+  const u64 pivot = st->pivot;
+  BucketParams p2;
+  p2.lo = st->p2lo;
+  p2.scale = st->p2scale;
+  const BucketParams prm = a.params[h];
+  const SegState* const cst0 = a.state + 2 * h + 1;
+  const SegState* const cst1 = a.state + 2 * h + 2;
+  const u32 cbs0 = cst0->bstar, cbs1 = cst1->bstar;
+  const u64 cpv0 = cst0->pivot, cpv1 = cst1->pivot;
+  const BucketParams cpr0 = a.params[2 * h + 1], cpr1 = a.params[2 * h + 2];
+  __syncthreads();
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  const i64 nc = a.ncol;
+  const int axis = a.axis, ax1 = a.next_axis, ax2 = ta.axis2, ax3 = ta.axis3;
+  const int w = threadIdx.x / 64;
+  const int ln = dev::lane();
+  // 3 * grandchild + zone, or 15 (absent row, or the median of level l or l+1)
+  auto classify = [&](float k0, float k1, float k2, u32 id, bool valid) -> u32 {
+    if (!valid) return 15u;
+    const u32 z0 = zone_of(k0, prm, a.bins, bstar, stage2, p2, sbstar);
+    u32 c = z0 == 0 ? 0u : 1u;
+    if (z0 == 1) {
+      const u64 ck = composite_key(k0, id);
+      if (ck == pivot) return 15u;
+      c = ck < pivot ? 0u : 1u;
+    }
+    const u32 b1 = bucket_of(k1, c == 0 ? cpr0 : cpr1, ta.bins1);
+    const u32 cb = c == 0 ? cbs0 : cbs1;
+    u32 g = b1 < cb ? 0u : 1u;
+    if (b1 == cb) {
+      const u64 ck = composite_key(k1, id);
+      const u64 cp = c == 0 ? cpv0 : cpv1;
+      if (ck == cp) return 15u;
+      g = ck < cp ? 0u : 1u;
+    }
+    const u32 gi = 2 * c + g;
+    const u32 b2 = bucket_of(k2, gpar[gi], ta.bins2), gb = gbs[gi];
+    return 3 * gi + (b2 < gb ? 0u : (b2 == gb ? 1u : 2u));
+  };
+  const i64 cstart = ((lo + b0) & ~i64(3)) - lo;
+  for (i64 c0 = cstart; c0 < b1; c0 += kChunk) {
+    float row[kItems][NCOL];
+    bool vld[kItems];
+#pragma unroll
+    for (int g = 0; g < kItems / 4; ++g) {
+      const i64 e4 = c0 + (i64(g) * kBlock + threadIdx.x) * 4;  // relative row of sub-item 0
+      const bool any = e4 < b1;
+      const i64 p4 = lo + (any ? e4 : cstart);
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(c == D && a.id_implicit)) v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
+        row[4 * g + 0][c] = v.x;
+        row[4 * g + 1][c] = v.y;
+        row[4 * g + 2][c] = v.z;
+        row[4 * g + 3][c] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const i64 e = e4 + j;
+        vld[4 * g + j] = e >= b0 && e < b1;
+        if (a.id_implicit) row[4 * g + j][D] = __uint_as_float(a.id_base0 + u32(lo + e));
+      }
+    }
+    u32 zone_pre[kItems];  // (zone << 16) | rank among the wave's rows of that zone in this chunk
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      float k0 = row[i][0], k1 = row[i][0], k2 = row[i][0], k3 = row[i][0];
+#pragma unroll
+      for (int c = 1; c < D; ++c) {
+        k0 = c == axis ? row[i][c] : k0;
+        k1 = c == ax1 ? row[i][c] : k1;
+        k2 = c == ax2 ? row[i][c] : k2;
+        k3 = c == ax3 ? row[i][c] : k3;
+      }
+      const u32 id = __float_as_uint(row[i][D]);
+      const u32 q = classify(k0, k1, k2, id, vld[i]);
+      if constexpr (ATOM) {
+        zone_pre[i] = (q << 16) | atomicAdd(&wcnt[w][q], 1u);
+      } else {
+        u32 my = 0;
+#pragma unroll
+        for (int z = 0; z < NZ; ++z) {
+          const u64 m = __ballot(q == u32(z));
+          if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
+          if (q == u32(z)) my = mbcnt(m);
+        }
+        zone_pre[i] = (q << 16) | my;
+      }
+      const u32 zz = q % 3;
+      if (fuse && q < u32(NZ) && zz != 1) {
+        const u32 gg = 2 * (q / 3) + (zz == 2 ? 1u : 0u);
+        atomicAdd(&nh[gg * u32(nb3) + bucket_of(k3, ggp[gg], nb3)], 1u);
+      }
+      if (__ballot(q < u32(NZ) && zz == 1)) {  // level l+2 middle zones: track their composite key ranges
+        const u64 ck = composite_key(k2, id);
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) wave_minmax_atomic(q == u32(3 * gi + 1), ck, &bmin[gi], &bmax[gi]);
+      }
+    }
+    __syncthreads();
+    if constexpr (!ATOM) {
+      for (int z = w; z < NZ; z += W) {  // wave w scans zones w, w+4, w+8
+        const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
+        const u32 incl = dev::wave_incl_scan(v);
+        const u32 tot = __shfl(incl, 63, 64);
+        u32 base = 0;
+        if (ln == 0 && tot) base = atomicAdd(&a.state[g0 + z / 3].cur[z % 3], tot);
+        base = __shfl(base, 0, 64);
+        gcnt[z][ln] = base + incl - v;
+      }
+    } else if (threadIdx.x < NZ) {  // thread z: zone z's waves, scanned, reserved in the grandchild at once
+      const int z = int(threadIdx.x);
+      u32 c[W], tot = 0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        c[k] = wcnt[k][z];
+        tot += c[k];
+      }
+      u32 base = tot ? atomicAdd(&a.state[g0 + z / 3].cur[z % 3], tot) : 0u;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        wbase[k][z] = base;
+        base += c[k];
+        wcnt[k][z] = 0;  // the next chunk's counters (read by no one else before the barrier)
+      }
+    }
+    if (ATOM && threadIdx.x >= NZ && threadIdx.x < NZ + W) wcnt[threadIdx.x - NZ][15] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const u32 zi = zone_pre[i] >> 16;
+      i64 dest = -1;
+      if (zi < u32(NZ)) {
+        const u32 gi = zi / 3;
+        const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
+        if (i64(off) >= gn[gi]) {
+          atomicOr(a.err, 1u);
+        } else {
+          dest = glo[gi] + off;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c)
+        if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
+    }
+    // ATOM: the next chunk's atomics only touch the zeroed counters and its reads of wbase
+    // follow two more barriers; ballots: the next chunk rewrites gcnt
+    if (!ATOM) __syncthreads();
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 && bmin[threadIdx.x] != ~0ull) {
+    SegState* gs = a.state + g0 + threadIdx.x;
+    atomicMin(&gs->mid_min, bmin[threadIdx.x]);
+    atomicMax(&gs->mid_max, bmax[threadIdx.x]);
+  }
+  if (fuse) {
+    u32* hn = ta.hist3 + (8 * s) * nb3;
+    for (int b = threadIdx.x; b < 8 * nb3; b += kBlock) {
       const u32 v = nh[b];
       if (v) atomicAdd(&hn[b], v);
     }
@@ -1995,6 +2441,10 @@ Tuning Tuning::from_env() {
   if (impl) throw std::invalid_argument("PKD_SUBTREE_IMPL was removed: one subtree kernel ships (k_subtree_rank)");
   t.narrow = env_i("PKD_NARROW", 1) != 0;
   t.pairs = env_i("PKD_PAIR", 1) != 0;
+  t.triples = env_i("PKD_TRIPLE", 1) != 0;
+  t.triple_from = int(env_i("PKD_TRIPLE_FROM", 3));
+  t.atomic_ranks = int(env_i("PKD_PART_ATOMIC", -1));
+  t.atomic_ranks3 = int(env_i("PKD_PART3_ATOMIC", -1));
   t.prefix = env_i("PKD_PART_PREFIX", 1) != 0;
   t.split = env_i("PKD_SPLIT", 1) != 0;
   t.split_trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
@@ -2096,17 +2546,31 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     max_bins_ = std::max(max_bins_, lp.bins);
     max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
   }
-  // Pair level l with l+1 (one fused scatter pass) when rows fit the register path and
-  // l+1 needs no second-stage histogram.
+  // Levels l, l+1, l+2 move in ONE fused scatter pass (a triple) when rows fit the register
+  // path and neither l+1 nor l+2 needs a second-stage histogram (their median buckets are
+  // narrowed by the two key sweeps k_scan / k_scan2 and k_refine alone); otherwise l and l+1
+  // pair up. A triple never straddles the split level of a split build.
   const bool pairs = dim <= 8 && tune_.pairs;
-  for (int l = 0; pairs && l + 1 < lg_; ++l) {
-    levels_[size_t(l)].pair = true;
-    if (l + 2 < lg_) {  // the pair's scatter fuses 4 grandchild histograms in LDS
-      LevelPlan& g = levels_[size_t(l + 2)];
-      g.bins = std::min(g.bins, tune_.pair_bins);
-      levels_[size_t(l + 1)].next_bins = g.bins;
+  const bool may_split = tune_.split && opt.allow_split && n_ >= tune_.split_min_n;
+  auto cap_bins = [&](int l, int cap) {  // level l's bins, fused into the previous pass's LDS
+    if (l >= lg_) return;
+    LevelPlan& g = levels_[size_t(l)];
+    g.bins = std::min(g.bins, cap);
+    levels_[size_t(l - 1)].next_bins = g.bins;
+  };
+  for (int l = 0; pairs && l + 1 < lg_;) {
+    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lg_ && !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
+    int next = l + (tri ? 3 : 2);
+    if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
+    if (next - l == 3) {
+      levels_[size_t(l)].triple = true;
+      cap_bins(l + 2, tune_.pair_bins);   // k_scan2: 4 grandchild histograms in LDS
+      cap_bins(l + 3, kTripleBins);       // k_partition3: 8 great-grandchild histograms in LDS
+    } else if (next - l == 2) {
+      levels_[size_t(l)].pair = true;
+      cap_bins(l + 2, tune_.pair_bins);   // the pair's scatter fuses 4 grandchild histograms in LDS
     }
-    ++l;  // l+1 is the second level of the pair
+    l = next;
   }
   for (size_t l = 0; l < levels_.size(); ++l) {
     max_bins_ = std::max(max_bins_, levels_[l].bins);
@@ -2138,8 +2602,13 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   {
     const Tuning& sc = tune_;
     const int L = sc.split_level;
-    const bool paired = lg_ >= 2 && levels_[0].pair;
-    if (sc.split && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.split_min_n && L >= 2 && L % 2 == 0 &&
+    const bool paired = lg_ >= 2 && (levels_[0].pair || levels_[0].triple);
+    bool boundary = false;  // L starts a pass (single level, pair or triple)
+    for (int l = 0; l < lg_;) {
+      boundary = boundary || l == L;
+      l += levels_[size_t(l)].triple ? 3 : (levels_[size_t(l)].pair ? 2 : 1);
+    }
+    if (sc.split && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.split_min_n && L >= 2 && boundary &&
         L < lg_ && sc.split_parts >= 2 && sc.split_streams >= 1) {
       const int P = std::min(pow2_floor(sc.split_parts), 1 << L);
       split_level_ = L;
@@ -2177,7 +2646,7 @@ std::string GpuBuilder::describe() const {
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
        << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
-       << (lp.pair ? " pair" : "");
+       << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "");
   return os.str();
 }
 
@@ -2232,7 +2701,7 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
     // generated ids are synthesised by the first pair's kernels instead of written here
     // (-4 B written and -4 B read per point); the first level must be a pair for that
-    const bool implicit = ids == nullptr && lg_ >= 2 && levels_[0].pair && tune_.implicit_ids;
+    const bool implicit = ids == nullptr && lg_ >= 2 && (levels_[0].pair || levels_[0].triple) && tune_.implicit_ids;
     k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part, implicit ? 0 : 1);
     PKD_LAUNCH_CHECK();
     k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, g, dim_, bbox);
@@ -2325,6 +2794,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     u32* h2;
     u32* bcnt;
   };
+  // Zone ranks of the scatter passes: LDS atomics below 64 M points, wave ballots above
+  // (A/B in profiles/r3_partition_subtree_experiments.txt); knob -1 = by size.
+  auto atomic_ranks = [&](int knob) { return knob >= 0 ? knob != 0 : n_ < (i64(64) << 20); };
   auto run_range = [&](int base, int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs,
                        float*& src, float*& dst) {
     auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
@@ -2417,6 +2889,50 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         PKD_LAUNCH_CHECK();
       }
       const int grid = int(segs * a.bps);
+      if (lp.triple) {
+        const LevelPlan& lq = levels_[size_t(l + 1)];
+        const LevelPlan& lr = levels_[size_t(l + 2)];
+        const i64 segs1 = lq.segs / nparts, segs2 = lr.segs / nparts;
+        const int gs = int((segs + 3) / 4), gs1 = int((segs1 + 3) / 4);
+        LevelArgs b = level_args(l + 1);
+        LevelArgs c = level_args(l + 2);
+        TripleArgs ta;
+        ta.bins1 = lq.bins;
+        ta.axis2 = lr.axis;
+        ta.bins2 = lr.bins;
+        ta.hist2 = hist_of(l + 2);
+        ta.axis3 = (opt_.depth0 + l + 3) % dim_;
+        ta.bins3 = lr.next_bins;
+        ta.hist3 = l + 3 < lg_ ? hist_of(l + 3) : nullptr;
+        with_ncol(dim_, [&](auto nc) {
+          constexpr int NC = decltype(nc)::value;
+          if constexpr (NC > 0) {
+            LevelArgs as = a;  // the key sweeps' own block split (their histogram flush scales with blocks)
+            as.bps = std::max(1, a.bps / tune_.scan_div);
+            k_scan<NC><<<int(segs * as.bps), kBlock, size_t(2 * lp.next_bins + 64) * 4, st>>>(as);
+            PKD_LAUNCH_CHECK();
+            k_pivot_both<NC><<<gs + int(segs), kBlock, 0, st>>>(a, segs, gs);
+            PKD_LAUNCH_CHECK();
+            k_select<<<int(segs1), kBlock, 0, st>>>(b);
+            PKD_LAUNCH_CHECK();
+            k_scan2<NC><<<int(segs * as.bps), kBlock, size_t(4 * lr.bins + 64) * 4, st>>>(as, ta);
+            PKD_LAUNCH_CHECK();
+            k_pivot_both<NC><<<gs1 + int(segs1), kBlock, 0, st>>>(b, segs1, gs1);
+            PKD_LAUNCH_CHECK();
+            k_select<<<int(segs2), kBlock, 0, st>>>(c);
+            PKD_LAUNCH_CHECK();
+            constexpr int KI = NC <= 5 ? 8 : 4;
+            const size_t lds3 = size_t(std::max(1, 8 * ta.bins3)) * 4;
+            if (atomic_ranks(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
+            else k_partition3<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ta);
+            PKD_LAUNCH_CHECK();
+          }
+        });
+        refine(c, segs2);
+        std::swap(src, dst);
+        l += 3;
+        continue;
+      }
       if (lp.pair) {
         const LevelPlan& lq = levels_[size_t(l + 1)];
         const i64 segs1 = lq.segs / nparts;
@@ -2469,8 +2985,13 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             // 4 rows per column; the pass is bound by requests in flight per CU, not by HBM
             // (profiles/r2_split_build.txt, CU masks). 100M x 3D 12.73 -> 12.52 ms one-stream,
             // 12.22 -> 12.12 split.
-            if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
-            else k_partition2<NC, KI, false><<<grid, kBlock, lds_b, st>>>(a, pa);
+            if (atomic_ranks(tune_.atomic_ranks)) {
+              if (pfx) k_partition2<NC, KI, true, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+              else k_partition2<NC, KI, false, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+            } else {
+              if (pfx) k_partition2<NC, KI, true><<<grid, kBlock, lds_b, st>>>(a, pa);
+              else k_partition2<NC, KI, false><<<grid, kBlock, lds_b, st>>>(a, pa);
+            }
           }
         });
         PKD_LAUNCH_CHECK();

@@ -269,9 +269,13 @@ void k_subtree_rank(SubArgs a) {
     const float* kcol = rows + (narrow ? t : axis) * NM;
     u16* cr = crank + size_t(axis) * NM;
     const int S = 1 << t;
-    const int Wt = words_of(t);
+    const bool alone = (n >> t) <= 1;  // every sub-segment holds at most one point: it is the median
+    const int Wt = alone ? 0 : words_of(t);
     u32 rank[ITEMS];
-    if (Wt > 0) {
+    if (alone) {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) rank[i] = 0;
+    } else if (Wt > 0) {
       // ---- compressed ranks: one bitmap of Wt words per sub-segment ----
       // (already zeroed by the previous level; its readers finished before this level's barrier)
       u32* bmp = cb ? bm1 : work;

@@ -40,6 +40,10 @@ struct Tuning {
   bool implicit_ids = true;   // PKD_IMPLICIT_IDS=0: the prep writes generated ids
   bool narrow = true;         // PKD_NARROW=0: full columns at high dims
   bool pairs = true;          // PKD_PAIR=0: one level per row-moving pass
+  bool triples = true;        // PKD_TRIPLE=0: at most two levels per row-moving pass
+  int triple_from = 3;        // PKD_TRIPLE_FROM: first level a triple may start at (8+ segments)
+  int atomic_ranks = -1;      // PKD_PART_ATOMIC: pair scatter ranks zones by LDS atomics (1) or
+  int atomic_ranks3 = -1;     //   wave ballots (0); PKD_PART3_ATOMIC the same for triples; -1: by n
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
@@ -64,6 +68,7 @@ struct LevelPlan {
   int axis;         // split axis at this level
   bool stage2 = false;  // median bucket split by a second (key-only) histogram pass
   bool pair = false;    // this level and the next are moved by ONE fused partition pass
+  bool triple = false;  // this level and the next two are moved by ONE fused partition pass
 };
 
 struct SplitStreams;  // side HIP streams + fork / join events of a split build

@@ -47,6 +47,24 @@ def test_duplicates(gpu_device):
     check_same(torch.randint(0, 2, (20_000, 3)).float(), gpu_device)
 
 
+@pytest.mark.parametrize("atomic", ["0", "1"])
+@pytest.mark.parametrize("triple_from", ["0", "3"])
+def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic):
+    """Three levels per scatter pass (k_scan2 + k_partition3, from level 0 or 3) with zone ranks
+    from wave ballots or LDS atomics (also in the pair scatters): slot for slot the CPU exact
+    tree on uniform, duplicate-heavy, 2-D, 8-D and odd-depth inputs."""
+    monkeypatch.setenv("PKD_TRIPLE_FROM", triple_from)
+    monkeypatch.setenv("PKD_PART_ATOMIC", atomic)
+    monkeypatch.setenv("PKD_PART3_ATOMIC", atomic)
+    b = ops.GpuTreeBuilder(1_000_000, 3)
+    assert "triple" in b.describe(), b.describe()
+    check_same(pk.generate_problem(11, 3, 1_000_000), gpu_device)
+    check_same(torch.randint(0, 7, (600_000, 3)).float(), gpu_device)
+    check_same(pk.generate_problem(12, 2, 700_001), gpu_device)
+    check_same(pk.generate_problem(13, 8, 400_000), gpu_device)
+    check_same(pk.generate_problem(14, 3, 900_000), gpu_device, depth0=2)
+
+
 def test_depth0(gpu_device):
     check_same(pk.generate_problem(8, 3, 100_000), gpu_device, depth0=1)
 
