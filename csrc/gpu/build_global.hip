@@ -2382,6 +2382,357 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
   }
 }
 
+// =====================================================================================
+// Tail levels: the last three global levels of a segment (<= 16 Ki rows) in ONE workgroup.
+// The segment's rows stay where the previous scatter put them; every row is read once per
+// level (only that level's key column, coalesced, one row per lane per item) and once more
+// when it moves, so the three levels cost 3 x 4 + 16 B read and 16 B written per row instead
+// of a triple's two key sweeps, its 12-zone scatter (8 + 12 + 32 B) and five small kernels
+// between them. Per level, for the level's 1 / 2 / 4 sub-segments at once:
+//   bins      a linear histogram of the key over the sub-segment's cell (LDS atomics), a
+//             block scan, and the bin holding the median rank (n_s / 2) of each sub-segment;
+//   select    the median bin's rows ((key, id) composite) ranked by one wave per sub-segment
+//             (<= 64 candidates), or a block-wide radix select over the composite key (8-bit
+//             digits, any number of candidates: heavy duplicates);
+//   classify  every live row goes left / right of its sub-segment's pivot (a row's id is read
+//             only when its key equals the pivot key); the median row is written to its
+//             output slot; the children's cells are set.
+// Then every row gets its position in its leaf from one LDS atomic on its wave's leaf counter
+// plus the waves' prefix, and each column is staged through LDS in leaf order and written
+// back with coalesced stores (the 7 median slots carry garbage in the scratch columns; the
+// subtree kernel reads only leaf ranges).
+constexpr int kTailThreads = 1024;
+constexpr int kTailBins = 4096;  // bins of a level, split evenly among its sub-segments
+constexpr int kTailCand = 64;    // median-bin candidates one wave ranks
+
+struct TailArgs {
+  const float* src;
+  float* dst;
+  i64 ncol;
+  const i64* seg_lo;
+  const i64* seg_n;
+  float* cells;  // heap-indexed [h][dim][2]
+  i64 heap0;     // first segment (of this part) at level L
+  int level;     // L: the first tail level
+  int depth0;
+  float* out_pts;
+  u32* out_ids;
+  u32* err;
+};
+
+// exclusive scan over the 1024 threads of a block (one value each); *total = the sum.
+// Caller: a barrier between two uses (wsum is reused).
+__device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total, int tid) {
+  const int w = tid / 64, ln = tid & 63;
+  const u32 incl = dev::wave_incl_scan(v);
+  if (ln == 63) wsum[w] = incl;
+  __syncthreads();
+  const u32 wi = dev::wave_incl_scan(ln < kTailThreads / 64 ? wsum[ln] : 0u);
+  const u32 before = w > 0 ? u32(__shfl(wi, w - 1, 64)) : 0u;
+  *total = u32(__shfl(wi, kTailThreads / 64 - 1, 64));
+  return before + incl - v;
+}
+
+template <int D, int ITEMS, int WPE>
+__global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_tail3(TailArgs a) {
+  constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
+  constexpr u32 kDead = 0xffffffffu;
+  static_assert(ITEMS % 4 == 0, "16-B groups of 4 rows");
+  static_assert(CAP >= NB, "the stage buffer holds the bins");
+  extern __shared__ __align__(16) u32 stage[];  // CAP words: the output columns; the levels' bins alias it
+  u32* bins = stage;
+  __shared__ u32 ckey[4][kTailCand], crow[4][kTailCand];
+  __shared__ u32 ccnt[4], sbst[4], sbelow[4], srank[4], sstart[4], sn[4], wsum[W];
+  __shared__ unsigned long long spiv[4];
+  __shared__ float scell[2][8][D][2];  // cells of the level's sub-segments / of their children
+  __shared__ BucketParams sprm[4];
+  __shared__ u32 wc[W][8], wbase[W][8];
+  __shared__ u32 sbig, smrow[4];
+  const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
+  const i64 h = a.heap0 + blockIdx.x;
+  const i64 lo = a.seg_lo[h];
+  const int n = int(a.seg_n[h]);
+  if (n <= 0) return;
+  const int shift = int(lo & 3);  // rows are read in 16-B aligned groups of 4 from lo - shift
+  if (n + shift > CAP) {  // the host sizes ITEMS from the largest segment; never expected
+    if (tid == 0) atomicOr(a.err, 16u);
+    return;
+  }
+  const i64 nc = a.ncol;
+  // Item i = 4 g + j of a thread is row (g * T + tid) * 4 + j - shift of the segment: one 16-B
+  // load per group of 4 rows. Rows are addressed through buffer descriptors (one per column,
+  // wave-uniform): the lane offset tid * 16 is the only per-lane address register, g's
+  // g * 16 KiB the scalar offset, j's 4 j the immediate.
+  const u32 vo = u32(tid) * 16u;
+  const i64 alo = lo - shift;
+  const int recs = (shift + n + 3) & ~3;
+  auto col = [&](const float* base, int c) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + i64(c) * nc + alo), 0, recs * 4, 0x00020000);
+  };
+  const auto idr = col(a.src, D);
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, u32 row) {  // row relative to lo
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (row + u32(shift)) * 4u, 0, 0);
+  };
+  auto ld4 = [&](const __amdgpu_buffer_rsrc_t& r, int g) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, vo, u32(g * T * 16), 0);
+  };
+  auto ldi = [&](const __amdgpu_buffer_rsrc_t& r, int i) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + u32(i % 4) * 4u, u32((i / 4) * T * 16), 0);
+  };
+  // row (relative to lo) of item i, recomputed at each (rare) use: kept opaque so the
+  // compiler does not hold one register per item for it across the whole kernel
+  auto rowof = [&](int i) {
+    u32 t4 = u32(tid);
+    asm volatile("" : "+v"(t4));
+    return (u32((i / 4) * T) + t4) * 4u + u32(i % 4) - u32(shift);
+  };
+  if (tid < 2 * D) (&scell[0][0][0][0])[tid] = a.cells[h * 2 * D + tid];
+  if (tid < W * 8) (&wc[0][0])[tid] = 0;
+  // path: the row's sub-segment at the current level (while a level bins, its bin: the
+  // sub-segment is bin >> lgB), kDead for absent / median rows
+  u32 path[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int r = (i / 4 * T + tid) * 4 + i % 4 - shift;
+    path[i] = (r >= 0 && r < n) ? 0u : kDead;
+  }
+#pragma unroll 1
+  for (int t = 0; t < 3; ++t) {
+    // the thread index, opaque per level: values derived from it (LDS and global addresses of
+    // the few-thread steps) are recomputed each level instead of being hoisted into registers
+    // that live across the whole kernel
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int wq = tq / 64, lq = tq & 63;
+    const int S = 1 << t, B = NB >> t, lgB = 12 - t;
+    static_assert(NB == 4096, "lgB");
+    const int axis = (a.depth0 + a.level + t) % D;
+    const i64 hs0 = (h + 1) * S - 1;  // the level's first sub-segment (heap index)
+    const auto kr = col(a.src, axis);
+    float key[ITEMS];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto v = ld4(kr, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) key[4 * g + j] = __uint_as_float(v[j]);
+    }
+    for (int b = tq; b < NB; b += T) bins[b] = 0;
+    if (tq < 4) {
+      ccnt[tq] = 0;
+      smrow[tq] = 0xffffffffu;
+      sbst[tq] = 0xffffffffu;
+      spiv[tq] = ~0ull;
+    }
+    if (tq == 0) {
+      u32 run = 0;
+      for (int s = 0; s < S; ++s) {
+        sn[s] = u32(a.seg_n[hs0 + s]);
+        sstart[s] = run;
+        run += sn[s];
+      }
+    }
+    if (tq < S) {
+      const float* c = &scell[t & 1][tq][axis][0];
+      sprm[tq] = make_params(c[0], c[1], B);
+    }
+    __syncthreads();
+    // ---- bins ----
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      if (path[i] != kDead) {
+        const u32 sp = path[i];
+        path[i] = sp * u32(B) + bucket_of(key[i], sprm[sp], B);
+        atomicAdd(&bins[path[i]], 1u);
+      }
+    }
+    __syncthreads();
+    {
+      u32 c[NB / T], sum = 0;
+#pragma unroll
+      for (int j = 0; j < NB / T; ++j) {
+        c[j] = bins[tq * (NB / T) + j];
+        sum += c[j];
+      }
+      u32 total;
+      const u32 ex = block_excl_scan1024(sum, wsum, &total, tq);
+      const int sp = tq * (NB / T) / B;  // B is a multiple of NB / T: a thread's bins share a sub-segment
+      u32 run = ex - sstart[sp];
+      const u32 m = sn[sp] / 2;
+#pragma unroll
+      for (int j = 0; j < NB / T; ++j) {
+        if (run <= m && m < run + c[j]) {
+          sbst[sp] = u32(tq * (NB / T) + j);
+          sbelow[sp] = run;
+          srank[sp] = m - run;
+        }
+        run += c[j];
+      }
+    }
+    __syncthreads();
+    // ---- candidates of the median bins ----
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const u32 sp = path[i] >> lgB;
+      if (path[i] != kDead && path[i] == sbst[sp]) {
+        const u32 k = atomicAdd(&ccnt[sp], 1u);
+        if (k < u32(kTailCand)) {
+          ckey[sp][k] = orderable(key[i]);
+          crow[sp][k] = rowof(i);
+        }
+      }
+    }
+    __syncthreads();
+    if (tq == 0) {
+      u32 big = 0;
+      for (int s = 0; s < S; ++s) big |= ccnt[s] > u32(kTailCand) ? 1u : 0u;
+      sbig = big;
+    }
+    if (wq < S) {  // wave s ranks sub-segment s's candidates (results unused if any list overflowed)
+      const int sp = wq;
+      const int m = int(min(ccnt[sp], u32(kTailCand)));
+      u64 ck = ~0ull;
+      if (lq < m) ck = (u64(ckey[sp][lq]) << 32) | u64(ld(idr, crow[sp][lq]));
+      u32 rank = 0;
+#pragma unroll 1
+      for (int j = 0; j < m; ++j) rank += dev::shfl_u64(ck, j) < ck ? 1u : 0u;
+      if (lq < m && rank == srank[sp] && ccnt[sp] <= u32(kTailCand)) spiv[sp] = ck;
+    }
+    __syncthreads();
+    if (sbig) {
+      // radix select over the composite (key, id) of every sub-segment's median-bin rows,
+      // 8 bits per pass from the top (ids are distinct, so 8 passes leave one row)
+      if (tq < 4) spiv[tq] = 0;
+#pragma unroll 1
+      for (int pass = 0; pass < 8; ++pass) {
+        const int sh = 56 - 8 * pass;
+        const u64 known = pass == 0 ? 0ull : (~0ull << (sh + 8));  // digits fixed by earlier passes
+        for (int b = tq; b < 4 * 256; b += T) bins[b] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+          const u32 sp = path[i] >> lgB;
+          if (path[i] != kDead && path[i] == sbst[sp]) {  // (rare path: ids re-read per pass)
+            const u64 ck = (u64(orderable(key[i])) << 32) | u64(ldi(idr, i));
+            if (((ck ^ spiv[sp]) & known) == 0) atomicAdd(&bins[sp * 256 + u32((ck >> sh) & 255u)], 1u);
+          }
+        }
+        __syncthreads();
+        if (wq < S) {  // wave s: digits 4 lq .. 4 lq + 3 of sub-segment s
+          const int sp = wq;
+          u32 c4[4], sum = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            c4[j] = bins[sp * 256 + 4 * lq + j];
+            sum += c4[j];
+          }
+          u32 run = dev::wave_incl_scan(sum) - sum;
+          const u32 r = srank[sp];
+          u32 found = 0xffffffffu, nr = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (run <= r && r < run + c4[j]) {
+              found = u32(4 * lq + j);
+              nr = r - run;
+            }
+            run += c4[j];
+          }
+          if (found != 0xffffffffu) {
+            spiv[sp] |= u64(found) << sh;
+            srank[sp] = nr;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // ---- classify: left / right of the pivot; the median row goes to its output slot ----
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      if (path[i] == kDead) continue;
+      const u32 sp = path[i] >> lgB;
+      const u64 pv = spiv[sp];
+      const u32 ok = orderable(key[i]), pk = u32(pv >> 32);
+      u32 right = ok > pk ? 1u : 0u;
+      if (ok == pk) {
+        const u32 id = ldi(idr, i);
+        const u64 ck = (u64(ok) << 32) | u64(id);
+        if (ck == pv) {  // the median row: written to its slot after the barrier
+          smrow[sp] = rowof(i);
+          path[i] = kDead;
+          continue;
+        }
+        right = ck > pv ? 1u : 0u;
+      }
+      path[i] = 2 * sp + right;
+    }
+    __syncthreads();
+    if (tq < S * (D + 1)) {  // the medians' rows to their output slots, one column per thread
+      const int sp = tq / (D + 1), c = tq % (D + 1);
+      const i64 hs = hs0 + sp;
+      const i64 slot = a.seg_lo[hs] + a.seg_n[hs] / 2;
+      const u32 r = smrow[sp];
+      if (r < u32(n)) {
+        const float v = a.src[i64(c) * nc + lo + r];
+        if (c < D) a.out_pts[slot * D + c] = v;
+        else a.out_ids[slot] = __float_as_uint(v);
+      }
+    }
+    if (tq < 2 * S) {  // children cells: the pivot key bounds the split axis
+      const int sp = tq / 2, side = tq & 1;
+      const float pkf = from_orderable(u32(spiv[sp] >> 32));
+      float* gc = a.cells + (2 * (hs0 + sp) + 1 + side) * 2 * D;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        float clo = scell[t & 1][sp][c][0], chi = scell[t & 1][sp][c][1];
+        if (c == axis) {
+          if (side == 0) chi = pkf;
+          else clo = pkf;
+        }
+        scell[(t + 1) & 1][tq][c][0] = clo;
+        scell[(t + 1) & 1][tq][c][1] = chi;
+        gc[2 * c] = clo;
+        gc[2 * c + 1] = chi;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- move: position inside the leaf, then each column through LDS in leaf order ----
+  u32 pos[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) pos[i] = path[i] != kDead ? atomicAdd(&wc[w][path[i]], 1u) : 0u;
+  __syncthreads();
+  if (tid < 8) {
+    const i64 hl = (h + 1) * 8 - 1 + tid;
+    const u32 first = u32(a.seg_lo[hl] - lo);
+    u32 off = first;
+    for (int k = 0; k < W; ++k) {
+      wbase[k][tid] = off;
+      off += wc[k][tid];
+    }
+    if (i64(off - first) != a.seg_n[hl]) atomicOr(a.err, 16u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i)
+    if (path[i] != kDead) pos[i] += wbase[w][path[i]];
+#pragma unroll 1
+  for (int c = 0; c <= D; ++c) {
+    const auto sr = col(a.src, c);
+    const auto dr = col(a.dst, c);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto v = ld4(sr, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (path[4 * g + j] != kDead) stage[pos[4 * g + j]] = v[j];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int p = tid; p < n; p += T) __builtin_amdgcn_raw_buffer_store_b32(stage[p], dr, u32(p + shift) * 4u, 0, 0);
+    __syncthreads();
+  }
+}
+
 // Calls f(std::integral_constant<int, dim + 1>) for dim <= 8 (rows in registers), else
 // f(std::integral_constant<int, 0>) (runtime dim).
 template <class F>
@@ -2446,6 +2797,7 @@ Tuning Tuning::from_env() {
   t.atomic_ranks = int(env_i("PKD_PART_ATOMIC", -1));
   t.atomic_ranks3 = int(env_i("PKD_PART3_ATOMIC", -1));
   t.prefix = env_i("PKD_PART_PREFIX", 1) != 0;
+  t.tail = env_i("PKD_TAIL", 0) != 0;
   t.split = env_i("PKD_SPLIT", 1) != 0;
   t.split_trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
   t.colgroup = int(env_i("PKD_COLGROUP", 0));
@@ -2558,8 +2910,22 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     g.bins = std::min(g.bins, cap);
     levels_[size_t(l - 1)].next_bins = g.bins;
   };
-  for (int l = 0; pairs && l + 1 < lg_;) {
-    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lg_ && !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
+  // The last three global levels: one workgroup per segment (k_tail3) when a segment fits its
+  // 1024 threads x 8 / 12 / 16 rows (always, below the subtree capacity of 2048) and rows fit
+  // registers (dim <= 8, full columns).
+  // (A split build's parts start at split_level: the tail may not begin above it.)
+  const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min_n;
+  if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - 3 >= tune_.split_level)) {
+    const i64 nl = (n_ >> (lg_ - 3)) + 3;  // + the 16-B alignment shift of the segment start
+    tail_items_ = nl <= 8 * 1024 ? 8 : (nl <= 12 * 1024 ? 12 : (nl <= 16 * 1024 ? 16 : 0));
+    if (tail_items_ > 0) {
+      tail_ = lg_ - 3;
+      for (int l = tail_; l < lg_; ++l) levels_[size_t(l)].tail = true;
+    }
+  }
+  const int lgrp = tail_ >= 0 ? tail_ : lg_;  // levels the pairs / triples cover
+  for (int l = 0; pairs && l + 1 < lgrp;) {
+    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
     int next = l + (tri ? 3 : 2);
     if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
     if (next - l == 3) {
@@ -2572,6 +2938,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     }
     l = next;
   }
+  if (tail_ > 0) levels_[size_t(tail_ - 1)].next_bins = 0;  // k_tail3 bins its levels itself
   for (size_t l = 0; l < levels_.size(); ++l) {
     max_bins_ = std::max(max_bins_, levels_[l].bins);
     max_hist_ = std::max<i64>(max_hist_, levels_[l].segs * levels_[l].bins);
@@ -2646,7 +3013,7 @@ std::string GpuBuilder::describe() const {
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
        << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
-       << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "");
+       << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "") << (lp.tail ? " tail" : "");
   return os.str();
 }
 
@@ -2867,7 +3234,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     static const char* const kLevelNames[] = {"pkd.level0", "pkd.level1", "pkd.level2", "pkd.level3",
                                               "pkd.level4", "pkd.level5", "pkd.level6", "pkd.level7",
                                               "pkd.level8", "pkd.level9", "pkd.level10", "pkd.level11+"};
-    for (int l = l0; l < l1;) {
+    const int lend = tail_ >= 0 ? std::min(l1, tail_) : l1;
+    for (int l = l0; l < lend;) {
       const LevelPlan& lp = levels_[size_t(l)];
       const i64 segs = lp.segs / nparts;  // this part's segments at level l
       TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
@@ -3011,12 +3379,37 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       std::swap(src, dst);
       l += 1;
     }
+    if (tail_ >= 0 && l1 == lg_) {  // the last three levels of this part's segments
+      TraceRange trt("pkd.tail");
+      const LevelPlan& lp = levels_[size_t(tail_)];
+      const i64 segs = lp.segs / nparts;
+      TailArgs ta{src, dst, ncol_, seg_lo, seg_n, cells, lp.segs - 1 + i64(part) * segs, tail_, opt_.depth0,
+                  out_pts, out_ids, err};
+      const size_t lds = size_t(tail_items_) * kTailThreads * 4;
+      with_ncol(dim_, [&](auto nc) {
+        constexpr int D = decltype(nc)::value - 1;
+        if constexpr (D >= 1) {
+          auto go = [&](auto kern) {
+            ensure_dynamic_lds(reinterpret_cast<const void*>(kern), int(lds));
+            kern<<<int(segs), kTailThreads, lds, st>>>(ta);
+          };
+          static const bool one = std::getenv("PKD_TAIL_ONE") != nullptr;  // A/B: one block per CU
+          if (tail_items_ == 8) one ? go(&k_tail3<D, 8, 4>) : go(&k_tail3<D, 8, 8>);
+          else if (tail_items_ == 12) one ? go(&k_tail3<D, 12, 4>) : go(&k_tail3<D, 12, 8>);
+          else go(&k_tail3<D, 16, 4>);
+        }
+      });
+      PKD_LAUNCH_CHECK();
+      std::swap(src, dst);
+    }
   };
   auto subtree = [&](int part, int nparts, hipStream_t st, const float* src) {
     const i64 leaves = i64(1) << lg_;
     const i64 heap0 = leaves - 1 + i64(part) * (leaves / nparts);
     TraceRange trs("pkd.subtree");
-    launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, leaves / nparts, opt_.depth0 + lg_, nsub_, out_pts,
+    // the largest segment of level lg_ holds floor(n / 2^lg_) points (a child never exceeds half its parent)
+    const int nmax = int(std::min<i64>(nsub_, n_ >> lg_));
+    launch_subtree(src, ncol_, dim_, seg_lo, seg_n, cells, heap0, leaves / nparts, opt_.depth0 + lg_, nmax, out_pts,
                    out_ids, err, st, in_rows ? narrow_k : -1, in_rows, in_rs);
   };
 

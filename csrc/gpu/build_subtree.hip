@@ -62,17 +62,18 @@ __device__ __forceinline__ u32 pow2_ceil(u32 v) { return v <= 1 ? 1u : 1u << (32
 // Axes whose compressed ranks are kept: only useful if an axis is used twice (dim < height).
 __host__ __device__ inline int kept_axes(int dim, int nm) { return dim < bitlen(u32(nm)) ? dim : 0; }
 
-// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+68 | aux nm+64 | fin nm+64 | tmpi u16 nm+64 |
-//               root cell 2*dim. The 64 dummy entries at the end of work / aux / fin / tmpi take the writes
-//               of finished points, one per lane, so those writes never share an address.
-//               + the second bitmap buffer of the compressed levels, nm/2 + 64.
+// 32-bit words: rows (dim+1)*nm | crank u16 kept*nm | work nm+68 | aux nm+64 | fin u16 nm+64 |
+//               tmpi u16 / bm1 nm/2+64 | root cell 2*dim. The 64 dummy entries at the end of work / aux /
+//               fin / tmpi take the writes of finished points, one per lane, so those writes never share an
+//               address. bm1 (the compressed levels' second bitmap buffer) aliases tmpi (first-use levels only).
 size_t lds_words(int dim, int nm) {
-  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 68 + 2 * (size_t(nm) + 64) +
-         size_t(nm) / 2 + 32 + 2 * size_t(dim) + size_t(nm) / 2 + 64;
+  return size_t(dim + 1) * nm + (size_t(kept_axes(dim, nm)) * nm + 1) / 2 + size_t(nm) + 68 + size_t(nm) + 64 +
+         (size_t(nm) + 64) / 2 + size_t(nm) / 2 + 64 + 2 * size_t(dim);
 }
 // narrow mode: ldim key slots + ids + input row indices, no compressed ranks (ldim <= dim)
 size_t lds_words_narrow(int dim, int nm, int ldim) {
-  return size_t(ldim + 2) * nm + size_t(nm) + 68 + 2 * (size_t(nm) + 64) + size_t(nm) / 2 + 32 + 2 * size_t(dim);
+  return size_t(ldim + 2) * nm + size_t(nm) + 68 + size_t(nm) + 64 + (size_t(nm) + 64) / 2 + size_t(nm) / 2 + 64 +
+         2 * size_t(dim);
 }
 
 // In-place exclusive scan of v[0, m) by the whole block; v[m] = total. Caller syncs after.
@@ -97,7 +98,7 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum, u32 du
   if (ln == 63) wsum[w] = incl;
   __syncthreads();
   // prefix of the wave totals: inclusive scan of wsum over lanes, read at lane w - 1
-  const u32 ws = wsum[ln & (W - 1)];
+  const u32 ws = wsum[(W & (W - 1)) == 0 ? (ln & (W - 1)) : (ln < W ? ln : 0)];
   const u32 pin = dev::wave_incl_scan(ln < W ? ws : 0u);
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: a scalar select, no exec juggling
   const u32 pl = u32(__builtin_amdgcn_readlane(int(pin), wu > 0 ? wu - 1 : 0));
@@ -121,13 +122,14 @@ __device__ __forceinline__ void block_excl_scan(u32* v, int m, u32* wsum, u32 du
 // behind the other's work): the register budget is pinned to that many waves per SIMD, since one SGPR over the
 // granule halves the resident blocks (82 SGPRs: 100M x 3D subtree 3.3 -> 4.9 ms, resident
 // waves 63 -> 32 in profiles/r2_subtree_pmc.txt).
-template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0>
-__global__ __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((ITEMS * THREADS >= 4096 ? 1 : 2) * THREADS / 256)))  // blocks/CU x waves/SIMD
-void k_subtree_rank(SubArgs a) {
+// NM = ITEMS * THREADS need not be a power of two (3 x 512 = 1536 holds the 1525-point segments
+// of 100M / 2^16 and 12.5M / 2^13 without idle waves).
+template <int ITEMS, int THREADS, bool NARROW, int DIMC>
+__device__ __forceinline__ void subtree_rank_body(const SubArgs& a) {
   extern __shared__ __align__(16) u32 smem[];
   __shared__ u32 wsum[THREADS / 64];
   constexpr int NM = ITEMS * THREADS;
+  constexpr bool kPow2 = (NM & (NM - 1)) == 0;
   const int dim = DIMC > 0 ? DIMC : a.dim;
   const i64 h = a.heap0 + blockIdx.x;
   const int n = int(a.seg_n[h]);
@@ -152,13 +154,16 @@ void k_subtree_rank(SubArgs a) {
   u16* crank = reinterpret_cast<u16*>(smem + size_t(rcols) * NM);
   u32* work = smem + size_t(rcols) * NM + (size_t(kept_layout) * NM + 1) / 2;
   u32* aux = work + NM + 4 + 64;  // work: NM buckets, sentinel, 64 per-lane dummy words
-  u32* fin = aux + NM + 64;           // aux / fin: NM entries + 64 per-lane dummies each
-  u16* tmpi = reinterpret_cast<u16*>(fin + NM + 64);  // NM + 64 entries
-  float* cellv = reinterpret_cast<float*>(tmpi + NM + 64);  // [dim][2] root cell of the segment
-  // Compressed levels alternate their bitmaps between bm1 (NM/2 words + 64 dummies; classic
-  // layout only) and work: each level zeroes the buffer of the next one after its first
-  // barrier, so a compressed level needs no zero phase of its own: 2 barriers instead of 3-4.
-  u32* bm1 = reinterpret_cast<u32*>(cellv + 2 * dim);
+  u16* fin = reinterpret_cast<u16*>(aux + NM + 64);  // aux / fin: NM entries + 64 per-lane dummies each
+  u32* tmpw = aux + NM + 64 + (NM + 64) / 2;
+  u16* tmpi = reinterpret_cast<u16*>(tmpw);  // NM + 64 entries (first-use levels)
+  float* cellv = reinterpret_cast<float*>(tmpw + NM / 2 + 64);  // [dim][2] root cell of the segment
+  // Compressed levels alternate their bitmaps between work and bm1 (NM/2 words + 64 dummies,
+  // aliasing tmpi, which only first-use levels use): each level zeroes the buffer of the next
+  // one after its first barrier, so a compressed level needs no zero phase of its own (2
+  // barriers instead of 3-4); a first-use level zeroes work for whatever level follows it, so
+  // the first compressed level after it ORs into work and zeroes bm1 once tmpi is dead.
+  u32* bm1 = tmpw;
   const u32 lane_dummy = u32(dev::lane());
   const u32 dummy = u32(NM + 4) + lane_dummy;
   // Item i of a thread is point kid(i): wave w owns the contiguous points [w*64*ITEMS,
@@ -235,10 +240,8 @@ void k_subtree_rank(SubArgs a) {
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
     const int k = tid + i * THREADS;
-    fin[k < n ? u32(k) : u32(NM) + lane_dummy] = 0xffffffffu;
+    fin[k < n ? u32(k) : u32(NM) + lane_dummy] = 0xffffu;
   }
-  if constexpr (!NARROW)
-    for (int w = tid; w < NM / 2; w += THREADS) bm1[w] = 0;  // the first compressed level's bitmaps
 #pragma unroll
   for (int j = 0; j <= ITEMS; ++j) {  // the first level's histogram (buckets + sentinel)
     const int w = tid + j * THREADS;
@@ -254,7 +257,7 @@ void k_subtree_rank(SubArgs a) {
   __syncthreads();
   stamp(a, 1);
 
-  int cb = 1;          // bitmap buffer of the next compressed level: 1 = bm1, 0 = work
+  int cb = 0;          // bitmap buffer of the next compressed level: 1 = bm1, 0 = work
   bool synced = true;  // false after a compressed level (it ends without a barrier)
   bool wz = true;      // work holds zeros (a first-use level zeroes it for the next one)
   // Wt of level t: > 0 when its ranks come from the compressed ranks of the axis's last use
@@ -322,7 +325,7 @@ void k_subtree_rank(SubArgs a) {
       if (wlive) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
-          const u32 below = Wt > 1 ? aux[wi[i] & (NM - 1)] : 0u;
+          const u32 below = Wt > 1 ? aux[kPow2 ? (wi[i] & (NM - 1)) : min(wi[i], u32(NM - 1))] : 0u;
           rank[i] = below + u32(__popc(bmp[wi[i]] & ((1u << (c[i] & 31)) - 1u)));
         }
       }
@@ -335,7 +338,7 @@ void k_subtree_rank(SubArgs a) {
       // is a valid (wider) range. Any monotone bucketing gives exact ranks.
       // About one point per bucket (S * B <= NM): most buckets need no comparison at all.
       const int maxsize = n >> t;
-      const int B = maxsize > rk::kSmallSeg ? int(rk::pow2_ceil(u32(maxsize))) : 1;
+      const int B = maxsize > rk::kSmallSeg ? min(int(rk::pow2_ceil(u32(maxsize))), NM >> t) : 1;
       const int nb = S * B;  // <= NM; work[nb] is the scan's total (sentinel)
       u32* tmpk = aux;       // orderable keys in bucket order
       const BucketParams pr = make_params(cellv[2 * axis], cellv[2 * axis + 1], B);
@@ -385,8 +388,10 @@ void k_subtree_rank(SubArgs a) {
       }
       __syncthreads();
       if (t == 0) stamp(a, 23);
-      wz = t + 1 < lsub && words_of(t + 1) == 0;
-      if (wz) {  // the next level ranks by histogram too: its buckets + sentinel, zeroed now
+      // the next level's buckets + sentinel (first use) or bitmaps (compressed), zeroed now
+      wz = t + 1 < lsub;
+      cb = 0;
+      if (wz) {
 #pragma unroll
         for (int j = 0; j <= ITEMS; ++j) {
           const int w = tid + j * THREADS;
@@ -444,7 +449,7 @@ void k_subtree_rank(SubArgs a) {
         const u32 is_mid = u32(n0 != 0) & u32(r == mid);
         const u32 right = u32(r > mid);
         const u32 fslot = lo[i] + mid, rr = r - mid - 1, lr = lo[i] + mid + 1, nr = n0 - mid - 1;
-        fin[is_mid ? fslot : u32(NM) + lane_dummy] = u32(kid(i));
+        fin[is_mid ? fslot : u32(NM) + lane_dummy] = u16(kid(i));
         cn[i] = right ? rr : r;
         if (keep && ITEMS != 2) cr[tid + i * THREADS] = u16(cn[i]);
         lo[i] = right ? lr : lo[i];
@@ -508,7 +513,16 @@ void k_subtree_rank(SubArgs a) {
   stamp(a, 31);
 }
 
-template <int ITEMS, int THREADS>
+// WPE: waves per SIMD the register budget is pinned to (0: two blocks per CU below capacity
+// 4096, else one; a CU holds at most 8 waves per SIMD)
+template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0, int WPE = 0>
+__global__ __launch_bounds__(THREADS)
+__attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (ITEMS * THREADS >= 4096 ? 1 : 2) * THREADS / 256)))
+void k_subtree_rank(SubArgs a) {
+  subtree_rank_body<ITEMS, THREADS, NARROW, DIMC>(a);
+}
+
+template <int ITEMS, int THREADS, int WPE3 = 0>
 void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
   SubArgs a = a0;
   if (a.ldim > 0) {  // a key slot for every level a segment of this capacity can have
@@ -526,10 +540,10 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
     k_subtree_rank<ITEMS, THREADS, true><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
     done = true;
   }
-  if constexpr (ITEMS == 2) {
+  if constexpr (ITEMS == 2 || ITEMS * THREADS == 1536) {
     if (!done && a.dim == 3) {
-      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 3>), int(kLdsMax));
-      k_subtree_rank<ITEMS, THREADS, false, 3><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
+      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 3, WPE3>), int(kLdsMax));
+      k_subtree_rank<ITEMS, THREADS, false, 3, WPE3><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
       done = true;
     }
   }
@@ -639,7 +653,18 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
       const char* e = std::getenv("PKD_SUBTREE_CFG");
       return std::string(e ? e : "");
     }();
+    static const bool c1536 = [] {
+      const char* e = std::getenv("PKD_SUBTREE_1536");
+      return !(e && std::string(e) == "0");
+    }();
     if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);
+    // 3-D segments of 1025..1536 points (100M / 2^16 and 12.5M / 2^13: 1525 points): capacity
+    // 1536 = 3 items x 512 threads, 52 KiB of LDS, three workgroups (24 waves) per CU. Against
+    // 2 x 1024 (4 idle waves of 16 at 1525 points, two workgroups per CU): 100M x 3D 11.64 ->
+    // 11.14-11.43 ms, 12.5M 1.753 -> 1.680 ms; 2 x 768 (two workgroups of 12 waves) was in
+    // between (profiles/r3_subtree_1536.txt)
+    else if (nmax > 1024 && nmax <= 1536 && wide && c1536 && dim == 3 && a.ldim == 0)
+      launch_rank_cfg<3, 512, 6>(a, segs, stream);
     else if (nmax > 1024 && wide) launch_rank_cfg<2, 1024>(a, segs, stream);
     else if (nmax > 1024) launch_rank_cfg<4, 512>(a, segs, stream);
     // Segments of 513..1024 / 257..512 points (dims >= 4, whose rows fill the LDS sooner): the

@@ -45,6 +45,7 @@ struct Tuning {
   int atomic_ranks = -1;      // PKD_PART_ATOMIC: pair scatter ranks zones by LDS atomics (1) or
   int atomic_ranks3 = -1;     //   wave ballots (0); PKD_PART3_ATOMIC the same for triples; -1: by n
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
+  bool tail = false;          // PKD_TAIL=1: the last three global levels in one workgroup per segment (k_tail3)
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
   int colgroup = 0;           // PKD_COLGROUP: columns per load round of wide rows (0: by dim)
@@ -69,6 +70,7 @@ struct LevelPlan {
   bool stage2 = false;  // median bucket split by a second (key-only) histogram pass
   bool pair = false;    // this level and the next are moved by ONE fused partition pass
   bool triple = false;  // this level and the next two are moved by ONE fused partition pass
+  bool tail = false;    // this level and the next two: one workgroup per segment (k_tail3)
 };
 
 struct SplitStreams;  // side HIP streams + fork / join events of a split build
@@ -146,6 +148,8 @@ class GpuBuilder {
   i64 max_hist_ = 0;
   i64 max_hist2_ = 0;
   bool narrow_ = false;  // high-dim: narrow columns + key-slot subtree (capacity nsub_ sized for it)
+  int tail_ = -1;        // first of the last three global levels, built by k_tail3 (-1: none)
+  int tail_items_ = 0;   // rows per thread of its 1024-thread workgroups
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,

@@ -65,6 +65,45 @@ def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic):
     check_same(pk.generate_problem(14, 3, 900_000), gpu_device, depth0=2)
 
 
+@pytest.mark.parametrize("n", [1025, 1100, 1525, 1536, 1537, 3100, 6143, 12_500_000])
+def test_subtree_capacity_1536(gpu_device, n):
+    """3-D leaf segments of 1025..1536 points take the non-power-of-two LDS subtree shape
+    (3 items x 512 threads: bucket counts capped at the capacity, u16 slot
+    table, bitmaps aliasing the bucket-order index list): slot for slot the CPU exact tree,
+    also with heavy duplicates."""
+    check_same(pk.generate_problem(n % 97, 3, n), gpu_device)
+    if n < 100_000:
+        check_same(torch.randint(0, 3, (n, 3)).float(), gpu_device)
+        check_same(pk.generate_problem(n % 89, 3, n), gpu_device, depth0=1)
+
+
+@pytest.mark.parametrize("n,dim", [(40_000, 3), (70_000, 3), (100_000, 3), (200_000, 1), (150_000, 2), (120_000, 5),
+                                   (60_000, 8)])
+def test_tail_levels(gpu_device, monkeypatch, n, dim):
+    """The last three global levels in one workgroup per segment (k_tail3: bucket bins, wave
+    ranking of the median bin or the radix-select fallback for heavy duplicates, LDS-staged
+    leaf scatter): slot for slot the CPU exact tree."""
+    monkeypatch.setenv("PKD_TAIL", "1")
+    b = ops.GpuTreeBuilder(n, dim)
+    assert "tail" in b.describe(), b.describe()
+    check_same(pk.generate_problem(n % 101, dim, n), gpu_device)
+    check_same(torch.randint(0, 3, (n, dim)).float(), gpu_device)
+    check_same(torch.randint(0, 200, (n, dim)).float(), gpu_device)
+    check_same(pk.generate_problem(n % 103, dim, n), gpu_device, depth0=dim + 1)
+
+
+def test_tail_levels_off_equal(gpu_device, monkeypatch):
+    x = pk.generate_problem(5, 3, 3_000_000).to(gpu_device)
+    monkeypatch.setenv("PKD_TAIL", "1")
+    _, ti = ops.GpuTreeBuilder(3_000_000, 3).build(x)
+    monkeypatch.setenv("PKD_TAIL", "0")
+    b = ops.GpuTreeBuilder(3_000_000, 3)
+    assert "tail" not in b.describe()
+    _, ti0 = b.build(x)
+    torch.cuda.synchronize()
+    assert torch.equal(ti, ti0)
+
+
 def test_depth0(gpu_device):
     check_same(pk.generate_problem(8, 3, 100_000), gpu_device, depth0=1)
 
