@@ -2797,7 +2797,7 @@ Tuning Tuning::from_env() {
   t.atomic_ranks = int(env_i("PKD_PART_ATOMIC", -1));
   t.atomic_ranks3 = int(env_i("PKD_PART3_ATOMIC", -1));
   t.prefix = env_i("PKD_PART_PREFIX", 1) != 0;
-  t.tail = env_i("PKD_TAIL", 0) != 0;
+  t.tail = env_i("PKD_TAIL", 1) != 0;
   t.split = env_i("PKD_SPLIT", 1) != 0;
   t.split_trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
   t.colgroup = int(env_i("PKD_COLGROUP", 0));
@@ -3393,9 +3393,10 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             ensure_dynamic_lds(reinterpret_cast<const void*>(kern), int(lds));
             kern<<<int(segs), kTailThreads, lds, st>>>(ta);
           };
-          static const bool one = std::getenv("PKD_TAIL_ONE") != nullptr;  // A/B: one block per CU
-          if (tail_items_ == 8) one ? go(&k_tail3<D, 8, 4>) : go(&k_tail3<D, 8, 8>);
-          else if (tail_items_ == 12) one ? go(&k_tail3<D, 12, 4>) : go(&k_tail3<D, 12, 8>);
+          // one 1024-thread workgroup per CU (128 registers): the two-per-CU shape (64 registers)
+          // spills and was slower (100M x 3D k_tail3 1.41 vs 1.32 ms, profiles/r3_tail.txt)
+          if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
+          else if (tail_items_ == 12) go(&k_tail3<D, 12, 4>);
           else go(&k_tail3<D, 16, 4>);
         }
       });

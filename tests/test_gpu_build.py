@@ -53,6 +53,7 @@ def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic):
     """Three levels per scatter pass (k_scan2 + k_partition3, from level 0 or 3) with zone ranks
     from wave ballots or LDS atomics (also in the pair scatters): slot for slot the CPU exact
     tree on uniform, duplicate-heavy, 2-D, 8-D and odd-depth inputs."""
+    monkeypatch.setenv("PKD_TAIL", "0")  # the last three levels stay triples too
     monkeypatch.setenv("PKD_TRIPLE_FROM", triple_from)
     monkeypatch.setenv("PKD_PART_ATOMIC", atomic)
     monkeypatch.setenv("PKD_PART3_ATOMIC", atomic)
