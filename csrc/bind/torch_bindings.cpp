@@ -21,6 +21,7 @@
 
 namespace pkdtree {
 std::string subtree_stamp_report();
+std::string tail_stamp_report();
 }
 
 namespace pk = pkdtree;
@@ -357,5 +358,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nn_finalize", &nn_finalize, py::arg("packed"));
   m.def("subtree_capacity", &pk::default_subtree_max);
   m.def("subtree_stamp_report", &pk::subtree_stamp_report);
+  m.def("tail_stamp_report", &pk::tail_stamp_report);
   pkdtree::bind_dist_ops(m);
 }

@@ -19,6 +19,7 @@
 #include <string>
 #include <type_traits>
 #include <sstream>
+#include <vector>
 
 #include "device_utils.hpp"
 #include "pkdtree/gpu_build.hpp"
@@ -2418,7 +2419,13 @@ struct TailArgs {
   float* out_pts;
   u32* out_ids;
   u32* err;
+  unsigned long long* stamps;  // diagnostic (PKD_TAIL_STAMPS=1): [block][kTailStampSlots] s_memtime, else null
 };
+constexpr int kTailStampSlots = 24, kTailStampBlocks = 2048;
+__device__ __forceinline__ void tail_stamp(const TailArgs& a, int slot) {
+  if (a.stamps != nullptr && blockIdx.x < kTailStampBlocks && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64)
+    a.stamps[blockIdx.x * kTailStampSlots + slot] = __builtin_amdgcn_s_memtime();
+}
 
 // exclusive scan over the 1024 threads of a block (one value each); *total = the sum.
 // Caller: a barrier between two uses (wsum is reused).
@@ -2437,18 +2444,21 @@ template <int D, int ITEMS, int WPE>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
-  constexpr u32 kDead = 0xffffffffu;
+  // columns kept in registers: every column for D < 3, else the three levels' key columns
+  constexpr int KC = D < 3 ? D : 3;
+  constexpr u32 kDead = 0xffffffffu, kMed = 0x80000000u;  // absent row / median of tail node (low bits)
   static_assert(ITEMS % 4 == 0, "16-B groups of 4 rows");
   static_assert(CAP >= NB, "the stage buffer holds the bins");
-  extern __shared__ __align__(16) u32 stage[];  // CAP words: the output columns; the levels' bins alias it
+  extern __shared__ __align__(16) u32 stage[];  // CAP words: the output columns; bins / counters alias it
   u32* bins = stage;
-  __shared__ u32 ckey[4][kTailCand], crow[4][kTailCand];
-  __shared__ u32 ccnt[4], sbst[4], sbelow[4], srank[4], sstart[4], sn[4], wsum[W];
+  __shared__ u32 ckey[4][kTailCand], cid[4][kTailCand];
+  __shared__ u32 ccnt[4], sbst[4], srank[4], wsum[W];
   __shared__ unsigned long long spiv[4];
   __shared__ float scell[2][8][D][2];  // cells of the level's sub-segments / of their children
   __shared__ BucketParams sprm[4];
-  __shared__ u32 wc[W][8], wbase[W][8];
-  __shared__ u32 sbig, smrow[4];
+  __shared__ i64 nlo[15];              // segment starts of the tail's 15 nodes (heap order below h)
+  __shared__ u32 nn[15];
+  __shared__ u32 sbig;
   const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
   const i64 h = a.heap0 + blockIdx.x;
   const i64 lo = a.seg_lo[h];
@@ -2459,90 +2469,91 @@ void k_tail3(TailArgs a) {
     if (tid == 0) atomicOr(a.err, 16u);
     return;
   }
+  tail_stamp(a, 0);
   const i64 nc = a.ncol;
   // Item i = 4 g + j of a thread is row (g * T + tid) * 4 + j - shift of the segment: one 16-B
   // load per group of 4 rows. Rows are addressed through buffer descriptors (one per column,
   // wave-uniform): the lane offset tid * 16 is the only per-lane address register, g's
-  // g * 16 KiB the scalar offset, j's 4 j the immediate.
+  // g * 16 KiB the scalar offset.
   const u32 vo = u32(tid) * 16u;
   const i64 alo = lo - shift;
   const int recs = (shift + n + 3) & ~3;
   auto col = [&](const float* base, int c) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + i64(c) * nc + alo), 0, recs * 4, 0x00020000);
   };
-  const auto idr = col(a.src, D);
-  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, u32 row) {  // row relative to lo
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (row + u32(shift)) * 4u, 0, 0);
-  };
   auto ld4 = [&](const __amdgpu_buffer_rsrc_t& r, int g) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, vo, u32(g * T * 16), 0);
   };
-  auto ldi = [&](const __amdgpu_buffer_rsrc_t& r, int i) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + u32(i % 4) * 4u, u32((i / 4) * T * 16), 0);
-  };
-  // row (relative to lo) of item i, recomputed at each (rare) use: kept opaque so the
-  // compiler does not hold one register per item for it across the whole kernel
-  auto rowof = [&](int i) {
-    u32 t4 = u32(tid);
-    asm volatile("" : "+v"(t4));
-    return (u32((i / 4) * T) + t4) * 4u + u32(i % 4) - u32(shift);
-  };
+  // every row's level keys and id, loaded at once (the whole segment in flight)
+  int axis_of[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
+  float xs[KC][ITEMS];
+  u32 ids[ITEMS];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const auto r = col(a.src, D < 3 ? k : axis_of[k]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto v = ld4(r, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xs[k][4 * g + j] = __uint_as_float(v[j]);
+    }
+  }
+  {
+    const auto r = col(a.src, D);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto v = ld4(r, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ids[4 * g + j] = v[j];
+    }
+  }
+  if (tid < 15) {  // node k (heap order: 0 = h, 1-2 children, 3-6 grandchildren, 7-14 leaves)
+    const int lev = tid >= 7 ? 3 : (tid >= 3 ? 2 : (tid >= 1 ? 1 : 0));
+    const i64 hk = (h + 1) * (i64(1) << lev) - 1 + (tid - ((1 << lev) - 1));
+    nlo[tid] = a.seg_lo[hk];
+    nn[tid] = u32(a.seg_n[hk]);
+  }
   if (tid < 2 * D) (&scell[0][0][0][0])[tid] = a.cells[h * 2 * D + tid];
-  if (tid < W * 8) (&wc[0][0])[tid] = 0;
   // path: the row's sub-segment at the current level (while a level bins, its bin: the
-  // sub-segment is bin >> lgB), kDead for absent / median rows
+  // sub-segment is bin >> lgB); kDead for absent rows, kMed | node for the tail's medians
   u32 path[ITEMS];
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
     const int r = (i / 4 * T + tid) * 4 + i % 4 - shift;
     path[i] = (r >= 0 && r < n) ? 0u : kDead;
   }
-#pragma unroll 1
+#pragma unroll
   for (int t = 0; t < 3; ++t) {
-    // the thread index, opaque per level: values derived from it (LDS and global addresses of
-    // the few-thread steps) are recomputed each level instead of being hoisted into registers
-    // that live across the whole kernel
+    // the thread index, opaque per level: addresses derived from it (LDS and global, of the
+    // few-thread steps) are recomputed per level instead of held in registers across levels
     int tq = tid;
     asm volatile("" : "+v"(tq));
     const int wq = tq / 64, lq = tq & 63;
     const int S = 1 << t, B = NB >> t, lgB = 12 - t;
     static_assert(NB == 4096, "lgB");
-    const int axis = (a.depth0 + a.level + t) % D;
-    const i64 hs0 = (h + 1) * S - 1;  // the level's first sub-segment (heap index)
-    const auto kr = col(a.src, axis);
-    float key[ITEMS];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const auto v = ld4(kr, g);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) key[4 * g + j] = __uint_as_float(v[j]);
-    }
+    const int axis = axis_of[t];
+    const int kx = D < 3 ? axis : t;  // register set of this level's keys
     for (int b = tq; b < NB; b += T) bins[b] = 0;
     if (tq < 4) {
       ccnt[tq] = 0;
-      smrow[tq] = 0xffffffffu;
       sbst[tq] = 0xffffffffu;
       spiv[tq] = ~0ull;
     }
-    if (tq == 0) {
-      u32 run = 0;
-      for (int s = 0; s < S; ++s) {
-        sn[s] = u32(a.seg_n[hs0 + s]);
-        sstart[s] = run;
-        run += sn[s];
-      }
-    }
+    if (t == 0) __syncthreads();  // nn / scell
     if (tq < S) {
       const float* c = &scell[t & 1][tq][axis][0];
       sprm[tq] = make_params(c[0], c[1], B);
     }
     __syncthreads();
+    tail_stamp(a, 1 + 4 * t);
     // ---- bins ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      if (path[i] != kDead) {
+      if (path[i] < kMed) {
         const u32 sp = path[i];
-        path[i] = sp * u32(B) + bucket_of(key[i], sprm[sp], B);
+        path[i] = sp * u32(B) + bucket_of(xs[kx][i], sprm[sp], B);
         atomicAdd(&bins[path[i]], 1u);
       }
     }
@@ -2557,42 +2568,43 @@ void k_tail3(TailArgs a) {
       u32 total;
       const u32 ex = block_excl_scan1024(sum, wsum, &total, tq);
       const int sp = tq * (NB / T) / B;  // B is a multiple of NB / T: a thread's bins share a sub-segment
-      u32 run = ex - sstart[sp];
-      const u32 m = sn[sp] / 2;
+      u32 start = 0;
+      for (int q = 0; q < sp; ++q) start += nn[S - 1 + q];
+      u32 run = ex - start;
+      const u32 m = nn[S - 1 + sp] / 2;
 #pragma unroll
       for (int j = 0; j < NB / T; ++j) {
         if (run <= m && m < run + c[j]) {
           sbst[sp] = u32(tq * (NB / T) + j);
-          sbelow[sp] = run;
           srank[sp] = m - run;
         }
         run += c[j];
       }
     }
     __syncthreads();
-    // ---- candidates of the median bins ----
+    tail_stamp(a, 2 + 4 * t);
+    // ---- candidates of the median bins: (key, id) straight from registers ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const u32 sp = path[i] >> lgB;
-      if (path[i] != kDead && path[i] == sbst[sp]) {
+      if (path[i] < kMed && path[i] == sbst[sp]) {
         const u32 k = atomicAdd(&ccnt[sp], 1u);
         if (k < u32(kTailCand)) {
-          ckey[sp][k] = orderable(key[i]);
-          crow[sp][k] = rowof(i);
+          ckey[sp][k] = orderable(xs[kx][i]);
+          cid[sp][k] = ids[i];
         }
       }
     }
     __syncthreads();
     if (tq == 0) {
       u32 big = 0;
-      for (int s = 0; s < S; ++s) big |= ccnt[s] > u32(kTailCand) ? 1u : 0u;
+      for (int q = 0; q < S; ++q) big |= ccnt[q] > u32(kTailCand) ? 1u : 0u;
       sbig = big;
     }
     if (wq < S) {  // wave s ranks sub-segment s's candidates (results unused if any list overflowed)
       const int sp = wq;
       const int m = int(min(ccnt[sp], u32(kTailCand)));
-      u64 ck = ~0ull;
-      if (lq < m) ck = (u64(ckey[sp][lq]) << 32) | u64(ld(idr, crow[sp][lq]));
+      const u64 ck = lq < m ? (u64(ckey[sp][lq]) << 32) | u64(cid[sp][lq]) : ~0ull;
       u32 rank = 0;
 #pragma unroll 1
       for (int j = 0; j < m; ++j) rank += dev::shfl_u64(ck, j) < ck ? 1u : 0u;
@@ -2612,8 +2624,8 @@ void k_tail3(TailArgs a) {
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
           const u32 sp = path[i] >> lgB;
-          if (path[i] != kDead && path[i] == sbst[sp]) {  // (rare path: ids re-read per pass)
-            const u64 ck = (u64(orderable(key[i])) << 32) | u64(ldi(idr, i));
+          if (path[i] < kMed && path[i] == sbst[sp]) {
+            const u64 ck = (u64(orderable(xs[kx][i])) << 32) | u64(ids[i]);
             if (((ck ^ spiv[sp]) & known) == 0) atomicAdd(&bins[sp * 256 + u32((ck >> sh) & 255u)], 1u);
           }
         }
@@ -2645,42 +2657,21 @@ void k_tail3(TailArgs a) {
         __syncthreads();
       }
     }
-    // ---- classify: left / right of the pivot; the median row goes to its output slot ----
+    tail_stamp(a, 3 + 4 * t);
+    // ---- classify: left / right of the pivot; the median row is marked (written with the columns) ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      if (path[i] == kDead) continue;
+      if (path[i] >= kMed) continue;
       const u32 sp = path[i] >> lgB;
       const u64 pv = spiv[sp];
-      const u32 ok = orderable(key[i]), pk = u32(pv >> 32);
-      u32 right = ok > pk ? 1u : 0u;
-      if (ok == pk) {
-        const u32 id = ldi(idr, i);
-        const u64 ck = (u64(ok) << 32) | u64(id);
-        if (ck == pv) {  // the median row: written to its slot after the barrier
-          smrow[sp] = rowof(i);
-          path[i] = kDead;
-          continue;
-        }
-        right = ck > pv ? 1u : 0u;
-      }
-      path[i] = 2 * sp + right;
-    }
-    __syncthreads();
-    if (tq < S * (D + 1)) {  // the medians' rows to their output slots, one column per thread
-      const int sp = tq / (D + 1), c = tq % (D + 1);
-      const i64 hs = hs0 + sp;
-      const i64 slot = a.seg_lo[hs] + a.seg_n[hs] / 2;
-      const u32 r = smrow[sp];
-      if (r < u32(n)) {
-        const float v = a.src[i64(c) * nc + lo + r];
-        if (c < D) a.out_pts[slot * D + c] = v;
-        else a.out_ids[slot] = __float_as_uint(v);
-      }
+      const u64 ck = (u64(orderable(xs[kx][i])) << 32) | u64(ids[i]);
+      path[i] = ck == pv ? (kMed | u32(S - 1 + sp)) : 2 * sp + (ck > pv ? 1u : 0u);
     }
     if (tq < 2 * S) {  // children cells: the pivot key bounds the split axis
       const int sp = tq / 2, side = tq & 1;
       const float pkf = from_orderable(u32(spiv[sp] >> 32));
-      float* gc = a.cells + (2 * (hs0 + sp) + 1 + side) * 2 * D;
+      const i64 hs = (h + 1) * S - 1 + sp;
+      float* gc = a.cells + (2 * hs + 1 + side) * 2 * D;
 #pragma unroll
       for (int c = 0; c < D; ++c) {
         float clo = scell[t & 1][sp][c][0], chi = scell[t & 1][sp][c][1];
@@ -2695,42 +2686,95 @@ void k_tail3(TailArgs a) {
       }
     }
     __syncthreads();
+    tail_stamp(a, 4 + 4 * t);
   }
-  // ---- move: position inside the leaf, then each column through LDS in leaf order ----
+  // ---- move: position inside the leaf (one LDS counter per 16 lanes and leaf), then each
+  // column staged through LDS in leaf order and written back coalesced ----
+  constexpr int kGroups = W * 4;
+  static_assert(CAP >= kGroups * 8, "counters in the stage buffer");
+  __shared__ u32 gbase[kGroups][8];
+  u32* gcnt = stage;
+  const int grp = tid / 16;
+  if (tid < kGroups * 8) gcnt[tid] = 0;
+  __syncthreads();
   u32 pos[ITEMS];
 #pragma unroll
-  for (int i = 0; i < ITEMS; ++i) pos[i] = path[i] != kDead ? atomicAdd(&wc[w][path[i]], 1u) : 0u;
+  for (int i = 0; i < ITEMS; ++i) pos[i] = path[i] < kMed ? atomicAdd(&gcnt[grp * 8 + path[i]], 1u) : 0u;
   __syncthreads();
   if (tid < 8) {
-    const i64 hl = (h + 1) * 8 - 1 + tid;
-    const u32 first = u32(a.seg_lo[hl] - lo);
+    const u32 first = u32(nlo[7 + tid] - lo);
     u32 off = first;
-    for (int k = 0; k < W; ++k) {
-      wbase[k][tid] = off;
-      off += wc[k][tid];
+    for (int k = 0; k < kGroups; ++k) {
+      gbase[k][tid] = off;
+      off += gcnt[k * 8 + tid];
     }
-    if (i64(off - first) != a.seg_n[hl]) atomicOr(a.err, 16u);
+    if (off - first != nn[7 + tid]) atomicOr(a.err, 16u);
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i)
-    if (path[i] != kDead) pos[i] += wbase[w][path[i]];
-#pragma unroll 1
+    if (path[i] < kMed) path[i] = pos[i] + gbase[grp][path[i]];
+  tail_stamp(a, 13);
+#pragma unroll
   for (int c = 0; c <= D; ++c) {
-    const auto sr = col(a.src, c);
-    const auto dr = col(a.dst, c);
+    // column c: from registers (a level's keys or the ids), else loaded
+    int kreg = -1;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const auto v = ld4(sr, g);
+    for (int k = 0; k < KC; ++k)
+      if ((D < 3 ? k : axis_of[k]) == c) kreg = k;
+    u32 v[ITEMS];
+    if (c == D) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (path[4 * g + j] != kDead) stage[pos[4 * g + j]] = v[j];
+      for (int i = 0; i < ITEMS; ++i) v[i] = ids[i];
+    } else if (kreg >= 0) {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        u32 x = 0;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) x = k == kreg ? __float_as_uint(xs[k][i]) : x;
+        v[i] = x;
+      }
+    } else {
+      const auto r = col(a.src, c);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const auto q = ld4(r, g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * g + j] = q[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      if (path[i] < kMed) {
+        stage[path[i]] = v[i];
+      } else if (path[i] != kDead) {  // a tail median: straight to its output slot
+        const int k = int(path[i] & 15u);
+        const i64 slot = nlo[k] + nn[k] / 2;
+        if (c < D) a.out_pts[slot * D + c] = __uint_as_float(v[i]);
+        else a.out_ids[slot] = v[i];
+      }
     }
     __syncthreads();
+    const auto dr = col(a.dst, c);
 #pragma unroll 4
     for (int p = tid; p < n; p += T) __builtin_amdgcn_raw_buffer_store_b32(stage[p], dr, u32(p + shift) * 4u, 0, 0);
     __syncthreads();
+    tail_stamp(a, 14 + c);
   }
+}
+
+size_t tail_lds_bytes(int items) { return size_t(items) * kTailThreads * 4; }  // k_tail3's dynamic LDS
+
+unsigned long long* tail_stamp_buffer() {  // PKD_TAIL_STAMPS=1 (diagnostic): allocated once, else null
+  static unsigned long long* p = [] {
+    unsigned long long* q = nullptr;
+    if (std::getenv("PKD_TAIL_STAMPS")) {
+      PKD_HIP_CHECK(hipMalloc(&q, size_t(kTailStampBlocks) * kTailStampSlots * 8));
+      PKD_HIP_CHECK(hipMemset(q, 0, size_t(kTailStampBlocks) * kTailStampSlots * 8));
+    }
+    return q;
+  }();
+  return p;
 }
 
 // Calls f(std::integral_constant<int, dim + 1>) for dim <= 8 (rows in registers), else
@@ -3384,8 +3428,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const LevelPlan& lp = levels_[size_t(tail_)];
       const i64 segs = lp.segs / nparts;
       TailArgs ta{src, dst, ncol_, seg_lo, seg_n, cells, lp.segs - 1 + i64(part) * segs, tail_, opt_.depth0,
-                  out_pts, out_ids, err};
-      const size_t lds = size_t(tail_items_) * kTailThreads * 4;
+                  out_pts, out_ids, err, tail_stamp_buffer()};
+      const size_t lds = tail_lds_bytes(tail_items_);
       with_ncol(dim_, [&](auto nc) {
         constexpr int D = decltype(nc)::value - 1;
         if constexpr (D >= 1) {
@@ -3481,6 +3525,34 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     std::fprintf(stderr, "%s\n", os.str().c_str());
     for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   }
+}
+
+// Diagnostic: mean cycles of each k_tail3 phase (PKD_TAIL_STAMPS=1) over the recorded blocks.
+std::string tail_stamp_report() {
+  unsigned long long* d = tail_stamp_buffer();
+  if (!d) return "tail stamps disabled (set PKD_TAIL_STAMPS=1)";
+  std::vector<unsigned long long> h(size_t(kTailStampBlocks) * kTailStampSlots);
+  PKD_HIP_CHECK(hipDeviceSynchronize());
+  PKD_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+  static const char* names[kTailStampSlots] = {"start", "L0.load", "L0.bins", "L0.select", "L0.classify", "L1.load",
+                                               "L1.bins", "L1.select", "L1.classify", "L2.load", "L2.bins",
+                                               "L2.select", "L2.classify", "move.rank", "col0", "col1", "col2", "col3",
+                                               "col4", "col5", "col6", "col7", "col8", "x"};
+  double acc[kTailStampSlots] = {};
+  int cnt[kTailStampSlots] = {};
+  for (int b = 0; b < kTailStampBlocks; ++b) {
+    const unsigned long long* s = &h[size_t(b) * kTailStampSlots];
+    for (int i = 1; i < kTailStampSlots; ++i)
+      if (s[i] && s[i - 1]) {
+        acc[i] += double(s[i] - s[i - 1]);
+        ++cnt[i];
+      }
+  }
+  std::ostringstream os;
+  os << "tail stamps (mean cycles per phase):";
+  for (int i = 1; i < kTailStampSlots; ++i)
+    if (cnt[i]) os << " " << names[i] << "=" << long(acc[i] / cnt[i]);
+  return os.str();
 }
 
 }  // namespace pkdtree

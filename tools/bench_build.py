@@ -45,6 +45,9 @@ for dim in args.dim:
             if os.environ.get("PKD_SUBTREE_STAMPS"):
                 from parallel_kd_tree_amd.ops import native
                 print(native().subtree_stamp_report(), flush=True)
+            if os.environ.get("PKD_TAIL_STAMPS"):
+                from parallel_kd_tree_amd.ops import native
+                print(native().tail_stamp_report(), flush=True)
             print(json.dumps({"n": n, "dim": dim, "subtree_max": b.subtree_max, "global_levels": b.global_levels,
                               "ms": round(ms, 3), "mpts_s": round(n / ms / 1e3, 1), "err": err, "same_as_first": same}),
                   flush=True)
