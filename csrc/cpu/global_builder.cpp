@@ -29,11 +29,18 @@ double Comm::default_timeout() {
 }
 
 void Comm::wait(hipStream_t stream, const char* what) { poll_until_done(stream, what, {}); }
+void Comm::wait_event(hipEvent_t event, const char* what) {
+  poll_query([&] { return hipEventQuery(event); }, what, {});
+}
 
 void Comm::poll_until_done(hipStream_t stream, const char* what, const std::function<void()>& probe) {
+  poll_query([&] { return hipStreamQuery(stream); }, what, probe);
+}
+
+void Comm::poll_query(const std::function<hipError_t()>& query, const char* what, const std::function<void()>& probe) {
   const auto t0 = std::chrono::steady_clock::now();
   for (long it = 0;; ++it) {
-    const hipError_t q = hipStreamQuery(stream);
+    const hipError_t q = query();
     if (q == hipSuccess) return;
     if (q != hipErrorNotReady)
       throw std::runtime_error("rank " + std::to_string(rank()) + ": " + what + ": " + hipGetErrorString(q));
@@ -256,6 +263,8 @@ GlobalBuilder::GlobalBuilder(Comm& comm, i64 n_total, int dim, int pipeline_k)
   arrived_.assign(size_t(lay_.R), nullptr);
   for (auto& e : arrived_) PKD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   PKD_HIP_CHECK(hipEventCreateWithFlags(&packed_, hipEventDisableTiming));
+  PKD_HIP_CHECK(hipEventCreateWithFlags(&counted_, hipEventDisableTiming));
+  PKD_HIP_CHECK(hipEventCreateWithFlags(&plan_ready_, hipEventDisableTiming));
 }
 
 GlobalBuilder::~GlobalBuilder() {
@@ -267,6 +276,8 @@ GlobalBuilder::~GlobalBuilder() {
   for (hipEvent_t e : arrived_) (void)hipEventDestroy(e);
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   if (packed_) (void)hipEventDestroy(packed_);
+  if (counted_) (void)hipEventDestroy(counted_);
+  if (plan_ready_) (void)hipEventDestroy(plan_ready_);
   if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   if (host_counts_) (void)hipHostFree(host_counts_);
 }
@@ -411,20 +422,25 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     top_counts_init(counts, T, i64(id_base), n_local, s);
     auto* bm = static_cast<u32*>(buf(12, size_t(T) * send_words * 4));
     void* scratch = buf(13, top_pack_scratch_bytes(n_local, T));
-    top_pack(tp, node, LL, send, dim, send_stride, bm, send_words, counts, err, scratch, s);
-    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvPack), s));
-    // 4. the count matrix, all-gathered: the one host read-back of the build (bounded wait)
+    top_pack_count(tp, node, LL, counts, err, scratch, s);
+    // 4. the count matrix, all-gathered on the communication stream and read back to the host
+    // (the one host read-back of the build, bounded wait) while the pack's scatter runs
     auto* all = static_cast<i64*>(buf(14, size_t(P) * T * 4 * 8));
-    comm_.allgather(counts, all, size_t(T) * 4 * 8, s);
     const size_t nall = size_t(P) * T * 4;
     if (host_counts_n_ < nall) {
       if (host_counts_) PKD_HIP_CHECK(hipHostFree(host_counts_));
       PKD_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counts_), nall * 8, hipHostMallocDefault));
       host_counts_n_ = nall;
     }
-    PKD_HIP_CHECK(hipMemcpyAsync(host_counts_, all, nall * 8, hipMemcpyDeviceToHost, s));
+    PKD_HIP_CHECK(hipEventRecord(counted_, s));
+    PKD_HIP_CHECK(hipStreamWaitEvent(comm_stream_, counted_, 0));
+    comm_.allgather(counts, all, size_t(T) * 4 * 8, comm_stream_);
+    PKD_HIP_CHECK(hipMemcpyAsync(host_counts_, all, nall * 8, hipMemcpyDeviceToHost, comm_stream_));
+    PKD_HIP_CHECK(hipEventRecord(plan_ready_, comm_stream_));
+    top_pack_scatter(tp, node, LL, send, dim, send_stride, bm, send_words, scratch, s);
+    if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(kEvPack), s));
     const auto w0 = std::chrono::steady_clock::now();
-    comm_.wait(s, "exchange plan");
+    comm_.wait_event(plan_ready_, "exchange plan");
     info.plan_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     const std::vector<i64> hall(host_counts_, host_counts_ + nall);
     if (global_plan::make_plan(hall, lay_, me, &plan) == 0) break;

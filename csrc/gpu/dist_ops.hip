@@ -782,6 +782,27 @@ size_t top_pack_scratch_bytes(i64 n, int T) { return size_t(2) * pack_blocks(n) 
 
 void top_pack(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
               u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch, hipStream_t stream) {
+  top_pack_count(p, node, levels, counts, err, scratch, stream);
+  top_pack_scatter(p, node, levels, out, row_stride, col_stride, bitmaps, bitmap_words, scratch, stream);
+}
+
+void top_pack_count(const TopPoints& p, const u32* node, int levels, i64* counts, const u32* err, void* scratch,
+                    hipStream_t stream) {
+  if (levels < 0 || levels > 6) throw std::invalid_argument("top_pack: at most 6 top levels (64 leaves)");
+  const int T = 1 << levels;
+  const int blocks = pack_blocks(p.n);
+  const i64 per_block = ((std::max<i64>(p.n, 1) + blocks - 1) / blocks + 255) / 256 * 256;
+  u32* bcount = static_cast<u32*>(scratch);
+  u32* offsets = bcount + size_t(blocks) * T;
+  k_pack_count<<<blocks, kBlock, 0, stream>>>(node, p.n, levels, T, per_block, bcount);
+  PKD_LAUNCH_CHECK();
+  static_assert(2 * kScanThreads >= 2048, "k_pack_scan covers at most 2 * kScanThreads blocks");
+  k_pack_scan<<<T, kScanThreads, 0, stream>>>(bcount, blocks, T, offsets, counts, err);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_pack_scatter(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
+                      u32* bitmaps, i64 bitmap_words, const void* scratch, hipStream_t stream) {
   if (levels < 0 || levels > 6) throw std::invalid_argument("top_pack: at most 6 top levels (64 leaves)");
   const int T = 1 << levels;
   if (col_stride > 0 && (col_stride < p.n || p.ids != nullptr))
@@ -792,13 +813,7 @@ void top_pack(const TopPoints& p, const u32* node, int levels, float* out, int r
   const int blocks = pack_blocks(p.n);
   // rows per block a multiple of 256: every wave's 64 rows of a chunk are two whole bitmap words
   const i64 per_block = ((std::max<i64>(p.n, 1) + blocks - 1) / blocks + 255) / 256 * 256;
-  u32* bcount = static_cast<u32*>(scratch);
-  u32* offsets = bcount + size_t(blocks) * T;
-  k_pack_count<<<blocks, kBlock, 0, stream>>>(node, p.n, levels, T, per_block, bcount);
-  PKD_LAUNCH_CHECK();
-  static_assert(2 * kScanThreads >= 2048, "k_pack_scan covers at most 2 * kScanThreads blocks");
-  k_pack_scan<<<T, kScanThreads, 0, stream>>>(bcount, blocks, T, offsets, counts, err);
-  PKD_LAUNCH_CHECK();
+  const u32* offsets = static_cast<const u32*>(scratch) + size_t(blocks) * T;
   k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, levels, T, per_block, offsets, out, row_stride, col_stride,
                                                 bitmaps, bitmap_words);
   PKD_LAUNCH_CHECK();

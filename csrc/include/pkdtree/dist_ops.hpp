@@ -100,6 +100,13 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
 size_t top_pack_scratch_bytes(i64 n, int T);
 void top_pack(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
               u32* bitmaps, i64 bitmap_words, i64* counts, const u32* err, void* scratch, hipStream_t stream);
+// top_pack in two steps: the per-leaf counts (written to `counts`; the scatter offsets stay in
+// `scratch`), then the scatter. The global builder starts the counts' all-gather and host
+// read-back between them, so the host's exchange planning overlaps the scatter.
+void top_pack_count(const TopPoints& p, const u32* node, int levels, i64* counts, const u32* err, void* scratch,
+                    hipStream_t stream);
+void top_pack_scatter(const TopPoints& p, const u32* node, int levels, float* out, int row_stride, i64 col_stride,
+                      u32* bitmaps, i64 bitmap_words, const void* scratch, hipStream_t stream);
 
 // Copies top-tree rows (dim + 1 floats: coordinates, id bits; heap order) into output slots:
 // out_pts[slot[i]] / out_ids[slot[i]] = top_rows[heap[i]] for i < count (<= 64).

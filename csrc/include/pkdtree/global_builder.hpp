@@ -42,6 +42,8 @@ class Comm {
   // The base implementation polls the stream; RcclComm also polls ncclCommGetAsyncError and
   // aborts the communicator before throwing.
   virtual void wait(hipStream_t stream, const char* what);
+  // The same bound for an event (work enqueued after it on its stream may still be running).
+  virtual void wait_event(hipEvent_t event, const char* what);
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   double timeout() const { return timeout_s_; }
   virtual void allreduce_sum_u32(u32* buf, size_t count, hipStream_t stream) = 0;
@@ -66,6 +68,8 @@ class Comm {
   // between polls and throws on a communicator error. Spins briefly (the plan wait is on the
   // build's critical path), then yields, then sleeps.
   void poll_until_done(hipStream_t stream, const char* what, const std::function<void()>& probe);
+  // `query` returns hipSuccess when done, hipErrorNotReady while pending (hipStreamQuery / hipEventQuery)
+  void poll_query(const std::function<hipError_t()>& query, const char* what, const std::function<void()>& probe);
   double timeout_s_ = default_timeout();
 
  private:
@@ -187,6 +191,8 @@ class GlobalBuilder {
   size_t leaf_ws_bytes_ = 0;
   std::vector<hipEvent_t> arrived_;  // per round (untimed), created once
   hipEvent_t packed_ = nullptr;
+  hipEvent_t counted_ = nullptr;     // the per-leaf counts are written (the pack's first step)
+  hipEvent_t plan_ready_ = nullptr;  // the all-gathered counts are in host memory
   bool profile_ = false;
   std::vector<hipEvent_t> events_;  // timed events of a profiled build (see set_profile)
   GlobalPhases last_;               // host-side parts of the last profiled build

@@ -42,8 +42,14 @@ class RcclComm final : public Comm {
   }
 
   void wait(hipStream_t s, const char* what) override {
+    wait_query([&] { return hipStreamQuery(s); }, what);
+  }
+  void wait_event(hipEvent_t e, const char* what) override {
+    wait_query([&] { return hipEventQuery(e); }, what);
+  }
+  void wait_query(const std::function<hipError_t()>& query, const char* what) {
     try {
-      poll_until_done(s, what, [&] {
+      poll_query(query, what, [&] {
         ncclResult_t async = ncclSuccess;
         PKD_RCCL(ncclCommGetAsyncError(c_, &async));
         if (async != ncclSuccess)
