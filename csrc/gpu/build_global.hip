@@ -2969,7 +2969,10 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   }
   const int lgrp = tail_ >= 0 ? tail_ : lg_;  // levels the pairs / triples cover
   for (int l = 0; pairs && l + 1 < lgrp;) {
-    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
+    // (four levels left: two pairs, not a triple and a lone level, whose single-level pass moves
+    // every row for one level: 100M x 8D level 13 alone took 1.7 ms)
+    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && lgrp - l != 4 &&
+                     !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
     int next = l + (tri ? 3 : 2);
     if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
     if (next - l == 3) {
