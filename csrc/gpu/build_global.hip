@@ -2855,6 +2855,7 @@ Tuning Tuning::from_env() {
   t.split_parts = int(env_i("PKD_SPLIT_PARTS", 4));
   t.split_streams = int(env_i("PKD_SPLIT_STREAMS", 4));
   t.split_min_n = env_i("PKD_SPLIT_MIN_N", i64(64) << 20);
+  t.split_min_n_3d = env_i("PKD_SPLIT_MIN_N_3D", std::getenv("PKD_SPLIT_MIN_N") ? t.split_min_n : i64(512) << 20);
   return t;
 }
 
@@ -2947,7 +2948,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   // narrowed by the two key sweeps k_scan / k_scan2 and k_refine alone); otherwise l and l+1
   // pair up. A triple never straddles the split level of a split build.
   const bool pairs = dim <= 8 && tune_.pairs;
-  const bool may_split = tune_.split && opt.allow_split && n_ >= tune_.split_min_n;
+  const bool may_split = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
   auto cap_bins = [&](int l, int cap) {  // level l's bins, fused into the previous pass's LDS
     if (l >= lg_) return;
     LevelPlan& g = levels_[size_t(l)];
@@ -2958,7 +2959,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   // 1024 threads x 8 / 12 / 16 rows (always, below the subtree capacity of 2048) and rows fit
   // registers (dim <= 8, full columns).
   // (A split build's parts start at split_level: the tail may not begin above it.)
-  const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min_n;
+  const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
   if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - 3 >= tune_.split_level)) {
     const i64 nl = (n_ >> (lg_ - 3)) + 3;  // + the 16-B alignment shift of the segment start
     tail_items_ = nl <= 8 * 1024 ? 8 : (nl <= 12 * 1024 ? 12 : (nl <= 16 * 1024 ? 16 : 0));
@@ -3022,7 +3023,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
       boundary = boundary || l == L;
       l += levels_[size_t(l)].triple ? 3 : (levels_[size_t(l)].pair ? 2 : 1);
     }
-    if (sc.split && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.split_min_n && L >= 2 && boundary &&
+    if (sc.split && opt.allow_split && paired && !narrow_ && dim <= 8 && n_ >= sc.split_min(dim) && L >= 2 && boundary &&
         L < lg_ && sc.split_parts >= 2 && sc.split_streams >= 1) {
       const int P = std::min(pow2_floor(sc.split_parts), 1 << L);
       split_level_ = L;
