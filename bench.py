@@ -81,6 +81,19 @@ def _parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _ensure_built(who: str) -> None:
+    """Bring the in-tree extension / executables up to date (file-locked, no GPU involved).
+    PKD_BENCH_TRACE_BUILD=1 reports on stderr what this process compiled and how long it took."""
+    if os.environ.get("PKD_SKIP_BUILD") == "1":
+        return
+    from parallel_kd_tree_amd import _build
+    _build.build()
+    if os.environ.get("PKD_BENCH_TRACE_BUILD") == "1":
+        lb = _build.LAST_BUILD
+        what = ",".join(lb["compiled"]) if lb["compiled"] else "up to date"
+        print(f"bench.py: {who}: build {what} ({lb['seconds'] * 1e3:.0f} ms)", file=sys.stderr, flush=True)
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -177,6 +190,9 @@ def main(argv=None):
     args = _parse(argv)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
+        # the launcher never touches the GPU: it is the place to compile, before any rank exists
+        # (a rank building while its peers wait in a collective could outlast their timeout)
+        _ensure_built("launcher")
         sys.exit(launch(args.gpus, sys.argv[1:] if argv is None else argv))
     world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
@@ -202,13 +218,13 @@ def main(argv=None):
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
 
+    # Every rank checks the in-tree build BEFORE joining the communicator: under torchrun there
+    # is no launcher of ours, so the first rank to take the build lock compiles (if anything is
+    # stale) and the rest find the signatures up to date; nobody waits inside a collective.
+    _ensure_built(f"rank {rank}")
     from parallel_kd_tree_amd.parallel import comm
     if world > 1:
         comm.init(backend="gloo" if cpu else os.environ.get("PKD_BENCH_BACKEND", "nccl"), device=dev)
-    if rank == 0 and os.environ.get("PKD_SKIP_BUILD") != "1":
-        from parallel_kd_tree_amd import _build
-        _build.build()  # no-op when the in-tree extension is up to date
-    if world > 1:
         comm.barrier()
     if os.environ.get("PKD_BENCH_FAIL_RANK") == str(rank):  # launcher test: this rank dies, the rest block
         os._exit(7)

@@ -324,7 +324,7 @@ std::vector<i64> GlobalBuilder::top_slots() const {
 }
 
 u32 GlobalBuilder::read_error(hipStream_t stream) const {
-  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  comm_.wait(stream, "read error");  // bounded: a stuck peer aborts the communicator instead of hanging here
   if (bufs_.size() <= 5 || !bufs_[5].first) return 0;
   u32 w[4];
   PKD_HIP_CHECK(hipMemcpy(w, bufs_[5].first, 16, hipMemcpyDeviceToHost));

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_top_collect_route(TopPoints p, u32* 
       const i64 ii = i < p.n ? i : 0;
       hn[u] = level > 0 ? node[ii] : 0u;
       ka[u] = p.pts[ii * p.dim + axis];
-      kn[u] = p.pts[ii * p.dim + next_axis];
+      kn[u] = has_next ? p.pts[ii * p.dim + next_axis] : 0.0f;  // the last top level has no next histogram
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -706,6 +706,18 @@ void fill_u64(void* p, i64 n, u64 v, hipStream_t stream) {
   PKD_LAUNCH_CHECK();
 }
 
+namespace {
+__global__ void k_fill32(u32* __restrict__ p, i64 n, u32 v) {
+  for (i64 i = i64(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += i64(gridDim.x) * blockDim.x) p[i] = v;
+}
+}  // namespace
+
+void fill_u32(void* p, i64 n, u32 v, hipStream_t stream) {
+  if (n <= 0) return;
+  k_fill32<<<int(std::min<i64>(1024, (n + 255) / 256)), 256, 0, stream>>>(static_cast<u32*>(p), n, v);
+  PKD_LAUNCH_CHECK();
+}
+
 void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream_t stream) {
   k_fill64<<<1, 256, 0, stream>>>(reinterpret_cast<u64*>(counts), i64(slots) * 4, 0, 4, 2, u64(id_base), 3,
                                   u64(n_local));
@@ -814,6 +826,11 @@ void top_pack_scatter(const TopPoints& p, const u32* node, int levels, float* ou
   // rows per block a multiple of 256: every wave's 64 rows of a chunk are two whole bitmap words
   const i64 per_block = ((std::max<i64>(p.n, 1) + blocks - 1) / blocks + 255) / 256 * 256;
   const u32* offsets = static_cast<const u32*>(scratch) + size_t(blocks) * T;
+  if (bitmaps && p.n == 0) {
+    // no chunk runs, so no ballot writes the (one-word) bitmaps: zero them (the receiver pops
+    // bitmap_words words per leaf even from an empty sender)
+    fill_u32(bitmaps, i64(T) * bitmap_words, 0u, stream);
+  }
   k_pack_scatter<<<blocks, kBlock, 0, stream>>>(p, node, levels, T, per_block, offsets, out, row_stride, col_stride,
                                                 bitmaps, bitmap_words);
   PKD_LAUNCH_CHECK();

@@ -43,6 +43,7 @@ struct TopSizes {
 // Device-side fills (kernels, so no host staging and graph-capturable): n 64-bit words of v;
 // the [slots][4] count matrix of top_pack with its id-base / n_local columns set.
 void fill_u64(void* p, i64 n, u64 v, hipStream_t stream);
+void fill_u32(void* p, i64 n, u32 v, hipStream_t stream);
 void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream_t stream);
 
 void top_bbox(const TopPoints& p, i64* box, hipStream_t stream);

@@ -121,11 +121,32 @@ def _compile(src: str, flags, verbose, sig: str) -> Path:
     return o
 
 
+LAST_BUILD = {"compiled": [], "seconds": 0.0}  # what the last build() in this process did
+
+
 def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, jobs: int | None = None) -> dict:
     """Compile every HIP/C++ source for gfx950 and link the extension + executables.
 
     Every output carries a signature (``<output>.sig``) of everything it was built from; an
-    output whose signature matches is kept without looking at (or needing) its objects."""
+    output whose signature matches is kept without looking at (or needing) its objects.
+    Concurrent callers (the ranks of a multi-process run) serialise on a file lock: the first
+    one builds, the others find every signature up to date."""
+    import fcntl
+    import time
+    t0 = time.perf_counter()
+    (ROOT / "build").mkdir(parents=True, exist_ok=True)
+    with open(ROOT / "build" / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            res, done = _build_locked(verbose, with_ext, with_cli, jobs)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+    LAST_BUILD["compiled"] = done
+    LAST_BUILD["seconds"] = time.perf_counter() - t0
+    return res
+
+
+def _build_locked(verbose, with_ext, with_cli, jobs):
     hdr = _hdr_digest()
     hipflags = [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
     tflags, tld = _torch_flags() if with_ext else ([], [])
@@ -154,7 +175,7 @@ def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, j
     todo = {k for k, (path, _, _, _) in outs.items() if _stale(path, lsig[k])}
     result = {k: str(path) for k, (path, _, _, _) in outs.items()}
     if not todo:
-        return result
+        return result, []
     OBJ.mkdir(parents=True, exist_ok=True)
     BIN.mkdir(parents=True, exist_ok=True)
     need = sorted({s for k in todo for s in outs[k][1]})
@@ -166,7 +187,7 @@ def build(verbose: bool = False, with_ext: bool = True, with_cli: bool = True, j
         path, srcs, tail, pre = outs[k]
         _run(["g++", *pre, "-o", path, *(objs[s] for s in srcs), *tail], verbose)
         _mark(path, lsig[k])
-    return result
+    return result, sorted(todo)
 
 
 def clean():

@@ -69,3 +69,19 @@ def test_bench_launcher_propagates_rank_failure():
 def test_bench_world_mismatch_rejected():
     r = _bench("--gpus", "2", "--device", "cpu", env={"WORLD_SIZE": "1"})
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_builds_in_launcher_before_ranks():
+    """The self-launcher brings the build up to date before any rank exists; the ranks then only
+    verify signatures (no compile, O(1) work) before they join the communicator."""
+    r = _bench("--gpus", "2", "--device", "cpu", "--points", "20000", "--steps", "1", "--warmup", "0",
+               env={"PKD_SKIP_BUILD": "0", "PKD_BENCH_TRACE_BUILD": "1"}, timeout=1200)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stderr.splitlines() if l.startswith("bench.py:") and ": build " in l]
+    assert lines and lines[0].startswith("bench.py: launcher: build"), r.stderr
+    ranks = [l for l in lines if l.startswith("bench.py: rank ")]
+    assert len(ranks) == 2, r.stderr
+    for l in ranks:
+        assert "build up to date" in l, l
+        ms = float(l.rsplit("(", 1)[1].split(" ms")[0])
+        assert ms < 20_000, l

@@ -251,3 +251,22 @@ def test_build_rows_equals_build(gpu_device):
     tp, ti = b.build_rows(rows)
     cp, ci = ops.build_cpu(x, ids, "exact", 2, 4)
     assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_pack_empty_rank_zeroes_bitmaps(gpu_device, P):
+    """A rank with no rows (N < P) still sends one bitmap word per leaf: the pack must write it
+    (zero), whatever the buffer held before, so the receiver's id rebuild sees no stray bits."""
+    L = P.bit_length() - 1
+    nat = ops.native()
+    x = torch.empty((0, 3), dtype=torch.float32, device=gpu_device)
+    node = torch.empty(0, dtype=torch.int32, device=gpu_device)
+    outc = torch.empty((1, 3), dtype=torch.float32, device=gpu_device)
+    counts = torch.empty(4 * P, dtype=torch.int64, device=gpu_device)
+    err = torch.zeros(4, dtype=torch.int32, device=gpu_device)
+    scratch = torch.empty(max(1, nat.top_pack_scratch_bytes(0, P)), dtype=torch.uint8, device=gpu_device)
+    bm = torch.full((P, 1), -1, dtype=torch.int32, device=gpu_device)  # poisoned: every bit set
+    nat.top_pack(x, None, 1, node, L, outc, 0, bm, counts, err, scratch)
+    torch.cuda.synchronize()
+    assert int(bm.abs().sum()) == 0, bm
+    assert int(counts.cpu().view(P, 4)[:, 0].sum()) == 0
