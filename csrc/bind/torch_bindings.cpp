@@ -56,8 +56,8 @@ const pk::u32* opt_ids(const c10::optional<torch::Tensor>& ids, int64_t n, const
 struct Builder {
   pk::GpuBuilder b;
   torch::Tensor ws;
-  Builder(int64_t n, int64_t dim, int64_t depth0, int64_t subtree_max)
-      : b(n, int(dim), pk::BuildOptions{int(subtree_max), int(depth0)}) {}
+  Builder(int64_t n, int64_t dim, int64_t depth0, int64_t subtree_max, bool allow_top)
+      : b(n, int(dim), pk::BuildOptions{int(subtree_max), int(depth0), true, allow_top}) {}
 
   void ensure_ws(const torch::Device& dev) {
     if (!ws.defined() || ws.device() != dev)
@@ -305,8 +305,8 @@ std::vector<torch::Tensor> nn_finalize(const torch::Tensor& packed) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native kd-tree core (HIP/CDNA4 kernels + C++ runtime)";
   py::class_<Builder>(m, "GpuBuilder")
-      .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0,
-           py::arg("subtree_max") = 0)
+      .def(py::init<int64_t, int64_t, int64_t, int64_t, bool>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0,
+           py::arg("subtree_max") = 0, py::arg("allow_top") = true)
       .def("build", &Builder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0,
            py::arg("out_pts") = c10::nullopt, py::arg("out_ids") = c10::nullopt)
       .def("build_rows", &Builder::build_rows, py::arg("rows"))
@@ -319,6 +319,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("split_level", [](const Builder& b) { return b.b.split_level(); })
       .def_property_readonly("split_streams", [](const Builder& b) { return b.b.split_streams(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
+      .def_property_readonly("sampled_top", [](const Builder& b) { return b.b.sampled_top(); })
+      .def("top_band_report", [](Builder& b) {  // per top node: band rows, rank in the median's bin, staged rows
+        TORCH_CHECK(b.ws.defined(), "no build yet");
+        const auto v = b.b.top_band_report(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());
+        return std::vector<int64_t>(v.begin(), v.end());
+      })
       .def("error_words", [](Builder& b) {  // view of the workspace's 4 error words (int32)
         TORCH_CHECK(b.ws.defined(), "no build yet");
         return torch::from_blob(const_cast<pk::u32*>(b.b.error_word(b.ws.data_ptr())), {4},

@@ -25,6 +25,9 @@
 // (build_reference.hip) and searches it with the reference's procedure, as kdtree_mpi does.
 // --save PATH writes the tree(s) (tree_io.hpp; forest: PATH.rank<r>), --leaf-threshold N caps
 // the LDS subtree segments, --share-gpu puts every rank on --device (one-GPU rehearsal).
+// --ranks R (forest, R >= P): R logical forest ranks over the P processes -- the reference's own
+// `mpirun -np 16 --oversubscribe` (Makefile:36) on fewer GPUs; each process builds and searches
+// the trees of its R / P logical slices and MIN-combines them before the reduce.
 // Every collective is waited on with a watchdog (RcclComm::wait): the stream is polled and
 // ncclCommGetAsyncError checked until a deadline (--timeout seconds, default 300); a stuck or
 // failed collective aborts the communicator and the rank exits non-zero, after which the
@@ -96,8 +99,8 @@ void read_all(int fd, void* p, size_t n) {
   }
 }
 
-int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vector<int>& id_pipes, double timeout_s,
-             std::chrono::high_resolution_clock::time_point tick) {
+int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const std::vector<int>& id_pipes,
+             double timeout_s, std::chrono::high_resolution_clock::time_point tick) {
   g_rank = rank;
   if (o.share_gpu) {
     // every rank on one device (rehearsal on a one-GPU box): RCCL accepts several ranks per
@@ -145,10 +148,25 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   const int dim = cfg.dim, Q = o.num_queries;
   const i64 N = cfg.num_points;
 
-  // forest slice (kdtree_mpi.cpp:204-224): equal parts, remainder to the last rank
-  i64 local = N / P;
-  const i64 first = local * rank;
-  if (rank == P - 1) local += N % P;
+  // forest slices (kdtree_mpi.cpp:204-224) of the R logical ranks (the reference's mpirun -np R,
+  // Makefile:36 runs 16): equal parts, remainder to the last logical rank; this process owns the
+  // contiguous logical ranks [lr0, lr1) (R / P each, the first R % P one more), i.e. one
+  // contiguous run of generation order, built as lr1 - lr0 independent trees
+  const int lr0 = rank * (R / P) + std::min(rank, R % P), lr1 = lr0 + R / P + (rank < R % P ? 1 : 0);
+  struct Slice {
+    int lr;
+    i64 first, n;
+  };
+  std::vector<Slice> slices;
+  for (int lr = lr0; lr < lr1; ++lr) {
+    i64 ln = N / R;
+    const i64 lf = ln * lr;
+    if (lr == R - 1) ln += N % R;
+    slices.push_back({lr, lf, ln});
+  }
+  const i64 first = slices.front().first;
+  i64 local = 0;
+  for (const Slice& sl : slices) local += sl.n;
 
   const auto g0 = std::chrono::high_resolution_clock::now();
   float* d_x = nullptr;
@@ -171,8 +189,8 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   float* d_tree = nullptr;
   u32* d_ids = nullptr;
   void* ws = nullptr;
-  std::unique_ptr<GpuBuilder> b;
-  std::unique_ptr<ReferenceBuilder> rb;  // --mode reference (forest): the reference's own tree per rank
+  std::vector<std::unique_ptr<GpuBuilder>> bs;        // forest: one per logical rank of this process
+  std::vector<std::unique_ptr<ReferenceBuilder>> rbs;  // --mode reference (forest): the reference's own trees
   const bool ref = o.mode == "reference";
   const bool global = o.decomp == "global";
   std::unique_ptr<GlobalBuilder> gb;
@@ -184,12 +202,14 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
     PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(gb->layout().T) * 4));
   } else if (local > 0) {  // allocations outside the timed region
     size_t wsb = 0;
-    if (ref) {
-      rb = std::make_unique<ReferenceBuilder>(local, dim);
-      wsb = rb->workspace_bytes();
-    } else {
-      b = std::make_unique<GpuBuilder>(local, dim, BuildOptions{o.leaf_threshold, 0});
-      wsb = b->workspace_bytes();
+    for (const Slice& sl : slices) {
+      if (ref) {
+        rbs.push_back(std::make_unique<ReferenceBuilder>(sl.n, dim));
+        wsb = std::max(wsb, rbs.back()->workspace_bytes());
+      } else {
+        bs.push_back(std::make_unique<GpuBuilder>(sl.n, dim, BuildOptions{o.leaf_threshold, 0}));
+        wsb = std::max(wsb, bs.back()->workspace_bytes());
+      }
     }
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(local) * 4));
@@ -198,9 +218,35 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventRecord(e0, s));
   nn_init(d_res, Q, s);
   // global 1-based ids (kdtree_mpi.cpp:223)
-  if (global) gb->build(d_x, local, u32(first + 1), s);
-  else if (local > 0 && ref) rb->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);
-  else if (local > 0) b->build(d_x, nullptr, u32(first + 1), d_tree, d_ids, ws, s);
+  // (forest: the trees of this process's logical ranks one after another, one workspace; a
+  // sampled-top build that reports a band miss is redone unsampled after the queries)
+  auto build_slice = [&](size_t k, bool allow_top) {
+    const Slice& sl = slices[k];
+    const i64 off = sl.first - first;
+    if (sl.n <= 0) return;
+    if (ref) rbs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+    else if (allow_top) bs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+    else GpuBuilder(sl.n, dim, BuildOptions{o.leaf_threshold, 0, true, false})
+             .build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+  };
+  u32 slice_err = 0;
+  if (global) {
+    gb->build(d_x, local, u32(first + 1), s);
+  } else if (local > 0) {
+    for (size_t k = 0; k < slices.size(); ++k) {
+      build_slice(k, true);
+      // the shared workspace holds one build's error words; a sampled build is checked here, on
+      // this rank alone, BEFORE any collective (its rebuild must not skew the collective order)
+      if (!ref && (slices.size() > 1 || bs[k]->sampled_top())) {
+        u32 e = slices[k].n > 0 ? bs[k]->read_error(ws, s) : 0u;
+        if ((e & top4_band_miss_bit()) && bs[k]->sampled_top()) {
+          build_slice(k, false);
+          e = slices[k].n > 0 ? bs[k]->read_error(ws, s) : 0u;
+        }
+        slice_err |= e;
+      }
+    }
+  }
   PKD_HIP_CHECK(hipEventRecord(e1, s));
   const float* d_q = d_x + size_t(local) * dim;
   const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
@@ -235,9 +281,15 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
       if (nt > 0) nn_brute(d_top, d_top_ids, 0, nt, dim, d_q, Q, d_res, s);
     }
   } else if (local > 0) {
-    if (ref) nn_traverse_reference(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);  // kdtree_mpi.cpp:234-243
-    else if (traverse) nn_traverse(d_tree, d_ids, local, dim, 0, d_q, Q, d_res, s);
-    else nn_brute(d_tree, d_ids, 0, local, dim, d_q, Q, d_res, s);
+    for (const Slice& sl : slices) {  // every tree of this process: MIN into the same results
+      if (sl.n <= 0) continue;
+      const i64 off = sl.first - first;
+      const float* tp = d_tree + off * dim;
+      const u32* ti = d_ids + off;
+      if (ref) nn_traverse_reference(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);  // kdtree_mpi.cpp:234-243
+      else if (traverse) nn_traverse(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);
+      else nn_brute(tp, ti, 0, sl.n, dim, d_q, Q, d_res, s);
+    }
   }
   // MPI_Reduce(MIN) to rank 0 (kdtree_mpi.cpp:253), the id riding along in the low bits
   PKD_NCCL_CHECK(ncclReduce(d_res, d_res, size_t(Q), ncclUint64, ncclMin, 0, comm, s));
@@ -252,7 +304,8 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
   PKD_HIP_CHECK(hipEventElapsedTime(&qry, e1, e2));
   const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
   // the build's device error word rides along (MAX over ranks: non-zero iff any rank failed)
-  const u32 berr = global ? gb->read_error(s) : (local > 0 && b) ? b->read_error(ws, s) : 0u;
+  u32 berr = global ? gb->read_error(s) : slice_err;
+  if (!global && !ref && slices.size() == 1 && local > 0 && !bs[0]->sampled_top()) berr = bs[0]->read_error(ws, s);
   float* d_t = nullptr;
   PKD_HIP_CHECK(hipMalloc(&d_t, 4 * sizeof(float)));
   const float ht[4] = {gen, bld, qry, float(berr & 0xFFFFFFu) + (berr >> 24 ? 1.0f : 0.0f)};
@@ -282,17 +335,20 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
                    "{\"ranks\": %d, \"decomp\": \"%s\", \"gen_ms\": %.3f, \"build_ms\": %.3f, "
                    "\"query_reduce_ms\": %.3f, \"build_mpts_per_s\": %.2f, \"local_global_levels\": %d, "
                    "\"top_levels\": %d}\n",
-                   P, o.decomp.c_str(), mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f),
-                   b ? b->global_levels() : 0, gb ? gb->top_levels() : 0);
+                   R, o.decomp.c_str(), mt[0], mt[1], mt[2], double(N) / 1e3 / std::max(mt[1], 1e-6f),
+                   bs.empty() ? 0 : bs[0]->global_levels(), gb ? gb->top_levels() : 0);
   }
   // --save: forest ranks write their own trees (<path>.rank<r>, like kdtree_mpi's independent
   // trees); the global tree is one file, every rank writing its share into its slot range
   if (!o.save.empty()) {
     const int mode = ref ? kTreeModeReference : kTreeModeExact;
     if (!global) {
-      const std::string path = o.save + ".rank" + std::to_string(rank);
-      tree_file_create(path, local, dim, 0, mode);
-      if (local > 0) tree_file_write_device(path, local, dim, 0, local, d_tree, d_ids, s);
+      for (const Slice& sl : slices) {
+        const std::string path = o.save + ".rank" + std::to_string(sl.lr);
+        tree_file_create(path, sl.n, dim, 0, mode);
+        const i64 off = sl.first - first;
+        if (sl.n > 0) tree_file_write_device(path, sl.n, dim, 0, sl.n, d_tree + off * dim, d_ids + off, s);
+      }
     } else {
       if (rank == 0) tree_file_create(o.save, N, dim, 0, mode);
       PKD_NCCL_CHECK(ncclAllReduce(d_t, d_t, 1, ncclFloat32, ncclMax, comm, s));  // barrier: the file exists
@@ -330,13 +386,17 @@ int run_rank(int rank, int P, Config cfg, const cli::Options& o, const std::vect
 
 int main(int argc, char** argv) {
   // --gpus / --timeout are ours; everything else goes to the shared front-end
-  int P = 1;
+  int P = 1, R = 0;
   double timeout_s = 300.0;
   std::vector<char*> rest{argv[0]};
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if ((a == "--gpus" || a == "--timeout") && i + 1 < argc) {
       (a == "--gpus" ? void(P = std::atoi(argv[++i])) : void(timeout_s = std::atof(argv[++i])));
+    } else if (a == "--ranks" && i + 1 < argc) {
+      R = std::atoi(argv[++i]);
+    } else if (a.rfind("--ranks=", 0) == 0) {
+      R = std::atoi(a.c_str() + 8);
     } else if (a.rfind("--gpus=", 0) == 0) {
       P = std::atoi(a.c_str() + 7);
     } else if (a.rfind("--timeout=", 0) == 0) {
@@ -349,7 +409,16 @@ int main(int argc, char** argv) {
     std::cerr << "--gpus must be in [1, 64]" << std::endl;
     return 1;
   }
+  if (R == 0) R = P;
+  if (R < P || R > 4096) {
+    std::cerr << "--ranks must be in [--gpus, 4096]" << std::endl;
+    return 1;
+  }
   cli::Options o = cli::parse(int(rest.size()), rest.data());
+  if (R != P && o.decomp == "global") {
+    std::cerr << "kdtree_dist --ranks (logical forest ranks) applies to --decomp forest" << std::endl;
+    return 1;
+  }
   if (o.mode != "exact" && o.decomp == "global") {
     std::cerr << "kdtree_dist --decomp global builds exact trees only (the reference's quirky tree depends on "
                  "array positions, which the redistribution does not keep); use --decomp forest"
@@ -380,7 +449,7 @@ int main(int argc, char** argv) {
     if (pid == 0) {
       int rc = 0;
       try {
-        rc = run_rank(r, P, cfg, o, fds, timeout_s, tick);
+        rc = run_rank(r, P, R, cfg, o, fds, timeout_s, tick);
       } catch (const std::exception& ex) {
         std::cerr << "kdtree_dist: " << ex.what() << std::endl;
         rc = 2;

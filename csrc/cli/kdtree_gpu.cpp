@@ -74,15 +74,28 @@ int main(int argc, char** argv) {
     const float* d_q = d_x + size_t(N) * dim;
     nn_init(d_res, Q, s);
     const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
-    if (ref) nn_traverse_reference(d_tree, d_ids, N, dim, 0, d_q, Q, d_res, s);  // the reference's search
-    else if (traverse) nn_traverse(d_tree, d_ids, N, dim, 0, d_q, Q, d_res, s);
-    else nn_brute(d_tree, d_ids, 0, N, dim, d_q, Q, d_res, s);
+    auto query = [&] {
+      if (ref) nn_traverse_reference(d_tree, d_ids, N, dim, 0, d_q, Q, d_res, s);  // the reference's search
+      else if (traverse) nn_traverse(d_tree, d_ids, N, dim, 0, d_q, Q, d_res, s);
+      else nn_brute(d_tree, d_ids, 0, N, dim, d_q, Q, d_res, s);
+    };
+    query();
     PKD_HIP_CHECK(hipEventRecord(e3, s));
     std::vector<u64> res(static_cast<size_t>(Q));
     PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
     PKD_HIP_CHECK(hipStreamSynchronize(s));
     u32 detail[3] = {0, 0, 0};
-    if (const u32 err = ref ? 0u : b.read_error(ws, s, detail)) {  // after the queries: no extra sync in the build
+    u32 err0 = ref ? 0u : b.read_error(ws, s, detail);
+    if ((err0 & top4_band_miss_bit()) && b.sampled_top()) {
+      // a sampled top band missed its median (reported, never silent): rebuild unsampled
+      GpuBuilder fb(N, dim, BuildOptions{o.leaf_threshold, 0, true, false});
+      fb.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);
+      nn_init(d_res, Q, s);
+      query();
+      PKD_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, size_t(Q) * 8, hipMemcpyDeviceToHost, s));
+      err0 = fb.read_error(ws, s, detail);
+    }
+    if (const u32 err = err0) {  // after the queries: no extra sync in the build
       std::cerr << "kdtree_gpu: device build error word 0x" << std::hex << err << std::dec << " (code " << detail[0]
                 << ", level " << detail[1] << ", value " << detail[2] << "); no results printed" << std::endl;
       return 3;

@@ -303,7 +303,7 @@ GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth) {
   // no split build inside a distributed build: its side streams plus the caller's and the
   // communication stream would exceed the 4 hardware queues, and RCCL's kernels would queue
   // behind partition passes
-  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false});
+  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false, false});
   leaves_.push_back(std::move(l));
   return *leaves_.back()->b;
 }

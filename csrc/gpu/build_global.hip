@@ -26,6 +26,7 @@
 #include "pkdtree/hip_check.hpp"
 #include "pkdtree/trace.hpp"
 #include "subtree.hpp"
+#include "top4.hpp"
 
 namespace pkdtree {
 
@@ -2856,6 +2857,11 @@ Tuning Tuning::from_env() {
   t.split_streams = int(env_i("PKD_SPLIT_STREAMS", 4));
   t.split_min_n = env_i("PKD_SPLIT_MIN_N", i64(64) << 20);
   t.split_min_n_3d = env_i("PKD_SPLIT_MIN_N_3D", std::getenv("PKD_SPLIT_MIN_N") ? t.split_min_n : i64(512) << 20);
+  t.top = env_i("PKD_TOP", 1) != 0;
+  t.top_min_n = env_i("PKD_TOP_MIN_N", t.top_min_n);
+  t.top_sample_log2 = int(env_i("PKD_TOP_SAMPLE", t.top_sample_log2));
+  if (const char* z = std::getenv("PKD_TOP_Z")) t.top_z = float(std::atof(z));
+  t.top_blocks = int(env_i("PKD_TOP_BLOCKS", 0));
   return t;
 }
 
@@ -2918,6 +2924,9 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   lg_ = 0;
   while ((n_ >> lg_) > nsub_) ++lg_;
   heap_nodes_ = (i64(1) << (lg_ + 1)) - 1;
+  // Sampled top levels: full-column AoS builds large enough that one scatter pass plus the
+  // sample and the band fix-up beat the paired levels 0..3 (level 4 must still be global).
+  top_ = tune_.top && opt.allow_top && dim >= 2 && dim <= 8 && !narrow_ && n_ >= tune_.top_min_n && lg_ >= top4::kLevels + 1;
   max_bins_ = 0;
   max_hist_ = 1;
   const i64 level_blocks =
@@ -2969,7 +2978,10 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     }
   }
   const int lgrp = tail_ >= 0 ? tail_ : lg_;  // levels the pairs / triples cover
-  for (int l = 0; pairs && l + 1 < lgrp;) {
+  const int lfirst = top_ ? top4::kLevels : 0;
+  if (top_)
+    for (int l = 0; l < top4::kLevels; ++l) levels_[size_t(l)].sampled = true;
+  for (int l = lfirst; pairs && l + 1 < lgrp;) {
     // (four levels left: two pairs, not a triple and a lone level, whose single-level pass moves
     // every row for one level: 100M x 8D level 13 alone took 1.7 ms)
     const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && lgrp - l != 4 &&
@@ -3014,6 +3026,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   i64 max_grid = 1;
   for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
   off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
+  if (top_) off_top_ = take(top4::workspace_bytes());
   {
     const Tuning& sc = tune_;
     const int L = sc.split_level;
@@ -3061,7 +3074,8 @@ std::string GpuBuilder::describe() const {
   for (const auto& lp : levels_)
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
        << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
-       << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "") << (lp.tail ? " tail" : "");
+       << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "") << (lp.tail ? " tail" : "")
+       << (lp.sampled ? " sampled" : "");
   return os.str();
 }
 
@@ -3110,6 +3124,56 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   // through the global levels (lg_ + 2 columns instead of dim + 1); the subtree kernel and the
   // median writes gather whole rows from the input, which outlives the build.
   const bool narrow = narrow_ && tiled;
+  if (top_ && !ids_in_row && rs == dim_) {
+    // levels 0..3 straight from the AoS input (no prep pass): see top4.hpp
+    u32* err = reinterpret_cast<u32*>(ws + off_err_);
+    zero_u32(err, 4, stream);
+    top4::Geom g{};
+    for (int h = 0; h < top4::kHeap; ++h) {  // the heap geometry of k_geometry, levels 0..4
+      int l = 0;
+      while (((h + 1) >> (l + 1)) > 0) ++l;
+      const i64 j = h + 1 - (i64(1) << l);
+      i64 lo = 0, m = n_;
+      for (int b = l - 1; b >= 0; --b) {
+        if ((j >> b) & 1) {
+          lo = lo + m / 2 + 1;
+          m = m - m / 2 - 1;
+        } else {
+          m = m / 2;
+        }
+        if (m < 0) m = 0;
+      }
+      g.lo[h] = lo;
+      g.n[h] = m;
+    }
+    for (int l = 0; l <= top4::kLevels; ++l) g.axis[l] = (opt_.depth0 + l) % dim_;
+    g.dim = dim_;
+    top4::IO io{};
+    io.pts = pts;
+    io.ids = ids;
+    io.id_base = id_base;
+    io.n = n_;
+    io.cols = colsA;
+    io.stage = reinterpret_cast<float*>(ws + off_cols_b_);
+    io.ncol = ncol_;
+    io.out_pts = out_pts;
+    io.out_ids = out_ids;
+    io.cells = reinterpret_cast<float*>(ws + off_cells_);
+    io.params = reinterpret_cast<BucketParams*>(ws + off_params_);
+    io.bins4 = levels_[size_t(top4::kLevels)].bins;
+    io.err = err;
+    io.ws = ws + off_top_;
+    top4::Tune tt;
+    tt.sample_log2 = tune_.top_sample_log2;
+    tt.z = tune_.top_z;
+    tt.scatter_blocks = tune_.top_blocks;
+    {
+      TraceRange trt("pkd.top4");
+      top4::run(g, io, tt, stream);
+    }
+    run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, nullptr, top4::kLevels);
+    return;
+  }
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
                     (ids == nullptr || reinterpret_cast<uintptr_t>(ids) % 16 == 0);
   if (vec3) {
@@ -3179,7 +3243,7 @@ void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* 
 }
 
 void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
-                            u32 id_base, const float* in_rows, i64 in_rs, float* cols_a) const {
+                            u32 id_base, const float* in_rows, i64 in_rs, float* cols_a, int first_level) const {
   const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
   float* colsA = cols_a ? cols_a : reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
@@ -3191,13 +3255,15 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   u32* hist[2] = {reinterpret_cast<u32*>(ws + off_hist0_), reinterpret_cast<u32*>(ws + off_hist1_)};
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   u32* err = reinterpret_cast<u32*>(ws + off_err_);
-  zero_u32(err, 4, stream);
+  if (first_level == 0) zero_u32(err, 4, stream);
 
   k_geometry<<<int((heap_nodes_ + kBlock - 1) / kBlock), kBlock, 0, stream>>>(seg_lo, seg_n, heap_nodes_, n_);
   PKD_LAUNCH_CHECK();
   const int axis0 = opt_.depth0 % dim_;
-  k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
-  PKD_LAUNCH_CHECK();
+  if (first_level == 0) {
+    k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
+    PKD_LAUNCH_CHECK();
+  }
 
   // Levels [l0, l1) of segment range `part` of `nparts` (at level l: segments
   // [part * segs / nparts, (part + 1) * segs / nparts)) on stream `st`. The per-segment arrays
@@ -3288,11 +3354,11 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const i64 segs = lp.segs / nparts;  // this part's segments at level l
       TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
       LevelArgs a = level_args(l);
-      if (l == 0) {
-        zero_u32(hist[0], lp.segs * lp.bins, st);
+      if (l == first_level) {  // no previous pass fused this level's histogram
+        zero_u32(hist[l & 1], lp.segs * lp.bins, st);
         LevelArgs ah = a;  // like k_scan: fewer blocks, fewer histogram flush atomics
         ah.bps = std::max(1, a.bps / tune_.hist_div);
-        k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, st>>>(ah, hist[0]);
+        k_hist<<<int(lp.segs * ah.bps), kBlock, size_t(lp.bins) * 4, st>>>(ah, hist[l & 1]);
         PKD_LAUNCH_CHECK();
       }
       k_select<<<int(segs), kBlock, 0, st>>>(a);
@@ -3467,7 +3533,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   const HistSet whole{{hist[0], hist[1]}, reinterpret_cast<u32*>(ws + off_hist2_), reinterpret_cast<u32*>(ws + off_bcnt_)};
   SplitStreams* sp = (split_parts_ > 1 && !in_rows) ? split_streams_for(stream) : nullptr;
   if (!sp) {
-    run_range(0, 0, lg_, 0, 1, stream, whole, src, dst);
+    run_range(0, first_level, lg_, 0, 1, stream, whole, src, dst);
     subtree(0, 1, stream, src);
     return;
   }
@@ -3529,6 +3595,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     std::fprintf(stderr, "%s\n", os.str().c_str());
     for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   }
+}
+
+std::vector<u32> GpuBuilder::top_band_report(const void* workspace, hipStream_t stream) const {
+  std::vector<u32> r;
+  if (!top_) return r;
+  u32 b[top4::kNodes][3];
+  top4::band_report(static_cast<const char*>(workspace) + off_top_, stream, b);
+  for (int x = 0; x < top4::kNodes; ++x)
+    for (int k = 0; k < 3; ++k) r.push_back(b[x][k]);
+  return r;
 }
 
 // Diagnostic: mean cycles of each k_tail3 phase (PKD_TAIL_STAMPS=1) over the recorded blocks.

@@ -1,0 +1,1094 @@
+// Sampled top levels (levels 0..3 in one row-moving pass): see top4.hpp for the scheme.
+//
+// Kernel sequence of one build (all on the caller's stream, no host round trip, graph-safe):
+//   k_zero_top      state, histograms
+//   k_samp_gather   2^sample_log2 stratified random rows: the keys of the four level axes
+//   k_samp_hist/sel per level: 64 Ki-bin histogram of the node's sample keys (bins linear over
+//                   the node's sample range in orderable-key space), then per node the bins of
+//                   the sample ranks c/2 - h, c/2, c/2 + h (h = z sqrt(c) / 2): band [a, b] and
+//                   the estimated pivot that routes the sample to the children
+//   k_scatter       every input row once: certain rows into their level-4 segment, band rows
+//                   into the staging arena (tag = node), SoA columns + ids, bounding box
+//   per level j:    k_res_classify (route the staged rows by level j-1's exact pivot, classify
+//                   the level-j ones against the band, 16-bit histogram of the band's (key, id)
+//                   composites), k_res_sel1 (exact rank of the median in the band from the
+//                   counts; its bin), k_res_collect (the bin's rows), k_res_sel2 (radix select:
+//                   the exact pivot)
+//   k_res_insert    staged rows into the free slots of their level-4 segments
+//   k_finish        bounding box, the 15 medians to the output, cells of nodes 0..30, the
+//                   level-4 histogram parameters, consistency checks
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <stdexcept>
+
+#include "device_utils.hpp"
+#include "pkdtree/hip_check.hpp"
+#include "top4.hpp"
+
+namespace pkdtree {
+namespace top4 {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kFine = 1 << 16;       // fine bins per node (16-bit digit)
+constexpr int kCoarse = 256;         // coarse bins per node (fine >> 8)
+constexpr int kSmallCap = 4096;      // rows of a median's fine bin selected in LDS
+constexpr u32 kMed = 0x80000000u;    // tag of a median row: kMed | node
+constexpr int kMaxParts = 2048;      // scatter blocks (one bounding-box partial each)
+constexpr int kMaxSampleLog2 = 21;
+constexpr int kInsChunk = kBlock * 16;
+
+struct State {
+  u32 nbox_lo[8];  // ~(min sample key) per axis (0: none)
+  u32 box_hi[8];   // max sample key per axis
+  u32 rlo[kNodes], rhi[kNodes], sshift[kNodes];  // sample binning of the node on its axis
+  u32 scount[kNodes];
+  u32 a[kNodes], b[kNodes], phat[kNodes];  // band (inclusive, orderable keys), estimated pivot
+  u32 rshift[kNodes];                       // fine digit of a band composite: (c - comp_lo) >> rshift
+  u32 staged_orig[kNodes];                  // rows the scatter staged at the node
+  u32 late[kNodes][3];                      // staged rows of the node: left of / in / right of the band
+  u32 sel[kNodes], sel_rank[kNodes], sel_cnt[kNodes], small_cnt[kNodes];
+  u32 med_idx1[kNodes];                     // staging row + 1 of the median (0: not found)
+  u32 cursor[kCells + 1];                   // rows the scatter put in each level-4 segment; [16]: staged
+  u32 ins[kCells];                          // staged rows inserted per segment
+  u32 pad[2];
+  u64 comp_lo[kNodes];
+  u64 pivot[kNodes];                        // exact (key, id) composite of the node's median
+};
+
+struct Layout {
+  size_t state, fine_s, coarse_s, fine_r, coarse_r, zero_end, skey, small, part, total;
+};
+
+inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+Layout layout() {
+  Layout L{};
+  size_t o = 0;
+  L.state = o;
+  o = al(o + sizeof(State));
+  L.fine_s = o;
+  o = al(o + size_t(kNodes) * kFine * 4);
+  L.coarse_s = o;
+  o = al(o + size_t(kNodes) * kCoarse * 4);
+  L.fine_r = o;
+  o = al(o + size_t(kNodes) * kFine * 4);
+  L.coarse_r = o;
+  o = al(o + size_t(kNodes) * kCoarse * 4);
+  L.zero_end = o;
+  L.skey = o;
+  o = al(o + size_t(kLevels) * (size_t(1) << kMaxSampleLog2) * 4);
+  L.small = o;
+  o = al(o + size_t(8) * kSmallCap * 8);
+  L.part = o;
+  o = al(o + size_t(kMaxParts) * 16 * 4);
+  L.total = o;
+  return L;
+}
+
+__device__ __forceinline__ int heap_level(u32 h) { return 31 - __builtin_clz(h + 1u); }
+
+__device__ __forceinline__ u32 shift_for32(u32 span) {
+  const int bits = span ? 32 - __builtin_clz(span) : 0;
+  return u32(bits > 16 ? bits - 16 : 0);
+}
+__device__ __forceinline__ u32 shift_for64(u64 span) {
+  const int bits = span ? 64 - __builtin_clzll(span) : 0;
+  return u32(bits > 16 ? bits - 16 : 0);
+}
+
+__device__ __forceinline__ u32 mix32(u32 x) {  // murmur3 finaliser
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+// Bin of the rank-th element (0-based) of a 256-bin histogram h (16-B aligned, global or
+// LDS); every lane of the wave calls it. *below = elements in the bins before it, *total = all
+// elements; returns 256 when rank >= total.
+__device__ __forceinline__ u32 wave_find256(const u32* h, u32 rank, u32* below, u32* total) {
+  const int ln = dev::lane();
+  const uint4 v = reinterpret_cast<const uint4*>(h)[ln];
+  const u32 s = v.x + v.y + v.z + v.w;
+  const u32 incl = dev::wave_incl_scan(s);
+  const u32 excl = incl - s;
+  const u32 tot = __shfl(incl, 63, 64);
+  const bool mine = rank >= excl && rank < incl;
+  const u64 m = __ballot(mine);
+  u32 bin = 256, bel = tot;
+  if (m) {
+    const int src = __ffsll((long long)m) - 1;
+    u32 lb = 0, c = excl;
+    if (mine) {
+      if (rank >= c + v.x) {
+        c += v.x;
+        lb = 1;
+        if (rank >= c + v.y) {
+          c += v.y;
+          lb = 2;
+          if (rank >= c + v.z) {
+            c += v.z;
+            lb = 3;
+          }
+        }
+      }
+    }
+    bin = u32(__shfl(int(4 * ln + lb), src, 64));
+    bel = u32(__shfl(int(c), src, 64));
+  }
+  *below = bel;
+  *total = tot;
+  return bin;
+}
+
+// Fine bin (of 65536) holding the rank-th element of a node's two-level histogram.
+__device__ __forceinline__ u32 wave_find_fine(const u32* coarse, const u32* fine, u32 rank, u32* below, u32* total) {
+  u32 b1 = 0, b2 = 0, t2 = 0;
+  const u32 cb = wave_find256(coarse, rank, &b1, total);
+  if (cb >= 256) {
+    *below = *total;
+    return u32(kFine);
+  }
+  const u32 fb = wave_find256(fine + size_t(cb) * 256, rank - b1, &b2, &t2);
+  *below = b1 + b2;
+  return cb * 256 + min(fb, 255u);
+}
+
+__device__ __forceinline__ u32 wave_sum(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += u32(__shfl_xor(int(v), o, 64));
+  return v;
+}
+
+__device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
+  atomicOr(err, kErrBit);
+  if (atomicCAS(err + 1, 0u, code) == 0u) {
+    err[2] = t;
+    err[3] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_zero_top(u32* __restrict__ p, i64 n) {
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) p[i] = 0u;
+}
+
+// ---- sample -----------------------------------------------------------------------------
+struct SampArgs {
+  const float* pts;
+  int dim;
+  i64 n;
+  int S;
+  int ax[kLevels];
+  u32* skey;  // [kLevels][S]
+  State* st;
+};
+
+__global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
+  __shared__ u32 red[kBlock / 64][2 * kLevels];
+  u32 mn[kLevels], mx[kLevels];
+#pragma unroll
+  for (int j = 0; j < kLevels; ++j) {
+    mn[j] = 0xffffffffu;
+    mx[j] = 0u;
+  }
+  for (int k = blockIdx.x * kBlock + threadIdx.x; k < a.S; k += gridDim.x * kBlock) {
+    const i64 w0 = (i64(k) * a.n) / a.S, w1 = (i64(k + 1) * a.n) / a.S;
+    const u32 win = u32(max<i64>(1, w1 - w0));
+    const i64 r = w0 + i64(mix32(u32(k) * 0x9e3779b9u + 0x7f4a7c15u) % win);
+    float v[kLevels];
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) v[j] = a.pts[r * a.dim + a.ax[j]];
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) {
+      const u32 key = orderable(v[j]);
+      a.skey[size_t(j) * a.S + k] = key;
+      mn[j] = min(mn[j], key);
+      mx[j] = max(mx[j], key);
+    }
+  }
+  const int w = threadIdx.x / 64;
+#pragma unroll
+  for (int j = 0; j < kLevels; ++j) {
+    const u32 lo = dev::wave_min_u32(mn[j]), hi = dev::wave_max_u32(mx[j]);
+    if (dev::lane() == 0) {
+      red[w][j] = lo;
+      red[w][kLevels + j] = hi;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kLevels) {
+    const int c = threadIdx.x;
+    u32 v = red[0][c];
+    for (int k = 1; k < kBlock / 64; ++k) v = c < kLevels ? min(v, red[k][c]) : max(v, red[k][c]);
+    const int j = c % kLevels;
+    if (c < kLevels) atomicMax(&a.st->nbox_lo[a.ax[j]], ~v);
+    else atomicMax(&a.st->box_hi[a.ax[j]], v);
+  }
+}
+
+struct SampLevelArgs {
+  const u32* skey;
+  int S;
+  int j;
+  int ax[kLevels + 1];
+  State* st;
+  u32* fine;    // [kNodes][kFine]
+  u32* coarse;  // [kNodes][kCoarse]
+  float z;
+};
+
+__global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
+  __shared__ u32 lc[8 * kCoarse];
+  __shared__ u32 ph[kNodes], rl[8], rh[8], sh[8];
+  const int j = a.j, nodes = 1 << j, first = nodes - 1;
+  for (int i = threadIdx.x; i < nodes * kCoarse; i += kBlock) lc[i] = 0;
+  if (threadIdx.x < first) ph[threadIdx.x] = a.st->phat[threadIdx.x];
+  if (threadIdx.x < nodes) {
+    const int X = first + threadIdx.x;
+    u32 lo, hi;
+    if (j == 0) {
+      lo = ~a.st->nbox_lo[a.ax[0]];
+      hi = a.st->box_hi[a.ax[0]];
+      if (hi < lo) hi = lo;
+      if (blockIdx.x == 0) {
+        a.st->rlo[0] = lo;
+        a.st->rhi[0] = hi;
+        a.st->sshift[0] = shift_for32(hi - lo);
+      }
+    } else {
+      lo = a.st->rlo[X];
+      hi = a.st->rhi[X];
+    }
+    rl[threadIdx.x] = lo;
+    rh[threadIdx.x] = hi;
+    sh[threadIdx.x] = shift_for32(hi - lo);
+  }
+  __syncthreads();
+  for (int k = blockIdx.x * kBlock + threadIdx.x; k < a.S; k += gridDim.x * kBlock) {
+    int X = 0;
+    for (int i = 0; i < j; ++i) X = 2 * X + 1 + (a.skey[size_t(i) * a.S + k] >= ph[X] ? 1 : 0);
+    const int x = X - first;
+    u32 key = a.skey[size_t(j) * a.S + k];
+    key = min(max(key, rl[x]), rh[x]);
+    const u32 bin = min((key - rl[x]) >> sh[x], u32(kFine - 1));
+    atomicAdd(&a.fine[size_t(X) * kFine + bin], 1u);
+    atomicAdd(&lc[x * kCoarse + (bin >> 8)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nodes * kCoarse; i += kBlock) {
+    const u32 v = lc[i];
+    if (v) atomicAdd(&a.coarse[size_t(first) * kCoarse + i], v);
+  }
+}
+
+// One wave per node of level j: the band and estimated pivot from the sample ranks, then the
+// children's sample ranges (the root box on their axis, clipped by every ancestor pivot on it).
+__global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
+  const int j = a.j, first = (1 << j) - 1;
+  const int X = first + blockIdx.x;
+  State* st = a.st;
+  const u32 lo = st->rlo[X], hi = st->rhi[X], shift = shift_for32(hi - lo);
+  const u32* co = a.coarse + size_t(X) * kCoarse;
+  const u32* fi = a.fine + size_t(X) * kFine;
+  u32 below = 0, c = 0;
+  (void)wave_find256(co, 0, &below, &c);
+  u32 A = 0, B = 0xffffffffu, P = lo;
+  if (c > 0) {
+    const u32 half = u32(ceilf(a.z * sqrtf(float(c)) * 0.5f)) + 2u;
+    const u32 rm = c / 2, rlo = rm > half ? rm - half : 0u, rhi = min(c - 1, rm + half);
+    u32 t = 0;
+    const u32 bl = wave_find_fine(co, fi, rlo, &below, &t);
+    const u32 bm = wave_find_fine(co, fi, rm, &below, &t);
+    const u32 bh = wave_find_fine(co, fi, rhi, &below, &t);
+    const u64 edge_lo = u64(lo) + (u64(bl) << shift);
+    const u64 edge_hi = u64(lo) + (u64(bh + 1) << shift) - 1;
+    A = rlo == 0 ? 0u : u32(min<u64>(edge_lo, hi));
+    B = rhi >= c - 1 ? 0xffffffffu : u32(min<u64>(edge_hi, hi));
+    P = u32(min<u64>(u64(lo) + (u64(bm) << shift) + ((u64(1) << shift) >> 1), hi));
+  }
+  if (dev::lane() == 0) {
+    st->scount[X] = c;
+    st->a[X] = A;
+    st->b[X] = B;
+    st->phat[X] = P;
+    const u64 clo = u64(A) << 32, chi = (u64(B) << 32) | 0xffffffffull;
+    st->comp_lo[X] = clo;
+    st->rshift[X] = shift_for64(chi - clo);
+    if (j + 1 < kLevels) {
+      const int ac = a.ax[j + 1];
+      for (int s = 0; s < 2; ++s) {
+        const int C = 2 * X + 1 + s;
+        u32 clo2 = ~st->nbox_lo[ac], chi2 = st->box_hi[ac];
+        int child = C, Y = X;
+        for (;;) {
+          if (a.ax[heap_level(u32(Y))] == ac) {
+            const u32 pY = Y == X ? P : st->phat[Y];
+            if (child == 2 * Y + 1) chi2 = min(chi2, pY > 0 ? pY - 1 : 0u);
+            else clo2 = max(clo2, pY);
+          }
+          if (Y == 0) break;
+          child = Y;
+          Y = (Y - 1) / 2;
+        }
+        if (chi2 < clo2) chi2 = clo2;
+        st->rlo[C] = clo2;
+        st->rhi[C] = chi2;
+        st->sshift[C] = shift_for32(chi2 - clo2);
+      }
+    }
+  }
+}
+
+// ---- scatter ----------------------------------------------------------------------------
+struct ScatArgs {
+  const float* pts;
+  const u32* ids;
+  u32 id_base;
+  i64 n;
+  float* cols;
+  float* stage;
+  u32* tags;
+  i64 ncol;
+  State* st;
+  u32* part;
+  u32* err;
+  i64 tiles;
+  i64 cell_lo[kCells];
+  u32 cell_n[kCells];
+  int ax[kLevels];
+};
+
+// Rows of one scatter tile held by a thread: v[u][c], id[u]; VEC (dim 3, 16-B aligned input):
+// 4 consecutive rows per quad from three 16-B loads (rows 4 q .. 4 q + 3, q = tile quad base +
+// u4 * kBlock + tid); otherwise row t0 + u * kBlock + tid.
+template <int D, int R, bool VEC>
+__device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R][D], u32 (&id)[R]) {
+  u32 valid = 0;  // bit u: row u of this thread exists
+  const int tid = threadIdx.x;
+  if constexpr (VEC) {
+    static_assert(D == 3 && R % 4 == 0, "vector tile: dim 3");
+    const i64 q0 = t0 / 4;
+    const float4* in = reinterpret_cast<const float4*>(a.pts);
+#pragma unroll
+    for (int u4 = 0; u4 < R / 4; ++u4) {
+      const i64 q = q0 + i64(u4) * kBlock + tid;
+      const i64 r0 = 4 * q;
+      if (r0 + 3 < a.n) {
+        const float4 x = in[3 * q], y = in[3 * q + 1], z = in[3 * q + 2];
+        v[4 * u4][0] = x.x; v[4 * u4][1] = x.y; v[4 * u4][2] = x.z;
+        v[4 * u4 + 1][0] = x.w; v[4 * u4 + 1][1] = y.x; v[4 * u4 + 1][2] = y.y;
+        v[4 * u4 + 2][0] = y.z; v[4 * u4 + 2][1] = y.w; v[4 * u4 + 2][2] = z.x;
+        v[4 * u4 + 3][0] = z.y; v[4 * u4 + 3][1] = z.z; v[4 * u4 + 3][2] = z.w;
+        if (a.ids) {
+          const uint4 iv = reinterpret_cast<const uint4*>(a.ids)[q];
+          id[4 * u4] = iv.x; id[4 * u4 + 1] = iv.y; id[4 * u4 + 2] = iv.z; id[4 * u4 + 3] = iv.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) id[4 * u4 + e] = a.id_base + u32(r0 + e);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const i64 r = r0 + e;
+          const i64 rr = r < a.n ? r : 0;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[4 * u4 + e][c] = a.pts[rr * 3 + c];
+          id[4 * u4 + e] = a.ids ? a.ids[rr] : a.id_base + u32(r);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) valid |= (r0 + e < a.n ? 1u : 0u) << (4 * u4 + e);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const i64 r = t0 + i64(u) * kBlock + tid;
+      const i64 rr = r < a.n ? r : 0;
+#pragma unroll
+      for (int c = 0; c < D; ++c) v[u][c] = a.pts[rr * D + c];
+      id[u] = a.ids ? a.ids[rr] : a.id_base + u32(r);
+      valid |= (r < a.n ? 1u : 0u) << u;
+    }
+  }
+  return valid;
+}
+
+template <int D, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
+  constexpr int R = D <= 4 ? 16 : 8;  // rows per thread per tile
+  constexpr int TILE = kBlock * R;
+  __shared__ u32 sa[16], sb[16];
+  __shared__ u32 wcnt[2][4][kCells + 1];
+  __shared__ u32 zoff[2][4][kCells + 1];
+  __shared__ u32 red[kBlock / 64][2 * D];
+  const int tid = threadIdx.x, w = tid >> 6;
+  if (tid < kNodes) {
+    sa[tid] = a.st->a[tid];
+    sb[tid] = a.st->b[tid];
+  }
+  if (tid < 2 * 4 * (kCells + 1)) (&wcnt[0][0][0])[tid] = 0u;
+  u32 mn[D], mx[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    mn[c] = 0xffffffffu;
+    mx[c] = 0u;
+  }
+  __syncthreads();
+  int par = 0;
+  for (i64 tile = blockIdx.x; tile < a.tiles; tile += gridDim.x, par ^= 1) {
+    const i64 t0 = tile * TILE;
+    float v[R][D];
+    u32 id[R];
+    const u32 vmask = load_tile<D, R, VEC>(a, t0, v, id);
+    u32 code[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const bool valid = (vmask >> u) & 1u;
+      u32 X = 0, T = 0;
+      bool staged = false;
+#pragma unroll
+      for (int j = 0; j < kLevels; ++j) {
+        float kv = v[u][0];
+#pragma unroll
+        for (int c = 1; c < D; ++c) kv = c == a.ax[j] ? v[u][c] : kv;
+        const u32 k = orderable(kv);
+        if (!staged) {
+          if (k < sa[X]) X = 2 * X + 1;
+          else if (k > sb[X]) X = 2 * X + 2;
+          else {
+            staged = true;
+            T = X;
+          }
+        }
+      }
+      const u32 z = !valid ? 31u : (staged ? u32(kCells) : X - u32(kNodes));
+      u32 r = 0;
+      if (valid) {
+        r = atomicAdd(&wcnt[par][w][z], 1u);
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          const u32 k = orderable(v[u][c]);
+          mn[c] = min(mn[c], k);
+          mx[c] = max(mx[c], k);
+        }
+      }
+      code[u] = r | (z << 12) | (T << 20);
+    }
+    __syncthreads();
+    if (tid <= kCells) {
+      u32 tot = 0;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        zoff[par][ww][tid] = tot;
+        tot += wcnt[par][ww][tid];
+      }
+      const u32 base = tot ? atomicAdd(&a.st->cursor[tid], tot) : 0u;
+      if (tid < kCells && base + tot > a.cell_n[tid]) report(a.err, 0x2001u, u32(tid), base + tot);
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        zoff[par][ww][tid] += base;
+        wcnt[par ^ 1][ww][tid] = 0u;  // the next tile's counters (last read two barriers ago)
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const u32 z = (code[u] >> 12) & 31u;
+      if (z == 31u) continue;
+      const u32 pos = zoff[par][w][z] + (code[u] & 0xfffu);
+      if (z < u32(kCells)) {
+        if (pos < a.cell_n[z]) {
+          const i64 q = a.cell_lo[z] + pos;
+#pragma unroll
+          for (int c = 0; c < D; ++c) a.cols[i64(c) * a.ncol + q] = v[u][c];
+          a.cols[i64(D) * a.ncol + q] = __uint_as_float(id[u]);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < D; ++c) a.stage[i64(c) * a.ncol + pos] = v[u][c];
+        a.stage[i64(D) * a.ncol + pos] = __uint_as_float(id[u]);
+        a.tags[pos] = code[u] >> 20;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    const u32 lo = dev::wave_min_u32(mn[c]), hi = dev::wave_max_u32(mx[c]);
+    if (dev::lane() == 0) {
+      red[w][c] = lo;
+      red[w][D + c] = hi;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * D) {
+    u32 r = red[0][tid];
+    for (int k = 1; k < kBlock / 64; ++k) r = tid < D ? min(r, red[k][tid]) : max(r, red[k][tid]);
+    a.part[size_t(blockIdx.x) * 2 * D + tid] = r;
+  }
+}
+
+// ---- resolution ---------------------------------------------------------------------------
+struct ResArgs {
+  const float* stage;
+  u32* tags;
+  i64 ncol;
+  int dim;
+  int j;
+  int ax[kLevels];
+  State* st;
+  u32* fine;    // resolution histograms [kNodes][kFine]
+  u32* coarse;  // [kNodes][kCoarse]
+  u64* small;   // [8][kSmallCap]
+  u32* err;
+};
+
+__device__ __forceinline__ u64 comp_of(const ResArgs& a, int axis, i64 i) {
+  const u32 k = orderable(a.stage[i64(axis) * a.ncol + i]);
+  const u32 id = __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+  return (u64(k) << 32) | id;
+}
+
+__global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
+  __shared__ u32 lc[8][3];
+  __shared__ u32 lco[8 * kCoarse];
+  __shared__ u32 lorig[16];
+  __shared__ u32 sa[8], sb[8], srs[8];
+  __shared__ u64 scl[8], spv[4];
+  const int j = a.j, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < nodes * kCoarse; i += kBlock) lco[i] = 0;
+  if (tid < 24) (&lc[0][0])[tid] = 0;
+  if (tid < 16) lorig[tid] = 0;
+  if (tid < nodes) {
+    sa[tid] = a.st->a[first + tid];
+    sb[tid] = a.st->b[first + tid];
+    srs[tid] = a.st->rshift[first + tid];
+    scl[tid] = a.st->comp_lo[first + tid];
+  }
+  if (j > 0 && tid < nodes / 2) spv[tid] = a.st->pivot[firstp + tid];
+  __syncthreads();
+  const i64 staged = a.st->cursor[kCells];
+  const int axj = a.ax[j], axp = j > 0 ? a.ax[j - 1] : 0;
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + tid; i < staged; i += stride) {
+    u32 T = a.tags[i];
+    if (T & kMed) continue;
+    if (j == 0) atomicAdd(&lorig[T & 15u], 1u);
+    int lvl = heap_level(T);
+    if (j > 0 && lvl == j - 1) {
+      const u64 comp = comp_of(a, axp, i);
+      const u64 P = spv[T - u32(firstp)];
+      T = comp < P ? 2 * T + 1 : (comp > P ? 2 * T + 2 : (kMed | T));
+      a.tags[i] = T;
+      if (T & kMed) {
+        a.st->med_idx1[T & 0xffu] = u32(i) + 1u;
+        continue;
+      }
+      lvl = j;
+    }
+    if (lvl != j) continue;
+    const u32 x = T - u32(first);
+    const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+    const int cls = k < sa[x] ? 0 : (k > sb[x] ? 2 : 1);
+    atomicAdd(&lc[x][cls], 1u);
+    if (cls == 1) {
+      const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+      const u32 d = u32(min<u64>((comp - scl[x]) >> srs[x], u64(kFine - 1)));
+      atomicAdd(&a.fine[size_t(T) * kFine + d], 1u);
+      atomicAdd(&lco[x * kCoarse + (d >> 8)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < nodes * kCoarse; i += kBlock) {
+    const u32 v = lco[i];
+    if (v) atomicAdd(&a.coarse[size_t(first) * kCoarse + i], v);
+  }
+  if (tid < nodes * 3) {
+    const u32 v = (&lc[0][0])[tid];
+    if (v) atomicAdd(&a.st->late[first + tid / 3][tid % 3], v);
+  }
+  if (j == 0 && tid < kNodes && lorig[tid]) atomicAdd(&a.st->staged_orig[tid], lorig[tid]);
+}
+
+// One wave per node of level j: the median's rank inside the band from the exact counts
+// (rows certain left / right from the scatter, staged rows classified by k_res_classify),
+// then the fine bin holding it.
+__global__ __launch_bounds__(64) void k_res_sel1(ResArgs a, Geom g) {
+  const int j = a.j, first = (1 << j) - 1;
+  const int X = first + blockIdx.x;
+  State* st = a.st;
+  const int ln = dev::lane();
+  u32 cl = 0, cr = 0;
+  if (ln < kHeap) {
+    const int Y = ln, ly = heap_level(u32(Y));
+    if (ly > j) {
+      const int anc = ((Y + 1) >> (ly - j - 1)) - 1;  // Y's ancestor at level j + 1
+      if (anc == 2 * X + 1 || anc == 2 * X + 2) {
+        const u32 cnt = Y >= kNodes ? st->cursor[Y - kNodes] : st->staged_orig[Y];
+        if (anc == 2 * X + 1) cl = cnt;
+        else cr = cnt;
+      }
+    }
+  }
+  cl = wave_sum(cl);
+  cr = wave_sum(cr);
+  const i64 L = i64(cl) + st->late[X][0], B = st->late[X][1], R = i64(cr) + st->late[X][2];
+  const i64 nX = g.n[X], t = nX / 2 - L;
+  const bool ok = L + B + R == nX && t >= 0 && t < B;
+  if (!ok) {
+    if (ln == 0) {
+      report(a.err, L + B + R != nX ? 0x2002u : 0x2003u, u32(X), u32(t < 0 ? 0 : (t >= B ? 1 : 2)));
+      st->sel[X] = 0xffffffffu;
+    }
+    return;
+  }
+  u32 below = 0, tot = 0;
+  const u32 bin = wave_find_fine(a.coarse + size_t(X) * kCoarse, a.fine + size_t(X) * kFine, u32(t), &below, &tot);
+  if (ln == 0) {
+    if (bin >= u32(kFine) || tot != u32(B)) {
+      report(a.err, 0x2004u, u32(X), tot);
+      st->sel[X] = 0xffffffffu;
+      return;
+    }
+    st->sel[X] = bin;
+    st->sel_rank[X] = u32(t) - below;
+    st->sel_cnt[X] = a.fine[size_t(X) * kFine + bin];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
+  __shared__ u32 sa[8], sb[8], srs[8], ssel[8];
+  __shared__ u64 scl[8];
+  const int j = a.j, nodes = 1 << j, first = nodes - 1;
+  const int tid = threadIdx.x;
+  if (tid < nodes) {
+    sa[tid] = a.st->a[first + tid];
+    sb[tid] = a.st->b[first + tid];
+    srs[tid] = a.st->rshift[first + tid];
+    scl[tid] = a.st->comp_lo[first + tid];
+    ssel[tid] = a.st->sel[first + tid];
+  }
+  __syncthreads();
+  const i64 staged = a.st->cursor[kCells];
+  const int axj = a.ax[j];
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + tid; i < staged; i += stride) {
+    const u32 T = a.tags[i];
+    if ((T & kMed) || heap_level(T) != j) continue;
+    const u32 x = T - u32(first);
+    const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+    if (k < sa[x] || k > sb[x]) continue;
+    const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+    const u32 d = u32(min<u64>((comp - scl[x]) >> srs[x], u64(kFine - 1)));
+    if (d != ssel[x]) continue;
+    const u32 p = atomicAdd(&a.st->small_cnt[T], 1u);
+    if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
+  }
+}
+
+// rank-th smallest (0-based) of the candidate composites visited by each(f) (f(u64) per
+// candidate; every thread of the block calls it, visiting its share): MSD radix select with
+// 8-bit digits below the highest bit in which the candidates differ.
+template <class Each>
+__device__ u64 block_select(Each each, u32 rank) {
+  __shared__ __align__(16) u32 hist[256];
+  __shared__ u64 rmn[kBlock / 64], rmx[kBlock / 64];
+  __shared__ u32 info[2];
+  u64 mn = ~0ull, mx = 0ull;
+  each([&](u64 v) {
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  });
+  mn = dev::wave_min_u64(mn);
+  mx = dev::wave_max_u64(mx);
+  if (dev::lane() == 0) {
+    rmn[threadIdx.x / 64] = mn;
+    rmx[threadIdx.x / 64] = mx;
+  }
+  __syncthreads();
+  mn = rmn[0];
+  mx = rmx[0];
+  for (int k = 1; k < kBlock / 64; ++k) {
+    mn = rmn[k] < mn ? rmn[k] : mn;
+    mx = rmx[k] > mx ? rmx[k] : mx;
+  }
+  const u64 diff = mn ^ mx;
+  if (!diff) return mn;
+  int hb = 63 - __builtin_clzll(diff);
+  u64 prefix = hb >= 63 ? 0ull : (mn & ~((2ull << hb) - 1ull));
+  while (hb >= 0) {
+    const int sh = hb >= 7 ? hb - 7 : 0;
+    const u32 dmask = (2u << (hb - sh)) - 1u;
+    const u64 himask = hb >= 63 ? 0ull : ~((2ull << hb) - 1ull);
+    __syncthreads();
+    hist[threadIdx.x] = 0u;
+    __syncthreads();
+    each([&](u64 v) {
+      if ((v & himask) == prefix) atomicAdd(&hist[u32(v >> sh) & dmask], 1u);
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      u32 below = 0, tot = 0;
+      const u32 b = wave_find256(hist, rank, &below, &tot);
+      if (threadIdx.x == 0) {
+        info[0] = b;
+        info[1] = below;
+      }
+    }
+    __syncthreads();
+    prefix |= u64(info[0] & dmask) << sh;
+    rank -= info[1];
+    hb = sh - 1;
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
+  __shared__ u64 buf[kSmallCap];
+  const int j = a.j, first = (1 << j) - 1;
+  const int X = first + blockIdx.x, x = blockIdx.x;
+  State* st = a.st;
+  const u32 sel = st->sel[X];
+  if (sel == 0xffffffffu) return;
+  const u32 cnt = st->sel_cnt[X], rank = st->sel_rank[X];
+  u64 pivot;
+  if (cnt <= u32(kSmallCap)) {
+    if (st->small_cnt[X] != cnt) {
+      if (threadIdx.x == 0) report(a.err, 0x2005u, u32(X), st->small_cnt[X]);
+      return;
+    }
+    for (u32 e = threadIdx.x; e < cnt; e += kBlock) buf[e] = a.small[size_t(x) * kSmallCap + e];
+    __syncthreads();
+    pivot = block_select(
+        [&](auto f) {
+          for (u32 e = threadIdx.x; e < cnt; e += kBlock) f(buf[e]);
+        },
+        rank);
+  } else {
+    // heavy duplicates: the bin holds more rows than LDS takes; select over the staging arena
+    // (every pass streams the staged rows: slow, but exact for any input)
+    const i64 staged = st->cursor[kCells];
+    const u32 A = st->a[X], B = st->b[X], rs = st->rshift[X];
+    const u64 clo = st->comp_lo[X];
+    const int axj = a.ax[j];
+    pivot = block_select(
+        [&](auto f) {
+          for (i64 i = threadIdx.x; i < staged; i += kBlock) {
+            if (a.tags[i] != u32(X)) continue;
+            const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+            if (k < A || k > B) continue;
+            const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+            if (u32(min<u64>((comp - clo) >> rs, u64(kFine - 1))) == sel) f(comp);
+          }
+        },
+        rank);
+  }
+  if (threadIdx.x == 0) st->pivot[X] = pivot;
+}
+
+struct InsArgs {
+  const float* stage;
+  const u32* tags;
+  float* cols;
+  i64 ncol;
+  int dim;
+  int ax3;
+  State* st;
+  u32* err;
+  i64 cell_lo[kCells];
+  u32 cell_n[kCells];
+};
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
+  constexpr int R = kInsChunk / kBlock;
+  __shared__ u32 wcnt[4][kCells], zoff[4][kCells], cert[kCells];
+  __shared__ u64 spv[8];
+  const int tid = threadIdx.x, w = tid >> 6;
+  if (tid < 8) spv[tid] = a.st->pivot[7 + tid];
+  if (tid < kCells) cert[tid] = a.st->cursor[tid];
+  if (tid < 4 * kCells) (&wcnt[0][0])[tid] = 0u;
+  __syncthreads();
+  const i64 staged = a.st->cursor[kCells];
+  const i64 chunks = (staged + kInsChunk - 1) / kInsChunk;
+  for (i64 ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
+    const i64 c0 = ch * kInsChunk;
+    u32 code[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const i64 i = c0 + i64(u) * kBlock + tid;
+      u32 z = 31u, r = 0;
+      if (i < staged) {
+        const u32 T = a.tags[i];
+        if (!(T & kMed)) {
+          if (heap_level(T) != kLevels - 1) {
+            report(a.err, 0x2006u, T, u32(i));
+          } else {
+            const u64 comp = (u64(orderable(a.stage[i64(a.ax3) * a.ncol + i])) << 32) |
+                             __float_as_uint(a.stage[i64(D) * a.ncol + i]);
+            const u64 P = spv[T - 7u];
+            if (comp == P) {
+              a.st->med_idx1[T] = u32(i) + 1u;
+            } else {
+              z = (comp < P ? 2 * T + 1 : 2 * T + 2) - u32(kNodes);
+              r = atomicAdd(&wcnt[w][z], 1u);
+            }
+          }
+        }
+      }
+      code[u] = r | (z << 16);
+    }
+    __syncthreads();
+    if (tid < kCells) {
+      u32 tot = 0;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        zoff[ww][tid] = tot;
+        tot += wcnt[ww][tid];
+        wcnt[ww][tid] = 0u;
+      }
+      const u32 base = tot ? atomicAdd(&a.st->ins[tid], tot) : 0u;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) zoff[ww][tid] += base + cert[tid];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const u32 z = code[u] >> 16;
+      if (z == 31u) continue;
+      const i64 i = c0 + i64(u) * kBlock + tid;
+      const u32 pos = zoff[w][z] + (code[u] & 0xffffu);
+      if (pos >= a.cell_n[z]) {
+        report(a.err, 0x2007u, z, pos);
+        continue;
+      }
+      const i64 q = a.cell_lo[z] + pos;
+#pragma unroll
+      for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + q] = a.stage[i64(c) * a.ncol + i];
+    }
+    __syncthreads();
+  }
+}
+
+struct FinArgs {
+  const float* stage;
+  i64 ncol;
+  int dim;
+  State* st;
+  const u32* part;
+  int nparts;
+  float* out_pts;
+  u32* out_ids;
+  float* cells;
+  dev::BucketParams* params;
+  int bins4;
+  u32* err;
+};
+
+__global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
+  __shared__ u32 box[16];
+  __shared__ float split[kNodes];
+  __shared__ u32 have[kNodes];
+  __shared__ u32 red[kBlock / 64];
+  const int D = a.dim, tid = threadIdx.x;
+  for (int c = 0; c < 2 * D; ++c) {  // bounding box from the scatter blocks' partials
+    u32 v = c < D ? 0xffffffffu : 0u;
+    for (int p = tid; p < a.nparts; p += kBlock) {
+      const u32 x = a.part[size_t(p) * 2 * D + c];
+      v = c < D ? min(v, x) : max(v, x);
+    }
+    v = c < D ? dev::wave_min_u32(v) : dev::wave_max_u32(v);
+    if (dev::lane() == 0) red[tid / 64] = v;
+    __syncthreads();
+    if (tid == 0) {
+      u32 r = red[0];
+      for (int k = 1; k < kBlock / 64; ++k) r = c < D ? min(r, red[k]) : max(r, red[k]);
+      box[c] = r;
+    }
+    __syncthreads();
+  }
+  if (tid < kCells && a.st->cursor[tid] + a.st->ins[tid] != u32(g.n[kNodes + tid]))
+    report(a.err, 0x2008u, u32(tid), a.st->cursor[tid] + a.st->ins[tid]);
+  if (tid < kNodes) {
+    const u32 i1 = a.st->med_idx1[tid];
+    have[tid] = i1 != 0u;
+    split[tid] = 0.0f;
+    if (i1 == 0u) {
+      if (!(*a.err & kErrBit)) report(a.err, 0x2009u, u32(tid), 0u);
+    } else {
+      const i64 i = i64(i1) - 1;
+      const i64 mpos = g.lo[tid] + g.n[tid] / 2;
+      for (int c = 0; c < D; ++c) a.out_pts[mpos * D + c] = a.stage[i64(c) * a.ncol + i];
+      a.out_ids[mpos] = __float_as_uint(a.stage[i64(D) * a.ncol + i]);
+      split[tid] = a.stage[i64(g.axis[heap_level(u32(tid))]) * a.ncol + i];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float* cells = a.cells;
+    for (int c = 0; c < D; ++c) {
+      cells[2 * c] = from_orderable(box[c]);
+      cells[2 * c + 1] = from_orderable(box[D + c]);
+    }
+    for (int X = 0; X < kNodes; ++X) {
+      const int ax = g.axis[heap_level(u32(X))];
+      const float* cp = cells + size_t(X) * 2 * D;
+      float* cl = cells + size_t(2 * X + 1) * 2 * D;
+      float* cr = cells + size_t(2 * X + 2) * 2 * D;
+      for (int c = 0; c < 2 * D; ++c) {
+        cl[c] = cp[c];
+        cr[c] = cp[c];
+      }
+      if (have[X]) {
+        cl[2 * ax + 1] = split[X];
+        cr[2 * ax] = split[X];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < kCells) {
+    const int h = kNodes + tid, ax = g.axis[kLevels];
+    const float* c = a.cells + size_t(h) * 2 * D;
+    a.params[h] = dev::make_params(c[2 * ax], c[2 * ax + 1], a.bins4);
+  }
+}
+
+}  // namespace
+
+size_t workspace_bytes() { return layout().total; }
+
+void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
+  const Layout L = layout();
+  char* ws = static_cast<char*>(io.ws);
+  State* st = reinterpret_cast<State*>(ws + L.state);
+  u32* fine_s = reinterpret_cast<u32*>(ws + L.fine_s);
+  u32* coarse_s = reinterpret_cast<u32*>(ws + L.coarse_s);
+  u32* fine_r = reinterpret_cast<u32*>(ws + L.fine_r);
+  u32* coarse_r = reinterpret_cast<u32*>(ws + L.coarse_r);
+  u32* skey = reinterpret_cast<u32*>(ws + L.skey);
+  u64* small = reinterpret_cast<u64*>(ws + L.small);
+  u32* part = reinterpret_cast<u32*>(ws + L.part);
+  const int D = g.dim;
+  if (D < 2 || D > 8) throw std::invalid_argument("top4: dim 2..8");
+  const i64 n = io.n;
+  int sl = std::min(kMaxSampleLog2, std::max(8, t.sample_log2));
+  while (sl > 8 && (i64(1) << sl) > n / 4) --sl;
+  const int S = 1 << sl;
+
+  const i64 zwords = i64(L.zero_end - L.state) / 4;
+  k_zero_top<<<int(std::min<i64>(1024, (zwords + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
+      reinterpret_cast<u32*>(ws + L.state), zwords);
+  PKD_LAUNCH_CHECK();
+
+  SampArgs sa{io.pts, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, st};
+  const int sgrid = std::max(1, std::min(256, S / kBlock));
+  k_samp_gather<<<sgrid, kBlock, 0, stream>>>(sa);
+  PKD_LAUNCH_CHECK();
+  for (int j = 0; j < kLevels; ++j) {
+    SampLevelArgs la{skey, S, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3], g.axis[4]}, st, fine_s, coarse_s, t.z};
+    k_samp_hist<<<sgrid, kBlock, 0, stream>>>(la);
+    PKD_LAUNCH_CHECK();
+    k_samp_sel<<<1 << j, 64, 0, stream>>>(la);
+    PKD_LAUNCH_CHECK();
+  }
+
+  ScatArgs sc{};
+  sc.pts = io.pts;
+  sc.ids = io.ids;
+  sc.id_base = io.id_base;
+  sc.n = n;
+  sc.cols = io.cols;
+  sc.stage = io.stage;
+  sc.tags = io.out_ids;
+  sc.ncol = io.ncol;
+  sc.st = st;
+  sc.part = part;
+  sc.err = io.err;
+  for (int c = 0; c < kCells; ++c) {
+    sc.cell_lo[c] = g.lo[kNodes + c];
+    sc.cell_n[c] = u32(g.n[kNodes + c]);
+  }
+  for (int j = 0; j < kLevels; ++j) sc.ax[j] = g.axis[j];
+  const int R = D <= 4 ? 16 : 8;
+  const i64 tile = i64(kBlock) * R;
+  sc.tiles = (n + tile - 1) / tile;
+  const int sblocks = int(std::max<i64>(1, std::min<i64>(t.scatter_blocks > 0 ? t.scatter_blocks : kMaxParts, sc.tiles)));
+  const bool vec = D == 3 && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
+                   (io.ids == nullptr || reinterpret_cast<uintptr_t>(io.ids) % 16 == 0);
+  switch (D) {
+    case 2: k_scatter<2, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 3:
+      if (vec) k_scatter<3, true><<<sblocks, kBlock, 0, stream>>>(sc);
+      else k_scatter<3, false><<<sblocks, kBlock, 0, stream>>>(sc);
+      break;
+    case 4: k_scatter<4, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 5: k_scatter<5, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 6: k_scatter<6, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 7: k_scatter<7, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    default: k_scatter<8, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+  }
+  PKD_LAUNCH_CHECK();
+
+  // staged rows are a few percent of n: grids sized for ~16 % of the rows, grid-stride beyond
+  const int rgrid = int(std::max<i64>(64, std::min<i64>(2048, (n / 6 + kBlock * 4 - 1) / (kBlock * 4))));
+  for (int j = 0; j < kLevels; ++j) {
+    ResArgs ra{io.stage, io.out_ids, io.ncol, D, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, st, fine_r,
+               coarse_r, small, io.err};
+    k_res_classify<<<rgrid, kBlock, 0, stream>>>(ra);
+    PKD_LAUNCH_CHECK();
+    k_res_sel1<<<1 << j, 64, 0, stream>>>(ra, g);
+    PKD_LAUNCH_CHECK();
+    k_res_collect<<<rgrid, kBlock, 0, stream>>>(ra);
+    PKD_LAUNCH_CHECK();
+    k_res_sel2<<<1 << j, kBlock, 0, stream>>>(ra);
+    PKD_LAUNCH_CHECK();
+  }
+  InsArgs ia{};
+  ia.stage = io.stage;
+  ia.tags = io.out_ids;
+  ia.cols = io.cols;
+  ia.ncol = io.ncol;
+  ia.dim = D;
+  ia.ax3 = g.axis[3];
+  ia.st = st;
+  ia.err = io.err;
+  for (int c = 0; c < kCells; ++c) {
+    ia.cell_lo[c] = g.lo[kNodes + c];
+    ia.cell_n[c] = u32(g.n[kNodes + c]);
+  }
+  const int igrid = int(std::max<i64>(16, std::min<i64>(1024, (n / 6 + kInsChunk - 1) / kInsChunk)));
+  switch (D) {
+    case 2: k_res_insert<2><<<igrid, kBlock, 0, stream>>>(ia); break;
+    case 3: k_res_insert<3><<<igrid, kBlock, 0, stream>>>(ia); break;
+    case 4: k_res_insert<4><<<igrid, kBlock, 0, stream>>>(ia); break;
+    case 5: k_res_insert<5><<<igrid, kBlock, 0, stream>>>(ia); break;
+    case 6: k_res_insert<6><<<igrid, kBlock, 0, stream>>>(ia); break;
+    case 7: k_res_insert<7><<<igrid, kBlock, 0, stream>>>(ia); break;
+    default: k_res_insert<8><<<igrid, kBlock, 0, stream>>>(ia); break;
+  }
+  PKD_LAUNCH_CHECK();
+  FinArgs fa{io.stage, io.ncol, D, st, part, sblocks, io.out_pts, io.out_ids, io.cells, io.params, io.bins4, io.err};
+  k_finish<<<1, kBlock, 0, stream>>>(fa, g);
+  PKD_LAUNCH_CHECK();
+}
+
+void band_report(const void* ws, hipStream_t stream, u32 (*out)[3]) {
+  const Layout L = layout();
+  State h{};
+  PKD_HIP_CHECK(hipMemcpyAsync(&h, static_cast<const char*>(ws) + L.state, sizeof(State), hipMemcpyDeviceToHost,
+                               stream));
+  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  for (int X = 0; X < kNodes; ++X) {
+    out[X][0] = h.late[X][1];
+    out[X][1] = h.sel_rank[X];  // rank inside the median's fine bin (see sel for the bin)
+    out[X][2] = h.staged_orig[X];
+  }
+}
+
+}  // namespace top4
+}  // namespace pkdtree

@@ -31,6 +31,9 @@ struct BuildOptions {
   // off for its leaf builds: their streams plus its communication stream would exceed the
   // hardware queues (GPU_MAX_HW_QUEUES = 4), and RCCL's kernels would queue behind partitions.
   bool allow_split = true;
+  // Sampled top levels allowed (AoS-input builds of >= Tuning::top_min_n points). Off for the
+  // distributed builder's leaf builds: they start from received SoA columns.
+  bool allow_top = true;
 };
 
 // A/B and diagnostic knobs of the builder (PKD_* environment variables, README "Tuning"),
@@ -60,6 +63,13 @@ struct Tuning {
                                         // since k_tail3 a 100 M x 3D split build is ~1% slower than one stream,
                                         // 1 B x 3D 0.4% faster, 100 M x 8D 1.5-6% faster (r3_ab_split_s3.txt)
   i64 split_min(int dim) const { return dim <= 3 ? split_min_n_3d : split_min_n; }
+  // Sampled top levels (csrc/gpu/top4.hpp): levels 0..3 from an estimated band per node, one
+  // scatter pass from the AoS input, exact fix-up of the staged band rows.
+  bool top = true;            // PKD_TOP=0: levels 0..3 by the exact pairs
+  i64 top_min_n = i64(16) << 20;  // PKD_TOP_MIN_N: smallest build that samples its top levels
+  int top_sample_log2 = 20;   // PKD_TOP_SAMPLE: log2 of the sample rows
+  float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
+  int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
   static Tuning from_env();
 };
 
@@ -75,6 +85,7 @@ struct LevelPlan {
   bool pair = false;    // this level and the next are moved by ONE fused partition pass
   bool triple = false;  // this level and the next two are moved by ONE fused partition pass
   bool tail = false;    // this level and the next two: one workgroup per segment (k_tail3)
+  bool sampled = false; // built by the sampled top levels (top4::run)
 };
 
 struct SplitStreams;  // side HIP streams + fork / join events of a split build
@@ -87,6 +98,11 @@ class GpuBuilder {
   i64 column_stride() const { return ncol_; }
   int dim() const { return dim_; }
   int global_levels() const { return lg_; }
+  // Levels 0..3 built by the sampled top pass (AoS input builds; see top4.hpp).
+  bool sampled_top() const { return top_; }
+  // Diagnostic: per top node {band rows, rank inside the median's fine bin, rows staged at
+  // the node} of the last build on `workspace` (synchronises).
+  std::vector<u32> top_band_report(const void* workspace, hipStream_t stream) const;
   int subtree_max() const { return nsub_; }
   // Split build (0 parts: off): from level split_level() on, the 2^split_level segments are
   // built as split_parts() independent parts on split_streams() HIP streams.
@@ -133,8 +149,11 @@ class GpuBuilder {
   // in_rows != nullptr: narrow columns (the lg_ global levels' keys, ids, input row index);
   // full rows are gathered from the AoS input `in_rows` (stride in_rs floats).
   // cols_a != nullptr: replaces the workspace's first column buffer (the input of the first pass).
+  // first_level > 0: levels [0, first_level) are already built (the sampled top levels): their
+  // cells, the first level's histogram parameters and the error word are set.
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
-                  u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0, float* cols_a = nullptr) const;
+                  u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0, float* cols_a = nullptr,
+                  int first_level = 0) const;
   // Side streams for a split build on the current device (nullptr: run unsplit, e.g. when
   // the streams do not exist yet and `stream` is being captured into a graph).
   SplitStreams* split_streams_for(hipStream_t stream) const;
@@ -154,6 +173,8 @@ class GpuBuilder {
   bool narrow_ = false;  // high-dim: narrow columns + key-slot subtree (capacity nsub_ sized for it)
   int tail_ = -1;        // first of the last three global levels, built by k_tail3 (-1: none)
   int tail_items_ = 0;   // rows per thread of its 1024-thread workgroups
+  bool top_ = false;     // levels 0..3 by the sampled top pass (AoS input builds)
+  size_t off_top_ = 0;
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,
@@ -167,6 +188,10 @@ class GpuBuilder {
   size_t split_hist_ = 0, split_hist2_ = 0, split_bcnt_ = 0;  // u32 words per set
   std::shared_ptr<SplitStreams> split_;
 };
+
+// Error-word bit of the sampled top levels: a band missed its median (the build is invalid and
+// must be redone with BuildOptions::allow_top = false).
+constexpr u32 top4_band_miss_bit() { return 0x20u; }
 
 // Subtree kernel capacity for a dimension (largest power of two whose LDS image fits).
 int default_subtree_max(int dim);

@@ -49,6 +49,9 @@ def main(argv=None) -> int:
                     "(<path>.rank<r>), global: the assembled tree from rank 0")
     ap.add_argument("--leaf-threshold", type=int, default=0,
                     help="largest segment finished by the LDS subtree kernel (0 = auto from dim)")
+    ap.add_argument("--ranks", type=int, default=0,
+                    help="--decomp forest: logical forest ranks (the reference's mpirun -np R, Makefile:36) spread "
+                         "over the processes; 0 = one per process")
     ap.add_argument("positional", nargs="*")
     a = ap.parse_args(argv)
     tick = time.perf_counter()
@@ -85,8 +88,11 @@ def main(argv=None) -> int:
         first, cnt = 0, n
     else:
         first, cnt = comm.forest_slice(n, world, rank)
+    R = a.ranks or world
+    if R != world and decomp != "forest":
+        raise SystemExit("--ranks applies to --decomp forest")
     gen_dev = device if (device.type == "cuda" and not a.host_gen) else None
-    x = pk.generate_slice(seed, dim, first, cnt, device=gen_dev).to(device)
+    x = pk.generate_slice(seed, dim, first, cnt, device=gen_dev).to(device) if R == world else None
     q = pk.generate_slice(seed, dim, n, Q, device=gen_dev).to(device)
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -99,12 +105,21 @@ def main(argv=None) -> int:
         if a.save:
             tree.save(a.save)
     elif decomp == "forest":
-        from .parallel.forest import ForestTree
-        f = ForestTree.build(x, first, n, id_base=1, mode=a.mode)
-        packed = f.query_packed(q, a.query)
-        _all_ok(comm, f.local_error(), device)
+        from .parallel.forest import ForestTree, forest_min_packed, logical_ranks
+        # R logical ranks over the processes (R = world: one each, the reference's mpirun -np P)
+        trees = []
+        for lr in logical_ranks(R, world, rank):
+            f0, c0 = comm.forest_slice(n, R, lr)
+            xs = x if R == world else pk.generate_slice(seed, dim, f0, c0, device=gen_dev).to(device)
+            trees.append((lr, ForestTree.build(xs, f0, n, id_base=1, mode=a.mode)))
+        packed = forest_min_packed([t for _, t in trees], q, a.query)
+        err = 0
+        for _, t in trees:
+            err |= t.local_error()
+        _all_ok(comm, err, device)
         if a.save:
-            f.local.save(f"{a.save}.rank{rank}")
+            for lr, t in trees:
+                t.local.save(f"{a.save}.rank{lr}")
     else:
         if a.mode != "exact":
             raise SystemExit("--decomp global builds exact trees only")

@@ -53,8 +53,8 @@ class KDTree:
         if check_ids:
             ops.check_unique_ids(ids)
         if points.is_cuda and mode == "exact":
-            b = ops.gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
-            tp, ti = b.build(points, ids, id_base)
+            # (a sampled-top build is checked on the host and rebuilt unsampled if a band missed)
+            tp, ti, b = ops.build_gpu_checked(points, ids, id_base, depth0, subtree_max)
             t = cls(tp, ti, depth0, mode)
             t._err = b.error_words()  # this build's error words (device copy, stream-ordered)
             return t

@@ -21,9 +21,12 @@ class GpuTreeBuilder:
     (benchmarks, rebuilds of a streaming index) allocate nothing.
     """
 
-    def __init__(self, n: int, dim: int, depth0: int = 0, subtree_max: int = 0):
-        self._b = native().GpuBuilder(int(n), int(dim), int(depth0), int(subtree_max))
+    TOP_BAND_MISS = 0x20  # error bit: a sampled top band missed its median (rebuild unsampled)
+
+    def __init__(self, n: int, dim: int, depth0: int = 0, subtree_max: int = 0, allow_top: bool = True):
+        self._b = native().GpuBuilder(int(n), int(dim), int(depth0), int(subtree_max), bool(allow_top))
         self.n, self.dim, self.depth0 = int(n), int(dim), int(depth0)
+        self.subtree_max_arg = int(subtree_max)
 
     @property
     def workspace_bytes(self) -> int:
@@ -44,6 +47,17 @@ class GpuTreeBuilder:
 
     def describe(self) -> str:
         return self._b.describe()
+
+    @property
+    def sampled_top(self) -> bool:
+        """Levels 0..3 come from the sampled top pass (csrc/gpu/top4.hpp)."""
+        return bool(self._b.sampled_top)
+
+    def top_band_report(self):
+        """Per top node (heap 0..14) of the last build: (band rows, rank inside the median's
+        fine bin, rows the scatter staged at the node). Synchronises."""
+        v = list(self._b.top_band_report())
+        return [tuple(v[3 * i:3 * i + 3]) for i in range(len(v) // 3)]
 
     def read_error(self) -> int:
         """Sticky device error word of the last build (0 = ok). Synchronises."""
@@ -119,6 +133,26 @@ def build_gpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base:
     points = points.contiguous()
     b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
     return b.build(points, ids, id_base)
+
+
+def build_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
+                      depth0: int = 0, subtree_max: int = 0):
+    """build_gpu, then -- for builds whose top levels were sampled -- a host check of the error
+    word: a band that missed its median (error bit TOP_BAND_MISS; ~1e-12 per node at the
+    default z, for any input order) is rebuilt without sampling. Returns (tree_pts, tree_ids,
+    builder). Synchronises only for sampled builds."""
+    points = points.contiguous()
+    b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
+    tp, ti = b.build(points, ids, id_base)
+    if b.sampled_top and (b.read_error() & GpuTreeBuilder.TOP_BAND_MISS):
+        key = ("unsampled", points.shape[0], points.shape[1], depth0, subtree_max, points.device)
+        fb = _builders.get(key)
+        if fb is None:
+            fb = _builders[key] = GpuTreeBuilder(points.shape[0], points.shape[1], depth0, subtree_max,
+                                                 allow_top=False)
+        tp, ti = fb.build(points, ids, id_base, tp, ti)
+        b = fb
+    return tp, ti, b
 
 
 def check_unique_ids(ids: Optional[torch.Tensor]) -> None:

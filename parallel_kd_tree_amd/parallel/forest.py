@@ -35,7 +35,33 @@ class ForestTree:
         e = self.local._err
         return int(e[0].item()) & 0xFFFFFFFF if e is not None else 0
 
+    def local_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
+        """Packed (d2, global id) of the nearest point of THIS slice (no communication)."""
+        return _local_packed(self.local, queries, method)
+
     def query_packed(self, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
         """Packed (d2, global id) of the nearest point over all ranks. Reference-mode forests
         use the reference search on each rank (so results match kdtree_mpi exactly)."""
-        return comm.min_packed_(_local_packed(self.local, queries, method).to(comm.device()))
+        return comm.min_packed_(self.local_packed(queries, method).to(comm.device()))
+
+
+def logical_ranks(ranks: int, world: int, rank: int) -> range:
+    """The logical forest ranks a process owns when R logical ranks (the reference's `mpirun
+    -np R`, Makefile:36 runs 16) are spread over P processes / GPUs: a contiguous block of
+    R / P (the first R % P processes take one more). Each logical rank keeps the reference's
+    slicing of the generation order (kdtree_mpi.cpp:204-224) at R, so the forest -- and in
+    reference mode its answers, which depend on R -- is the reference's at -np R."""
+    if ranks < world:
+        raise ValueError(f"--ranks {ranks} < {world} processes")
+    q, r = divmod(ranks, world)
+    lo = rank * q + min(rank, r)
+    return range(lo, lo + q + (1 if rank < r else 0))
+
+
+def forest_min_packed(trees, queries: torch.Tensor, method: str = "auto") -> torch.Tensor:
+    """MIN over this process's forest slices, then over the processes (one reduction)."""
+    best = None
+    for t in trees:
+        p = t.local_packed(queries, method).to(comm.device())
+        best = p if best is None else torch.minimum(best, p)
+    return comm.min_packed_(best)  # (every process owns at least one logical rank)

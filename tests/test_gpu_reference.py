@@ -121,3 +121,33 @@ def test_kdtree_dist_global_save_share_gpu(tmp_path, gpus):
     x = pk.generate_problem(13, 3, 250_001)
     cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
     assert torch.equal(t.tree_ids, ci + 1) and torch.equal(t.tree_pts, cp)
+
+
+@pytest.mark.parametrize("ranks,gpus,cfg", [(16, 2, (42, 3, 20000)), (16, 3, (5, 3, 16003)), (5, 2, (7, 2, 9001))])
+def test_kdtree_dist_logical_ranks_reference(ranks, gpus, cfg):
+    """kdtree_dist --ranks R --gpus P: the reference's `mpirun -np 16` (Makefile:36) forest on
+    fewer GPUs. Every logical rank keeps the reference slicing at R, so reference-mode answers
+    (which depend on the forest) are those of R reference ranks: here the CPU
+    reference-mode builder per slice, which the parity tests pin to the reference MPI driver at
+    -np 16 (tests/test_reference_parity.py::test_mpi_16_ranks_on_fewer_processes)."""
+    seed, dim, n = cfg
+    g = _run([BIN / "kdtree_dist", "--gpus", gpus, "--ranks", ranks, "--share-gpu", "--mode", "reference",
+              seed, dim, n])
+    assert g.returncode == 0, g.stderr[-2000:]
+    lines = [l for l in g.stdout.splitlines() if l.startswith("ID:")]
+    x = pk.generate_problem(seed, dim, n + 10)
+    q = x[n:]
+    best = None
+    local = n // ranks
+    for r in range(ranks):
+        first, cnt = local * r, local + (n % ranks if r == ranks - 1 else 0)
+        t = pk.KDTree.build(x[first:first + cnt], id_base=first + 1, mode="reference")
+        d, _ = t.query(q)
+        best = d if best is None else torch.minimum(best, d)
+    from parallel_kd_tree_amd.utils import protocol
+    assert lines == [protocol.result_line(n + i, float(best[i])) for i in range(10)]
+    e = _run([BIN / "kdtree_dist", "--gpus", gpus, "--ranks", ranks, "--share-gpu", seed, dim, n])
+    assert e.returncode == 0, e.stderr[-2000:]
+    c = _run([BIN / "kdtree_sequential", seed, dim, n])  # exact mode: any forest answers the true NN
+    strip = lambda out: [l for l in out.splitlines() if l.startswith("ID:")]  # noqa: E731
+    assert strip(e.stdout) == strip(c.stdout)

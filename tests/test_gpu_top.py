@@ -1,0 +1,107 @@
+"""Sampled top levels (csrc/gpu/top4.hpp): levels 0..3 from estimated bands + one scatter
+pass + exact fix-up must give the SAME tree as the CPU exact builder, slot for slot, for any
+input: sizes, dims 2..8, depth0, explicit ids, heavy duplicates, sorted input. A band that
+misses its median is reported (error bit 0x20) and KDTree.build rebuilds without sampling."""
+import pytest
+import torch
+
+import parallel_kd_tree_amd as pk
+from parallel_kd_tree_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_as_cpu(x, dev, depth0=0, ids=None, expect_top=True):
+    b = ops.GpuTreeBuilder(x.shape[0], x.shape[1], depth0, 0)
+    assert b.sampled_top == expect_top, b.describe()
+    tp, ti = b.build(x.to(dev), None if ids is None else ids.to(dev))
+    cp, ci = ops.build_cpu(x, ids, "exact", depth0, 8)
+    torch.cuda.synchronize()
+    assert b.read_error_detail()[0] == 0, b.read_error_detail()
+    assert torch.equal(ti.cpu(), ci), "GPU tree differs from the CPU exact tree"
+    assert torch.equal(tp.cpu(), cp)
+    return b
+
+
+@pytest.fixture
+def top_always(monkeypatch):
+    monkeypatch.setenv("PKD_TOP_MIN_N", "0")
+
+
+@pytest.mark.parametrize("n,dim,depth0", [(200_000, 3, 0), (300_001, 2, 0), (1_000_003, 3, 1), (500_000, 5, 2),
+                                          (400_000, 8, 0), (2_000_000, 4, 3), (700_000, 7, 6), (250_000, 6, 0)])
+def test_top_equals_cpu_exact(gpu_device, top_always, n, dim, depth0):
+    b = _same_as_cpu(pk.generate_problem(n + dim, dim, n), gpu_device, depth0)
+    rep = b.top_band_report()
+    assert len(rep) == 15 and all(r[0] > 0 for r in rep), rep  # every node resolved from a non-empty band
+
+
+def test_top_explicit_ids(gpu_device, top_always):
+    n = 300_000
+    x = pk.generate_problem(77, 3, n)
+    ids = torch.randperm(n, dtype=torch.int64).to(torch.int32) * 3 + 11
+    _same_as_cpu(x, gpu_device, 0, ids)
+
+
+@pytest.mark.parametrize("vals", [2, 7, 1000])
+def test_top_duplicates(gpu_device, top_always, vals):
+    """Few distinct values: bands are key ranges holding whole runs of equal keys, the median
+    is selected on (key, id); with 2 values a median bin overflows LDS (the exact slow path)."""
+    torch.manual_seed(vals)
+    _same_as_cpu(torch.randint(0, vals, (400_000, 3)).float(), gpu_device)
+
+
+def test_top_sorted_and_constant_axis(gpu_device, top_always):
+    x = pk.generate_problem(9, 3, 300_000)
+    _same_as_cpu(x[torch.argsort(x[:, 0])].contiguous(), gpu_device)   # sorted on the first axis
+    y = pk.generate_problem(10, 3, 300_000)
+    y[:, 1] = 5.0                                                        # a constant axis
+    _same_as_cpu(y, gpu_device)
+
+
+def test_top_unaligned_input(gpu_device, top_always):
+    """A row-offset view (not 16-B aligned) takes the scalar-load scatter."""
+    x = pk.generate_problem(12, 3, 300_001)
+    xg = x.to(gpu_device)[1:]
+    b = ops.GpuTreeBuilder(300_000, 3, 0, 0)
+    tp, ti = b.build(xg, None, 0)
+    cp, ci = ops.build_cpu(x[1:].contiguous(), None, "exact", 0, 8)
+    torch.cuda.synchronize()
+    assert b.read_error() == 0 and torch.equal(ti.cpu(), ci)
+
+
+def test_top_off_below_threshold(gpu_device):
+    """Default threshold: small builds keep the paired levels."""
+    b = ops.GpuTreeBuilder(1_000_000, 3, 0, 0)
+    assert not b.sampled_top
+
+
+def test_top_20m_equals_pairs(gpu_device, monkeypatch):
+    """At the default threshold (20 M points): the sampled tree equals the paired-levels tree."""
+    x = pk.generate_slice(3, 3, 0, 20_000_000, device=gpu_device)
+    b = ops.GpuTreeBuilder(x.shape[0], 3, 0, 0)
+    assert b.sampled_top
+    tp, ti = b.build(x, None, 1)
+    monkeypatch.setenv("PKD_TOP", "0")
+    b0 = ops.GpuTreeBuilder(x.shape[0], 3, 0, 0)
+    assert not b0.sampled_top
+    tp0, ti0 = b0.build(x, None, 1)
+    torch.cuda.synchronize()
+    assert b.read_error() == 0 and b0.read_error() == 0
+    assert torch.equal(ti, ti0) and torch.equal(tp, tp0)
+
+
+def test_top_band_miss_detected_and_rebuilt(gpu_device, top_always, monkeypatch):
+    """Bands far too narrow (z = 0.01) miss their medians: the build must REPORT it (bit 0x20),
+    never return a wrong tree silently, and KDTree.build must rebuild it exactly."""
+    monkeypatch.setenv("PKD_TOP_Z", "0.01")
+    x = pk.generate_problem(21, 3, 400_000)
+    b = ops.GpuTreeBuilder(x.shape[0], 3, 0, 0)
+    b.build(x.to(gpu_device))
+    torch.cuda.synchronize()
+    assert b.read_error() & 0x20
+    ops._builders.clear()
+    t = pk.KDTree.build(x.to(gpu_device))
+    t.check()
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    assert torch.equal(t.tree_ids.cpu(), ci)

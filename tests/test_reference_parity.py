@@ -83,12 +83,12 @@ def _free_port():
     return p
 
 
-def _ours_forest(P, args):
+def _ours_forest(P, args, extra=()):
     """Our Python CLI, P gloo ranks on the CPU, forest decomposition in reference mode."""
     env = dict(os.environ, PKD_SKIP_BUILD="1", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "parallel_kd_tree_amd.cli",
-           "--device", "cpu", "--decomp", "forest", "--mode", "reference", *map(str, args)]
+           "--device", "cpu", "--decomp", "forest", "--mode", "reference", *extra, *map(str, args)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout
@@ -142,3 +142,15 @@ def test_mpi_forest_parity_low_dim(ref_mpi, tmp_path, P, cfg):
     lines = _results(out)
     assert lines[0] == "READY" and lines[-1] == "DONE" and len(lines) == 12
     assert _results(_ours_forest(P, cfg)) == lines
+
+
+@pytest.mark.parametrize("procs,cfg", [(2, (42, 3, 20000)), (1, (7, 2, 9001)), (3, (5, 3, 16003))])
+def test_mpi_16_ranks_on_fewer_processes(ref_mpi, tmp_path, procs, cfg):
+    """The reference's own launch, `mpirun -np 16 --oversubscribe` (Makefile:36), reproduced by
+    fewer processes (GPUs): --ranks 16 spreads the 16 logical forest ranks over them, each keeping
+    the reference's slicing at P = 16, so reference-mode answers (which depend on P)
+    equal the reference MPI driver's at 16 processes, byte for byte."""
+    out, _ = _run_mpi(ref_mpi[True], 16, tmp_path, args=cfg)
+    lines = _results(out)
+    assert lines[0] == "READY" and lines[-1] == "DONE" and len(lines) == 12
+    assert _results(_ours_forest(procs, cfg, extra=["--ranks", "16"])) == lines
