@@ -580,7 +580,9 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     if (n_j > 0) {
       GpuBuilder& b = *lb[size_t(j)];
       const i64 a = lay_.leaf_slot[size_t(t)] - lay_.share_lo[size_t(me)];
-      if (planar_) b.build_columns(recv[size_t(j)], tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s);
+      // the leaf's top-level cell bounds its points: no bounding-box pass over the received columns
+      const float* leaf_cell = static_cast<const float*>(bufs_[1].first) + size_t(T - 1 + t) * dim * 2;
+      if (planar_) b.build_columns(recv[size_t(j)], tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s, leaf_cell);
       else b.build(recv[size_t(j)], lids[size_t(j)], 0, tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s);
       or_error_word(b.error_word(leaf_ws_), err + 1, s);  // the leaves share one workspace
     }

@@ -365,6 +365,13 @@ __global__ void k_root(const u32* __restrict__ bbox, int dim, float* __restrict_
     params[0] = make_params(from_orderable(bbox[axis0]), from_orderable(bbox[dim + axis0]), bins0);
 }
 
+// Root cell given by the caller (a box holding every point, e.g. a distributed leaf's cell).
+__global__ void k_cell_root(const float* __restrict__ cell, int dim, float* __restrict__ cells,
+                            BucketParams* __restrict__ params, int axis0, int bins0) {
+  for (int c = threadIdx.x; c < 2 * dim; c += blockDim.x) cells[c] = cell[c];
+  if (threadIdx.x == 0) params[0] = make_params(cell[2 * axis0], cell[2 * axis0 + 1], bins0);
+}
+
 // ---------------------------------------------------------------------------------------
 struct LevelArgs {
   const float* src;      // SoA columns of this level's input (dim coords + ids)
@@ -3226,12 +3233,21 @@ void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, h
   run_levels(out_pts, out_ids, ws, stream);
 }
 
-void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
+void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream,
+                               const float* root_cell) const {
   if (n_ == 0) return;
   if (narrow_) throw std::runtime_error("pkdtree: build_columns needs the full-column layout (dim <= 8)");
   if (reinterpret_cast<uintptr_t>(cols) % 256 != 0) throw std::invalid_argument("pkdtree: columns must be 256-B aligned");
   TraceRange tr("pkd.build");
   char* ws = static_cast<char*>(workspace);
+  if (root_cell) {  // the caller's box of the points: no bounding-box pass over the columns
+    k_cell_root<<<1, 64, 0, stream>>>(root_cell, dim_, reinterpret_cast<float*>(ws + off_cells_),
+                                      reinterpret_cast<BucketParams*>(ws + off_params_), opt_.depth0 % dim_,
+                                      lg_ > 0 ? levels_[0].bins : 1);
+    PKD_LAUNCH_CHECK();
+    run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, cols, 0, true);
+    return;
+  }
   u32* bbox = reinterpret_cast<u32*>(ws + off_bbox_);
   u32* part = bbox + 2 * dim_;
   const int grid = int(std::min<i64>(2048, std::max<i64>(1, (n_ + kBlock - 1) / kBlock)));
@@ -3243,7 +3259,8 @@ void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* 
 }
 
 void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids,
-                            u32 id_base, const float* in_rows, i64 in_rs, float* cols_a, int first_level) const {
+                            u32 id_base, const float* in_rows, i64 in_rs, float* cols_a, int first_level,
+                            bool root_ready) const {
   const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
   float* colsA = cols_a ? cols_a : reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
@@ -3260,7 +3277,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   k_geometry<<<int((heap_nodes_ + kBlock - 1) / kBlock), kBlock, 0, stream>>>(seg_lo, seg_n, heap_nodes_, n_);
   PKD_LAUNCH_CHECK();
   const int axis0 = opt_.depth0 % dim_;
-  if (first_level == 0) {
+  if (first_level == 0 && !root_ready) {
     k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
     PKD_LAUNCH_CHECK();
   }

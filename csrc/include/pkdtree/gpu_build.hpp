@@ -139,7 +139,10 @@ class GpuBuilder {
   // CLOBBERED: they serve as one of the build's two ping-pong buffers, so no AoS -> SoA pass
   // and no copy into the workspace is needed. The distributed builder receives its exchange
   // straight into such columns. Needs dim <= 8 (the full-column layout).
-  void build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const;
+  // root_cell (optional, device [dim][2] floats): a box holding every point (the distributed
+  // builder's top-level cell of the leaf); it replaces the bounding-box pass over the columns.
+  void build_columns(float* cols, float* out_pts, u32* out_ids, void* workspace, hipStream_t stream,
+                     const float* root_cell = nullptr) const;
 
  private:
   void prep_and_run(const float* pts, int rs, bool ids_in_row, const u32* ids, u32 id_base, float* out_pts,
@@ -153,7 +156,7 @@ class GpuBuilder {
   // cells, the first level's histogram parameters and the error word are set.
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
                   u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0, float* cols_a = nullptr,
-                  int first_level = 0) const;
+                  int first_level = 0, bool root_ready = false) const;
   // Side streams for a split build on the current device (nullptr: run unsplit, e.g. when
   // the streams do not exist yet and `stream` is being captured into a graph).
   SplitStreams* split_streams_for(hipStream_t stream) const;
