@@ -416,6 +416,25 @@ void bind_dist_ops(pybind11::module& m) {
       .def("read_error", &NativeGlobal::read_error)
       .def("set_profile", &NativeGlobal::set_profile)
       .def("phases", &NativeGlobal::phases);
+  m.def(
+      "global_emulate_rank",
+      [](const torch::Tensor& x, int64_t P, int64_t rank, int64_t k, int64_t reps) {
+        TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
+                    "x: contiguous float32 [N, dim] host tensor");
+        pybind11::gil_scoped_release nogil;
+        const RankEmulation e =
+            emulate_rank(x.data_ptr<float>(), x.size(0), int(x.size(1)), int(P), int(rank), int(k), int(reps));
+        pybind11::gil_scoped_acquire gil;
+        pybind11::dict d;
+        for (const auto& kv : e.phases.as_map()) d[pybind11::str(kv.first)] = kv.second;
+        d["total_ms_reps"] = e.total_ms;
+        d["same_tree"] = e.same_tree;
+        d["error"] = int64_t(e.error);
+        d["collectives"] = e.collectives;
+        return d;
+      },
+      pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("rank") = 0, pybind11::arg("k") = -1,
+      pybind11::arg("reps") = 5);
   m.def("global_layout", &layout_py, pybind11::arg("n_total"), pybind11::arg("P"), pybind11::arg("k") = -1);
   m.def("global_plan", &plan_py, pybind11::arg("counts"), pybind11::arg("n_total"), pybind11::arg("P"),
         pybind11::arg("k"), pybind11::arg("me"));

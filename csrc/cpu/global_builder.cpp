@@ -696,4 +696,210 @@ std::vector<std::unique_ptr<Comm>> make_thread_comms(int size) {
   return out;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Rank emulation: record one rank's collective outputs, replay them as device copies.
+namespace {
+
+struct Recorded {  // one collective's output: byte chunks at offsets of the destination buffer
+  std::vector<std::pair<size_t, std::vector<char>>> chunks;
+};
+
+class RecordingComm final : public Comm {
+ public:
+  RecordingComm(Comm& inner, std::vector<Recorded>* out) : in_(inner), out_(out) { set_timeout(inner.timeout()); }
+  int rank() const override { return in_.rank(); }
+  int size() const override { return in_.size(); }
+  void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
+    in_.allreduce_sum_u32(buf, count, s);
+    record1(buf, count * 4, s);
+  }
+  void allreduce_min_i64(i64* buf, size_t count, hipStream_t s) override {
+    in_.allreduce_min_i64(buf, count, s);
+    record1(buf, count * 8, s);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    in_.allgather(send, recv, bytes, s);
+    record1(recv, bytes * size_t(size()), s);
+  }
+  void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                 const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
+    in_.alltoallv(send, send_bytes, send_off, recv, recv_bytes, recv_off, s);
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    Recorded r;
+    for (int p = 0; p < size(); ++p) {
+      if (!recv_bytes[p]) continue;
+      std::vector<char> v(recv_bytes[p]);
+      PKD_HIP_CHECK(hipMemcpy(v.data(), static_cast<const char*>(recv) + recv_off[p], v.size(), hipMemcpyDeviceToHost));
+      r.chunks.emplace_back(recv_off[p], std::move(v));
+    }
+    out_->push_back(std::move(r));
+  }
+  void group_begin() override { in_.group_begin(); }
+  void group_end() override { in_.group_end(); }
+
+ private:
+  void record1(const void* dst, size_t bytes, hipStream_t s) {
+    PKD_HIP_CHECK(hipStreamSynchronize(s));
+    Recorded r;
+    std::vector<char> v(bytes);
+    if (bytes) PKD_HIP_CHECK(hipMemcpy(v.data(), dst, bytes, hipMemcpyDeviceToHost));
+    r.chunks.emplace_back(0, std::move(v));
+    out_->push_back(std::move(r));
+  }
+  Comm& in_;
+  std::vector<Recorded>* out_;
+};
+
+class ReplayComm final : public Comm {
+ public:
+  ReplayComm(int rank, int size, const std::vector<Recorded>& recs) : rank_(rank), size_(size) {
+    for (const Recorded& r : recs) {
+      std::vector<Chunk> cs;
+      for (const auto& c : r.chunks) {
+        Chunk d{c.first, c.second.size(), nullptr};
+        if (d.bytes) {
+          PKD_HIP_CHECK(hipMalloc(&d.dev, d.bytes));
+          PKD_HIP_CHECK(hipMemcpy(d.dev, c.second.data(), d.bytes, hipMemcpyHostToDevice));
+        }
+        cs.push_back(d);
+      }
+      calls_.push_back(std::move(cs));
+    }
+  }
+  ~ReplayComm() override {
+    for (auto& cs : calls_)
+      for (auto& c : cs)
+        if (c.dev) (void)hipFree(c.dev);
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  void rewind() { next_ = 0; }
+  int calls() const { return int(calls_.size()); }
+  void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override { replay1(buf, count * 4, s); }
+  void allreduce_min_i64(i64* buf, size_t count, hipStream_t s) override { replay1(buf, count * 8, s); }
+  void allgather(const void*, void* recv, size_t bytes, hipStream_t s) override {
+    replay1(recv, bytes * size_t(size_), s);
+  }
+  void alltoallv(const void*, const size_t*, const size_t*, void* recv, const size_t* recv_bytes,
+                 const size_t* recv_off, hipStream_t s) override {
+    const auto& cs = take();
+    size_t k = 0;
+    for (int p = 0; p < size_; ++p) {
+      if (!recv_bytes[p]) continue;
+      if (k >= cs.size() || cs[k].off != recv_off[p] || cs[k].bytes != recv_bytes[p])
+        throw std::runtime_error("replay communicator: all-to-all layout differs from the recording");
+      PKD_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + recv_off[p], cs[k].dev, cs[k].bytes,
+                                   hipMemcpyDeviceToDevice, s));
+      ++k;
+    }
+  }
+
+ private:
+  struct Chunk {
+    size_t off, bytes;
+    void* dev;
+  };
+  const std::vector<Chunk>& take() {
+    if (next_ >= calls_.size()) throw std::runtime_error("replay communicator: more collectives than recorded");
+    return calls_[next_++];
+  }
+  void replay1(void* dst, size_t bytes, hipStream_t s) {
+    const auto& cs = take();
+    if (cs.size() != 1 || cs[0].bytes != bytes)
+      throw std::runtime_error("replay communicator: collective size differs from the recording");
+    if (bytes) PKD_HIP_CHECK(hipMemcpyAsync(dst, cs[0].dev, bytes, hipMemcpyDeviceToDevice, s));
+  }
+  int rank_, size_;
+  std::vector<std::vector<Chunk>> calls_;
+  size_t next_ = 0;
+};
+
+}  // namespace
+
+RankEmulation emulate_rank(const float* x_host, i64 N, int dim, int P, int rank, int pipeline_k, int reps) {
+  if (rank < 0 || rank >= P) throw std::invalid_argument("emulate_rank: rank out of range");
+  int dev = 0;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  auto slice = [&](int r, i64* first, i64* local) {
+    const i64 base = N / P;
+    *first = base * r;
+    *local = base + (r == P - 1 ? N % P : 0);
+  };
+  std::vector<Recorded> recs;
+  std::vector<float> ref_pts;
+  std::vector<u32> ref_ids;
+  {  // 1. the P ranks as threads; rank `rank` records its collective outputs
+    auto comms = make_thread_comms(P);
+    RecordingComm recorder(*comms[size_t(rank)], &recs);
+    std::vector<std::exception_ptr> errs(static_cast<size_t>(P));
+    std::vector<std::thread> th;
+    for (int r = 0; r < P; ++r)
+      th.emplace_back([&, r] {
+        float* d = nullptr;
+        hipStream_t s = nullptr;
+        try {
+          PKD_HIP_CHECK(hipSetDevice(dev));
+          i64 first = 0, local = 0;
+          slice(r, &first, &local);
+          PKD_HIP_CHECK(hipStreamCreate(&s));
+          PKD_HIP_CHECK(hipMalloc(&d, size_t(std::max<i64>(local, 1)) * dim * 4));
+          PKD_HIP_CHECK(hipMemcpy(d, x_host + first * dim, size_t(local) * dim * 4, hipMemcpyHostToDevice));
+          Comm& c = r == rank ? static_cast<Comm&>(recorder) : *comms[size_t(r)];
+          GlobalBuilder gb(c, N, dim, pipeline_k);
+          gb.build(d, local, u32(first + 1), s);
+          gb.wait(s);
+          if (r == rank) {
+            ref_pts.resize(size_t(gb.n_leaf()) * dim);
+            ref_ids.resize(size_t(gb.n_leaf()));
+            if (gb.n_leaf() > 0) {
+              PKD_HIP_CHECK(hipMemcpy(ref_pts.data(), gb.tree_pts(), ref_pts.size() * 4, hipMemcpyDeviceToHost));
+              PKD_HIP_CHECK(hipMemcpy(ref_ids.data(), gb.tree_ids(), ref_ids.size() * 4, hipMemcpyDeviceToHost));
+            }
+          }
+        } catch (...) {
+          errs[size_t(r)] = std::current_exception();
+        }
+        if (d) (void)hipFree(d);
+        if (s) (void)hipStreamDestroy(s);
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  // 2. rank `rank` alone against the recording, profiled
+  RankEmulation out;
+  out.collectives = int(recs.size());
+  ReplayComm replay(rank, P, recs);
+  recs.clear();
+  i64 first = 0, local = 0;
+  slice(rank, &first, &local);
+  float* d = nullptr;
+  hipStream_t s = nullptr;
+  PKD_HIP_CHECK(hipStreamCreate(&s));
+  PKD_HIP_CHECK(hipMalloc(&d, size_t(std::max<i64>(local, 1)) * dim * 4));
+  PKD_HIP_CHECK(hipMemcpy(d, x_host + first * dim, size_t(local) * dim * 4, hipMemcpyHostToDevice));
+  {
+    GlobalBuilder gb(replay, N, dim, pipeline_k);
+    gb.set_profile(true);
+    for (int i = 0; i < std::max(1, reps) + 1; ++i) {  // the first build warms up (allocations)
+      replay.rewind();
+      gb.build(d, local, u32(first + 1), s);
+      gb.wait(s);
+      if (i > 0) out.total_ms.push_back(gb.phases(s).total_ms);
+    }
+    out.phases = gb.phases(s);
+    out.error = gb.read_error(s);
+    std::vector<float> tp(size_t(gb.n_leaf()) * dim);
+    std::vector<u32> ti(size_t(gb.n_leaf()));
+    if (gb.n_leaf() > 0) {
+      PKD_HIP_CHECK(hipMemcpy(tp.data(), gb.tree_pts(), tp.size() * 4, hipMemcpyDeviceToHost));
+      PKD_HIP_CHECK(hipMemcpy(ti.data(), gb.tree_ids(), ti.size() * 4, hipMemcpyDeviceToHost));
+    }
+    out.same_tree = tp == ref_pts && ti == ref_ids;
+  }
+  (void)hipFree(d);
+  (void)hipStreamDestroy(s);
+  return out;
+}
+
 }  // namespace pkdtree

@@ -203,4 +203,21 @@ class GlobalBuilder {
 // orchestration without several GPUs.
 std::vector<std::unique_ptr<Comm>> make_thread_comms(int size);
 
+// Emulation of ONE rank of a P-rank global build on one GPU, timed as a whole chain: the P ranks
+// first run once as threads over the loopback communicator, with every collective output of
+// rank `rank` recorded; then rank `rank` alone builds again (profiled, `reps` times) against a
+// replay communicator whose collectives are stream-ordered device copies of those recorded
+// outputs. Its kernels, host waits and stream dependencies are the real ones; the exchange
+// costs a device copy instead of the xGMI transfer (report it separately). x: the host points
+// [N][dim] (rank r holds the reference's MPI slice r). Returns the phases of the last replay
+// and whether its share equals the loopback run's share slot for slot.
+struct RankEmulation {
+  GlobalPhases phases;
+  std::vector<double> total_ms;  // per replay
+  bool same_tree = false;
+  u32 error = 0;
+  int collectives = 0;
+};
+RankEmulation emulate_rank(const float* x_host, i64 N, int dim, int P, int rank, int pipeline_k, int reps);
+
 }  // namespace pkdtree
