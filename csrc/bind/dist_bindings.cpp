@@ -372,6 +372,24 @@ class NativeGlobal {
     return int64_t(gb_->read_error(c10::hip::getCurrentHIPStream(device_).stream()));
   }
   void set_profile(bool on) { gb_->set_profile(on); }
+  // routed exact 1-NN over the whole tree (collective: every rank calls it with the same queries)
+  std::tuple<torch::Tensor, int64_t> query(const torch::Tensor& q, bool count_work) {
+    check_cuda(q, torch::kFloat32, "queries");
+    TORCH_CHECK(q.dim() == 2 && q.size(1) == dim_ && q.is_contiguous(), "queries must be contiguous [Q, dim]");
+    TORCH_CHECK(q.device().index() == device_, "queries must live on the builder's device");
+    const c10::DeviceGuard g(q.device());
+    torch::Tensor out = torch::empty({q.size(0)}, opts(torch::kInt64));
+    const hipStream_t s = stream_of(q);
+    const float* qp = q.data_ptr<float>();
+    u64* op = reinterpret_cast<u64*>(out.data_ptr<int64_t>());
+    const int64_t Q = q.size(0);
+    int64_t work = 0;
+    {
+      pybind11::gil_scoped_release nogil;
+      work = gb_->query(qp, Q, op, s, count_work);
+    }
+    return {out, work};
+  }
   std::map<std::string, double> phases() const {
     const c10::DeviceGuard g(torch::Device(torch::kCUDA, device_));
     return gb_->phases(c10::hip::getCurrentHIPStream(device_).stream()).as_map();
@@ -415,6 +433,7 @@ void bind_dist_ops(pybind11::module& m) {
       .def("middle_scale", &NativeGlobal::middle_scale)
       .def("read_error", &NativeGlobal::read_error)
       .def("set_profile", &NativeGlobal::set_profile)
+      .def("query", &NativeGlobal::query, pybind11::arg("queries"), pybind11::arg("count_work") = false)
       .def("phases", &NativeGlobal::phases);
   m.def(
       "global_emulate_rank",

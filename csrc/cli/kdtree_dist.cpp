@@ -194,12 +194,8 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
   const bool ref = o.mode == "reference";
   const bool global = o.decomp == "global";
   std::unique_ptr<GlobalBuilder> gb;
-  float* d_top = nullptr;  // rank 0, global: the boundary top rows as a point set [T - 1][dim] + ids
-  u32* d_top_ids = nullptr;
   if (global) {
     gb = std::make_unique<GlobalBuilder>(rcomm, N, dim, o.pipeline_k);
-    PKD_HIP_CHECK(hipMalloc(&d_top, size_t(gb->layout().T) * dim * 4));
-    PKD_HIP_CHECK(hipMalloc(&d_top_ids, size_t(gb->layout().T) * 4));
   } else if (local > 0) {  // allocations outside the timed region
     size_t wsb = 0;
     for (const Slice& sl : slices) {
@@ -251,35 +247,10 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
   const float* d_q = d_x + size_t(local) * dim;
   const bool traverse = o.query == "traverse" || (o.query == "auto" && dim <= 16);
   if (global) {
-    // my share: complete subtrees ("blocks") of the one global tree plus the top rows between
-    // them (a single subtree at depth log2 P for a power-of-two P) ...
-    std::vector<global_plan::Block> blocks;
-    std::vector<i64> between;
-    global_plan::share_blocks(gb->layout(), rank, &blocks, &between);
-    for (const auto& bl : blocks) {
-      if (bl.n <= 0) continue;
-      const float* tp = gb->tree_pts() + size_t(bl.off) * dim;
-      const u32* ti = gb->tree_ids() + bl.off;
-      if (traverse) nn_traverse(tp, ti, bl.n, dim, bl.depth, d_q, Q, d_res, s);
-      else nn_brute(tp, ti, 0, bl.n, dim, d_q, Q, d_res, s);
-    }
-    for (i64 h : between) {
-      const i64 off = gb->layout().top_slot[size_t(h)] - gb->slot_lo();
-      nn_brute(gb->tree_pts() + size_t(off) * dim, gb->tree_ids() + off, 0, 1, dim, d_q, Q, d_res, s);
-    }
-    // ... and on rank 0 the boundary top rows (outside every share), split out of their rows
-    if (rank == 0 && P > 1) {
-      const std::vector<i64> slots = gb->top_slots();
-      i64 nt = 0;
-      for (size_t h = 0; h < slots.size(); ++h) {
-        if (slots[h] < 0) continue;
-        const float* row = gb->top_rows() + h * (dim + 1);
-        PKD_HIP_CHECK(hipMemcpyAsync(d_top + nt * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
-        PKD_HIP_CHECK(hipMemcpyAsync(d_top_ids + nt, row + dim, 4, hipMemcpyDeviceToDevice, s));
-        ++nt;
-      }
-      if (nt > 0) nn_brute(d_top, d_top_ids, 0, nt, dim, d_q, Q, d_res, s);
-    }
+    // routed (GlobalBuilder::query): each query searched in its home block, a MIN all-reduce
+    // gives it a radius, then only in the blocks that radius reaches, a second MIN all-reduce
+    // (the top rows between blocks and the boundary rows are brute-forced)
+    gb->query(d_q, Q, d_res, s);
   } else if (local > 0) {
     for (const Slice& sl : slices) {  // every tree of this process: MIN into the same results
       if (sl.n <= 0) continue;
@@ -371,8 +342,6 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
     }
   }
   (void)hipFree(d_x); (void)hipFree(d_res); (void)hipFree(d_cfg); (void)hipFree(d_t);
-  if (d_top) (void)hipFree(d_top);
-  if (d_top_ids) (void)hipFree(d_top_ids);
   gb.reset();
   if (d_tree) (void)hipFree(d_tree);
   if (d_ids) (void)hipFree(d_ids);

@@ -17,6 +17,7 @@
 
 #include "pkdtree/dist_ops.hpp"
 #include "pkdtree/gpu_build.hpp"
+#include "pkdtree/gpu_query.hpp"
 #include "pkdtree/hip_check.hpp"
 
 namespace pkdtree {
@@ -329,6 +330,90 @@ u32 GlobalBuilder::read_error(hipStream_t stream) const {
   u32 w[4];
   PKD_HIP_CHECK(hipMemcpy(w, bufs_[5].first, 16, hipMemcpyDeviceToHost));
   return (w[0] & 8u) | w[1];  // the compact exchange's bitmap check | the leaf builds' error words
+}
+
+i64 GlobalBuilder::query(const float* queries, i64 Q, u64* out, hipStream_t s, bool count_work) {
+  if (Q <= 0) return 0;
+  const int dim = dim_;
+  std::vector<global_plan::Block> all;
+  std::vector<i64> between;
+  global_plan::share_blocks(lay_, rank_, &all, &between);
+  std::vector<global_plan::Block> bl;
+  for (const auto& b : all)
+    if (b.n > 0) bl.push_back(b);
+  const int nb = int(bl.size());
+  if (nb > kRqMaxBlocks) throw std::runtime_error("GlobalBuilder::query: more than 64 blocks");
+  const bool routed = dim <= 16;
+  auto* counts = static_cast<u32*>(buf(301, size_t(std::max(nb, 1)) * 4));
+  nn_init(out, Q, s);
+  // the top rows between this rank's blocks, and on rank 0 the boundary top rows: brute force
+  auto brute_tops = [&] {
+    for (i64 h : between) {
+      const i64 off = lay_.top_slot[size_t(h)] - slot_lo();
+      nn_brute(tree_pts_ + off * dim, tree_ids_ + off, 0, 1, dim, queries, Q, out, s);
+    }
+    if (rank_ == 0 && P_ > 1) {
+      const std::vector<i64> slots = top_slots();
+      std::vector<int> hs;
+      for (size_t h = 0; h < slots.size(); ++h)
+        if (slots[h] >= 0) hs.push_back(int(h));
+      if (!hs.empty()) {
+        auto* tp = static_cast<float*>(buf(304, hs.size() * size_t(dim) * 4));
+        auto* ti = static_cast<u32*>(buf(305, hs.size() * 4));
+        for (size_t k = 0; k < hs.size(); ++k) {
+          const float* row = top_rows_ + size_t(hs[k]) * (dim + 1);
+          PKD_HIP_CHECK(hipMemcpyAsync(tp + k * dim, row, size_t(dim) * 4, hipMemcpyDeviceToDevice, s));
+          PKD_HIP_CHECK(hipMemcpyAsync(ti + k, row + dim, 4, hipMemcpyDeviceToDevice, s));
+        }
+        nn_brute(tp, ti, 0, i64(hs.size()), dim, queries, Q, out, s);
+      }
+    }
+  };
+  if (!routed) {
+    for (const auto& b : bl)
+      nn_brute(tree_pts_ + b.off * dim, tree_ids_ + b.off, 0, b.n, dim, queries, Q, out, s);
+    brute_tops();
+    comm_.allreduce_min_i64(reinterpret_cast<i64*>(out), size_t(Q), s);
+    return count_work ? i64(nb) * Q : -1;
+  }
+  RqBlocks rb{};
+  rb.nb = nb;
+  rb.LL = lay_.LL;
+  rb.T = lay_.T;
+  rb.depth0 = 0;
+  for (int t = 0; t < 64; ++t) rb.leaf_block[t] = -1;
+  for (int i = 0; i < nb; ++i) {
+    rb.heap[i] = bl[size_t(i)].heap;
+    const int sh = lay_.LL - bl[size_t(i)].depth;  // levels between the block root and the leaves
+    const i64 first = ((bl[size_t(i)].heap + 1) << sh) - lay_.T;
+    for (i64 t = first; t < first + (i64(1) << sh); ++t) rb.leaf_block[t] = i;
+  }
+  auto* lists = static_cast<u32*>(buf(300, size_t(std::max(nb, 1)) * size_t(Q) * 4));
+  auto* home = static_cast<int*>(buf(302, size_t(Q) * 4));
+  i64 work = 0;
+  auto search = [&] {
+    for (int i = 0; i < nb; ++i)
+      nn_traverse_sel(tree_pts_ + bl[size_t(i)].off * dim, tree_ids_ + bl[size_t(i)].off, bl[size_t(i)].n, dim,
+                      bl[size_t(i)].depth, queries, lists + size_t(i) * Q, counts + i, Q, out, s);
+    if (count_work && nb > 0) {
+      std::vector<u32> c(static_cast<size_t>(nb));
+      PKD_HIP_CHECK(hipMemcpyAsync(c.data(), counts, size_t(nb) * 4, hipMemcpyDeviceToHost, s));
+      comm_.wait(s, "query work count");
+      for (u32 v : c) work += v;
+    }
+  };
+  // 1. home blocks
+  fill_u32(counts, std::max(nb, 1), 0u, s);
+  rq_home(queries, Q, dim, top_rows_, rb, lists, counts, home, s);
+  search();
+  brute_tops();
+  comm_.allreduce_min_i64(reinterpret_cast<i64*>(out), size_t(Q), s);
+  // 2. blocks the best ball reaches
+  fill_u32(counts, std::max(nb, 1), 0u, s);
+  rq_reach(queries, Q, dim, top_rows_, rb, out, home, lists, counts, s);
+  search();
+  comm_.allreduce_min_i64(reinterpret_cast<i64*>(out), size_t(Q), s);
+  return count_work ? work : -1;
 }
 
 void GlobalBuilder::set_profile(bool on) {

@@ -866,6 +866,89 @@ void top_place_rows(const float* top_rows, int dim, const TopPlacement& pl, floa
   PKD_LAUNCH_CHECK();
 }
 
+namespace {
+// axis of heap node h (top tree rooted at depth depth0)
+__device__ __forceinline__ int rq_axis(i64 h, int depth0, int dim) {
+  int l = 0;
+  while (((h + 1) >> (l + 1)) > 0) ++l;
+  return (depth0 + l) % dim;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rq_home(const float* __restrict__ q, i64 Q, int dim,
+                                                    const float* __restrict__ top_rows, RqBlocks bl,
+                                                    u32* __restrict__ lists, u32* __restrict__ counts,
+                                                    int* __restrict__ home) {
+  const i64 i = i64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= Q) return;
+  i64 h = 0;
+  for (int l = 0; l < bl.LL; ++l) {
+    const int ax = (bl.depth0 + l) % dim;
+    const float piv = top_rows[h * (dim + 1) + ax];
+    h = 2 * h + 1 + (q[i * dim + ax] >= piv ? 1 : 0);
+  }
+  const int leaf = int(h - (bl.T - 1));
+  const int b = bl.leaf_block[leaf];
+  home[i] = b;
+  if (b >= 0) {
+    const u32 k = atomicAdd(&counts[b], 1u);
+    lists[i64(b) * Q + k] = u32(i);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rq_reach(const float* __restrict__ q, i64 Q, int dim,
+                                                     const float* __restrict__ top_rows, RqBlocks bl,
+                                                     const u64* __restrict__ best, const int* __restrict__ home,
+                                                     u32* __restrict__ lists, u32* __restrict__ counts) {
+  const i64 i = i64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= Q) return;
+  const double d2 = double(packed_dist(best[i]));
+  const int hb = home[i];
+  for (int b = 0; b < bl.nb; ++b) {
+    if (b == hb) continue;
+    // box distance: the pivots above the block root bound it (closed box)
+    double g2 = 0.0;
+    i64 child = bl.heap[b];
+    // per axis the tightest bounds; dims <= 64 walked pivot by pivot (<= LL of them)
+    for (int c = 0; c < dim; ++c) {
+      double lo = -1e300, hi = 1e300;
+      i64 ch = child;
+      while (ch > 0) {
+        const i64 h = (ch - 1) / 2;
+        if (rq_axis(h, bl.depth0, dim) == c) {
+          const double v = double(top_rows[h * (dim + 1) + c]);
+          if (ch == 2 * h + 1) hi = v < hi ? v : hi;
+          else lo = v > lo ? v : lo;
+        }
+        ch = h;
+      }
+      const double x = double(q[i * dim + c]);
+      const double gap = (x < lo ? lo - x : 0.0) + (x > hi ? x - hi : 0.0);
+      g2 += gap * gap;
+    }
+    if (g2 <= d2 * (1.0 + 1e-5)) {
+      const u32 k = atomicAdd(&counts[b], 1u);
+      lists[i64(b) * Q + k] = u32(i);
+    }
+  }
+}
+}  // namespace
+
+void rq_home(const float* queries, i64 Q, int dim, const float* top_rows, const RqBlocks& bl, u32* lists,
+             u32* counts, int* home, hipStream_t stream) {
+  if (Q <= 0) return;
+  if (bl.nb > kRqMaxBlocks || bl.T > 64) throw std::invalid_argument("rq_home: at most 64 blocks / leaves");
+  k_rq_home<<<int((Q + kBlock - 1) / kBlock), kBlock, 0, stream>>>(queries, Q, dim, top_rows, bl, lists, counts, home);
+  PKD_LAUNCH_CHECK();
+}
+
+void rq_reach(const float* queries, i64 Q, int dim, const float* top_rows, const RqBlocks& bl, const u64* best,
+              const int* home, u32* lists, u32* counts, hipStream_t stream) {
+  if (Q <= 0 || bl.nb == 0) return;
+  k_rq_reach<<<int((Q + kBlock - 1) / kBlock), kBlock, 0, stream>>>(queries, Q, dim, top_rows, bl, best, home, lists,
+                                                                    counts);
+  PKD_LAUNCH_CHECK();
+}
+
 size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P) {
   return size_t(P) * size_t(std::max<i64>(1, (max_words + kBmWords - 1) / kBmWords)) * 4;
 }

@@ -243,14 +243,19 @@ template <int DC>
 __global__ __launch_bounds__(kBlock) void k_nn_wave(const float* __restrict__ P, const u32* __restrict__ ids, i64 n,
                                                     int dim_rt, int depth0, u32 bucket,
                                                     const float* __restrict__ queries, i64 nq,
-                                                    u64* __restrict__ out) {
+                                                    u64* __restrict__ out, const u32* __restrict__ sel,
+                                                    const u32* __restrict__ sel_count) {
   constexpr int W = kBlock / 64;
   __shared__ u32 st_lo[W][kWaveStack], st_n[W][kWaveStack], st_d[W][kWaveStack];
   __shared__ float st_b[W][kWaveStack];
   __shared__ float qsh[W][DC > 0 ? 1 : 32];
   const int w = threadIdx.x / 64, ln = dev::lane();
-  const i64 qi = i64(blockIdx.x) * W + w;
+  i64 qi = i64(blockIdx.x) * W + w;
   if (qi >= nq || n <= 0) return;  // wave-uniform
+  if (sel) {  // selected queries only: entry qi of the device list names the query
+    if (qi >= i64(*sel_count)) return;
+    qi = sel[qi];
+  }
   const int dim = DC > 0 ? DC : dim_rt;
   float qr[DC > 0 ? DC : 1];
   const float* qg = queries + qi * dim;
@@ -360,9 +365,14 @@ __global__ __launch_bounds__(kBlock) void k_nn_wave(const float* __restrict__ P,
 template <bool REF>
 __global__ __launch_bounds__(kBlock) void k_traverse(const float* __restrict__ P, const u32* __restrict__ ids, i64 n,
                                                      int dim, int depth0, const float* __restrict__ queries, i64 nq,
-                                                     u64* __restrict__ out) {
-  const i64 qi = i64(blockIdx.x) * kBlock + threadIdx.x;
+                                                     u64* __restrict__ out, const u32* __restrict__ sel = nullptr,
+                                                     const u32* __restrict__ sel_count = nullptr) {
+  i64 qi = i64(blockIdx.x) * kBlock + threadIdx.x;
   if (qi >= nq || n <= 0) return;
+  if (sel) {
+    if (qi >= i64(*sel_count)) return;
+    qi = sel[qi];
+  }
   const float* q = queries + qi * dim;
   u32 st_lo[kStack], st_n[kStack];
   unsigned char st_d[kStack];
@@ -530,12 +540,19 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 namespace {
 template <int DC>
 void launch_nn_wave(const float* P, const u32* ids, i64 n, int dim, int depth0, u32 bucket, const float* q, i64 nq,
-                    u64* out, hipStream_t stream) {
+                    u64* out, hipStream_t stream, const u32* sel = nullptr, const u32* sel_count = nullptr) {
   constexpr int W = kBlock / 64;
+  if (sel) {  // one launch over the list's capacity; the device count ends it
+    if (nq > i64(W) * 1048576 * 64) throw std::invalid_argument("nn_traverse_sel: too many queries");
+    k_nn_wave<DC><<<int((nq + W - 1) / W), kBlock, 0, stream>>>(P, ids, n, dim, depth0, bucket, q, nq, out, sel,
+                                                                sel_count);
+    PKD_LAUNCH_CHECK();
+    return;
+  }
   for (i64 q0 = 0; q0 < nq; q0 += i64(W) * 1048576) {
     const i64 m = std::min<i64>(nq - q0, i64(W) * 1048576);
     k_nn_wave<DC><<<int((m + W - 1) / W), kBlock, 0, stream>>>(P, ids, n, dim, depth0, bucket, q + q0 * dim, m,
-                                                               out + q0);
+                                                               out + q0, nullptr, nullptr);
     PKD_LAUNCH_CHECK();
   }
 }
@@ -566,6 +583,29 @@ void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int
   }
   k_traverse<false><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries,
                                                                            nq, out);
+  PKD_LAUNCH_CHECK();
+}
+
+void nn_traverse_sel(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
+                     const u32* sel, const u32* sel_count, i64 max_sel, u64* out, hipStream_t stream) {
+  if (max_sel <= 0 || n <= 0) return;
+  TraceRange tr("pkd.nn_traverse_sel");
+  if (dim <= 32 && traverse_mode() == 0) {
+    const u32 bucket = 512;
+    switch (dim) {
+      case 1: launch_nn_wave<1>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 2: launch_nn_wave<2>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 3: launch_nn_wave<3>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 4: launch_nn_wave<4>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 5: launch_nn_wave<5>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 6: launch_nn_wave<6>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 7: launch_nn_wave<7>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      case 8: launch_nn_wave<8>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+      default: launch_nn_wave<0>(tree_pts, tree_ids, n, dim, depth0, bucket, queries, max_sel, out, stream, sel, sel_count); return;
+    }
+  }
+  k_traverse<false><<<int((max_sel + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0,
+                                                                                queries, max_sel, out, sel, sel_count);
   PKD_LAUNCH_CHECK();
 }
 

@@ -138,4 +138,26 @@ size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P);
 void ids_from_bitmaps(const u32* bitmaps, int P, const BmSources& src, u32* ids, void* scratch, u32* err,
                       hipStream_t stream);
 
+// ---- routed queries on the distributed tree ---------------------------------------------
+// A rank's blocks (complete subtrees of its share with points): which top-level leaf belongs
+// to which block, and each block's root heap node.
+constexpr int kRqMaxBlocks = 64;
+struct RqBlocks {
+  int nb;                      // blocks
+  int LL, T;                   // top levels, leaves
+  int depth0;
+  int leaf_block[64];          // [T]: index of the block holding leaf t, -1: another rank's
+  i64 heap[kRqMaxBlocks];      // root heap node of block b
+};
+// Home routing: every query descends the top tree (q[axis] >= pivot: right, the search's own
+// near side) to its leaf; a query whose leaf is in block b is appended to lists[b * Q ..] with
+// counts[b] (device words, zeroed by the caller); home[q] = b or -1.
+void rq_home(const float* queries, i64 Q, int dim, const float* top_rows, const RqBlocks& bl, u32* lists,
+             u32* counts, int* home, hipStream_t stream);
+// Reach routing: query q is appended to block b (b != home[q]) when the box of b (the top
+// pivots above its root, [lo, hi] per axis, closed) is within q's best distance so far:
+// gap^2 <= d2 * (1 + 1e-5) (conservative against the fp32 sequential distance sums).
+void rq_reach(const float* queries, i64 Q, int dim, const float* top_rows, const RqBlocks& bl, const u64* best,
+              const int* home, u32* lists, u32* counts, hipStream_t stream);
+
 }  // namespace pkdtree

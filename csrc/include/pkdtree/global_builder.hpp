@@ -162,6 +162,14 @@ class GlobalBuilder {
   std::vector<i64> top_slots() const;
   // OR of the device error words of the last build (0 = ok). Synchronises `stream`.
   u32 read_error(hipStream_t stream) const;
+  // Exact 1-NN of Q queries (device [Q][dim], replicated on every rank) over the whole tree of
+  // the last build, packed (d2 << 32 | id) into out[Q] on every rank. Routed (dim <= 16):
+  // each query is searched first only in its home block (the leaf its top-tree descent
+  // reaches; ~Q / P searches per rank), one MIN all-reduce gives it a radius, then only in the
+  // blocks whose cell that radius reaches, and a second MIN all-reduce combines. dim > 16
+  // (no pruning to gain): every block, one all-reduce. Every rank must call it (collectives).
+  // Returns this rank's (query, block) searches when `count_work` (synchronises), else -1.
+  i64 query(const float* queries, i64 Q, u64* out, hipStream_t stream, bool count_work = false);
   // Per-phase hipEvent timing of the following builds (adds event records, no host syncs).
   void set_profile(bool on);
   GlobalPhases phases(hipStream_t stream) const;  // of the last profiled build; synchronises

@@ -28,6 +28,12 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
 void nn_traverse(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
                  i64 nq, u64* out, hipStream_t stream);
 
+// The same search for the selected queries only: query sel[i] for i < *sel_count (a device
+// word; max_sel >= it bounds the launch). out is indexed by the query number. (Routed queries
+// of the distributed tree: each rank searches a query only in the blocks it can matter for.)
+void nn_traverse_sel(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, const float* queries,
+                     const u32* sel, const u32* sel_count, i64 max_sel, u64* out, hipStream_t stream);
+
 // The reference's search procedure (kdtree_sequential.cpp:75-130: near side first, far side
 // iff axis distance^2 < best, strict improvements only) for reference-mode trees: the same
 // visited nodes and the same (possibly non-nearest) answer as the reference. `out` should

@@ -203,6 +203,13 @@ class DistTree:
         dev = self.tree_pts.device
         q = queries.to(dev, torch.float32).contiguous()
         Q = q.shape[0]
+        native = getattr(self, "native", None)
+        if native is not None and routed and method == "auto":
+            # the native routed search (GlobalBuilder::query): home block, MIN all-reduce, reach
+            # blocks, MIN all-reduce -- device lists, no per-block Python loop
+            packed, work = native.query(q, True)
+            self.last_query_work = int(work)
+            return packed
         packed = torch.full((Q,), ops.query.INF_PACKED, dtype=torch.int64, device=dev)
         blocks = [b for b in self.blocks if b[1] > 0]
         work = 0

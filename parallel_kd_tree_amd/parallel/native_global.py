@@ -52,8 +52,10 @@ class NativeGlobalBuilder:
         the global tree (views of the builder's buffers, valid until the next build)."""
         x = points.to(self.device, torch.float32).contiguous()
         self._g.build(x, int(id_base))
-        return DistTree(self.n_total, self.dim, 0, self.P, self.rank, self._g.tree_pts(), self._g.tree_ids(),
-                        int(self._g.slot_lo()), list(self._g.top_slots()), self._g.top_rows(), {}, self.layout)
+        t = DistTree(self.n_total, self.dim, 0, self.P, self.rank, self._g.tree_pts(), self._g.tree_ids(),
+                     int(self._g.slot_lo()), list(self._g.top_slots()), self._g.top_rows(), {}, self.layout)
+        t.native = self._g  # routed queries run natively (GlobalBuilder::query)
+        return t
 
     def sync(self) -> None:
         """Bounded wait for the last build (raises instead of hanging on a stuck peer)."""

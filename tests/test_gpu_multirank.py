@@ -183,3 +183,19 @@ def _routed(rank, world, n, dim, nq):
 @pytest.mark.parametrize("world,dim", [(4, 3), (3, 4)])
 def test_routed_queries_rccl(world, dim):
     run_rccl(world, _routed, 400_000, dim, 10_000)
+
+
+@pytest.mark.parametrize("gpus,dim", [(3, 3), (4, 2)])
+def test_kdtree_dist_global_routed_queries_cli(gpus, dim):
+    """kdtree_dist --decomp global answers 10 000 queries by the native routed search
+    (GlobalBuilder::query: home block, MIN all-reduce, reach blocks, MIN all-reduce) and prints
+    exactly what the CPU executable prints."""
+    args = ["--queries", "10000", "7", str(dim), "200000"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    g = subprocess.run([str(ROOT / "bin" / "kdtree_dist"), "--gpus", str(gpus), "--share-gpu", "--decomp", "global",
+                        *args], capture_output=True, text=True, timeout=300, env=env)
+    assert g.returncode == 0, g.stderr[-2000:]
+    c = subprocess.run([str(ROOT / "bin" / "kdtree_sequential"), *args], capture_output=True, text=True, timeout=300)
+    assert c.returncode == 0, c.stderr[-2000:]
+    strip = lambda out: [l for l in out.splitlines() if l.startswith("ID:")]  # noqa: E731
+    assert len(strip(g.stdout)) == 10000 and strip(g.stdout) == strip(c.stdout)
