@@ -242,8 +242,8 @@ plan_py(const std::vector<int64_t>& counts, int64_t n_total, int64_t P, int64_t 
 // (loopback communicator): rank r holds rows [first_r, first_r + local_r) of `x` (the reference's
 // MPI slicing), ids 1..N. Returns the assembled in-order tree (rank shares + boundary top rows)
 // on the host, the OR of the ranks' error words and the middle-bucket scale they ended at.
-std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const torch::Tensor& x, int64_t P,
-                                                                           int64_t k) {
+std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t, bool> global_loopback(const torch::Tensor& x, int64_t P,
+                                                                                 int64_t k) {
   TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
               "x: contiguous float32 [N, dim] host tensor");
   const int64_t N = x.size(0);
@@ -256,6 +256,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const
   std::vector<std::exception_ptr> errs(static_cast<size_t>(P));
   std::vector<u32> ew(static_cast<size_t>(P), 0u);
   std::vector<int> scales(static_cast<size_t>(P), 0);
+  std::vector<char> radix(static_cast<size_t>(P), 0);
   std::vector<std::thread> th;
   for (int r = 0; r < int(P); ++r)
     th.emplace_back([&, r] {
@@ -272,6 +273,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const
         gb.wait(s);
         ew[size_t(r)] = gb.read_error(s);
         scales[size_t(r)] = gb.middle_scale();
+        radix[size_t(r)] = gb.radix_mode() ? 1 : 0;
         PKD_HIP_CHECK(hipMemcpy(tp.data_ptr<float>() + gb.slot_lo() * dim, gb.tree_pts(), size_t(gb.n_leaf()) * dim * 4,
                                 hipMemcpyDeviceToHost));
         PKD_HIP_CHECK(hipMemcpy(ti.data_ptr<int32_t>() + gb.slot_lo(), gb.tree_ids(), size_t(gb.n_leaf()) * 4,
@@ -298,7 +300,8 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t> global_loopback(const
     if (e) std::rethrow_exception(e);
   u32 e = 0;
   for (u32 v : ew) e |= v;
-  return {tp, ti, int64_t(e), int64_t(*std::max_element(scales.begin(), scales.end()))};
+  return {tp, ti, int64_t(e), int64_t(*std::max_element(scales.begin(), scales.end())),
+          *std::max_element(radix.begin(), radix.end()) != 0};
 }
 
 // The native global builder on its own RCCL communicator, one per process (rank). The

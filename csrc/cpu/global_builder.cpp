@@ -493,6 +493,29 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
       const size_t words = top_middle_words(dim, cap);
       auto* mid = static_cast<float*>(buf(8, words * 4));
       top_select(hcur, level, bins, sizes, sel, err, hnext, reinterpret_cast<u32*>(mid), s);
+      if (radix_) {
+        // duplicate-heavy / skewed data (a median bucket outgrew the all-gather slots once):
+        // the bucket's rows stay at their node; 8 rounds of a 256-bin digit histogram of the
+        // (key, id) composite with one all-reduce each fix the median byte by byte; the one
+        // rank holding the median row contributes it to a MIN all-reduce. No P x bucket buffer.
+        top_collect_route(tp, node, level, axis, next_axis, cells, bins, next_bins, sel, mid, 0, hnext, s, true);
+        auto* rs = static_cast<TopRadix*>(buf(306, size_t(kTopMaxNodes) * sizeof(TopRadix)));
+        auto* rh = static_cast<u32*>(buf(307, size_t(kTopMaxNodes) * 256 * 4));
+        auto* rowbuf = static_cast<i64*>(buf(308, size_t(kTopMaxNodes) * (dim + 1) * 8));
+        top_radix_init(sel, sizes, level, rs, s);
+        fill_u32(rh, i64(nodes) * 256, 0u, s);
+        for (int pass = 7; pass >= 0; --pass) {
+          top_radix_hist(tp, node, level, axis, rs, pass, rh, s);
+          comm_.allreduce_sum_u32(rh, size_t(nodes) * 256, s);
+          top_radix_sel(rh, level, pass, rs, err, s);  // also re-zeroes rh
+        }
+        fill_u64(rowbuf, i64(nodes) * (dim + 1), u64(INT64_MAX), s);
+        top_radix_row(tp, node, level, axis, rs, rowbuf, s);
+        comm_.allreduce_min_i64(rowbuf, size_t(nodes) * (dim + 1), s);
+        top_radix_pivot(rowbuf, rs, level, axis, dim, pivots, top_rows, cells, err, s);
+        top_radix_fixup(tp, node, level, axis, next_axis, pivots, cells, next_bins, hnext, s);
+        continue;
+      }
       top_collect_route(tp, node, level, axis, next_axis, cells, bins, next_bins, sel, mid, cap, hnext, s);
       auto* gathered = static_cast<float*>(buf(9, size_t(P) * words * 4));
       comm_.allgather(mid, gathered, words * 4, s);
@@ -529,9 +552,10 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
     info.plan_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     const std::vector<i64> hall(host_counts_, host_counts_ + nall);
     if (global_plan::make_plan(hall, lay_, me, &plan) == 0) break;
-    if (global_plan::middle_cap(n_total_, P, 0, scale_) >= n_total_)
-      throw std::runtime_error("global top levels: middle buckets inconsistent at full capacity");
-    scale_ *= 8;
+    // a median bucket outgrew its all-gather slot: redo the top levels by radix rounds (sticky
+    // for the builder; memory stays O(P x the default slot))
+    if (radix_) throw std::runtime_error("global top levels: median selection inconsistent in radix mode");
+    radix_ = true;
     ++info.retries;
   }
   top_rows_ = top_rows;  // buffer slot 4, exposed through top_rows()

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_top_collect_route(TopPoints p, u32* 
                                                               int axis, int next_axis, const float* __restrict__ cells,
                                                               int bins, int next_bins, const u32* __restrict__ sel,
                                                               float* __restrict__ buf, i64 cap,
-                                                              u32* __restrict__ hist_next) {
+                                                              u32* __restrict__ hist_next, int radix) {
   extern __shared__ __align__(16) u32 nh[];  // next level's histogram (2 * nodes * next_bins words)
   __shared__ BucketParams prm[kTopMaxNodes], nprm[kTopMaxNodes];
   __shared__ u32 bs[kTopMaxNodes];
@@ -282,6 +282,9 @@ __global__ __launch_bounds__(kBlock) void k_top_collect_route(TopPoints p, u32* 
           const u32 c = b < bst ? 0u : 1u;
           node[i] = 2 * h + 1 + c;
           if (has_next) atomicAdd(&nh[(2 * j + c) * next_bins + bucket_of(kn[u], nprm[j], next_bins)], 1u);
+        } else if (radix) {
+          node[i] = h;  // stays at its node: the distributed radix rounds find the pivot among these
+          take = false;
         }
       }
       const u64 m = __ballot(take);
@@ -761,14 +764,15 @@ size_t top_middle_words(int dim, i64 cap) { return 4 + size_t(cap) * size_t(dim 
 
 void top_collect_route(const TopPoints& p, u32* node, int level, int axis, int next_axis, const float* cells,
                        int bins, int next_bins, const u32* sel, float* buf, i64 cap, u32* hist_next,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool radix) {
   if ((1 << level) > kTopMaxNodes) throw std::invalid_argument("top_collect_route: too many nodes");
   if (hist_next && 2 * (1 << level) * next_bins > kTopBins)
     throw std::invalid_argument("top_collect_route: next level's nodes * bins exceeds 8192");
   if (p.n <= 0) return;
   const size_t lds = hist_next ? size_t(2) * (1 << level) * next_bins * 4 : 0;
   k_top_collect_route<<<stream_grid(p.n), kBlock, lds, stream>>>(p, node, level, axis, next_axis, cells, bins,
-                                                                  next_bins, sel, buf, cap, hist_next);
+                                                                  next_bins, sel, buf, cap, hist_next,
+                                                                  radix ? 1 : 0);
   PKD_LAUNCH_CHECK();
 }
 
@@ -787,6 +791,208 @@ void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int d
   ensure_dynamic_lds(reinterpret_cast<const void*>(&k_top_pivot), int(lds));
   MidView mv{gathered, i64(top_middle_words(dim, cap)), cap, P, dim, axis};
   k_top_pivot<<<1 << level, kPivotThreads, lds, stream>>>(mv, level, sizes, sel, pivots, top_rows, cells, err);
+  PKD_LAUNCH_CHECK();
+}
+
+// ---- median by distributed radix rounds (duplicate-heavy data) --------------------------
+namespace {
+// rows of level-l node h still at h after the radix-mode collect (its median bucket): 8-bit digit
+// `pass` of the composite key among those matching the node's prefix above it
+__global__ __launch_bounds__(kBlock) void k_top_radix_hist(TopPoints p, const u32* __restrict__ node, int level,
+                                                           int axis, const TopRadix* __restrict__ rs, int pass,
+                                                           u32* __restrict__ hist) {
+  __shared__ u32 h[kTopMaxNodes * 256];
+  __shared__ u64 pre[kTopMaxNodes];
+  const int nodes = 1 << level;
+  const u32 first = u32(nodes - 1);
+  for (int b = threadIdx.x; b < nodes * 256; b += kBlock) h[b] = 0;
+  for (int j = threadIdx.x; j < nodes; j += kBlock) pre[j] = rs[j].prefix;
+  __syncthreads();
+  const int shift = 8 * pass;
+  const u64 hmask = pass == 7 ? 0ull : (~0ull << (shift + 8));
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += stride) {
+    const u32 hn = node[i];
+    if (hn - first >= u32(nodes)) continue;
+    const u32 j = hn - first;
+    const u64 k = composite_key(p.pts[i * p.dim + axis], point_id(p, i));
+    if ((k & hmask) == (pre[j] & hmask)) atomicAdd(&h[j * 256 + (u32(k >> shift) & 255u)], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nodes * 256; b += kBlock) {
+    const u32 v = h[b];
+    if (v) atomicAdd(&hist[b], v);
+  }
+}
+
+// one wave per node: the digit holding the node's remaining rank (all ranks' histograms summed)
+__global__ __launch_bounds__(64) void k_top_radix_sel(u32* __restrict__ hist, int level, int pass,
+                                                      TopRadix* __restrict__ rs, u32* __restrict__ err) {
+  const int j = blockIdx.x, ln = dev::lane();
+  u32* hs = hist + size_t(j) * 256;
+  TopRadix r = rs[j];
+  if (r.active) {
+    u32 v[4], s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = hs[4 * ln + q];
+      s += v[q];
+    }
+    const u32 incl = dev::wave_incl_scan(s);
+    const u32 excl = incl - s;
+    const bool mine = r.rank >= excl && r.rank < incl;
+    const u64 m = __ballot(mine);
+    if (!m) {
+      if (ln == 0) atomicOr(err, 1u);
+    } else {
+      const int src = __ffsll((long long)m) - 1;
+      u32 c = excl, dg = 0;
+      if (mine) {
+        for (int q = 0; q < 4; ++q) {
+          if (r.rank < c + v[q]) {
+            dg = u32(4 * ln + q);
+            break;
+          }
+          c += v[q];
+        }
+      }
+      dg = u32(__shfl(int(dg), src, 64));
+      c = u32(__shfl(int(c), src, 64));
+      if (ln == 0) {
+        r.prefix |= u64(dg) << (8 * pass);
+        r.rank -= c;
+        rs[j] = r;
+      }
+    }
+  }
+  for (int q = 0; q < 4; ++q) hs[4 * ln + q] = 0u;  // ready for the next round
+}
+
+__global__ void k_top_radix_init(const u32* __restrict__ sel, TopSizes sizes, int level, TopRadix* __restrict__ rs) {
+  const int j = threadIdx.x;
+  if (j >= (1 << level)) return;
+  TopRadix r{};
+  r.prefix = 0;
+  r.active = sizes.n[j] > 0 ? 1u : 0u;
+  r.rank = r.active ? u32(sizes.n[j] / 2) - sel[4 * j + 1] : 0u;
+  rs[j] = r;
+}
+
+// the pivot's row (composite keys are unique: exactly one rank holds it) as i64 words for a
+// MIN all-reduce (absent: INT64_MAX, prefilled by the caller)
+__global__ __launch_bounds__(kBlock) void k_top_radix_row(TopPoints p, const u32* __restrict__ node, int level,
+                                                          int axis, const TopRadix* __restrict__ rs,
+                                                          i64* __restrict__ rowbuf) {
+  const int nodes = 1 << level;
+  const u32 first = u32(nodes - 1);
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += stride) {
+    const u32 hn = node[i];
+    if (hn - first >= u32(nodes)) continue;
+    const u32 j = hn - first;
+    const u32 id = point_id(p, i);
+    if (composite_key(p.pts[i * p.dim + axis], id) != rs[j].prefix) continue;
+    i64* o = rowbuf + size_t(j) * (p.dim + 1);
+    for (int c = 0; c < p.dim; ++c) o[c] = i64(__float_as_uint(p.pts[i * p.dim + c]));
+    o[p.dim] = i64(id);
+  }
+}
+
+// pivots, top rows and children cells from the all-reduced rows
+__global__ void k_top_radix_pivot(const i64* __restrict__ rowbuf, const TopRadix* __restrict__ rs, int level,
+                                  int axis, int dim, u64* __restrict__ pivots, float* __restrict__ top_rows,
+                                  float* __restrict__ cells, u32* __restrict__ err) {
+  const int j = blockIdx.x;
+  const u32 h = u32((1 << level) - 1 + j);
+  float* cl = cells + size_t(2 * h + 1) * dim * 2;
+  float* cr = cells + size_t(2 * h + 2) * dim * 2;
+  const float* cp = cells + size_t(h) * dim * 2;
+  for (int c = threadIdx.x; c < 2 * dim; c += blockDim.x) {
+    cl[c] = cp[c];
+    cr[c] = cp[c];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const TopRadix r = rs[j];
+  float* tr = top_rows + size_t(h) * (dim + 1);
+  if (!r.active) {
+    pivots[h] = ~0ull;
+    for (int c = 0; c <= dim; ++c) tr[c] = 0.0f;
+    return;
+  }
+  const i64* o = rowbuf + size_t(j) * (dim + 1);
+  if (o[dim] == INT64_MAX) {
+    atomicOr(err, 1u);
+    pivots[h] = ~0ull;
+    return;
+  }
+  pivots[h] = r.prefix;
+  for (int c = 0; c <= dim; ++c) tr[c] = __uint_as_float(u32(o[c]));
+  const float split = __uint_as_float(u32(o[axis]));
+  cl[2 * axis + 1] = split;
+  cr[2 * axis] = split;
+}
+
+// rows left at their level-l node (its median bucket): below / above the pivot, or the pivot
+__global__ __launch_bounds__(kBlock) void k_top_radix_fixup(TopPoints p, u32* __restrict__ node, int level, int axis,
+                                                            int next_axis, const u64* __restrict__ pivots,
+                                                            const float* __restrict__ cells, int next_bins,
+                                                            u32* __restrict__ hist_next) {
+  const int nodes = 1 << level;
+  const u32 first = u32(nodes - 1);
+  const i64 stride = i64(gridDim.x) * kBlock;
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += stride) {
+    const u32 h = node[i];
+    if (h - first >= u32(nodes)) continue;
+    const u64 ck = composite_key(p.pts[i * p.dim + axis], point_id(p, i));
+    const u64 pv = pivots[h];
+    const u32 child = ck < pv ? 2 * h + 1 : (ck > pv ? 2 * h + 2 : kTopDone);
+    node[i] = child;
+    if (hist_next != nullptr && child != kTopDone) {
+      const float* c = cells + (size_t(h) * p.dim + next_axis) * 2;
+      const BucketParams np = make_params(c[0], c[1], next_bins);
+      atomicAdd(&hist_next[(child - 2 * first - 1) * next_bins + bucket_of(p.pts[i * p.dim + next_axis], np, next_bins)],
+                1u);
+    }
+  }
+}
+}  // namespace
+
+void top_radix_init(const u32* sel, const TopSizes& sizes, int level, TopRadix* rs, hipStream_t stream) {
+  k_top_radix_init<<<1, kTopMaxNodes, 0, stream>>>(sel, sizes, level, rs);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_radix_hist(const TopPoints& p, const u32* node, int level, int axis, const TopRadix* rs, int pass,
+                    u32* hist, hipStream_t stream) {
+  if (p.n <= 0) return;
+  k_top_radix_hist<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, rs, pass, hist);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_radix_sel(u32* hist, int level, int pass, TopRadix* rs, u32* err, hipStream_t stream) {
+  k_top_radix_sel<<<1 << level, 64, 0, stream>>>(hist, level, pass, rs, err);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_radix_row(const TopPoints& p, const u32* node, int level, int axis, const TopRadix* rs, i64* rowbuf,
+                   hipStream_t stream) {
+  if (p.n <= 0) return;
+  k_top_radix_row<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, rs, rowbuf);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_radix_pivot(const i64* rowbuf, const TopRadix* rs, int level, int axis, int dim, u64* pivots, float* top_rows,
+                     float* cells, u32* err, hipStream_t stream) {
+  k_top_radix_pivot<<<1 << level, 64, 0, stream>>>(rowbuf, rs, level, axis, dim, pivots, top_rows, cells, err);
+  PKD_LAUNCH_CHECK();
+}
+
+void top_radix_fixup(const TopPoints& p, u32* node, int level, int axis, int next_axis, const u64* pivots,
+                     const float* cells, int next_bins, u32* hist_next, hipStream_t stream) {
+  if (p.n <= 0) return;
+  k_top_radix_fixup<<<stream_grid(p.n), kBlock, 0, stream>>>(p, node, level, axis, next_axis, pivots, cells,
+                                                              next_bins, hist_next);
   PKD_LAUNCH_CHECK();
 }
 

@@ -74,7 +74,7 @@ void top_select(const u32* hist, int level, int bins, const TopSizes& sizes, u32
 size_t top_middle_words(int dim, i64 cap);
 void top_collect_route(const TopPoints& p, u32* node, int level, int axis, int next_axis, const float* cells,
                        int bins, int next_bins, const u32* sel, float* buf, i64 cap, u32* hist_next,
-                       hipStream_t stream);
+                       hipStream_t stream, bool radix = false);
 // After the level's pivots: routes this rank's staged rows (buf from top_collect_route) below
 // their node's pivot and counts them into hist_next (may be null).
 void top_fixup(const float* buf, i64 cap, int dim, int level, int axis, int next_axis, const u64* pivots,
@@ -137,6 +137,30 @@ struct BmSources {
 size_t ids_from_bitmaps_scratch_bytes(i64 max_words, int P);
 void ids_from_bitmaps(const u32* bitmaps, int P, const BmSources& src, u32* ids, void* scratch, u32* err,
                       hipStream_t stream);
+
+// ---- the median by distributed radix rounds (duplicate-heavy / skewed data) -------------
+// When a median bucket outgrows the all-gather slots, the builder switches to this mode: the
+// bucket's rows stay at their node (top_collect_route radix=true), and 8 rounds of a per-node
+// 256-bin digit histogram of the (key, id) composite (top_radix_hist) + an all-reduce(SUM) +
+// top_radix_sel fix the exact median one byte at a time; its row comes from the one rank that
+// holds it by an all-reduce(MIN) of (dim + 1) i64 words per node (top_radix_row, INT64_MAX
+// elsewhere); top_radix_pivot sets pivots, top rows and children cells, top_radix_fixup routes
+// the bucket's rows. Memory O(nodes x 256) instead of P x (bucket rows).
+struct TopRadix {
+  u64 prefix;  // composite bits fixed so far
+  u32 rank;    // rank of the median among the rows matching the prefix
+  u32 active;  // node has points
+};
+void top_radix_init(const u32* sel, const TopSizes& sizes, int level, TopRadix* rs, hipStream_t stream);
+void top_radix_hist(const TopPoints& p, const u32* node, int level, int axis, const TopRadix* rs, int pass,
+                    u32* hist, hipStream_t stream);
+void top_radix_sel(u32* hist, int level, int pass, TopRadix* rs, u32* err, hipStream_t stream);
+void top_radix_row(const TopPoints& p, const u32* node, int level, int axis, const TopRadix* rs, i64* rowbuf,
+                   hipStream_t stream);
+void top_radix_pivot(const i64* rowbuf, const TopRadix* rs, int level, int axis, int dim, u64* pivots,
+                     float* top_rows, float* cells, u32* err, hipStream_t stream);
+void top_radix_fixup(const TopPoints& p, u32* node, int level, int axis, int next_axis, const u64* pivots,
+                     const float* cells, int next_bins, u32* hist_next, hipStream_t stream);
 
 // ---- routed queries on the distributed tree ---------------------------------------------
 // A rank's blocks (complete subtrees of its share with points): which top-level leaf belongs

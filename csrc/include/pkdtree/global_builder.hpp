@@ -152,8 +152,11 @@ class GlobalBuilder {
   i64 slot_lo() const { return lay_.share_lo[size_t(rank_)]; }
   i64 n_leaf() const { return lay_.share_n[size_t(rank_)]; }
   int top_levels() const { return lay_.LL; }
-  // all-gather slot scale of the middle buckets (x 8 per overflow retry; sticky across builds)
+  // all-gather slot scale of the middle buckets (stays 1: an overflow switches to radix rounds)
   int middle_scale() const { return scale_; }
+  // the top levels find their medians by distributed radix rounds (set by a middle-bucket
+  // overflow: duplicate-heavy or skewed data; sticky across builds)
+  bool radix_mode() const { return radix_; }
   const float* tree_pts() const { return tree_pts_; }
   const u32* tree_ids() const { return tree_ids_; }
   // The T - 1 top-tree rows, heap order: dim + 1 floats (coordinates, id bits) on the device.
@@ -186,6 +189,7 @@ class GlobalBuilder {
   global_plan::Layout lay_;
   bool planar_;  // dim <= 8: SoA planes into the leaf builder's columns
   int scale_ = 1;
+  bool radix_ = false;
   float* tree_pts_ = nullptr;
   u32* tree_ids_ = nullptr;
   float* top_rows_ = nullptr;

@@ -115,13 +115,13 @@ def test_native_plan_errors(native):
             native.global_plan(flat, n, P, k, me)
 
 
-def _loopback_equal(native, x, P, k):
-    tp, ti, err, scale = native.global_loopback(x, P, k)
+def _loopback_equal(native, x, P, k, with_radix=False):
+    tp, ti, err, scale, radix = native.global_loopback(x, P, k)
     assert err == 0
-    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 16)
     assert torch.equal(ti, ci + 1), "native global tree differs from the exact tree"
     assert torch.equal(tp, cp)
-    return scale
+    return (scale, radix) if with_radix else scale
 
 
 @pytest.mark.gpu
@@ -144,7 +144,8 @@ def test_native_global_loopback(gpu_device, native, P, k, n, dim):
 def test_native_global_loopback_hard_data(gpu_device, native, P, k, n, kind):
     """Duplicate-heavy data (3 distinct values per axis: every median bucket is huge) and skewed
     data (half the points in a tiny cube): the middle buckets overflow their all-gather slots,
-    the builder retries with larger slots, and the tree is still the exact one."""
+    the builder redoes the top levels by distributed radix rounds (no larger slots), and the
+    tree is still the exact one."""
     g = torch.Generator().manual_seed(n + P)
     if kind == "dupes":
         x = torch.randint(0, 3, (n, 3), generator=g).float()
@@ -152,6 +153,18 @@ def test_native_global_loopback_hard_data(gpu_device, native, P, k, n, kind):
         x = torch.rand((n, 3), generator=g) * 200 - 100
         x[: n // 2] = x[: n // 2] * 1e-4 + 3.0
         x = x[torch.randperm(n, generator=g)].contiguous()
-    scale = _loopback_equal(native, x, P, k)
+    scale, radix = _loopback_equal(native, x, P, k, with_radix=True)
+    assert scale == 1, "the all-gather slots never grow (O(P x default slot) memory)"
     if kind == "dupes":
-        assert scale > 1, "duplicate-heavy data must overflow the default all-gather slots"
+        assert radix, "duplicate-heavy data must overflow the default all-gather slots"
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_native_global_loopback_dupes_20m_p8(gpu_device, native):
+    """20 M points, 3 distinct values per axis, 8 ranks: the exact tree by radix rounds with
+    the default all-gather slots (middle_scale stays 1)."""
+    g = torch.Generator().manual_seed(20)
+    x = torch.randint(0, 3, (20_000_000, 3), generator=g).float()
+    scale, radix = _loopback_equal(native, x, 8, 0, with_radix=True)
+    assert scale == 1 and radix
