@@ -252,14 +252,28 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
     // (the top rows between blocks and the boundary rows are brute-forced)
     gb->query(d_q, Q, d_res, s);
   } else if (local > 0) {
+    u64* d_one = nullptr;  // reference mode: each tree's search starts afresh, as on its own rank
+    if (ref && slices.size() > 1) PKD_HIP_CHECK(hipMalloc(&d_one, size_t(Q) * 8));
     for (const Slice& sl : slices) {  // every tree of this process: MIN into the same results
       if (sl.n <= 0) continue;
       const i64 off = sl.first - first;
       const float* tp = d_tree + off * dim;
       const u32* ti = d_ids + off;
-      if (ref) nn_traverse_reference(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);  // kdtree_mpi.cpp:234-243
-      else if (traverse) nn_traverse(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);
-      else nn_brute(tp, ti, 0, sl.n, dim, d_q, Q, d_res, s);
+      if (ref && d_one) {
+        nn_init(d_one, Q, s);
+        nn_traverse_reference(tp, ti, sl.n, dim, 0, d_q, Q, d_one, s);  // kdtree_mpi.cpp:234-243
+        nn_min_into(d_one, d_res, Q, s);
+      } else if (ref) {
+        nn_traverse_reference(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);
+      } else if (traverse) {
+        nn_traverse(tp, ti, sl.n, dim, 0, d_q, Q, d_res, s);
+      } else {
+        nn_brute(tp, ti, 0, sl.n, dim, d_q, Q, d_res, s);
+      }
+    }
+    if (d_one) {
+      PKD_HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(d_one);
     }
   }
   // MPI_Reduce(MIN) to rank 0 (kdtree_mpi.cpp:253), the id riding along in the low bits

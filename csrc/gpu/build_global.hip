@@ -2869,6 +2869,7 @@ Tuning Tuning::from_env() {
   t.top_sample_log2 = int(env_i("PKD_TOP_SAMPLE", t.top_sample_log2));
   if (const char* z = std::getenv("PKD_TOP_Z")) t.top_z = float(std::atof(z));
   t.top_blocks = int(env_i("PKD_TOP_BLOCKS", 0));
+  t.top_diag = int(env_i("PKD_TOP_DIAG", 0));
   return t;
 }
 
@@ -3174,10 +3175,12 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     tt.sample_log2 = tune_.top_sample_log2;
     tt.z = tune_.top_z;
     tt.scatter_blocks = tune_.top_blocks;
+    tt.diag = tune_.top_diag;
     {
       TraceRange trt("pkd.top4");
       top4::run(g, io, tt, stream);
     }
+    if (tt.diag) return;  // timing diagnostic: no tree
     run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, nullptr, top4::kLevels);
     return;
   }

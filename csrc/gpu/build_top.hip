@@ -42,10 +42,10 @@ constexpr int kInsChunk = kBlock * 16;
 struct State {
   u32 nbox_lo[8];  // ~(min sample key) per axis (0: none)
   u32 box_hi[8];   // max sample key per axis
-  u32 rlo[kNodes], rhi[kNodes], sshift[kNodes];  // sample binning of the node on its axis
+  u32 rlo[kNodes], rhi[kNodes];             // sample range of the node on its axis (bins: sample_params)
   u32 scount[kNodes];
   u32 a[kNodes], b[kNodes], phat[kNodes];  // band (inclusive, orderable keys), estimated pivot
-  u32 rshift[kNodes];                       // fine digit of a band composite: (c - comp_lo) >> rshift
+  dev::BucketParams bparam[kNodes];         // fine digit of a band row: bucket_of(key) over the band
   u32 staged_orig[kNodes];                  // rows the scatter staged at the node
   u32 late[kNodes][3];                      // staged rows of the node: left of / in / right of the band
   u32 sel[kNodes], sel_rank[kNodes], sel_cnt[kNodes], small_cnt[kNodes];
@@ -53,7 +53,6 @@ struct State {
   u32 cursor[kCells + 1];                   // rows the scatter put in each level-4 segment; [16]: staged
   u32 ins[kCells];                          // staged rows inserted per segment
   u32 pad[2];
-  u64 comp_lo[kNodes];
   u64 pivot[kNodes];                        // exact (key, id) composite of the node's median
 };
 
@@ -89,13 +88,22 @@ Layout layout() {
 
 __device__ __forceinline__ int heap_level(u32 h) { return 31 - __builtin_clz(h + 1u); }
 
-__device__ __forceinline__ u32 shift_for32(u32 span) {
-  const int bits = span ? 32 - __builtin_clz(span) : 0;
-  return u32(bits > 16 ? bits - 16 : 0);
+
+// Histogram bins linear in the key's VALUE over [lo, hi] (orderable keys): occupancy follows
+// the data, not the float exponent (bins linear in the orderable code crowd the bulk of the
+// keys into a few hundred bins, and same-address atomics serialise).
+__device__ __forceinline__ dev::BucketParams sample_params(u32 lo, u32 hi) {
+  return dev::make_params(from_orderable(lo), from_orderable(hi), kFine);
 }
-__device__ __forceinline__ u32 shift_for64(u64 span) {
-  const int bits = span ? 64 - __builtin_clzll(span) : 0;
-  return u32(bits > 16 ? bits - 16 : 0);
+// A key below every value of bins >= b (b > 0) and one above every value of bins <= b: the
+// float edge of the bin widened by a margin that covers the bucketing's rounding.
+__device__ __forceinline__ u32 key_below_bin(dev::BucketParams p, u32 b, float span) {
+  const float e = p.lo + float(b) / p.scale;
+  return orderable(e - (fabsf(e) * 1e-5f + span * 1e-6f));
+}
+__device__ __forceinline__ u32 key_above_bin(dev::BucketParams p, u32 b, float span) {
+  const float e = p.lo + float(b + 1) / p.scale;
+  return orderable(e + (fabsf(e) * 1e-5f + span * 1e-6f));
 }
 
 __device__ __forceinline__ u32 mix32(u32 x) {  // murmur3 finaliser
@@ -244,7 +252,8 @@ struct SampLevelArgs {
 
 __global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
   __shared__ u32 lc[8 * kCoarse];
-  __shared__ u32 ph[kNodes], rl[8], rh[8], sh[8];
+  __shared__ u32 ph[kNodes], rl[8], rh[8];
+  __shared__ dev::BucketParams bp[8];
   const int j = a.j, nodes = 1 << j, first = nodes - 1;
   for (int i = threadIdx.x; i < nodes * kCoarse; i += kBlock) lc[i] = 0;
   if (threadIdx.x < first) ph[threadIdx.x] = a.st->phat[threadIdx.x];
@@ -258,7 +267,6 @@ __global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
       if (blockIdx.x == 0) {
         a.st->rlo[0] = lo;
         a.st->rhi[0] = hi;
-        a.st->sshift[0] = shift_for32(hi - lo);
       }
     } else {
       lo = a.st->rlo[X];
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
     }
     rl[threadIdx.x] = lo;
     rh[threadIdx.x] = hi;
-    sh[threadIdx.x] = shift_for32(hi - lo);
+    bp[threadIdx.x] = sample_params(lo, hi);
   }
   __syncthreads();
   for (int k = blockIdx.x * kBlock + threadIdx.x; k < a.S; k += gridDim.x * kBlock) {
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
     const int x = X - first;
     u32 key = a.skey[size_t(j) * a.S + k];
     key = min(max(key, rl[x]), rh[x]);
-    const u32 bin = min((key - rl[x]) >> sh[x], u32(kFine - 1));
+    const u32 bin = dev::bucket_of(from_orderable(key), bp[x], kFine);
     atomicAdd(&a.fine[size_t(X) * kFine + bin], 1u);
     atomicAdd(&lc[x * kCoarse + (bin >> 8)], 1u);
   }
@@ -292,7 +300,9 @@ __global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
   const int j = a.j, first = (1 << j) - 1;
   const int X = first + blockIdx.x;
   State* st = a.st;
-  const u32 lo = st->rlo[X], hi = st->rhi[X], shift = shift_for32(hi - lo);
+  const u32 lo = st->rlo[X], hi = st->rhi[X];
+  const dev::BucketParams bp = sample_params(lo, hi);
+  const float span = from_orderable(hi) - from_orderable(lo);
   const u32* co = a.coarse + size_t(X) * kCoarse;
   const u32* fi = a.fine + size_t(X) * kFine;
   u32 below = 0, c = 0;
@@ -305,20 +315,21 @@ __global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
     const u32 bl = wave_find_fine(co, fi, rlo, &below, &t);
     const u32 bm = wave_find_fine(co, fi, rm, &below, &t);
     const u32 bh = wave_find_fine(co, fi, rhi, &below, &t);
-    const u64 edge_lo = u64(lo) + (u64(bl) << shift);
-    const u64 edge_hi = u64(lo) + (u64(bh + 1) << shift) - 1;
-    A = rlo == 0 ? 0u : u32(min<u64>(edge_lo, hi));
-    B = rhi >= c - 1 ? 0xffffffffu : u32(min<u64>(edge_hi, hi));
-    P = u32(min<u64>(u64(lo) + (u64(bm) << shift) + ((u64(1) << shift) >> 1), hi));
+    // the band: from below every sample of bin bl to above every sample of bin bh (open
+    // ended where the sample rank range reaches the node's first / last sample, or the edge bins)
+    const bool zero_span = !(bp.scale > 0.0f);
+    A = (rlo == 0 || bl == 0 || zero_span) ? 0u : min(key_below_bin(bp, bl, span), hi);
+    B = (rhi >= c - 1 || bh >= u32(kFine - 1) || zero_span) ? 0xffffffffu : max(key_above_bin(bp, bh, span), lo);
+    P = zero_span ? lo : min(max(orderable(bp.lo + (float(bm) + 0.5f) / bp.scale), lo), hi);
   }
   if (dev::lane() == 0) {
     st->scount[X] = c;
     st->a[X] = A;
     st->b[X] = B;
     st->phat[X] = P;
-    const u64 clo = u64(A) << 32, chi = (u64(B) << 32) | 0xffffffffull;
-    st->comp_lo[X] = clo;
-    st->rshift[X] = shift_for64(chi - clo);
+    // fine digit of a band row: its key's value bin over the band (open ends: the node's
+    // sample range; keys beyond it fall into the edge bins)
+    st->bparam[X] = dev::make_params(from_orderable(A == 0 ? lo : A), from_orderable(B == 0xffffffffu ? hi : B), kFine);
     if (j + 1 < kLevels) {
       const int ac = a.ax[j + 1];
       for (int s = 0; s < 2; ++s) {
@@ -338,7 +349,6 @@ __global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
         if (chi2 < clo2) chi2 = clo2;
         st->rlo[C] = clo2;
         st->rhi[C] = chi2;
-        st->sshift[C] = shift_for32(chi2 - clo2);
       }
     }
   }
@@ -361,6 +371,7 @@ struct ScatArgs {
   i64 cell_lo[kCells];
   u32 cell_n[kCells];
   int ax[kLevels];
+  int diag;  // 2: no reservation atomics (timing diagnostic, output garbage)
 };
 
 // Rows of one scatter tile held by a thread: v[u][c], id[u]; VEC (dim 3, 16-B aligned input):
@@ -487,7 +498,13 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
         zoff[par][ww][tid] = tot;
         tot += wcnt[par][ww][tid];
       }
-      const u32 base = tot ? atomicAdd(&a.st->cursor[tid], tot) : 0u;
+      u32 base = 0;
+      if (a.diag == 2) {  // timing diagnostic: an in-range offset instead of the reservation
+        const u32 cap = tid < kCells ? a.cell_n[tid] : u32(a.n);
+        base = cap > u32(TILE) ? u32((u64(tile) * 977u) % u64(cap - u32(TILE))) : 0u;
+      } else {
+        base = tot ? atomicAdd(&a.st->cursor[tid], tot) : 0u;
+      }
       if (tid < kCells && base + tot > a.cell_n[tid]) report(a.err, 0x2001u, u32(tid), base + tot);
 #pragma unroll
       for (int ww = 0; ww < 4; ++ww) {
@@ -557,8 +574,9 @@ __global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
   __shared__ u32 lc[8][3];
   __shared__ u32 lco[8 * kCoarse];
   __shared__ u32 lorig[16];
-  __shared__ u32 sa[8], sb[8], srs[8];
-  __shared__ u64 scl[8], spv[4];
+  __shared__ u32 sa[8], sb[8];
+  __shared__ dev::BucketParams sbp[8];
+  __shared__ u64 spv[4];
   const int j = a.j, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1;
   const int tid = threadIdx.x;
   for (int i = tid; i < nodes * kCoarse; i += kBlock) lco[i] = 0;
@@ -567,8 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
   if (tid < nodes) {
     sa[tid] = a.st->a[first + tid];
     sb[tid] = a.st->b[first + tid];
-    srs[tid] = a.st->rshift[first + tid];
-    scl[tid] = a.st->comp_lo[first + tid];
+    sbp[tid] = a.st->bparam[first + tid];
   }
   if (j > 0 && tid < nodes / 2) spv[tid] = a.st->pivot[firstp + tid];
   __syncthreads();
@@ -593,12 +610,12 @@ __global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
     }
     if (lvl != j) continue;
     const u32 x = T - u32(first);
-    const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+    const float kf = a.stage[i64(axj) * a.ncol + i];
+    const u32 k = orderable(kf);
     const int cls = k < sa[x] ? 0 : (k > sb[x] ? 2 : 1);
     atomicAdd(&lc[x][cls], 1u);
     if (cls == 1) {
-      const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-      const u32 d = u32(min<u64>((comp - scl[x]) >> srs[x], u64(kFine - 1)));
+      const u32 d = dev::bucket_of(kf, sbp[x], kFine);
       atomicAdd(&a.fine[size_t(T) * kFine + d], 1u);
       atomicAdd(&lco[x * kCoarse + (d >> 8)], 1u);
     }
@@ -662,15 +679,14 @@ __global__ __launch_bounds__(64) void k_res_sel1(ResArgs a, Geom g) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
-  __shared__ u32 sa[8], sb[8], srs[8], ssel[8];
-  __shared__ u64 scl[8];
+  __shared__ u32 sa[8], sb[8], ssel[8];
+  __shared__ dev::BucketParams sbp[8];
   const int j = a.j, nodes = 1 << j, first = nodes - 1;
   const int tid = threadIdx.x;
   if (tid < nodes) {
     sa[tid] = a.st->a[first + tid];
     sb[tid] = a.st->b[first + tid];
-    srs[tid] = a.st->rshift[first + tid];
-    scl[tid] = a.st->comp_lo[first + tid];
+    sbp[tid] = a.st->bparam[first + tid];
     ssel[tid] = a.st->sel[first + tid];
   }
   __syncthreads();
@@ -681,11 +697,11 @@ __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
     const u32 T = a.tags[i];
     if ((T & kMed) || heap_level(T) != j) continue;
     const u32 x = T - u32(first);
-    const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+    const float kf = a.stage[i64(axj) * a.ncol + i];
+    const u32 k = orderable(kf);
     if (k < sa[x] || k > sb[x]) continue;
+    if (dev::bucket_of(kf, sbp[x], kFine) != ssel[x]) continue;
     const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-    const u32 d = u32(min<u64>((comp - scl[x]) >> srs[x], u64(kFine - 1)));
-    if (d != ssel[x]) continue;
     const u32 p = atomicAdd(&a.st->small_cnt[T], 1u);
     if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
   }
@@ -773,17 +789,18 @@ __global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
     // heavy duplicates: the bin holds more rows than LDS takes; select over the staging arena
     // (every pass streams the staged rows: slow, but exact for any input)
     const i64 staged = st->cursor[kCells];
-    const u32 A = st->a[X], B = st->b[X], rs = st->rshift[X];
-    const u64 clo = st->comp_lo[X];
+    const u32 A = st->a[X], B = st->b[X];
+    const dev::BucketParams bp = st->bparam[X];
     const int axj = a.ax[j];
     pivot = block_select(
         [&](auto f) {
           for (i64 i = threadIdx.x; i < staged; i += kBlock) {
             if (a.tags[i] != u32(X)) continue;
-            const u32 k = orderable(a.stage[i64(axj) * a.ncol + i]);
+            const float kf = a.stage[i64(axj) * a.ncol + i];
+            const u32 k = orderable(kf);
             if (k < A || k > B) continue;
-            const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-            if (u32(min<u64>((comp - clo) >> rs, u64(kFine - 1))) == sel) f(comp);
+            if (dev::bucket_of(kf, bp, kFine) != sel) continue;
+            f((u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]));
           }
         },
         rank);
@@ -1017,6 +1034,7 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   const int R = D <= 4 ? 16 : 8;
   const i64 tile = i64(kBlock) * R;
   sc.tiles = (n + tile - 1) / tile;
+  sc.diag = t.diag;
   const int sblocks = int(std::max<i64>(1, std::min<i64>(t.scatter_blocks > 0 ? t.scatter_blocks : kMaxParts, sc.tiles)));
   const bool vec = D == 3 && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
                    (io.ids == nullptr || reinterpret_cast<uintptr_t>(io.ids) % 16 == 0);
@@ -1033,6 +1051,7 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
     default: k_scatter<8, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
   }
   PKD_LAUNCH_CHECK();
+  if (t.diag) return;  // timing diagnostic: the rest is not run
 
   // staged rows are a few percent of n: grids sized for ~16 % of the rows, grid-stride beyond
   const int rgrid = int(std::max<i64>(64, std::min<i64>(2048, (n / 6 + kBlock * 4 - 1) / (kBlock * 4))));

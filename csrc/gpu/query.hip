@@ -487,6 +487,19 @@ void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t s
   PKD_LAUNCH_CHECK();
 }
 
+namespace {
+__global__ void k_min_into(const u64* __restrict__ src, u64* __restrict__ dst, i64 n) {
+  const i64 i = i64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i] < dst[i] ? src[i] : dst[i];
+}
+}  // namespace
+
+void nn_min_into(const u64* src, u64* dst, i64 nq, hipStream_t stream) {
+  if (nq <= 0) return;
+  k_min_into<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(src, dst, nq);
+  PKD_LAUNCH_CHECK();
+}
+
 void nn_init(u64* out, i64 nq, hipStream_t stream) {
   if (nq <= 0) return;
   k_init<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(out, nq);

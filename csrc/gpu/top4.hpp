@@ -70,6 +70,9 @@ struct Tune {
   int sample_log2 = 20;  // sample rows = 2^sample_log2 (capped at n / 4)
   float z = 9.0f;        // band half-width in sample-rank standard deviations (PKD_TOP_Z)
   int scatter_blocks = 0;  // 0: by size
+  // Diagnostics (PKD_TOP_DIAG; timing only, the tree is NOT built): 1 stop after the scatter,
+  // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets.
+  int diag = 0;
 };
 
 size_t workspace_bytes();

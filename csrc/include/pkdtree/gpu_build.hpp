@@ -70,6 +70,7 @@ struct Tuning {
   int top_sample_log2 = 20;   // PKD_TOP_SAMPLE: log2 of the sample rows
   float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
   int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
+  int top_diag = 0;           // PKD_TOP_DIAG: timing diagnostics of the scatter (no tree; top4::Tune::diag)
   static Tuning from_env();
 };
 

@@ -49,6 +49,10 @@ void nn_traverse_reference(const float* tree_pts, const u32* tree_ids, i64 n, in
 void check_tree(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0, unsigned long long* count,
                 hipStream_t stream);
 
+// dst[q] = min(dst[q], src[q]) (combining searches that must each start afresh, e.g. the
+// reference's procedure on several forest trees of one process)
+void nn_min_into(const u64* src, u64* dst, i64 nq, hipStream_t stream);
+
 // packed -> (sqrt(d2) correctly rounded, id)
 void nn_finalize(const u64* packed, i64 nq, float* dist, i64* ids, hipStream_t stream);
 
