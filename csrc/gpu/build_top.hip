@@ -2,21 +2,29 @@
 //
 // Kernel sequence of one build (all on the caller's stream, no host round trip, graph-safe):
 //   k_zero_top      state, histograms
-//   k_samp_gather   2^sample_log2 stratified random rows: the keys of the four level axes
-//   k_samp_hist/sel per level: 64 Ki-bin histogram of the node's sample keys (bins linear over
-//                   the node's sample range in orderable-key space), then per node the bins of
-//                   the sample ranks c/2 - h, c/2, c/2 + h (h = z sqrt(c) / 2): band [a, b] and
-//                   the estimated pivot that routes the sample to the children
+//   k_samp_gather   2^sample_log2 stratified random rows: the keys of the four level axes, and
+//                   per-block key ranges
+//   k_samp_hist/sel per level: histogram of the node's sample keys (kSampBins >> j bins per node,
+//                   linear in the key value over the node's sample range), then per node the
+//                   bins of the sample ranks c/2 - h, c/2, c/2 + h (h = z sqrt(c) / 2): band
+//                   [a, b] and the estimated pivot that routes the sample to the children
 //   k_scatter       every input row once: certain rows into their level-4 segment, band rows
 //                   into the staging arena (tag = node), SoA columns + ids, bounding box
 //   per level j:    k_res_classify (route the staged rows by level j-1's exact pivot, classify
-//                   the level-j ones against the band, 16-bit histogram of the band's (key, id)
-//                   composites), k_res_sel1 (exact rank of the median in the band from the
-//                   counts; its bin), k_res_collect (the bin's rows), k_res_sel2 (radix select:
-//                   the exact pivot)
+//                   the level-j ones against the band, kResBins >> j-bin histogram of the band
+//                   rows' keys), k_res_sel1 (exact rank of the median in the band from the
+//                   counts; its bin), k_res_collect (the bin's rows), k_res_sel2 (radix select
+//                   on the (key, id) composites: the exact pivot)
 //   k_res_insert    staged rows into the free slots of their level-4 segments
 //   k_finish        bounding box, the 15 medians to the output, cells of nodes 0..30, the
 //                   level-4 histogram parameters, consistency checks
+//
+// Histograms are built in LDS per workgroup and flushed with lane-contiguous atomics (one
+// 256-B wave-instruction per 64 bins): scattered one-lane-per-bin global atomics run an order
+// of magnitude below that rate on MI355X (they execute at the memory side), and were what
+// bounded the first version of these kernels. Row moves (scatter, insert) rank rows per zone
+// with wave ballots (no same-address LDS atomics) and reorder each tile through LDS, so every
+// zone's rows leave the workgroup as contiguous runs instead of 16-B fragments.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -31,13 +39,20 @@ namespace top4 {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kFine = 1 << 16;       // fine bins per node (16-bit digit)
-constexpr int kCoarse = 256;         // coarse bins per node (fine >> 8)
-constexpr int kSmallCap = 4096;      // rows of a median's fine bin selected in LDS
+constexpr int kSampBins = 1 << 14;   // sample histogram entries per level: kSampBins >> j per node
+constexpr int kResBins = 1 << 13;    // resolution histogram entries per level
+constexpr int kHistThreads = 1024;   // workgroup of the LDS histogram kernels
+constexpr int kSampBlocks = 64;
+constexpr int kResBlocks = 256;
+constexpr int kSmallCap = 4096;      // rows of a median's bin selected in LDS
 constexpr u32 kMed = 0x80000000u;    // tag of a median row: kMed | node
 constexpr int kMaxParts = 2048;      // scatter blocks (one bounding-box partial each)
 constexpr int kMaxSampleLog2 = 21;
-constexpr int kInsChunk = kBlock * 16;
+constexpr int kGatherRows = 4;       // sample rows per gather thread
+constexpr int kMaxGather = (1 << kMaxSampleLog2) / (kBlock * kGatherRows);
+
+__host__ __device__ constexpr int samp_bins(int j) { return kSampBins >> j; }
+__host__ __device__ constexpr int res_bins(int j) { return kResBins >> j; }
 
 struct State {
   u32 nbox_lo[8];  // ~(min sample key) per axis (0: none)
@@ -45,7 +60,7 @@ struct State {
   u32 rlo[kNodes], rhi[kNodes];             // sample range of the node on its axis (bins: sample_params)
   u32 scount[kNodes];
   u32 a[kNodes], b[kNodes], phat[kNodes];  // band (inclusive, orderable keys), estimated pivot
-  dev::BucketParams bparam[kNodes];         // fine digit of a band row: bucket_of(key) over the band
+  dev::BucketParams bparam[kNodes];         // bin of a band row: bucket_of(key) over the band
   u32 staged_orig[kNodes];                  // rows the scatter staged at the node
   u32 late[kNodes][3];                      // staged rows of the node: left of / in / right of the band
   u32 sel[kNodes], sel_rank[kNodes], sel_cnt[kNodes], small_cnt[kNodes];
@@ -57,7 +72,7 @@ struct State {
 };
 
 struct Layout {
-  size_t state, fine_s, coarse_s, fine_r, coarse_r, zero_end, skey, small, part, total;
+  size_t state, fine_s, fine_r, zero_end, skey, gpart, small, part, total;
 };
 
 inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
@@ -68,16 +83,14 @@ Layout layout() {
   L.state = o;
   o = al(o + sizeof(State));
   L.fine_s = o;
-  o = al(o + size_t(kNodes) * kFine * 4);
-  L.coarse_s = o;
-  o = al(o + size_t(kNodes) * kCoarse * 4);
+  o = al(o + size_t(kLevels) * kSampBins * 4);
   L.fine_r = o;
-  o = al(o + size_t(kNodes) * kFine * 4);
-  L.coarse_r = o;
-  o = al(o + size_t(kNodes) * kCoarse * 4);
+  o = al(o + size_t(kLevels) * kResBins * 4);
   L.zero_end = o;
   L.skey = o;
   o = al(o + size_t(kLevels) * (size_t(1) << kMaxSampleLog2) * 4);
+  L.gpart = o;
+  o = al(o + size_t(kMaxGather) * 2 * kLevels * 4);
   L.small = o;
   o = al(o + size_t(8) * kSmallCap * 8);
   L.part = o;
@@ -88,12 +101,10 @@ Layout layout() {
 
 __device__ __forceinline__ int heap_level(u32 h) { return 31 - __builtin_clz(h + 1u); }
 
-
 // Histogram bins linear in the key's VALUE over [lo, hi] (orderable keys): occupancy follows
-// the data, not the float exponent (bins linear in the orderable code crowd the bulk of the
-// keys into a few hundred bins, and same-address atomics serialise).
-__device__ __forceinline__ dev::BucketParams sample_params(u32 lo, u32 hi) {
-  return dev::make_params(from_orderable(lo), from_orderable(hi), kFine);
+// the data, not the float exponent.
+__device__ __forceinline__ dev::BucketParams sample_params(u32 lo, u32 hi, int bins) {
+  return dev::make_params(from_orderable(lo), from_orderable(hi), bins);
 }
 // A key below every value of bins >= b (b > 0) and one above every value of bins <= b: the
 // float edge of the bin widened by a margin that covers the bucketing's rounding.
@@ -153,23 +164,131 @@ __device__ __forceinline__ u32 wave_find256(const u32* h, u32 rank, u32* below, 
   return bin;
 }
 
-// Fine bin (of 65536) holding the rank-th element of a node's two-level histogram.
-__device__ __forceinline__ u32 wave_find_fine(const u32* coarse, const u32* fine, u32 rank, u32* below, u32* total) {
-  u32 b1 = 0, b2 = 0, t2 = 0;
-  const u32 cb = wave_find256(coarse, rank, &b1, total);
+// Entry of h[0, n) (n <= 64) holding the rank-th element; *below = elements before it.
+__device__ __forceinline__ u32 wave_find_small(const u32* h, int n, u32 rank, u32* below) {
+  const int ln = dev::lane();
+  const u32 v = ln < n ? h[ln] : 0u;
+  const u32 incl = dev::wave_incl_scan(v);
+  const u32 excl = incl - v;
+  const u64 m = __ballot(rank >= excl && rank < incl);
+  if (!m) {
+    *below = __shfl(incl, 63, 64);
+    return u32(n);
+  }
+  const int src = __ffsll((long long)m) - 1;
+  *below = u32(__shfl(int(excl), src, 64));
+  return u32(src);
+}
+
+// Coarse sums of a node's F = 256 * gs bin histogram into co[256] (LDS): every thread of a
+// kBlock workgroup calls it; the caller synchronises before reading co.
+__device__ __forceinline__ void coarse_of(const u32* fine, int gs, u32* co) {
+  const int t = threadIdx.x;
+  u32 s = 0;
+  for (int e = 0; e < gs; ++e) s += fine[t * gs + e];
+  co[t] = s;
+}
+
+// Bin (of 256 * gs) holding the rank-th element, from the coarse sums and the fine bins (wave).
+__device__ __forceinline__ u32 wave_find_fine(const u32* co, const u32* fine, int gs, u32 rank, u32* below,
+                                              u32* total) {
+  u32 b1 = 0, b2 = 0;
+  const u32 cb = wave_find256(co, rank, &b1, total);
   if (cb >= 256) {
     *below = *total;
-    return u32(kFine);
+    return u32(256 * gs);
   }
-  const u32 fb = wave_find256(fine + size_t(cb) * 256, rank - b1, &b2, &t2);
+  const u32 fb = wave_find_small(fine + size_t(cb) * gs, gs, rank - b1, &b2);
   *below = b1 + b2;
-  return cb * 256 + min(fb, 255u);
+  return cb * u32(gs) + min(fb, u32(gs - 1));
 }
 
 __device__ __forceinline__ u32 wave_sum(u32 v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += u32(__shfl_xor(int(v), o, 64));
   return v;
+}
+
+// cnt[idx] += 1 for every active lane, one LDS atomic per distinct idx of the wave (the wave
+// calls it uniformly).
+__device__ __forceinline__ void wave_count(u32* cnt, u32 idx, bool active) {
+  u64 act = __ballot(active);
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const u32 key = u32(__shfl(int(idx), leader, 64));
+    const u64 m = __ballot(active && idx == key);
+    if (dev::lane() == leader) atomicAdd(&cnt[key], u32(__popcll(m)));
+    act &= ~m;
+  }
+}
+
+// Lanes of the wave in the same zone as this one (valid lanes only; zones < 2^BITS).
+template <int BITS>
+__device__ __forceinline__ u64 match_zone(u32 z, bool valid) {
+  u64 m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const bool bit = (z >> b) & 1u;
+    const u64 bb = __ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return m;
+}
+
+// Rank of this lane's row among the wave's rows of its zone so far; wc = the wave's own zone
+// counters in LDS (no other wave touches them until the next barrier).
+template <int BITS>
+__device__ __forceinline__ u32 wave_rank(u32 z, bool valid, u32* wc) {
+  const u64 m = match_zone<BITS>(z, valid);
+  const u32 below = dev::mbcnt(m);
+  u32 r = 0;
+  if (valid) {
+    const u32 before = wc[z];
+    r = before + below;
+    if (below == 0) wc[z] = before + u32(__popcll(m));
+  }
+  return r;
+}
+
+// Per-tile zone bookkeeping of an LDS reorder (NH parts of a tile, NZ zones, 4 waves).
+template <int NZ, int NH>
+struct Reorder {
+  u32 wc[NH][4][NZ];  // per-wave zone counts; offsets of the wave's rows after scan()
+  u32 hoff[NH][NZ];   // LDS position of zone z's first row in part h
+  u32 hcnt[NH];       // rows of part h
+  u32 gbase[NH][NZ];  // destination index of zone z's first row of part h
+};
+
+// Wave 0: per-wave offsets, LDS zone offsets, and one reservation per zone for the whole tile
+// (base = reserve(z, rows)); the caller brackets it with barriers.
+template <int NZ, int NH, class Reserve>
+__device__ __forceinline__ void reorder_scan(Reorder<NZ, NH>& s, Reserve reserve) {
+  static_assert(NZ <= 32 && NH <= 2, "reorder: 32 zones, 2 parts");
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x, h = l >> 5, z = l & 31;
+  const bool ok = h < NH && z < NZ;
+  u32 c = 0;
+  if (ok) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const u32 t = s.wc[h][w][z];
+      s.wc[h][w][z] = c;
+      c += t;
+    }
+  }
+  const u32 incl = dev::wave_incl_scan(c);
+  const u32 tot0 = __shfl(incl, 31, 64);
+  const u32 excl = incl - c - (h ? tot0 : 0u);
+  const u32 c1 = u32(__shfl(int(c), (l + 32) & 63, 64));
+  if (ok) {
+    s.hoff[h][z] = excl;
+    if (z == NZ - 1) s.hcnt[h] = excl + c;
+  }
+  if (h == 0 && z < NZ) {
+    const u32 base = reserve(z, c + c1);
+    s.gbase[0][z] = base;
+    if (NH > 1) s.gbase[NH - 1][z] = base + c;
+  }
 }
 
 __device__ __forceinline__ void report(u32* err, u32 code, u32 t, u32 v) {
@@ -192,8 +311,8 @@ struct SampArgs {
   i64 n;
   int S;
   int ax[kLevels];
-  u32* skey;  // [kLevels][S]
-  State* st;
+  u32* skey;   // [kLevels][S]
+  u32* gpart;  // [gather blocks][2 kLevels]: per-block min / max key of each level's axis
 };
 
 __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
@@ -204,17 +323,26 @@ __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
     mn[j] = 0xffffffffu;
     mx[j] = 0u;
   }
-  for (int k = blockIdx.x * kBlock + threadIdx.x; k < a.S; k += gridDim.x * kBlock) {
-    const i64 w0 = (i64(k) * a.n) / a.S, w1 = (i64(k + 1) * a.n) / a.S;
-    const u32 win = u32(max<i64>(1, w1 - w0));
-    const i64 r = w0 + i64(mix32(u32(k) * 0x9e3779b9u + 0x7f4a7c15u) % win);
-    float v[kLevels];
+  float v[kGatherRows][kLevels];
+  int kk[kGatherRows];
 #pragma unroll
-    for (int j = 0; j < kLevels; ++j) v[j] = a.pts[r * a.dim + a.ax[j]];
+  for (int u = 0; u < kGatherRows; ++u) {  // all loads first: the rows are independent
+    const int k = (blockIdx.x * kGatherRows + u) * kBlock + threadIdx.x;
+    kk[u] = k;
+    const int kc = k < a.S ? k : a.S - 1;
+    const i64 w0 = (i64(kc) * a.n) / a.S, w1 = (i64(kc + 1) * a.n) / a.S;
+    const u32 win = u32(max<i64>(1, w1 - w0));
+    const i64 r = w0 + i64(mix32(u32(kc) * 0x9e3779b9u + 0x7f4a7c15u) % win);
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) v[u][j] = a.pts[r * a.dim + a.ax[j]];
+  }
+#pragma unroll
+  for (int u = 0; u < kGatherRows; ++u) {
+    if (kk[u] >= a.S) continue;
 #pragma unroll
     for (int j = 0; j < kLevels; ++j) {
-      const u32 key = orderable(v[j]);
-      a.skey[size_t(j) * a.S + k] = key;
+      const u32 key = orderable(v[u][j]);
+      a.skey[size_t(j) * a.S + kk[u]] = key;
       mn[j] = min(mn[j], key);
       mx[j] = max(mx[j], key);
     }
@@ -231,38 +359,75 @@ __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
   __syncthreads();
   if (threadIdx.x < 2 * kLevels) {
     const int c = threadIdx.x;
-    u32 v = red[0][c];
-    for (int k = 1; k < kBlock / 64; ++k) v = c < kLevels ? min(v, red[k][c]) : max(v, red[k][c]);
-    const int j = c % kLevels;
-    if (c < kLevels) atomicMax(&a.st->nbox_lo[a.ax[j]], ~v);
-    else atomicMax(&a.st->box_hi[a.ax[j]], v);
+    u32 r = red[0][c];
+    for (int k = 1; k < kBlock / 64; ++k) r = c < kLevels ? min(r, red[k][c]) : max(r, red[k][c]);
+    a.gpart[size_t(blockIdx.x) * 2 * kLevels + c] = r;
   }
 }
 
 struct SampLevelArgs {
   const u32* skey;
+  const u32* gpart;
+  int gblocks;
   int S;
   int j;
   int ax[kLevels + 1];
   State* st;
-  u32* fine;    // [kNodes][kFine]
-  u32* coarse;  // [kNodes][kCoarse]
+  u32* fine;  // [kLevels][kSampBins]: level j, node x at j * kSampBins + x * samp_bins(j)
   float z;
 };
 
-__global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
-  __shared__ u32 lc[8 * kCoarse];
+// LDS histogram of a contiguous share of the sample (every key routed to its level-j node by
+// the estimated pivots), flushed with lane-contiguous atomics.
+__global__ __launch_bounds__(kHistThreads) void k_samp_hist(SampLevelArgs a) {
+  __shared__ u32 h[kSampBins];
   __shared__ u32 ph[kNodes], rl[8], rh[8];
   __shared__ dev::BucketParams bp[8];
-  const int j = a.j, nodes = 1 << j, first = nodes - 1;
-  for (int i = threadIdx.x; i < nodes * kCoarse; i += kBlock) lc[i] = 0;
-  if (threadIdx.x < first) ph[threadIdx.x] = a.st->phat[threadIdx.x];
-  if (threadIdx.x < nodes) {
-    const int X = first + threadIdx.x;
+  __shared__ u32 red[kHistThreads / 64][2 * kLevels];
+  __shared__ u32 sbl[2 * kLevels];
+  const int j = a.j, nodes = 1 << j, first = nodes - 1, F = samp_bins(j);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kSampBins; i += kHistThreads) h[i] = 0u;
+  if (j == 0) {  // the sample's key range per level axis, from the gather blocks' partials
+#pragma unroll
+    for (int c = 0; c < 2 * kLevels; ++c) {
+      u32 r = c < kLevels ? 0xffffffffu : 0u;
+      for (int p = tid; p < a.gblocks; p += kHistThreads) {
+        const u32 v = a.gpart[size_t(p) * 2 * kLevels + c];
+        r = c < kLevels ? min(r, v) : max(r, v);
+      }
+      r = c < kLevels ? dev::wave_min_u32(r) : dev::wave_max_u32(r);
+      if (dev::lane() == 0) red[tid / 64][c] = r;
+    }
+    __syncthreads();
+    if (tid < 2 * kLevels) {
+      u32 r = red[0][tid];
+      for (int k = 1; k < kHistThreads / 64; ++k) r = tid < kLevels ? min(r, red[k][tid]) : max(r, red[k][tid]);
+      sbl[tid] = r;
+    }
+  }
+  if (tid < first) ph[tid] = a.st->phat[tid];
+  __syncthreads();
+  if (j == 0 && blockIdx.x == 0 && tid < 8) {  // per axis over the levels that split on it
+    u32 mn = 0xffffffffu, mx = 0u;
+    bool any = false;
+    for (int l = 0; l < kLevels; ++l)
+      if (a.ax[l] == tid) {
+        mn = min(mn, sbl[l]);
+        mx = max(mx, sbl[kLevels + l]);
+        any = true;
+      }
+    if (any) {
+      a.st->nbox_lo[tid] = ~mn;
+      a.st->box_hi[tid] = mx;
+    }
+  }
+  if (tid < nodes) {
+    const int X = first + tid;
     u32 lo, hi;
     if (j == 0) {
-      lo = ~a.st->nbox_lo[a.ax[0]];
-      hi = a.st->box_hi[a.ax[0]];
+      lo = sbl[0];
+      hi = sbl[kLevels];
       if (hi < lo) hi = lo;
       if (blockIdx.x == 0) {
         a.st->rlo[0] = lo;
@@ -272,39 +437,43 @@ __global__ __launch_bounds__(kBlock) void k_samp_hist(SampLevelArgs a) {
       lo = a.st->rlo[X];
       hi = a.st->rhi[X];
     }
-    rl[threadIdx.x] = lo;
-    rh[threadIdx.x] = hi;
-    bp[threadIdx.x] = sample_params(lo, hi);
+    rl[tid] = lo;
+    rh[tid] = hi;
+    bp[tid] = sample_params(lo, hi, F);
   }
   __syncthreads();
-  for (int k = blockIdx.x * kBlock + threadIdx.x; k < a.S; k += gridDim.x * kBlock) {
+  const int per = (a.S + int(gridDim.x) - 1) / int(gridDim.x);
+  const int k0 = int(blockIdx.x) * per, k1 = min(a.S, k0 + per);
+  for (int k = k0 + tid; k < k1; k += kHistThreads) {
     int X = 0;
     for (int i = 0; i < j; ++i) X = 2 * X + 1 + (a.skey[size_t(i) * a.S + k] >= ph[X] ? 1 : 0);
     const int x = X - first;
     u32 key = a.skey[size_t(j) * a.S + k];
     key = min(max(key, rl[x]), rh[x]);
-    const u32 bin = dev::bucket_of(from_orderable(key), bp[x], kFine);
-    atomicAdd(&a.fine[size_t(X) * kFine + bin], 1u);
-    atomicAdd(&lc[x * kCoarse + (bin >> 8)], 1u);
+    atomicAdd(&h[x * F + int(dev::bucket_of(from_orderable(key), bp[x], F))], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nodes * kCoarse; i += kBlock) {
-    const u32 v = lc[i];
-    if (v) atomicAdd(&a.coarse[size_t(first) * kCoarse + i], v);
+  u32* out = a.fine + size_t(j) * kSampBins;
+  for (int i = tid; i < kSampBins; i += kHistThreads) {
+    const u32 v = h[i];
+    if (v) atomicAdd(&out[i], v);
   }
 }
 
-// One wave per node of level j: the band and estimated pivot from the sample ranks, then the
-// children's sample ranges (the root box on their axis, clipped by every ancestor pivot on it).
-__global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
-  const int j = a.j, first = (1 << j) - 1;
+// One workgroup per node of level j: the band and estimated pivot from the sample ranks, then
+// the children's sample ranges (the root box on their axis, clipped by every ancestor pivot on it).
+__global__ __launch_bounds__(kBlock) void k_samp_sel(SampLevelArgs a) {
+  __shared__ __align__(16) u32 co[256];
+  const int j = a.j, first = (1 << j) - 1, F = samp_bins(j), gs = F / 256;
   const int X = first + blockIdx.x;
+  const u32* fi = a.fine + size_t(j) * kSampBins + size_t(blockIdx.x) * F;
+  coarse_of(fi, gs, co);
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
   State* st = a.st;
   const u32 lo = st->rlo[X], hi = st->rhi[X];
-  const dev::BucketParams bp = sample_params(lo, hi);
+  const dev::BucketParams bp = sample_params(lo, hi, F);
   const float span = from_orderable(hi) - from_orderable(lo);
-  const u32* co = a.coarse + size_t(X) * kCoarse;
-  const u32* fi = a.fine + size_t(X) * kFine;
   u32 below = 0, c = 0;
   (void)wave_find256(co, 0, &below, &c);
   u32 A = 0, B = 0xffffffffu, P = lo;
@@ -312,14 +481,14 @@ __global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
     const u32 half = u32(ceilf(a.z * sqrtf(float(c)) * 0.5f)) + 2u;
     const u32 rm = c / 2, rlo = rm > half ? rm - half : 0u, rhi = min(c - 1, rm + half);
     u32 t = 0;
-    const u32 bl = wave_find_fine(co, fi, rlo, &below, &t);
-    const u32 bm = wave_find_fine(co, fi, rm, &below, &t);
-    const u32 bh = wave_find_fine(co, fi, rhi, &below, &t);
+    const u32 bl = wave_find_fine(co, fi, gs, rlo, &below, &t);
+    const u32 bm = wave_find_fine(co, fi, gs, rm, &below, &t);
+    const u32 bh = wave_find_fine(co, fi, gs, rhi, &below, &t);
     // the band: from below every sample of bin bl to above every sample of bin bh (open
     // ended where the sample rank range reaches the node's first / last sample, or the edge bins)
     const bool zero_span = !(bp.scale > 0.0f);
     A = (rlo == 0 || bl == 0 || zero_span) ? 0u : min(key_below_bin(bp, bl, span), hi);
-    B = (rhi >= c - 1 || bh >= u32(kFine - 1) || zero_span) ? 0xffffffffu : max(key_above_bin(bp, bh, span), lo);
+    B = (rhi >= c - 1 || bh >= u32(F - 1) || zero_span) ? 0xffffffffu : max(key_above_bin(bp, bh, span), lo);
     P = zero_span ? lo : min(max(orderable(bp.lo + (float(bm) + 0.5f) / bp.scale), lo), hi);
   }
   if (dev::lane() == 0) {
@@ -327,9 +496,10 @@ __global__ __launch_bounds__(64) void k_samp_sel(SampLevelArgs a) {
     st->a[X] = A;
     st->b[X] = B;
     st->phat[X] = P;
-    // fine digit of a band row: its key's value bin over the band (open ends: the node's
-    // sample range; keys beyond it fall into the edge bins)
-    st->bparam[X] = dev::make_params(from_orderable(A == 0 ? lo : A), from_orderable(B == 0xffffffffu ? hi : B), kFine);
+    // bin of a band row: its key's value bin over the band (open ends: the node's sample
+    // range; keys beyond it fall into the edge bins)
+    st->bparam[X] = dev::make_params(from_orderable(A == 0 ? lo : A), from_orderable(B == 0xffffffffu ? hi : B),
+                                     res_bins(j));
     if (j + 1 < kLevels) {
       const int ac = a.ax[j + 1];
       for (int s = 0; s < 2; ++s) {
@@ -429,20 +599,22 @@ __device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R
   return valid;
 }
 
-template <int D, bool VEC>
+// Zone code of a scatter row: 0..15 its level-4 segment, 16 + T staged at node T, 31 none.
+template <int D, int R, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
-  constexpr int R = D <= 4 ? 16 : 8;  // rows per thread per tile
+  constexpr int NH = 2, HR = R / NH, HALF = kBlock * HR, NZ = kCells + 1;
   constexpr int TILE = kBlock * R;
   __shared__ u32 sa[16], sb[16];
-  __shared__ u32 wcnt[2][4][kCells + 1];
-  __shared__ u32 zoff[2][4][kCells + 1];
+  __shared__ Reorder<NZ, NH> ro;
+  __shared__ float buf[D + 1][HALF];
+  __shared__ unsigned char bz[HALF];
   __shared__ u32 red[kBlock / 64][2 * D];
-  const int tid = threadIdx.x, w = tid >> 6;
+  const int tid = threadIdx.x, w = tid >> 6, ln = tid & 63;
   if (tid < kNodes) {
     sa[tid] = a.st->a[tid];
     sb[tid] = a.st->b[tid];
   }
-  if (tid < 2 * 4 * (kCells + 1)) (&wcnt[0][0][0])[tid] = 0u;
+  if (tid < NH * 4 * NZ) (&ro.wc[0][0][0])[tid] = 0u;
   u32 mn[D], mx[D];
 #pragma unroll
   for (int c = 0; c < D; ++c) {
@@ -450,8 +622,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
     mx[c] = 0u;
   }
   __syncthreads();
-  int par = 0;
-  for (i64 tile = blockIdx.x; tile < a.tiles; tile += gridDim.x, par ^= 1) {
+  for (i64 tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
     const i64 t0 = tile * TILE;
     float v[R][D];
     u32 id[R];
@@ -477,10 +648,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
           }
         }
       }
-      const u32 z = !valid ? 31u : (staged ? u32(kCells) : X - u32(kNodes));
-      u32 r = 0;
+      const u32 zc = !valid ? 31u : (staged ? u32(kCells) + T : X - u32(kNodes));
+      const u32 r = wave_rank<5>(min(zc, u32(kCells)), valid, ro.wc[u / HR][w]);
       if (valid) {
-        r = atomicAdd(&wcnt[par][w][z], 1u);
 #pragma unroll
         for (int c = 0; c < D; ++c) {
           const u32 k = orderable(v[u][c]);
@@ -488,49 +658,55 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
           mx[c] = max(mx[c], k);
         }
       }
-      code[u] = r | (z << 12) | (T << 20);
+      code[u] = zc | (r << 8);
     }
     __syncthreads();
-    if (tid <= kCells) {
-      u32 tot = 0;
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
-        zoff[par][ww][tid] = tot;
-        tot += wcnt[par][ww][tid];
-      }
+    reorder_scan(ro, [&](int z, u32 tot) -> u32 {
       u32 base = 0;
       if (a.diag == 2) {  // timing diagnostic: an in-range offset instead of the reservation
-        const u32 cap = tid < kCells ? a.cell_n[tid] : u32(a.n);
+        const u32 cap = z < kCells ? a.cell_n[z] : u32(a.n);
         base = cap > u32(TILE) ? u32((u64(tile) * 977u) % u64(cap - u32(TILE))) : 0u;
       } else {
-        base = tot ? atomicAdd(&a.st->cursor[tid], tot) : 0u;
+        base = tot ? atomicAdd(&a.st->cursor[z], tot) : 0u;
       }
-      if (tid < kCells && base + tot > a.cell_n[tid]) report(a.err, 0x2001u, u32(tid), base + tot);
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
-        zoff[par][ww][tid] += base;
-        wcnt[par ^ 1][ww][tid] = 0u;  // the next tile's counters (last read two barriers ago)
-      }
-    }
+      if (z < kCells && base + tot > a.cell_n[z]) report(a.err, 0x2001u, u32(z), base + tot);
+      return base;
+    });
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const u32 z = (code[u] >> 12) & 31u;
-      if (z == 31u) continue;
-      const u32 pos = zoff[par][w][z] + (code[u] & 0xfffu);
-      if (z < u32(kCells)) {
-        if (pos < a.cell_n[z]) {
-          const i64 q = a.cell_lo[z] + pos;
+    for (int h = 0; h < NH; ++h) {
 #pragma unroll
-          for (int c = 0; c < D; ++c) a.cols[i64(c) * a.ncol + q] = v[u][c];
-          a.cols[i64(D) * a.ncol + q] = __uint_as_float(id[u]);
-        }
-      } else {
+      for (int uu = 0; uu < HR; ++uu) {
+        const int u = h * HR + uu;
+        const u32 zc = code[u] & 255u;
+        if (zc == 31u) continue;
+        const u32 z = min(zc, u32(kCells));
+        const u32 p = ro.hoff[h][z] + ro.wc[h][w][z] + (code[u] >> 8);
 #pragma unroll
-        for (int c = 0; c < D; ++c) a.stage[i64(c) * a.ncol + pos] = v[u][c];
-        a.stage[i64(D) * a.ncol + pos] = __uint_as_float(id[u]);
-        a.tags[pos] = code[u] >> 20;
+        for (int c = 0; c < D; ++c) buf[c][p] = v[u][c];
+        buf[D][p] = __uint_as_float(id[u]);
+        bz[p] = (unsigned char)zc;
       }
+      if (ln < NZ) ro.wc[h][w][ln] = 0u;  // this wave's counters for the next tile
+      __syncthreads();
+      const u32 tot = ro.hcnt[h];
+      for (u32 i = tid; i < tot; i += kBlock) {
+        const u32 zc = bz[i];
+        const u32 z = min(zc, u32(kCells));
+        const u32 q = ro.gbase[h][z] + (i - ro.hoff[h][z]);
+        if (z < u32(kCells)) {
+          if (q < a.cell_n[z]) {
+            const i64 d = a.cell_lo[z] + q;
+#pragma unroll
+            for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + d] = buf[c][i];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c <= D; ++c) a.stage[i64(c) * a.ncol + q] = buf[c][i];
+          a.tags[q] = zc - u32(kCells);
+        }
+      }
+      if (h + 1 < NH) __syncthreads();
     }
   }
 #pragma unroll
@@ -558,30 +734,21 @@ struct ResArgs {
   int j;
   int ax[kLevels];
   State* st;
-  u32* fine;    // resolution histograms [kNodes][kFine]
-  u32* coarse;  // [kNodes][kCoarse]
+  u32* fine;    // resolution histograms [kLevels][kResBins]
   u64* small;   // [8][kSmallCap]
   u32* err;
 };
 
-__device__ __forceinline__ u64 comp_of(const ResArgs& a, int axis, i64 i) {
-  const u32 k = orderable(a.stage[i64(axis) * a.ncol + i]);
-  const u32 id = __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-  return (u64(k) << 32) | id;
-}
-
-__global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
-  __shared__ u32 lc[8][3];
-  __shared__ u32 lco[8 * kCoarse];
-  __shared__ u32 lorig[16];
+__global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
+  __shared__ u32 h[kResBins];
+  __shared__ u32 cnt[8 * 3 + 16];  // [x][left / band / right], then the scatter's tags (j = 0)
   __shared__ u32 sa[8], sb[8];
   __shared__ dev::BucketParams sbp[8];
   __shared__ u64 spv[4];
-  const int j = a.j, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1;
+  const int j = a.j, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1, F = res_bins(j);
   const int tid = threadIdx.x;
-  for (int i = tid; i < nodes * kCoarse; i += kBlock) lco[i] = 0;
-  if (tid < 24) (&lc[0][0])[tid] = 0;
-  if (tid < 16) lorig[tid] = 0;
+  for (int i = tid; i < kResBins; i += kHistThreads) h[i] = 0u;
+  if (tid < 8 * 3 + 16) cnt[tid] = 0u;
   if (tid < nodes) {
     sa[tid] = a.st->a[first + tid];
     sb[tid] = a.st->b[first + tid];
@@ -590,54 +757,65 @@ __global__ __launch_bounds__(kBlock) void k_res_classify(ResArgs a) {
   if (j > 0 && tid < nodes / 2) spv[tid] = a.st->pivot[firstp + tid];
   __syncthreads();
   const i64 staged = a.st->cursor[kCells];
+  const i64 per = ((staged + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;
+  const i64 i0 = i64(blockIdx.x) * per, i1 = min(staged, i0 + per);
   const int axj = a.ax[j], axp = j > 0 ? a.ax[j - 1] : 0;
-  const i64 stride = i64(gridDim.x) * kBlock;
-  for (i64 i = i64(blockIdx.x) * kBlock + tid; i < staged; i += stride) {
-    u32 T = a.tags[i];
-    if (T & kMed) continue;
-    if (j == 0) atomicAdd(&lorig[T & 15u], 1u);
-    int lvl = heap_level(T);
-    if (j > 0 && lvl == j - 1) {
-      const u64 comp = comp_of(a, axp, i);
+  for (i64 ib = i0; ib < i1; ib += kHistThreads) {  // uniform trip count: the counts are wave ops
+    const i64 i = ib + tid;
+    u32 T = i < i1 ? a.tags[i] : kMed;
+    bool live = !(T & kMed);
+    const u32 orig = T;
+    const bool live0 = live;
+    int lvl = live ? heap_level(T) : -1;
+    if (j > 0 && live && lvl == j - 1) {
+      const u32 k = orderable(a.stage[i64(axp) * a.ncol + i]);
+      const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
       const u64 P = spv[T - u32(firstp)];
       T = comp < P ? 2 * T + 1 : (comp > P ? 2 * T + 2 : (kMed | T));
       a.tags[i] = T;
       if (T & kMed) {
         a.st->med_idx1[T & 0xffu] = u32(i) + 1u;
-        continue;
+        live = false;
       }
       lvl = j;
     }
-    if (lvl != j) continue;
-    const u32 x = T - u32(first);
-    const float kf = a.stage[i64(axj) * a.ncol + i];
-    const u32 k = orderable(kf);
-    const int cls = k < sa[x] ? 0 : (k > sb[x] ? 2 : 1);
-    atomicAdd(&lc[x][cls], 1u);
-    if (cls == 1) {
-      const u32 d = dev::bucket_of(kf, sbp[x], kFine);
-      atomicAdd(&a.fine[size_t(T) * kFine + d], 1u);
-      atomicAdd(&lco[x * kCoarse + (d >> 8)], 1u);
+    const bool at = live && lvl == j;
+    u32 idx = 0;
+    if (at) {
+      const u32 x = T - u32(first);
+      const float kf = a.stage[i64(axj) * a.ncol + i];
+      const u32 k = orderable(kf);
+      const u32 cls = k < sa[x] ? 0u : (k > sb[x] ? 2u : 1u);
+      idx = 3 * x + cls;
+      if (cls == 1u) atomicAdd(&h[int(x) * F + int(dev::bucket_of(kf, sbp[x], F))], 1u);
     }
+    wave_count(cnt, idx, at);
+    if (j == 0) wave_count(cnt + 24, orig & 15u, live0);
   }
   __syncthreads();
-  for (int i = tid; i < nodes * kCoarse; i += kBlock) {
-    const u32 v = lco[i];
-    if (v) atomicAdd(&a.coarse[size_t(first) * kCoarse + i], v);
+  u32* out = a.fine + size_t(j) * kResBins;
+  for (int i = tid; i < kResBins; i += kHistThreads) {
+    const u32 v = h[i];
+    if (v) atomicAdd(&out[i], v);
   }
   if (tid < nodes * 3) {
-    const u32 v = (&lc[0][0])[tid];
+    const u32 v = cnt[tid];
     if (v) atomicAdd(&a.st->late[first + tid / 3][tid % 3], v);
   }
-  if (j == 0 && tid < kNodes && lorig[tid]) atomicAdd(&a.st->staged_orig[tid], lorig[tid]);
+  if (j == 0 && tid < kNodes && cnt[24 + tid]) atomicAdd(&a.st->staged_orig[tid], cnt[24 + tid]);
 }
 
-// One wave per node of level j: the median's rank inside the band from the exact counts
+// One workgroup per node of level j: the median's rank inside the band from the exact counts
 // (rows certain left / right from the scatter, staged rows classified by k_res_classify),
-// then the fine bin holding it.
-__global__ __launch_bounds__(64) void k_res_sel1(ResArgs a, Geom g) {
-  const int j = a.j, first = (1 << j) - 1;
+// then the bin holding it.
+__global__ __launch_bounds__(kBlock) void k_res_sel1(ResArgs a, Geom g) {
+  __shared__ __align__(16) u32 co[256];
+  const int j = a.j, first = (1 << j) - 1, F = res_bins(j), gs = F / 256;
   const int X = first + blockIdx.x;
+  const u32* fi = a.fine + size_t(j) * kResBins + size_t(blockIdx.x) * F;
+  coarse_of(fi, gs, co);
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
   State* st = a.st;
   const int ln = dev::lane();
   u32 cl = 0, cr = 0;
@@ -646,9 +824,9 @@ __global__ __launch_bounds__(64) void k_res_sel1(ResArgs a, Geom g) {
     if (ly > j) {
       const int anc = ((Y + 1) >> (ly - j - 1)) - 1;  // Y's ancestor at level j + 1
       if (anc == 2 * X + 1 || anc == 2 * X + 2) {
-        const u32 cnt = Y >= kNodes ? st->cursor[Y - kNodes] : st->staged_orig[Y];
-        if (anc == 2 * X + 1) cl = cnt;
-        else cr = cnt;
+        const u32 c = Y >= kNodes ? st->cursor[Y - kNodes] : st->staged_orig[Y];
+        if (anc == 2 * X + 1) cl = c;
+        else cr = c;
       }
     }
   }
@@ -665,23 +843,23 @@ __global__ __launch_bounds__(64) void k_res_sel1(ResArgs a, Geom g) {
     return;
   }
   u32 below = 0, tot = 0;
-  const u32 bin = wave_find_fine(a.coarse + size_t(X) * kCoarse, a.fine + size_t(X) * kFine, u32(t), &below, &tot);
+  const u32 bin = wave_find_fine(co, fi, gs, u32(t), &below, &tot);
   if (ln == 0) {
-    if (bin >= u32(kFine) || tot != u32(B)) {
+    if (bin >= u32(F) || tot != u32(B)) {
       report(a.err, 0x2004u, u32(X), tot);
       st->sel[X] = 0xffffffffu;
       return;
     }
     st->sel[X] = bin;
     st->sel_rank[X] = u32(t) - below;
-    st->sel_cnt[X] = a.fine[size_t(X) * kFine + bin];
+    st->sel_cnt[X] = fi[bin];
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
   __shared__ u32 sa[8], sb[8], ssel[8];
   __shared__ dev::BucketParams sbp[8];
-  const int j = a.j, nodes = 1 << j, first = nodes - 1;
+  const int j = a.j, nodes = 1 << j, first = nodes - 1, F = res_bins(j);
   const int tid = threadIdx.x;
   if (tid < nodes) {
     sa[tid] = a.st->a[first + tid];
@@ -693,17 +871,38 @@ __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
   const i64 staged = a.st->cursor[kCells];
   const int axj = a.ax[j];
   const i64 stride = i64(gridDim.x) * kBlock;
-  for (i64 i = i64(blockIdx.x) * kBlock + tid; i < staged; i += stride) {
-    const u32 T = a.tags[i];
-    if ((T & kMed) || heap_level(T) != j) continue;
-    const u32 x = T - u32(first);
-    const float kf = a.stage[i64(axj) * a.ncol + i];
-    const u32 k = orderable(kf);
-    if (k < sa[x] || k > sb[x]) continue;
-    if (dev::bucket_of(kf, sbp[x], kFine) != ssel[x]) continue;
-    const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-    const u32 p = atomicAdd(&a.st->small_cnt[T], 1u);
-    if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
+  for (i64 ib = i64(blockIdx.x) * kBlock; ib < staged; ib += stride) {  // uniform per wave
+    const i64 i = ib + tid;
+    bool want = false;
+    u32 x = 0;
+    u64 comp = 0;
+    if (i < staged) {
+      const u32 T = a.tags[i];
+      if (!(T & kMed) && heap_level(T) == j) {
+        x = T - u32(first);
+        const float kf = a.stage[i64(axj) * a.ncol + i];
+        const u32 k = orderable(kf);
+        if (k >= sa[x] && k <= sb[x] && dev::bucket_of(kf, sbp[x], F) == ssel[x]) {
+          want = true;
+          comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+        }
+      }
+    }
+    // one reservation per (wave, node)
+    u64 act = __ballot(want);
+    while (act) {
+      const int leader = __ffsll((long long)act) - 1;
+      const u32 key = u32(__shfl(int(x), leader, 64));
+      const u64 m = __ballot(want && x == key);
+      u32 base = 0;
+      if (dev::lane() == leader) base = atomicAdd(&a.st->small_cnt[first + key], u32(__popcll(m)));
+      base = u32(__shfl(int(base), leader, 64));
+      if (want && x == key) {
+        const u32 p = base + dev::mbcnt(m);
+        if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
+      }
+      act &= ~m;
+    }
   }
 }
 
@@ -766,7 +965,7 @@ __device__ u64 block_select(Each each, u32 rank) {
 
 __global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
   __shared__ u64 buf[kSmallCap];
-  const int j = a.j, first = (1 << j) - 1;
+  const int j = a.j, first = (1 << j) - 1, F = res_bins(j);
   const int X = first + blockIdx.x, x = blockIdx.x;
   State* st = a.st;
   const u32 sel = st->sel[X];
@@ -799,7 +998,7 @@ __global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
             const float kf = a.stage[i64(axj) * a.ncol + i];
             const u32 k = orderable(kf);
             if (k < A || k > B) continue;
-            if (dev::bucket_of(kf, bp, kFine) != sel) continue;
+            if (dev::bucket_of(kf, bp, F) != sel) continue;
             f((u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]));
           }
         },
@@ -821,74 +1020,86 @@ struct InsArgs {
   u32 cell_n[kCells];
 };
 
+// Staged rows routed by the level-3 pivots into the free tails of their level-4 segments
+// (after the scatter's certain rows), reordered through LDS per tile like the scatter.
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
-  constexpr int R = kInsChunk / kBlock;
-  __shared__ u32 wcnt[4][kCells], zoff[4][kCells], cert[kCells];
+  constexpr int R = D <= 4 ? 16 : 8, NH = 2, HR = R / NH, HALF = kBlock * HR, NZ = kCells;
+  constexpr int TILE = kBlock * R;
+  __shared__ Reorder<NZ, NH> ro;
+  __shared__ float buf[D + 1][HALF];
+  __shared__ unsigned char bz[HALF];
+  __shared__ u32 cert[kCells];
   __shared__ u64 spv[8];
-  const int tid = threadIdx.x, w = tid >> 6;
+  const int tid = threadIdx.x, w = tid >> 6, ln = tid & 63;
   if (tid < 8) spv[tid] = a.st->pivot[7 + tid];
   if (tid < kCells) cert[tid] = a.st->cursor[tid];
-  if (tid < 4 * kCells) (&wcnt[0][0])[tid] = 0u;
+  if (tid < NH * 4 * NZ) (&ro.wc[0][0][0])[tid] = 0u;
   __syncthreads();
   const i64 staged = a.st->cursor[kCells];
-  const i64 chunks = (staged + kInsChunk - 1) / kInsChunk;
-  for (i64 ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
-    const i64 c0 = ch * kInsChunk;
+  const i64 tiles = (staged + TILE - 1) / TILE;
+  for (i64 tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const i64 t0 = tile * TILE;
+    float v[R][D + 1];
     u32 code[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      const i64 i = c0 + i64(u) * kBlock + tid;
-      u32 z = 31u, r = 0;
-      if (i < staged) {
-        const u32 T = a.tags[i];
-        if (!(T & kMed)) {
-          if (heap_level(T) != kLevels - 1) {
-            report(a.err, 0x2006u, T, u32(i));
-          } else {
-            const u64 comp = (u64(orderable(a.stage[i64(a.ax3) * a.ncol + i])) << 32) |
-                             __float_as_uint(a.stage[i64(D) * a.ncol + i]);
-            const u64 P = spv[T - 7u];
-            if (comp == P) {
-              a.st->med_idx1[T] = u32(i) + 1u;
-            } else {
-              z = (comp < P ? 2 * T + 1 : 2 * T + 2) - u32(kNodes);
-              r = atomicAdd(&wcnt[w][z], 1u);
-            }
-          }
+      const i64 i = t0 + i64(u) * kBlock + tid;
+      const i64 ic = i < staged ? i : 0;
+#pragma unroll
+      for (int c = 0; c <= D; ++c) v[u][c] = a.stage[i64(c) * a.ncol + ic];
+      const u32 T = i < staged ? a.tags[i] : kMed;
+      u32 z = 31u;
+      if (!(T & kMed)) {
+        if (heap_level(T) != kLevels - 1) {
+          report(a.err, 0x2006u, T, u32(i));
+        } else {
+          float kv = v[u][0];
+#pragma unroll
+          for (int c = 1; c < D; ++c) kv = c == a.ax3 ? v[u][c] : kv;  // no dynamic register index
+          const u64 comp = (u64(orderable(kv)) << 32) | __float_as_uint(v[u][D]);
+          const u64 P = spv[T - 7u];
+          if (comp == P) a.st->med_idx1[T] = u32(i) + 1u;
+          else z = (comp < P ? 2 * T + 1 : 2 * T + 2) - u32(kNodes);
         }
       }
-      code[u] = r | (z << 16);
+      const bool valid = z != 31u;
+      const u32 r = wave_rank<4>(z & 15u, valid, ro.wc[u / HR][w]);
+      code[u] = z | (r << 8);
     }
     __syncthreads();
-    if (tid < kCells) {
-      u32 tot = 0;
+    reorder_scan(ro, [&](int z, u32 tot) -> u32 {
+      const u32 base = (tot ? atomicAdd(&a.st->ins[z], tot) : 0u) + cert[z];
+      if (base + tot > a.cell_n[z]) report(a.err, 0x2007u, u32(z), base + tot);
+      return base;
+    });
+    __syncthreads();
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
-        zoff[ww][tid] = tot;
-        tot += wcnt[ww][tid];
-        wcnt[ww][tid] = 0u;
+    for (int h = 0; h < NH; ++h) {
+#pragma unroll
+      for (int uu = 0; uu < HR; ++uu) {
+        const int u = h * HR + uu;
+        const u32 z = code[u] & 255u;
+        if (z == 31u) continue;
+        const u32 p = ro.hoff[h][z] + ro.wc[h][w][z] + (code[u] >> 8);
+#pragma unroll
+        for (int c = 0; c <= D; ++c) buf[c][p] = v[u][c];
+        bz[p] = (unsigned char)z;
       }
-      const u32 base = tot ? atomicAdd(&a.st->ins[tid], tot) : 0u;
+      if (ln < NZ) ro.wc[h][w][ln] = 0u;
+      __syncthreads();
+      const u32 tot = ro.hcnt[h];
+      for (u32 i = tid; i < tot; i += kBlock) {
+        const u32 z = bz[i];
+        const u32 q = ro.gbase[h][z] + (i - ro.hoff[h][z]);
+        if (q < a.cell_n[z]) {
+          const i64 d = a.cell_lo[z] + q;
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) zoff[ww][tid] += base + cert[tid];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const u32 z = code[u] >> 16;
-      if (z == 31u) continue;
-      const i64 i = c0 + i64(u) * kBlock + tid;
-      const u32 pos = zoff[w][z] + (code[u] & 0xffffu);
-      if (pos >= a.cell_n[z]) {
-        report(a.err, 0x2007u, z, pos);
-        continue;
+          for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + d] = buf[c][i];
+        }
       }
-      const i64 q = a.cell_lo[z] + pos;
-#pragma unroll
-      for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + q] = a.stage[i64(c) * a.ncol + i];
+      if (h + 1 < NH) __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -975,6 +1186,12 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
   }
 }
 
+template <int D, bool VEC>
+void launch_scatter(int blocks, const ScatArgs& sc, hipStream_t stream) {
+  constexpr int R = D <= 4 ? 16 : 8;
+  k_scatter<D, R, VEC><<<blocks, kBlock, 0, stream>>>(sc);
+}
+
 }  // namespace
 
 size_t workspace_bytes() { return layout().total; }
@@ -984,17 +1201,16 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   char* ws = static_cast<char*>(io.ws);
   State* st = reinterpret_cast<State*>(ws + L.state);
   u32* fine_s = reinterpret_cast<u32*>(ws + L.fine_s);
-  u32* coarse_s = reinterpret_cast<u32*>(ws + L.coarse_s);
   u32* fine_r = reinterpret_cast<u32*>(ws + L.fine_r);
-  u32* coarse_r = reinterpret_cast<u32*>(ws + L.coarse_r);
   u32* skey = reinterpret_cast<u32*>(ws + L.skey);
+  u32* gpart = reinterpret_cast<u32*>(ws + L.gpart);
   u64* small = reinterpret_cast<u64*>(ws + L.small);
   u32* part = reinterpret_cast<u32*>(ws + L.part);
   const int D = g.dim;
   if (D < 2 || D > 8) throw std::invalid_argument("top4: dim 2..8");
   const i64 n = io.n;
-  int sl = std::min(kMaxSampleLog2, std::max(8, t.sample_log2));
-  while (sl > 8 && (i64(1) << sl) > n / 4) --sl;
+  int sl = std::min(kMaxSampleLog2, std::max(10, t.sample_log2));
+  while (sl > 10 && (i64(1) << sl) > n / 4) --sl;
   const int S = 1 << sl;
 
   const i64 zwords = i64(L.zero_end - L.state) / 4;
@@ -1002,15 +1218,17 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
       reinterpret_cast<u32*>(ws + L.state), zwords);
   PKD_LAUNCH_CHECK();
 
-  SampArgs sa{io.pts, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, st};
-  const int sgrid = std::max(1, std::min(256, S / kBlock));
-  k_samp_gather<<<sgrid, kBlock, 0, stream>>>(sa);
+  const int gblocks = (S + kBlock * kGatherRows - 1) / (kBlock * kGatherRows);
+  SampArgs sa{io.pts, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, gpart};
+  k_samp_gather<<<gblocks, kBlock, 0, stream>>>(sa);
   PKD_LAUNCH_CHECK();
+  const int hblocks = std::max(1, std::min(kSampBlocks, S / (kHistThreads * 4)));
   for (int j = 0; j < kLevels; ++j) {
-    SampLevelArgs la{skey, S, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3], g.axis[4]}, st, fine_s, coarse_s, t.z};
-    k_samp_hist<<<sgrid, kBlock, 0, stream>>>(la);
+    SampLevelArgs la{skey, gpart, gblocks, S, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3], g.axis[4]},
+                     st, fine_s, t.z};
+    k_samp_hist<<<hblocks, kHistThreads, 0, stream>>>(la);
     PKD_LAUNCH_CHECK();
-    k_samp_sel<<<1 << j, 64, 0, stream>>>(la);
+    k_samp_sel<<<1 << j, kBlock, 0, stream>>>(la);
     PKD_LAUNCH_CHECK();
   }
 
@@ -1039,28 +1257,29 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   const bool vec = D == 3 && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
                    (io.ids == nullptr || reinterpret_cast<uintptr_t>(io.ids) % 16 == 0);
   switch (D) {
-    case 2: k_scatter<2, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 2: launch_scatter<2, false>(sblocks, sc, stream); break;
     case 3:
-      if (vec) k_scatter<3, true><<<sblocks, kBlock, 0, stream>>>(sc);
-      else k_scatter<3, false><<<sblocks, kBlock, 0, stream>>>(sc);
+      if (vec) launch_scatter<3, true>(sblocks, sc, stream);
+      else launch_scatter<3, false>(sblocks, sc, stream);
       break;
-    case 4: k_scatter<4, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
-    case 5: k_scatter<5, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
-    case 6: k_scatter<6, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
-    case 7: k_scatter<7, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
-    default: k_scatter<8, false><<<sblocks, kBlock, 0, stream>>>(sc); break;
+    case 4: launch_scatter<4, false>(sblocks, sc, stream); break;
+    case 5: launch_scatter<5, false>(sblocks, sc, stream); break;
+    case 6: launch_scatter<6, false>(sblocks, sc, stream); break;
+    case 7: launch_scatter<7, false>(sblocks, sc, stream); break;
+    default: launch_scatter<8, false>(sblocks, sc, stream); break;
   }
   PKD_LAUNCH_CHECK();
   if (t.diag) return;  // timing diagnostic: the rest is not run
 
   // staged rows are a few percent of n: grids sized for ~16 % of the rows, grid-stride beyond
   const int rgrid = int(std::max<i64>(64, std::min<i64>(2048, (n / 6 + kBlock * 4 - 1) / (kBlock * 4))));
+  const int cgrid = int(std::max<i64>(1, std::min<i64>(kResBlocks, (n / 6 + kHistThreads * 16 - 1) / (kHistThreads * 16))));
   for (int j = 0; j < kLevels; ++j) {
-    ResArgs ra{io.stage, io.out_ids, io.ncol, D, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, st, fine_r,
-               coarse_r, small, io.err};
-    k_res_classify<<<rgrid, kBlock, 0, stream>>>(ra);
+    ResArgs ra{io.stage, io.out_ids, io.ncol, D, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, st, fine_r, small,
+               io.err};
+    k_res_classify<<<cgrid, kHistThreads, 0, stream>>>(ra);
     PKD_LAUNCH_CHECK();
-    k_res_sel1<<<1 << j, 64, 0, stream>>>(ra, g);
+    k_res_sel1<<<1 << j, kBlock, 0, stream>>>(ra, g);
     PKD_LAUNCH_CHECK();
     k_res_collect<<<rgrid, kBlock, 0, stream>>>(ra);
     PKD_LAUNCH_CHECK();
@@ -1080,7 +1299,8 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
     ia.cell_lo[c] = g.lo[kNodes + c];
     ia.cell_n[c] = u32(g.n[kNodes + c]);
   }
-  const int igrid = int(std::max<i64>(16, std::min<i64>(1024, (n / 6 + kInsChunk - 1) / kInsChunk)));
+  const i64 itile = i64(kBlock) * R;
+  const int igrid = int(std::max<i64>(16, std::min<i64>(1024, (n / 8 + itile - 1) / itile)));
   switch (D) {
     case 2: k_res_insert<2><<<igrid, kBlock, 0, stream>>>(ia); break;
     case 3: k_res_insert<3><<<igrid, kBlock, 0, stream>>>(ia); break;
@@ -1104,7 +1324,7 @@ void band_report(const void* ws, hipStream_t stream, u32 (*out)[3]) {
   PKD_HIP_CHECK(hipStreamSynchronize(stream));
   for (int X = 0; X < kNodes; ++X) {
     out[X][0] = h.late[X][1];
-    out[X][1] = h.sel_rank[X];  // rank inside the median's fine bin (see sel for the bin)
+    out[X][1] = h.sel_rank[X];  // rank inside the median's bin (see sel for the bin)
     out[X][2] = h.staged_orig[X];
   }
 }

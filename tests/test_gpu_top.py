@@ -2,6 +2,8 @@
 pass + exact fix-up must give the SAME tree as the CPU exact builder, slot for slot, for any
 input: sizes, dims 2..8, depth0, explicit ids, heavy duplicates, sorted input. A band that
 misses its median is reported (error bit 0x20) and KDTree.build rebuilds without sampling."""
+import importlib
+
 import pytest
 import torch
 
@@ -100,7 +102,7 @@ def test_top_band_miss_detected_and_rebuilt(gpu_device, top_always, monkeypatch)
     b.build(x.to(gpu_device))
     torch.cuda.synchronize()
     assert b.read_error() & 0x20
-    ops._builders.clear()
+    importlib.import_module("parallel_kd_tree_amd.ops.build")._builders.clear()
     t = pk.KDTree.build(x.to(gpu_device))
     t.check()
     cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
