@@ -541,7 +541,7 @@ struct ScatArgs {
   i64 cell_lo[kCells];
   u32 cell_n[kCells];
   int ax[kLevels];
-  int diag;  // 2: no reservation atomics (timing diagnostic, output garbage)
+  int diag;  // timing diagnostics (output garbage): 2 no reservation atomics, 3 no stores
 };
 
 // Rows of one scatter tile held by a thread: v[u][c], id[u]; VEC (dim 3, 16-B aligned input):
@@ -600,19 +600,23 @@ __device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R
 }
 
 // Zone code of a scatter row: 0..15 its level-4 segment, 16 + T staged at node T, 31 none.
-template <int D, int R, bool VEC>
+// (Loading the next tile while this one is reordered and stored measured no faster: the
+// registers it takes cost more occupancy than the overlap gains.)
+template <int D, int R, int NH, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
-  constexpr int NH = 2, HR = R / NH, HALF = kBlock * HR, NZ = kCells + 1;
+  constexpr int HR = R / NH, HALF = kBlock * HR, NZ = kCells + 1;
   constexpr int TILE = kBlock * R;
-  __shared__ u32 sa[16], sb[16];
+  __shared__ uint2 sab[16];           // band [a, b] of heap node X
+  __shared__ u32 zlo[NZ], zcap[NZ];   // first row and capacity of each zone's destination
   __shared__ Reorder<NZ, NH> ro;
   __shared__ float buf[D + 1][HALF];
   __shared__ unsigned char bz[HALF];
   __shared__ u32 red[kBlock / 64][2 * D];
   const int tid = threadIdx.x, w = tid >> 6, ln = tid & 63;
-  if (tid < kNodes) {
-    sa[tid] = a.st->a[tid];
-    sb[tid] = a.st->b[tid];
+  if (tid < kNodes) sab[tid] = make_uint2(a.st->a[tid], a.st->b[tid]);
+  if (tid < NZ) {
+    zlo[tid] = tid < kCells ? u32(a.cell_lo[tid]) : 0u;
+    zcap[tid] = tid < kCells ? a.cell_n[tid] : 0xffffffffu;
   }
   if (tid < NH * 4 * NZ) (&ro.wc[0][0][0])[tid] = 0u;
   u32 mn[D], mx[D];
@@ -623,39 +627,36 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
   }
   __syncthreads();
   for (i64 tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
-    const i64 t0 = tile * TILE;
     float v[R][D];
     u32 id[R];
-    const u32 vmask = load_tile<D, R, VEC>(a, t0, v, id);
+    const u32 vmask = load_tile<D, R, VEC>(a, tile * TILE, v, id);
     u32 code[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const bool valid = (vmask >> u) & 1u;
+      u32 ok[D];
+#pragma unroll
+      for (int c = 0; c < D; ++c) ok[c] = orderable(v[u][c]);
       u32 X = 0, T = 0;
       bool staged = false;
 #pragma unroll
       for (int j = 0; j < kLevels; ++j) {
-        float kv = v[u][0];
+        u32 k = ok[0];
 #pragma unroll
-        for (int c = 1; c < D; ++c) kv = c == a.ax[j] ? v[u][c] : kv;
-        const u32 k = orderable(kv);
-        if (!staged) {
-          if (k < sa[X]) X = 2 * X + 1;
-          else if (k > sb[X]) X = 2 * X + 2;
-          else {
-            staged = true;
-            T = X;
-          }
-        }
+        for (int c = 1; c < D; ++c) k = c == a.ax[j] ? ok[c] : k;
+        const uint2 ab = sab[X];
+        const bool lt = k < ab.x, gt = k > ab.y, in = !lt && !gt;
+        T = (!staged && in) ? X : T;
+        X = (staged || in) ? X : 2 * X + 1 + (gt ? 1u : 0u);
+        staged = staged || in;
       }
       const u32 zc = !valid ? 31u : (staged ? u32(kCells) + T : X - u32(kNodes));
       const u32 r = wave_rank<5>(min(zc, u32(kCells)), valid, ro.wc[u / HR][w]);
       if (valid) {
 #pragma unroll
         for (int c = 0; c < D; ++c) {
-          const u32 k = orderable(v[u][c]);
-          mn[c] = min(mn[c], k);
-          mx[c] = max(mx[c], k);
+          mn[c] = min(mn[c], ok[c]);
+          mx[c] = max(mx[c], ok[c]);
         }
       }
       code[u] = zc | (r << 8);
@@ -689,21 +690,16 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
       }
       if (ln < NZ) ro.wc[h][w][ln] = 0u;  // this wave's counters for the next tile
       __syncthreads();
-      const u32 tot = ro.hcnt[h];
+      const u32 tot = a.diag == 3 ? 0u : ro.hcnt[h];  // diag 3: no global stores
       for (u32 i = tid; i < tot; i += kBlock) {
         const u32 zc = bz[i];
         const u32 z = min(zc, u32(kCells));
         const u32 q = ro.gbase[h][z] + (i - ro.hoff[h][z]);
-        if (z < u32(kCells)) {
-          if (q < a.cell_n[z]) {
-            const i64 d = a.cell_lo[z] + q;
+        if (q < zcap[z]) {
+          float* dst = (z < u32(kCells) ? a.cols : a.stage) + (zlo[z] + q);
 #pragma unroll
-            for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + d] = buf[c][i];
-          }
-        } else {
-#pragma unroll
-          for (int c = 0; c <= D; ++c) a.stage[i64(c) * a.ncol + q] = buf[c][i];
-          a.tags[q] = zc - u32(kCells);
+          for (int c = 0; c <= D; ++c) dst[i64(c) * a.ncol] = buf[c][i];
+          if (z == u32(kCells)) a.tags[q] = zc - u32(kCells);
         }
       }
       if (h + 1 < NH) __syncthreads();
@@ -760,37 +756,58 @@ __global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
   const i64 per = ((staged + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;
   const i64 i0 = i64(blockIdx.x) * per, i1 = min(staged, i0 + per);
   const int axj = a.ax[j], axp = j > 0 ? a.ax[j - 1] : 0;
-  for (i64 ib = i0; ib < i1; ib += kHistThreads) {  // uniform trip count: the counts are wave ops
-    const i64 i = ib + tid;
-    u32 T = i < i1 ? a.tags[i] : kMed;
-    bool live = !(T & kMed);
-    const u32 orig = T;
-    const bool live0 = live;
-    int lvl = live ? heap_level(T) : -1;
-    if (j > 0 && live && lvl == j - 1) {
-      const u32 k = orderable(a.stage[i64(axp) * a.ncol + i]);
-      const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-      const u64 P = spv[T - u32(firstp)];
-      T = comp < P ? 2 * T + 1 : (comp > P ? 2 * T + 2 : (kMed | T));
-      a.tags[i] = T;
-      if (T & kMed) {
-        a.st->med_idx1[T & 0xffu] = u32(i) + 1u;
-        live = false;
+  constexpr int U = 4;  // rows per thread per round: their loads are in flight together
+  for (i64 ib = i0; ib < i1; ib += U * kHistThreads) {  // uniform trip count: the counts are wave ops
+    u32 T[U];
+    float kp[U], kj[U];
+    u32 idp[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kHistThreads + tid;
+      T[u] = i < i1 ? a.tags[i] : kMed;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kHistThreads + tid;
+      const int lvl = (T[u] & kMed) ? -1 : heap_level(T[u]);
+      kp[u] = kj[u] = 0.0f;
+      idp[u] = 0;
+      if (j > 0 && lvl == j - 1) {
+        kp[u] = a.stage[i64(axp) * a.ncol + i];
+        idp[u] = __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
       }
-      lvl = j;
+      if (lvl == j || (j > 0 && lvl == j - 1)) kj[u] = a.stage[i64(axj) * a.ncol + i];
     }
-    const bool at = live && lvl == j;
-    u32 idx = 0;
-    if (at) {
-      const u32 x = T - u32(first);
-      const float kf = a.stage[i64(axj) * a.ncol + i];
-      const u32 k = orderable(kf);
-      const u32 cls = k < sa[x] ? 0u : (k > sb[x] ? 2u : 1u);
-      idx = 3 * x + cls;
-      if (cls == 1u) atomicAdd(&h[int(x) * F + int(dev::bucket_of(kf, sbp[x], F))], 1u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kHistThreads + tid;
+      u32 t = T[u];
+      bool live = !(t & kMed);
+      const bool live0 = live;
+      int lvl = live ? heap_level(t) : -1;
+      if (j > 0 && live && lvl == j - 1) {
+        const u64 comp = (u64(orderable(kp[u])) << 32) | idp[u];
+        const u64 P = spv[t - u32(firstp)];
+        t = comp < P ? 2 * t + 1 : (comp > P ? 2 * t + 2 : (kMed | t));
+        a.tags[i] = t;
+        if (t & kMed) {
+          a.st->med_idx1[t & 0xffu] = u32(i) + 1u;
+          live = false;
+        }
+        lvl = j;
+      }
+      const bool at = live && lvl == j;
+      u32 idx = 0;
+      if (at) {
+        const u32 x = t - u32(first);
+        const u32 k = orderable(kj[u]);
+        const u32 cls = k < sa[x] ? 0u : (k > sb[x] ? 2u : 1u);
+        idx = 3 * x + cls;
+        if (cls == 1u) atomicAdd(&h[int(x) * F + int(dev::bucket_of(kj[u], sbp[x], F))], 1u);
+      }
+      wave_count(cnt, idx, at);
+      if (j == 0) wave_count(cnt + 24, T[u] & 15u, live0);
     }
-    wave_count(cnt, idx, at);
-    if (j == 0) wave_count(cnt + 24, orig & 15u, live0);
   }
   __syncthreads();
   u32* out = a.fine + size_t(j) * kResBins;
@@ -871,37 +888,47 @@ __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
   const i64 staged = a.st->cursor[kCells];
   const int axj = a.ax[j];
   const i64 stride = i64(gridDim.x) * kBlock;
-  for (i64 ib = i64(blockIdx.x) * kBlock; ib < staged; ib += stride) {  // uniform per wave
-    const i64 i = ib + tid;
-    bool want = false;
-    u32 x = 0;
-    u64 comp = 0;
-    if (i < staged) {
-      const u32 T = a.tags[i];
-      if (!(T & kMed) && heap_level(T) == j) {
-        x = T - u32(first);
-        const float kf = a.stage[i64(axj) * a.ncol + i];
-        const u32 k = orderable(kf);
-        if (k >= sa[x] && k <= sb[x] && dev::bucket_of(kf, sbp[x], F) == ssel[x]) {
-          want = true;
-          comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
-        }
-      }
+  constexpr int U = 4;  // rows per thread per round: their loads are in flight together
+  for (i64 ib = i64(blockIdx.x) * (U * kBlock); ib < staged; ib += U * stride) {  // uniform per wave
+    u32 T[U];
+    float kf[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kBlock + tid;
+      T[u] = i < staged ? a.tags[i] : kMed;
     }
-    // one reservation per (wave, node)
-    u64 act = __ballot(want);
-    while (act) {
-      const int leader = __ffsll((long long)act) - 1;
-      const u32 key = u32(__shfl(int(x), leader, 64));
-      const u64 m = __ballot(want && x == key);
-      u32 base = 0;
-      if (dev::lane() == leader) base = atomicAdd(&a.st->small_cnt[first + key], u32(__popcll(m)));
-      base = u32(__shfl(int(base), leader, 64));
-      if (want && x == key) {
-        const u32 p = base + dev::mbcnt(m);
-        if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kBlock + tid;
+      kf[u] = (!(T[u] & kMed) && heap_level(T[u]) == j) ? a.stage[i64(axj) * a.ncol + i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = ib + u * kBlock + tid;
+      bool want = false;
+      u32 x = 0;
+      u32 k = 0;
+      if (!(T[u] & kMed) && heap_level(T[u]) == j) {
+        x = T[u] - u32(first);
+        k = orderable(kf[u]);
+        want = k >= sa[x] && k <= sb[x] && dev::bucket_of(kf[u], sbp[x], F) == ssel[x];
       }
-      act &= ~m;
+      // one reservation per (wave, node)
+      u64 act = __ballot(want);
+      while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const u32 key = u32(__shfl(int(x), leader, 64));
+        const u64 m = __ballot(want && x == key);
+        u32 base = 0;
+        if (dev::lane() == leader) base = atomicAdd(&a.st->small_cnt[first + key], u32(__popcll(m)));
+        base = u32(__shfl(int(base), leader, 64));
+        if (want && x == key) {
+          const u32 p = base + dev::mbcnt(m);
+          const u64 comp = (u64(k) << 32) | __float_as_uint(a.stage[i64(a.dim) * a.ncol + i]);
+          if (p < u32(kSmallCap)) a.small[size_t(x) * kSmallCap + p] = comp;
+        }
+        act &= ~m;
+      }
     }
   }
 }
@@ -1029,11 +1056,15 @@ __global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
   __shared__ Reorder<NZ, NH> ro;
   __shared__ float buf[D + 1][HALF];
   __shared__ unsigned char bz[HALF];
-  __shared__ u32 cert[kCells];
+  __shared__ u32 cert[kCells], zlo[kCells], zcap[kCells];
   __shared__ u64 spv[8];
   const int tid = threadIdx.x, w = tid >> 6, ln = tid & 63;
   if (tid < 8) spv[tid] = a.st->pivot[7 + tid];
-  if (tid < kCells) cert[tid] = a.st->cursor[tid];
+  if (tid < kCells) {
+    cert[tid] = a.st->cursor[tid];
+    zlo[tid] = u32(a.cell_lo[tid]);
+    zcap[tid] = a.cell_n[tid];
+  }
   if (tid < NH * 4 * NZ) (&ro.wc[0][0][0])[tid] = 0u;
   __syncthreads();
   const i64 staged = a.st->cursor[kCells];
@@ -1070,7 +1101,7 @@ __global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
     __syncthreads();
     reorder_scan(ro, [&](int z, u32 tot) -> u32 {
       const u32 base = (tot ? atomicAdd(&a.st->ins[z], tot) : 0u) + cert[z];
-      if (base + tot > a.cell_n[z]) report(a.err, 0x2007u, u32(z), base + tot);
+      if (base + tot > zcap[z]) report(a.err, 0x2007u, u32(z), base + tot);
       return base;
     });
     __syncthreads();
@@ -1092,10 +1123,10 @@ __global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
       for (u32 i = tid; i < tot; i += kBlock) {
         const u32 z = bz[i];
         const u32 q = ro.gbase[h][z] + (i - ro.hoff[h][z]);
-        if (q < a.cell_n[z]) {
-          const i64 d = a.cell_lo[z] + q;
+        if (q < zcap[z]) {
+          float* dst = a.cols + (zlo[z] + q);
 #pragma unroll
-          for (int c = 0; c <= D; ++c) a.cols[i64(c) * a.ncol + d] = buf[c][i];
+          for (int c = 0; c <= D; ++c) dst[i64(c) * a.ncol] = buf[c][i];
         }
       }
       if (h + 1 < NH) __syncthreads();
@@ -1189,7 +1220,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
 template <int D, bool VEC>
 void launch_scatter(int blocks, const ScatArgs& sc, hipStream_t stream) {
   constexpr int R = D <= 4 ? 16 : 8;
-  k_scatter<D, R, VEC><<<blocks, kBlock, 0, stream>>>(sc);
+  k_scatter<D, R, 2, VEC><<<blocks, kBlock, 0, stream>>>(sc);
 }
 
 }  // namespace

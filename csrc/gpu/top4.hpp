@@ -71,7 +71,8 @@ struct Tune {
   float z = 9.0f;        // band half-width in sample-rank standard deviations (PKD_TOP_Z)
   int scatter_blocks = 0;  // 0: by size
   // Diagnostics (PKD_TOP_DIAG; timing only, the tree is NOT built): 1 stop after the scatter,
-  // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets.
+  // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets, 3 also
+  // without the scatter's global stores.
   int diag = 0;
 };
 

@@ -43,7 +43,8 @@ def timed(env, reps=10):
 
 for bl in blocks:
     r = {"n": n, "blocks": bl}
-    for name, env in (("full", {}), ("to_scatter", {"PKD_TOP_DIAG": 1}), ("to_scatter_noatomic", {"PKD_TOP_DIAG": 2})):
+    for name, env in (("full", {}), ("to_scatter", {"PKD_TOP_DIAG": 1}), ("to_scatter_noatomic", {"PKD_TOP_DIAG": 2}),
+                      ("scatter_nostore", {"PKD_TOP_DIAG": 3})):
         env = dict(env, PKD_TOP_BLOCKS=bl)
         r[name] = round(timed(env), 3)
     print(json.dumps(r), flush=True)
