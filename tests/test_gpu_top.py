@@ -79,7 +79,7 @@ def test_top_off_below_threshold(gpu_device):
 
 
 def test_top_20m_equals_pairs(gpu_device, monkeypatch):
-    """At the default threshold (20 M points): the sampled tree equals the paired-levels tree."""
+    """Above the default threshold (20 M points): the sampled tree equals the paired-levels tree."""
     x = pk.generate_slice(3, 3, 0, 20_000_000, device=gpu_device)
     b = ops.GpuTreeBuilder(x.shape[0], 3, 0, 0)
     assert b.sampled_top
