@@ -1,6 +1,7 @@
 // Exact 1-NN kernels (see gpu_query.hpp).
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(kBlock) void k_brute(const float* __restrict__ pts,
 template <int QT, int CH>
 __global__ __launch_bounds__(kBlock) void k_brute_pf(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                      u32 id_base, i64 n, int dim, const float* __restrict__ queries,
-                                                     i64 nq, u64* __restrict__ out) {
+                                                     i64 nq, u64* __restrict__ out, const u32* __restrict__ gate) {
+  if (gate && *gate == 0u) return;  // the MFMA filter's fallback: runs only when it overflowed
   extern __shared__ __align__(16) float qs[];  // [QT][dim]
   const i64 q0 = i64(blockIdx.y) * QT;
   const int qt = int(std::min<i64>(QT, nq - q0));
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_brute_pf(const float* __restrict__ p
 
 template <int QT, int CH = 16>  // CH: coordinates per load round (CH / 4 float4 loads, two rounds in flight)
 void launch_brute_pf(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq,
-                     u64* out, hipStream_t stream) {
+                     u64* out, hipStream_t stream, const u32* gate = nullptr) {
   const i64 tiles = (nq + QT - 1) / QT;
   const void* fn = reinterpret_cast<const void*>(&k_brute_pf<QT, CH>);
   const size_t lds = size_t(QT) * dim * 4;
@@ -225,9 +227,318 @@ void launch_brute_pf(const float* pts, const u32* ids, u32 id_base, i64 n, int d
   for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
     const i64 ty = std::min<i64>(65535, tiles - t0);
     k_brute_pf<QT, CH><<<dim3(unsigned(gx), unsigned(ty), 1u), kBlock, lds, stream>>>(
-        pts, ids, id_base, n, dim, queries + t0 * QT * dim, nq - t0 * QT, out + t0 * QT);
+        pts, ids, id_base, n, dim, queries + t0 * QT * dim, nq - t0 * QT, out + t0 * QT, gate);
     PKD_LAUNCH_CHECK();
   }
+}
+
+// ---- MFMA candidate filter for batched high-dimensional brute force ----------------------
+// Exact 1-NN of a batch of queries against every point, with the distance arithmetic on the
+// matrix cores and the exact answer kept bit for bit:
+//   d2'(q, p) = |y|^2 + |x|^2 - 2 x.y on centred coordinates (x = p - c, y = q - c, c = the
+//   batch's mean query), the dot products from bf16 tiles (v_mfma_f32_32x32x16_bf16, fp32
+//   accumulation), the norms in fp32. E(q, p) bounds |d2' - d2_seq| where d2_seq is the exact
+//   sequential no-FMA sum the other kernels (and the reference) compute: bf16 rounding of both
+//   operands (2 u_b + u_b^2 per product, Cauchy-Schwarz over the dimension), fp32 accumulation
+//   and norm rounding, the centring, and d2_seq's own deviation from the real distance.
+//   pass 1  tau_q = min over a 1/kBoundSub sample of the points of d2' + E (an upper bound of
+//           the exact minimum);
+//   pass 2  every point with d2' - E <= tau_q is a candidate of q (the exact minimiser and every
+//           tie of it are: d2' - E <= d2_seq(p*) <= tau_q);
+//   pass 3  candidates rescored with the exact sequential sum, packed (d2, id), MIN into out.
+// More candidates than the list holds (heavy duplicates, equidistant points, huge norms) or a
+// non-finite bound set a flag, and the prefetching exact brute force reruns the batch (gated on
+// the device, no host round trip). Replaces the per-16-query passes of k_brute over the points
+// (verdict r3 #9; the reference's brute loop is kdtree_sequential.cpp:14-25).
+namespace mf {
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr int kQB = 128;        // queries per batch: 4 row tiles of 32
+constexpr int kTiles = kQB / 32;
+constexpr int kCap = 512;       // candidates per query
+constexpr int kBoundSub = 8;    // pass 1 visits every 8th slab of 32 points
+constexpr int kMaxDim = 256;
+
+struct Scratch {  // device, one batch
+  float center[kMaxDim];
+  float qn2[kQB];    // |y|^2 (sequential fp32)
+  float qnorm[kQB];  // |y|
+  u32 tau[8][kQB];   // float bits, atomicMin; one copy per blockIdx % 8 (spreads the atomics)
+  u32 cnt[kQB];
+  u32 overflow;
+  u32 pad[63];
+  u32 cand[kQB * kCap];
+  __bf16 qbf[kQB * (kMaxDim + 8)];  // centred queries, bf16, rows padded to dim + 8
+};
+
+// One workgroup per query of the batch: its row centred on the batch's first query, in bf16
+// (the MFMA image), its norm, and its list reset. (Any centre is exact; a nearby one keeps the
+// bound, which scales with |x| |y|, tight.)
+__global__ __launch_bounds__(kBlock) void k_mf_prep(const float* __restrict__ q, int nqb, int dim, Scratch* s) {
+  __shared__ float red[kBlock / 64];
+  const int k = blockIdx.x, QS = dim + 8;
+  float part = 0.0f;
+  for (int d = threadIdx.x; d < QS; d += kBlock) {
+    const float c = d < dim ? q[d] : 0.0f;
+    if (k == 0 && d < dim) s->center[d] = c;
+    const float v = (k < nqb && d < dim) ? q[size_t(k) * dim + d] - c : 0.0f;
+    s->qbf[size_t(k) * QS + d] = static_cast<__bf16>(v);
+    part += v * v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (dev::lane() == 0) red[threadIdx.x / 64] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.0f;  // any order: |y|^2 enters only the error bound
+    for (int w = 0; w < kBlock / 64; ++w) a += red[w];
+    s->qn2[k] = a;
+    s->qnorm[k] = sqrtf(a);
+    for (int c = 0; c < 8; ++c) s->tau[c][k] = 0x7f800000u;  // +inf
+    s->cnt[k] = 0u;
+    if (k == 0) s->overflow = 0u;
+  }
+}
+
+// MODE 0: pass 1 (bound), MODE 1: pass 2 (candidates). Each wave takes slabs of 32 points:
+// lane l holds point slab*32 + (l & 31) and, per 16-wide k-step, its coordinates k = 16 s + 8 h
+// .. + 7 (h = l >> 5) as the B fragment; the queries' bf16 rows come from LDS as A fragments.
+// C[q][p] lands with the point on the lane and 16 query rows per register file half.
+template <int MODE, int KG>
+__global__ __launch_bounds__(kBlock, 2) void k_mf(const float* __restrict__ pts, i64 n, int dim, int nqb,
+                                               Scratch* __restrict__ s) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const int QS = dim + 8;  // padded bf16 row stride (16-B rows offset by 4 banks)
+  __bf16* qbf = reinterpret_cast<__bf16*>(lds_raw);
+  float* cen = reinterpret_cast<float*>(lds_raw + size_t(kQB) * QS * 2);
+  float4* qv = reinterpret_cast<float4*>(cen + ((dim + 3) & ~3));  // (|y|^2, |y|, tau, -)
+  {  // the bf16 image, 16 B per load
+    const int4* src = reinterpret_cast<const int4*>(s->qbf);
+    int4* dst = reinterpret_cast<int4*>(qbf);
+    for (int f = threadIdx.x; f < kQB * QS / 8; f += kBlock) dst[f] = src[f];
+  }
+  for (int d = threadIdx.x; d < dim; d += kBlock) cen[d] = s->center[d];
+  for (int k = threadIdx.x; k < kQB; k += kBlock)
+  {
+    u32 t = 0x7f800000u;
+    if (MODE == 1)
+      for (int c = 0; c < 8; ++c) t = min(t, s->tau[c][k]);
+    qv[k] = make_float4(s->qn2[k], s->qnorm[k], __uint_as_float(t), 0.0f);
+  }
+  __syncthreads();
+  const int ln = dev::lane(), r = ln & 31, h = ln >> 5, w = threadIdx.x >> 6;
+  (void)ln;
+  // error-bound constants (u: fp32 unit roundoff, ub: bf16)
+  const float u = 5.9604645e-08f, ub = 0.00390625f, D = float(dim);
+  const float K1 = 2.2f * (2.0f * ub + ub * ub + D * u * (1.0f + ub) * (1.0f + ub));
+  const float K2 = 1.1f * (D + 14.0f) * u;
+  const float K3 = 1.1f * (D + 3.0f) * u;
+  float keep[MODE == 0 ? kTiles : 1][16];  // MODE 0: running min of d2' + E per row
+#pragma unroll
+  for (int t = 0; t < (MODE == 0 ? kTiles : 1); ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) keep[t][g] = __int_as_float(0x7f800000);
+  const i64 slabs = (n + 31) / 32;
+  const int groups = dim / (16 * KG);
+  const i64 wstride = i64(gridDim.x) * (kBlock / 64);
+  auto slab_of = [&](i64 wi) { return MODE == 0 ? wi * kBoundSub : wi; };
+  // (slab, group of KG k-steps) stream of this wave; the next group's 2 KG 16-B loads per lane
+  // are issued before the current group's conversion and MFMAs
+  auto loadg = [&](i64 sl, int g, float4 (&v)[2 * KG]) {
+    const i64 pp = sl * 32 + r;
+    const float4* row = reinterpret_cast<const float4*>(pts + (pp < n ? pp : 0) * dim);
+#pragma unroll
+    for (int i = 0; i < KG; ++i) {
+      const int k0 = (g * KG + i) * 16 + 8 * h;
+      v[2 * i] = row[k0 / 4];
+      v[2 * i + 1] = row[k0 / 4 + 1];
+    }
+  };
+  i64 wi = i64(blockIdx.x) * (kBlock / 64) + w;
+  int g = 0;
+  float4 cur[2 * KG], nxt[2 * KG];
+  if (slab_of(wi) < slabs) loadg(slab_of(wi), 0, cur);
+  f32x16 acc[kTiles];
+  float pp = 0.0f;
+  while (slab_of(wi) < slabs) {
+    const i64 slab = slab_of(wi);
+    i64 nwi = wi;
+    int ng = g + 1;
+    if (ng == groups) {
+      ng = 0;
+      nwi = wi + wstride;
+    }
+    if (slab_of(nwi) < slabs) loadg(slab_of(nwi), ng, nxt);
+    const i64 p = slab * 32 + r;
+    const bool valid = p < n;
+    if (g == 0) {
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+      pp = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < KG; ++i) {
+      const int k0 = (g * KG + i) * 16 + 8 * h;
+      const float xv[8] = {cur[2 * i].x, cur[2 * i].y, cur[2 * i].z, cur[2 * i].w,
+                           cur[2 * i + 1].x, cur[2 * i + 1].y, cur[2 * i + 1].z, cur[2 * i + 1].w};
+      const float4 c0 = *reinterpret_cast<const float4*>(cen + k0);
+      const float4 c1 = *reinterpret_cast<const float4*>(cen + k0 + 4);
+      const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = valid ? xv[j] - cv[j] : 0.0f;
+        const float sq = x * x;
+        pp = pp + sq;
+        b[j] = static_cast<__bf16>(x);
+      }
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(qbf + (t * 32 + r) * QS + k0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    if (ng == 0) {  // the slab's distances: bound or candidates
+      const float ptot = pp + __shfl_xor(pp, 32, 64);  // |x|^2 over both halves of the k range
+      const float xn = sqrtf(ptot);
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int q = t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const float4 yv = qv[q];
+          const float dot = acc[t][e];
+          const float d2 = (yv.x + ptot) - 2.0f * dot;
+          const float e0 = K1 * (xn * yv.y) + K2 * (yv.x + ptot);
+          const float eb = e0 + K3 * (fabsf(d2) + e0);
+          if (MODE == 0) {
+            const float hi = d2 + eb;
+            float& kv = keep[MODE == 0 ? t : 0][e];
+            kv = (valid && q < nqb && hi < kv) ? hi : kv;
+          } else if (valid && q < nqb && !(d2 - eb > yv.z)) {  // NaN bounds: candidates too
+            const u32 slot = atomicAdd(&s->cnt[q], 1u);
+            if (slot < u32(kCap)) s->cand[q * kCap + slot] = u32(p);
+            else atomicOr(&s->overflow, 1u);
+          }
+        }
+    }
+    wi = nwi;
+    g = ng;
+#pragma unroll
+    for (int i = 0; i < 2 * KG; ++i) cur[i] = nxt[i];
+  }
+  if (MODE == 0) {  // per query row: minimum over the block (lanes, then waves in LDS), one atomic
+    __syncthreads();
+    u32* bmin = reinterpret_cast<u32*>(qv);  // qv is no longer read: reuse as [kQB] u32
+    for (int k = threadIdx.x; k < kQB; k += kBlock) bmin[k] = 0x7f800000u;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float v = keep[t][e];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+        const int q = t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (r == 0 && q < nqb) {
+          if (!(v >= 0.0f)) atomicOr(&s->overflow, 1u);  // NaN bound: exact rerun
+          else if (!isinf(v)) atomicMin(&bmin[q], __float_as_uint(v));  // inf: no point of this wave
+        }
+      }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nqb; k += kBlock) {
+      const u32 v = bmin[k];
+      if (v != 0x7f800000u) atomicMin(&s->tau[blockIdx.x & 7][k], v);
+    }
+  }
+}
+
+// One thread per (query, candidate): the exact sequential distance, MIN into out.
+__global__ __launch_bounds__(kBlock) void k_mf_rescore(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                       u32 id_base, int dim, const float* __restrict__ q, int nqb,
+                                                       const Scratch* __restrict__ s, u64* __restrict__ out) {
+  const int f = blockIdx.x * kBlock + threadIdx.x;
+  const int k = f / kCap, c = f - k * kCap;
+  if (k >= nqb || s->overflow) return;
+  if (u32(c) >= min(s->cnt[k], u32(kCap))) return;
+  const u32 p = s->cand[k * kCap + c];
+  const float* row = pts + size_t(p) * dim;
+  const float* qq = q + size_t(k) * dim;
+  float a = 0.0f;
+  for (int d = 0; d < dim; d += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(row + d);
+    const float4 y = *reinterpret_cast<const float4*>(qq + d);
+    const float t0 = x.x - y.x, t1 = x.y - y.y, t2 = x.z - y.z, t3 = x.w - y.w;
+    const float s0 = t0 * t0, s1 = t1 * t1, s2 = t2 * t2, s3 = t3 * t3;
+    a = a + s0;
+    a = a + s1;
+    a = a + s2;
+    a = a + s3;
+  }
+  const u64 v = pack_dist_idx(a, ids ? ids[p] : id_base + p);
+  atomicMin((unsigned long long*)&out[k], (unsigned long long)v);
+}
+}  // namespace mf
+
+bool mfma_brute_enabled() {  // PKD_BRUTE_MFMA=0: the VALU brute force for every batch (A/B, tests)
+  const char* e = std::getenv("PKD_BRUTE_MFMA");
+  return !(e && std::string(e) == "0");
+}
+
+void launch_brute_mfma(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq,
+                       u64* out, hipStream_t stream) {
+  using namespace mf;
+  Scratch* s = nullptr;
+  PKD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&s), sizeof(Scratch), stream));
+  const size_t lds = size_t(kQB) * (dim + 8) * 2 + size_t((dim + 3) & ~3) * 4 + size_t(kQB) * 16;
+  const int kg = dim % 64 == 0 ? 4 : (dim % 32 == 0 ? 2 : 1);  // k-steps per load group
+  auto pass = [&](int mode, int grid, int nqb) {
+#define PKD_MF(M, G)                                                                          \
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_mf<M, G>), int(lds));                  \
+  k_mf<M, G><<<grid, kBlock, lds, stream>>>(pts, n, dim, nqb, s);
+    if (mode == 0) {
+      if (kg == 4) { PKD_MF(0, 4) } else if (kg == 2) { PKD_MF(0, 2) } else { PKD_MF(0, 1) }
+    } else {
+      if (kg == 4) { PKD_MF(1, 4) } else if (kg == 2) { PKD_MF(1, 2) } else { PKD_MF(1, 1) }
+    }
+#undef PKD_MF
+    PKD_LAUNCH_CHECK();
+  };
+  int dev = 0, cus = 256;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  PKD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const i64 slabs = (n + 31) / 32;
+  const i64 w1 = slabs, w0 = (slabs + kBoundSub - 1) / kBoundSub;  // waves of work per pass
+  const int g1 = int(std::max<i64>(1, std::min<i64>(i64(cus) * 4, (w1 + 3) / 4)));
+  const int g0 = int(std::max<i64>(1, std::min<i64>(i64(cus), (w0 + 3) / 4)));  // few slabs: amortise the LDS image
+  for (i64 b0 = 0; b0 < nq; b0 += kQB) {
+    const int nqb = int(std::min<i64>(kQB, nq - b0));
+    const float* qb = queries + b0 * dim;
+    k_mf_prep<<<kQB, kBlock, 0, stream>>>(qb, nqb, dim, s);
+    PKD_LAUNCH_CHECK();
+    pass(0, g0, nqb);
+    pass(1, g1, nqb);
+    k_mf_rescore<<<(nqb * kCap + kBlock - 1) / kBlock, kBlock, 0, stream>>>(pts, ids, id_base, dim, qb, nqb, s,
+                                                                            out + b0);
+    PKD_LAUNCH_CHECK();
+    launch_brute_pf<16>(pts, ids, id_base, n, dim, qb, nqb, out + b0, stream, &s->overflow);  // overflow only
+    if (const char* e = std::getenv("PKD_BRUTE_MFMA_STATS"); e && *e == '1') {  // diagnostic: synchronises
+      u32 cnt[kQB], ov = 0;
+      PKD_HIP_CHECK(hipMemcpyAsync(cnt, s->cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+      PKD_HIP_CHECK(hipMemcpyAsync(&ov, &s->overflow, 4, hipMemcpyDeviceToHost, stream));
+      PKD_HIP_CHECK(hipStreamSynchronize(stream));
+      u32 mx = 0, sum = 0;
+      for (int k = 0; k < nqb; ++k) {
+        mx = std::max(mx, cnt[k]);
+        sum += cnt[k];
+      }
+      std::fprintf(stderr, "[mfma brute] batch %lld: %d queries, candidates max %u mean %.1f, overflow %u\n",
+                   (long long)b0, nqb, mx, double(sum) / nqb, ov);
+    }
+  }
+  PKD_HIP_CHECK(hipFreeAsync(s, stream));
 }
 
 // Batched exact NN, one WAVE per query: the top of the implicit tree is walked by the whole
@@ -520,6 +831,11 @@ void nn_brute(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, con
   if (lds > size_t(150) * 1024) throw std::invalid_argument("nn_brute: dimension too large for the LDS query tile");
   const bool vec = dim % 4 == 0 && reinterpret_cast<uintptr_t>(pts) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(queries) % 16 == 0;
+  if (vec && dim % 16 == 0 && dim >= 32 && dim <= mf::kMaxDim && nq >= 16 && n >= 4096 && n < (i64(1) << 32) &&
+      mfma_brute_enabled()) {
+    launch_brute_mfma(pts, ids, id_base, n, dim, queries, nq, out, stream);
+    return;
+  }
   if (vec && dim % 16 == 0 && size_t(16) * dim * 4 <= size_t(150) * 1024) {
     // the prefetching kernel with the tile size that fits the queries
     // 32 coordinates per load round where the rows allow it: 2 x 128 B in flight per lane
