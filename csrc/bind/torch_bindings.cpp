@@ -105,6 +105,21 @@ struct Builder {
                             torch::TensorOptions().dtype(torch::kFloat32).device(dev));
   }
 
+  // Columns [(dim+1), column_stride()] float32 (row dim holds id bits), 256-B aligned, NOT the
+  // workspace's own SoA view: the distributed leaves' input format (GpuBuilder::build_columns).
+  std::vector<torch::Tensor> build_columns(const torch::Tensor& cols) {
+    TORCH_CHECK(cols.is_cuda() && cols.scalar_type() == torch::kFloat32 && cols.is_contiguous(), "cols: cuda f32");
+    TORCH_CHECK(cols.dim() == 2 && cols.size(0) == b.dim() + 1 && cols.size(1) == b.column_stride(),
+                "cols must be [dim+1, column_stride]");
+    const c10::DeviceGuard guard(cols.device());
+    ensure_ws(cols.device());
+    torch::Tensor op = torch::empty({b.n(), b.dim()}, cols.options());
+    torch::Tensor oi = torch::empty({b.n()}, cols.options().dtype(torch::kInt32));
+    b.build_columns(cols.data_ptr<float>(), op.data_ptr<float>(), reinterpret_cast<pk::u32*>(oi.data_ptr<int32_t>()),
+                    ws.data_ptr(), cur_stream(cols));
+    return {op, oi};
+  }
+
   std::vector<torch::Tensor> build_from_soa(const torch::Device& dev) {
     const c10::DeviceGuard guard(dev);
     ensure_ws(dev);
@@ -311,6 +326,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("out_pts") = c10::nullopt, py::arg("out_ids") = c10::nullopt)
       .def("build_rows", &Builder::build_rows, py::arg("rows"))
       .def("soa_input", &Builder::soa_input)
+      .def("build_columns", &Builder::build_columns)
       .def("build_from_soa", &Builder::build_from_soa)
       .def_property_readonly("workspace_bytes", [](const Builder& b) { return int64_t(b.b.workspace_bytes()); })
       .def_property_readonly("global_levels", [](const Builder& b) { return b.b.global_levels(); })
@@ -320,6 +336,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("split_streams", [](const Builder& b) { return b.b.split_streams(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
       .def_property_readonly("sampled_top", [](const Builder& b) { return b.b.sampled_top(); })
+      .def_property_readonly("column_stride", [](const Builder& b) { return int64_t(b.b.column_stride()); })
       .def("top_band_report", [](Builder& b) {  // per top node: band rows, rank in the median's bin, staged rows
         TORCH_CHECK(b.ws.defined(), "no build yet");
         const auto v = b.b.top_band_report(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());

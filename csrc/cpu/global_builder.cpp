@@ -304,7 +304,9 @@ GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth) {
   // no split build inside a distributed build: its side streams plus the caller's and the
   // communication stream would exceed the 4 hardware queues, and RCCL's kernels would queue
   // behind partition passes
-  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false, false});
+  // sampled top levels from the received columns at >= 10 M points (a band miss, ~1e-18 per build,
+  // reports error bit 0x20: the build fails loudly, it is never wrong)
+  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false, true});
   leaves_.push_back(std::move(l));
   return *leaves_.back()->b;
 }

@@ -3132,56 +3132,8 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   // through the global levels (lg_ + 2 columns instead of dim + 1); the subtree kernel and the
   // median writes gather whole rows from the input, which outlives the build.
   const bool narrow = narrow_ && tiled;
-  if (top_ && !ids_in_row && rs == dim_) {
-    // levels 0..3 straight from the AoS input (no prep pass): see top4.hpp
-    u32* err = reinterpret_cast<u32*>(ws + off_err_);
-    zero_u32(err, 4, stream);
-    top4::Geom g{};
-    for (int h = 0; h < top4::kHeap; ++h) {  // the heap geometry of k_geometry, levels 0..4
-      int l = 0;
-      while (((h + 1) >> (l + 1)) > 0) ++l;
-      const i64 j = h + 1 - (i64(1) << l);
-      i64 lo = 0, m = n_;
-      for (int b = l - 1; b >= 0; --b) {
-        if ((j >> b) & 1) {
-          lo = lo + m / 2 + 1;
-          m = m - m / 2 - 1;
-        } else {
-          m = m / 2;
-        }
-        if (m < 0) m = 0;
-      }
-      g.lo[h] = lo;
-      g.n[h] = m;
-    }
-    for (int l = 0; l <= top4::kLevels; ++l) g.axis[l] = (opt_.depth0 + l) % dim_;
-    g.dim = dim_;
-    top4::IO io{};
-    io.pts = pts;
-    io.ids = ids;
-    io.id_base = id_base;
-    io.n = n_;
-    io.cols = colsA;
-    io.stage = reinterpret_cast<float*>(ws + off_cols_b_);
-    io.ncol = ncol_;
-    io.out_pts = out_pts;
-    io.out_ids = out_ids;
-    io.cells = reinterpret_cast<float*>(ws + off_cells_);
-    io.params = reinterpret_cast<BucketParams*>(ws + off_params_);
-    io.bins4 = levels_[size_t(top4::kLevels)].bins;
-    io.err = err;
-    io.ws = ws + off_top_;
-    top4::Tune tt;
-    tt.sample_log2 = tune_.top_sample_log2;
-    tt.z = tune_.top_z;
-    tt.scatter_blocks = tune_.top_blocks;
-    tt.diag = tune_.top_diag;
-    {
-      TraceRange trt("pkd.top4");
-      top4::run(g, io, tt, stream);
-    }
-    if (tt.diag) return;  // timing diagnostic: no tree
-    run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, nullptr, top4::kLevels);
+  if (top_ && !ids_in_row && rs == dim_) {  // levels 0..3 straight from the AoS input (no prep pass)
+    run_top(pts, nullptr, ids, id_base, out_pts, out_ids, ws, stream);
     return;
   }
   const bool vec3 = dim_ == 3 && !ids_in_row && rs == 3 && (reinterpret_cast<uintptr_t>(pts) % 16 == 0) &&
@@ -3220,6 +3172,64 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
   run_levels(out_pts, out_ids, ws, stream, false, 0, narrow ? pts : nullptr, rs);
 }
 
+// Levels 0..3 by the sampled top pass (top4.hpp), then the remaining levels from level 4: from
+// the AoS input (pts) or from SoA columns (in_cols: dim coordinate columns + the id column,
+// stride ncol_, not the workspace's own columns), no prep or bounding-box pass either way.
+void GpuBuilder::run_top(const float* pts, const float* in_cols, const u32* ids, u32 id_base, float* out_pts,
+                         u32* out_ids, char* ws, hipStream_t stream) const {
+  float* colsA = reinterpret_cast<float*>(ws + off_cols_a_);
+  u32* err = reinterpret_cast<u32*>(ws + off_err_);
+  zero_u32(err, 4, stream);
+  top4::Geom g{};
+  for (int h = 0; h < top4::kHeap; ++h) {  // the heap geometry of k_geometry, levels 0..4
+    int l = 0;
+    while (((h + 1) >> (l + 1)) > 0) ++l;
+    const i64 j = h + 1 - (i64(1) << l);
+    i64 lo = 0, m = n_;
+    for (int b = l - 1; b >= 0; --b) {
+      if ((j >> b) & 1) {
+        lo = lo + m / 2 + 1;
+        m = m - m / 2 - 1;
+      } else {
+        m = m / 2;
+      }
+      if (m < 0) m = 0;
+    }
+    g.lo[h] = lo;
+    g.n[h] = m;
+  }
+  for (int l = 0; l <= top4::kLevels; ++l) g.axis[l] = (opt_.depth0 + l) % dim_;
+  g.dim = dim_;
+  top4::IO io{};
+  io.pts = pts;
+  io.in_cols = in_cols;
+  io.in_ncol = ncol_;
+  io.ids = ids;
+  io.id_base = id_base;
+  io.n = n_;
+  io.cols = colsA;
+  io.stage = reinterpret_cast<float*>(ws + off_cols_b_);
+  io.ncol = ncol_;
+  io.out_pts = out_pts;
+  io.out_ids = out_ids;
+  io.cells = reinterpret_cast<float*>(ws + off_cells_);
+  io.params = reinterpret_cast<BucketParams*>(ws + off_params_);
+  io.bins4 = levels_[size_t(top4::kLevels)].bins;
+  io.err = err;
+  io.ws = ws + off_top_;
+  top4::Tune tt;
+  tt.sample_log2 = tune_.top_sample_log2;
+  tt.z = tune_.top_z;
+  tt.scatter_blocks = tune_.top_blocks;
+  tt.diag = tune_.top_diag;
+  {
+    TraceRange trt("pkd.top4");
+    top4::run(g, io, tt, stream);
+  }
+  if (tt.diag) return;  // timing diagnostic: no tree
+  run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, nullptr, top4::kLevels);
+}
+
 void GpuBuilder::build_from_soa(float* out_pts, u32* out_ids, void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
   if (narrow_) throw std::runtime_error("pkdtree: build_from_soa needs the full-column layout (set PKD_NARROW=0)");
@@ -3243,6 +3253,10 @@ void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* 
   if (reinterpret_cast<uintptr_t>(cols) % 256 != 0) throw std::invalid_argument("pkdtree: columns must be 256-B aligned");
   TraceRange tr("pkd.build");
   char* ws = static_cast<char*>(workspace);
+  if (top_ && cols != reinterpret_cast<float*>(ws + off_cols_a_)) {  // sampled top levels from the columns
+    run_top(nullptr, cols, nullptr, 0, out_pts, out_ids, ws, stream);
+    return;
+  }
   if (root_cell) {  // the caller's box of the points: no bounding-box pass over the columns
     k_cell_root<<<1, 64, 0, stream>>>(root_cell, dim_, reinterpret_cast<float*>(ws + off_cells_),
                                       reinterpret_cast<BucketParams*>(ws + off_params_), opt_.depth0 % dim_,

@@ -209,19 +209,6 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
   return v;
 }
 
-// cnt[idx] += 1 for every active lane, one LDS atomic per distinct idx of the wave (the wave
-// calls it uniformly).
-__device__ __forceinline__ void wave_count(u32* cnt, u32 idx, bool active) {
-  u64 act = __ballot(active);
-  while (act) {
-    const int leader = __ffsll((long long)act) - 1;
-    const u32 key = u32(__shfl(int(idx), leader, 64));
-    const u64 m = __ballot(active && idx == key);
-    if (dev::lane() == leader) atomicAdd(&cnt[key], u32(__popcll(m)));
-    act &= ~m;
-  }
-}
-
 // Lanes of the wave in the same zone as this one (valid lanes only; zones < 2^BITS).
 template <int BITS>
 __device__ __forceinline__ u64 match_zone(u32 z, bool valid) {
@@ -306,7 +293,9 @@ __global__ __launch_bounds__(kBlock) void k_zero_top(u32* __restrict__ p, i64 n)
 
 // ---- sample -----------------------------------------------------------------------------
 struct SampArgs {
-  const float* pts;
+  const float* pts;      // AoS input, or nullptr: columns
+  const float* in_cols;  // SoA input columns (stride in_ncol) when pts is null
+  i64 in_ncol;
   int dim;
   i64 n;
   int S;
@@ -334,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
     const u32 win = u32(max<i64>(1, w1 - w0));
     const i64 r = w0 + i64(mix32(u32(kc) * 0x9e3779b9u + 0x7f4a7c15u) % win);
 #pragma unroll
-    for (int j = 0; j < kLevels; ++j) v[u][j] = a.pts[r * a.dim + a.ax[j]];
+    for (int j = 0; j < kLevels; ++j) v[u][j] = a.pts ? a.pts[r * a.dim + a.ax[j]] : a.in_cols[a.ax[j] * a.in_ncol + r];
   }
 #pragma unroll
   for (int u = 0; u < kGatherRows; ++u) {
@@ -526,7 +515,9 @@ __global__ __launch_bounds__(kBlock) void k_samp_sel(SampLevelArgs a) {
 
 // ---- scatter ----------------------------------------------------------------------------
 struct ScatArgs {
-  const float* pts;
+  const float* pts;      // AoS input, or nullptr: the SoA columns below (ids in column dim)
+  const float* in_cols;
+  i64 in_ncol;
   const u32* ids;
   u32 id_base;
   i64 n;
@@ -585,7 +576,7 @@ __device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R
 #pragma unroll
       for (int e = 0; e < 4; ++e) valid |= (r0 + e < a.n ? 1u : 0u) << (4 * u4 + e);
     }
-  } else {
+  } else if (a.pts) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const i64 r = t0 + i64(u) * kBlock + tid;
@@ -593,6 +584,16 @@ __device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R
 #pragma unroll
       for (int c = 0; c < D; ++c) v[u][c] = a.pts[rr * D + c];
       id[u] = a.ids ? a.ids[rr] : a.id_base + u32(r);
+      valid |= (r < a.n ? 1u : 0u) << u;
+    }
+  } else {  // SoA columns: every load coalesced
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const i64 r = t0 + i64(u) * kBlock + tid;
+      const i64 rr = r < a.n ? r : 0;
+#pragma unroll
+      for (int c = 0; c < D; ++c) v[u][c] = a.in_cols[i64(c) * a.in_ncol + rr];
+      id[u] = __float_as_uint(a.in_cols[i64(D) * a.in_ncol + rr]);
       valid |= (r < a.n ? 1u : 0u) << u;
     }
   }
@@ -735,13 +736,20 @@ struct ResArgs {
   u32* err;
 };
 
+// J = level: the per-node counts live in registers (3 << J of them, plus the scatter's 15 tag
+// counts at level 0), summed over the wave and the block once at the end.
+template <int J>
 __global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
+  constexpr int NC = 3 << J, NO = J == 0 ? kNodes : 0;
   __shared__ u32 h[kResBins];
   __shared__ u32 cnt[8 * 3 + 16];  // [x][left / band / right], then the scatter's tags (j = 0)
   __shared__ u32 sa[8], sb[8];
   __shared__ dev::BucketParams sbp[8];
   __shared__ u64 spv[4];
-  const int j = a.j, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1, F = res_bins(j);
+  const int j = J, nodes = 1 << j, first = nodes - 1, firstp = nodes / 2 - 1, F = res_bins(j);
+  u32 rc[NC + NO];
+#pragma unroll
+  for (int c = 0; c < NC + NO; ++c) rc[c] = 0u;
   const int tid = threadIdx.x;
   for (int i = tid; i < kResBins; i += kHistThreads) h[i] = 0u;
   if (tid < 8 * 3 + 16) cnt[tid] = 0u;
@@ -805,9 +813,16 @@ __global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
         idx = 3 * x + cls;
         if (cls == 1u) atomicAdd(&h[int(x) * F + int(dev::bucket_of(kj[u], sbp[x], F))], 1u);
       }
-      wave_count(cnt, idx, at);
-      if (j == 0) wave_count(cnt + 24, T[u] & 15u, live0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) rc[c] += (at && idx == u32(c)) ? 1u : 0u;
+#pragma unroll
+      for (int c = 0; c < NO; ++c) rc[NC + c] += (live0 && (T[u] & 15u) == u32(c)) ? 1u : 0u;
     }
+  }
+#pragma unroll
+  for (int c = 0; c < NC + NO; ++c) {
+    const u32 v = wave_sum(rc[c]);
+    if (dev::lane() == 0 && v) atomicAdd(&cnt[c < NC ? c : 24 + (c - NC)], v);
   }
   __syncthreads();
   u32* out = a.fine + size_t(j) * kResBins;
@@ -1250,7 +1265,7 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   PKD_LAUNCH_CHECK();
 
   const int gblocks = (S + kBlock * kGatherRows - 1) / (kBlock * kGatherRows);
-  SampArgs sa{io.pts, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, gpart};
+  SampArgs sa{io.pts, io.in_cols, io.in_ncol, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, gpart};
   k_samp_gather<<<gblocks, kBlock, 0, stream>>>(sa);
   PKD_LAUNCH_CHECK();
   const int hblocks = std::max(1, std::min(kSampBlocks, S / (kHistThreads * 4)));
@@ -1265,6 +1280,8 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
 
   ScatArgs sc{};
   sc.pts = io.pts;
+  sc.in_cols = io.in_cols;
+  sc.in_ncol = io.in_ncol;
   sc.ids = io.ids;
   sc.id_base = io.id_base;
   sc.n = n;
@@ -1285,7 +1302,7 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   sc.tiles = (n + tile - 1) / tile;
   sc.diag = t.diag;
   const int sblocks = int(std::max<i64>(1, std::min<i64>(t.scatter_blocks > 0 ? t.scatter_blocks : kMaxParts, sc.tiles)));
-  const bool vec = D == 3 && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
+  const bool vec = D == 3 && io.pts && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
                    (io.ids == nullptr || reinterpret_cast<uintptr_t>(io.ids) % 16 == 0);
   switch (D) {
     case 2: launch_scatter<2, false>(sblocks, sc, stream); break;
@@ -1308,7 +1325,12 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   for (int j = 0; j < kLevels; ++j) {
     ResArgs ra{io.stage, io.out_ids, io.ncol, D, j, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, st, fine_r, small,
                io.err};
-    k_res_classify<<<cgrid, kHistThreads, 0, stream>>>(ra);
+    switch (j) {
+      case 0: k_res_classify<0><<<cgrid, kHistThreads, 0, stream>>>(ra); break;
+      case 1: k_res_classify<1><<<cgrid, kHistThreads, 0, stream>>>(ra); break;
+      case 2: k_res_classify<2><<<cgrid, kHistThreads, 0, stream>>>(ra); break;
+      default: k_res_classify<3><<<cgrid, kHistThreads, 0, stream>>>(ra); break;
+    }
     PKD_LAUNCH_CHECK();
     k_res_sel1<<<1 << j, kBlock, 0, stream>>>(ra, g);
     PKD_LAUNCH_CHECK();

@@ -50,8 +50,10 @@ struct Geom {       // host-computed segment geometry of the heap nodes of level
 };
 
 struct IO {
-  const float* pts;   // [n, dim] AoS input
-  const u32* ids;     // [n] or nullptr (id = id_base + row)
+  const float* pts;   // [n, dim] AoS input, or nullptr: SoA input columns below
+  const float* in_cols = nullptr;  // dim coordinate columns + the id column, stride in_ncol (must
+  i64 in_ncol = 0;                 // not alias cols / stage)
+  const u32* ids;     // [n] or nullptr (id = id_base + row); AoS input only
   u32 id_base;
   i64 n;
   float* cols;        // SoA output columns (dim coords + ids), stride ncol: level-4 segments

@@ -155,6 +155,8 @@ class GpuBuilder {
   // cols_a != nullptr: replaces the workspace's first column buffer (the input of the first pass).
   // first_level > 0: levels [0, first_level) are already built (the sampled top levels): their
   // cells, the first level's histogram parameters and the error word are set.
+  void run_top(const float* pts, const float* in_cols, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
+               char* ws, hipStream_t stream) const;
   void run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t stream, bool implicit_ids = false,
                   u32 id_base = 0, const float* in_rows = nullptr, i64 in_rs = 0, float* cols_a = nullptr,
                   int first_level = 0, bool root_ready = false) const;

@@ -49,6 +49,15 @@ class GpuTreeBuilder:
         return self._b.describe()
 
     @property
+    def column_stride(self) -> int:
+        return int(self._b.column_stride)
+
+    def build_columns(self, cols: torch.Tensor):
+        """Build from SoA columns [dim + 1, column_stride] (the last row holds the ids' bits), the
+        distributed leaves' input layout; returns (tree_pts, tree_ids)."""
+        return tuple(self._b.build_columns(cols))
+
+    @property
     def sampled_top(self) -> bool:
         """Levels 0..3 come from the sampled top pass (csrc/gpu/top4.hpp)."""
         return bool(self._b.sampled_top)

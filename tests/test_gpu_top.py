@@ -107,3 +107,21 @@ def test_top_band_miss_detected_and_rebuilt(gpu_device, top_always, monkeypatch)
     t.check()
     cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
     assert torch.equal(t.tree_ids.cpu(), ci)
+
+
+@pytest.mark.parametrize("n,dim,depth0", [(400_000, 3, 3), (300_001, 4, 1), (250_000, 8, 0)])
+def test_top_from_columns(gpu_device, top_always, n, dim, depth0):
+    """The distributed leaves' input layout (SoA columns + id column, GpuBuilder::build_columns):
+    the sampled top reads the columns directly; the tree equals the CPU exact tree."""
+    x = pk.generate_problem(n + dim, dim, n)
+    ids = torch.randperm(n, generator=torch.Generator().manual_seed(n)).to(torch.int32) + 3
+    b = ops.GpuTreeBuilder(n, dim, depth0, 0)
+    assert b.sampled_top
+    cols = torch.zeros((dim + 1, b.column_stride), dtype=torch.float32, device=gpu_device)
+    cols[:dim, :n] = x.t().to(gpu_device)
+    cols[dim, :n] = ids.to(gpu_device).view(torch.float32)
+    tp, ti = b.build_columns(cols)
+    torch.cuda.synchronize()
+    assert b.read_error() == 0
+    cp, ci = ops.build_cpu(x, ids, "exact", depth0, 8)
+    assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
