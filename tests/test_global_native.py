@@ -21,6 +21,16 @@ def _lay(native, n, P, k=-1):
     return native.global_layout(n, P, k)
 
 
+@pytest.mark.parametrize("P", [3, 5, 6, 7, 9, 10, 11, 12, 13, 14])  # (P = 15: 64 / 15, the 6-level cap)
+def test_layout_balance_non_power_of_two(native, P):
+    """Default leaf count for P not a power of two: the busiest rank owns at most ~13 % more
+    leaves than the mean (P = 3 at 16 leaves used to give 6 / 5 / 5, +20 %)."""
+    lay = _lay(native, 100_000_000, P)
+    lo = lay["leaf_lo"]
+    busiest = max(lo[r + 1] - lo[r] for r in range(P))
+    assert busiest <= 1.13 * lay["T"] / P
+
+
 @pytest.mark.parametrize("n", [0, 1, 5, 64, 1000, 100_003])
 @pytest.mark.parametrize("P,k", [(1, -1), (1, 2), (2, -1), (3, -1), (4, 0), (5, -1), (6, 1), (7, -1), (8, 0),
                                  (8, 2), (12, -1), (33, -1), (64, 0)])
