@@ -356,6 +356,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int64_t, int64_t, int64_t>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0)
       .def("build", &RefBuilder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0)
       .def_property_readonly("sorted_levels", [](const RefBuilder& b) { return b.b.sorted_levels(); })
+      .def_property_readonly("global_levels", [](const RefBuilder& b) { return b.b.global_levels(); })
       .def_property_readonly("workspace_bytes", [](const RefBuilder& b) { return int64_t(b.b.workspace_bytes()); });
   m.def("generate", &generate, py::arg("seed"), py::arg("dim"), py::arg("rows"), py::arg("first") = 0,
         py::arg("threads") = 0);
