@@ -16,7 +16,7 @@ def short(n):
     return m.group(1) if m else n[:40]
 
 
-first_kernel = next((k for k in ("k_zero_top", "k_bbox_init", "k_bbox_reduce", "k_prep") if any(k in r["Kernel_Name"] for r in rows)), None)
+first_kernel = next((k for k in ("k_samp_gather", "k_bbox_init", "k_bbox_reduce", "k_prep") if any(k in r["Kernel_Name"] for r in rows)), None)
 starts = [i for i, r in enumerate(rows) if first_kernel and first_kernel in r["Kernel_Name"]]
 last = rows[starts[-1]:] if starts else rows
 # the build ends at its subtree kernel (later dispatches belong to the caller)
