@@ -1195,23 +1195,26 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
   __shared__ u32 box[16];
   __shared__ float split[kNodes];
   __shared__ u32 have[kNodes];
-  __shared__ u32 red[kBlock / 64];
+  __shared__ u32 red[kBlock / 64][16];
+  __shared__ float scell[kHeap][16];
   const int D = a.dim, tid = threadIdx.x;
-  for (int c = 0; c < 2 * D; ++c) {  // bounding box from the scatter blocks' partials
-    u32 v = c < D ? 0xffffffffu : 0u;
+  {  // bounding box from the scatter blocks' partials: every value in one pass
+    u32 r[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) r[c] = c < D ? 0xffffffffu : 0u;
     for (int p = tid; p < a.nparts; p += kBlock) {
-      const u32 x = a.part[size_t(p) * 2 * D + c];
-      v = c < D ? min(v, x) : max(v, x);
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (c < 2 * D) {
+          const u32 x = a.part[size_t(p) * 2 * D + c];
+          r[c] = c < D ? min(r[c], x) : max(r[c], x);
+        }
     }
-    v = c < D ? dev::wave_min_u32(v) : dev::wave_max_u32(v);
-    if (dev::lane() == 0) red[tid / 64] = v;
-    __syncthreads();
-    if (tid == 0) {
-      u32 r = red[0];
-      for (int k = 1; k < kBlock / 64; ++k) r = c < D ? min(r, red[k]) : max(r, red[k]);
-      box[c] = r;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const u32 v = c < D ? dev::wave_min_u32(r[c]) : dev::wave_max_u32(r[c]);
+      if (dev::lane() == 0) red[tid / 64][c] = v;
     }
-    __syncthreads();
   }
   if (tid < kCells && a.st->cursor[tid] + a.st->ins[tid] != u32(g.n[kNodes + tid]))
     report(a.err, 0x2008u, u32(tid), a.st->cursor[tid] + a.st->ins[tid]);
@@ -1230,32 +1233,32 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    float* cells = a.cells;
-    for (int c = 0; c < D; ++c) {
-      cells[2 * c] = from_orderable(box[c]);
-      cells[2 * c + 1] = from_orderable(box[D + c]);
+  if (tid < 2 * D) {
+    u32 r = red[0][tid];
+    for (int k = 1; k < kBlock / 64; ++k) r = tid < D ? min(r, red[k][tid]) : max(r, red[k][tid]);
+    box[tid] = r;
+  }
+  __syncthreads();
+  // cells of nodes 0..30, one (node, bound) per thread: the root box narrowed by every
+  // ancestor split on that axis
+  for (int e = tid; e < kHeap * 2 * D; e += kBlock) {
+    const int h = e / (2 * D), q = e - h * 2 * D, c = q / 2, side = q & 1;
+    const int lh = heap_level(u32(h));
+    float v = from_orderable(side ? box[D + c] : box[c]);
+    for (int l = 0; l < lh; ++l) {
+      const int Y = ((h + 1) >> (lh - l)) - 1, C = ((h + 1) >> (lh - l - 1)) - 1;
+      if (g.axis[l] != c || !have[Y]) continue;
+      const bool left = C == 2 * Y + 1;
+      if (left && side == 1) v = split[Y];
+      if (!left && side == 0) v = split[Y];
     }
-    for (int X = 0; X < kNodes; ++X) {
-      const int ax = g.axis[heap_level(u32(X))];
-      const float* cp = cells + size_t(X) * 2 * D;
-      float* cl = cells + size_t(2 * X + 1) * 2 * D;
-      float* cr = cells + size_t(2 * X + 2) * 2 * D;
-      for (int c = 0; c < 2 * D; ++c) {
-        cl[c] = cp[c];
-        cr[c] = cp[c];
-      }
-      if (have[X]) {
-        cl[2 * ax + 1] = split[X];
-        cr[2 * ax] = split[X];
-      }
-    }
+    scell[h][q] = v;
+    a.cells[size_t(h) * 2 * D + q] = v;
   }
   __syncthreads();
   if (tid < kCells) {
     const int h = kNodes + tid, ax = g.axis[kLevels];
-    const float* c = a.cells + size_t(h) * 2 * D;
-    a.params[h] = dev::make_params(c[2 * ax], c[2 * ax + 1], a.bins4);
+    a.params[h] = dev::make_params(scell[h][2 * ax], scell[h][2 * ax + 1], a.bins4);
   }
 }
 
