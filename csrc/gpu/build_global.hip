@@ -2870,7 +2870,6 @@ Tuning Tuning::from_env() {
   if (const char* z = std::getenv("PKD_TOP_Z")) t.top_z = float(std::atof(z));
   t.top_blocks = int(env_i("PKD_TOP_BLOCKS", 0));
   t.top_diag = int(env_i("PKD_TOP_DIAG", 0));
-  t.top_lds_in = env_i("PKD_TOP_LDSIN", 0) != 0;
   return t;
 }
 
@@ -3223,7 +3222,6 @@ void GpuBuilder::run_top(const float* pts, const float* in_cols, const u32* ids,
   tt.z = tune_.top_z;
   tt.scatter_blocks = tune_.top_blocks;
   tt.diag = tune_.top_diag;
-  tt.lds_in = tune_.top_lds_in;
   {
     TraceRange trt("pkd.top4");
     top4::run(g, io, tt, stream);

@@ -600,21 +600,17 @@ __device__ __forceinline__ u32 load_tile(const ScatArgs& a, i64 t0, float (&v)[R
 // Zone code of a scatter row: 0..15 its level-4 segment, 16 + T staged at node T, 31 none.
 // (Loading the next tile while this one is reordered and stored measured no faster: the
 // registers it takes cost more occupancy than the overlap gains.)
-// LI (3-D AoS input): a full tile's 48 KB of rows are first copied into LDS with lane-linear
-// 16-B loads (each wave instruction reads 1 KB contiguous), then every thread reads its rows
-// from LDS; the reorder buffer aliases that staging area (it is written only after every
-// thread has read its rows).
-template <int D, int R, int NH, bool VEC, bool LI = false>
+// (Staging each tile's 48 KB of 3-D rows through LDS with lane-linear 16-B loads measured slower:
+// 1.02 vs 0.91 ms to the end of the scatter at 100 M, profiles/r4_top_sizes_diag.txt.)
+template <int D, int R, int NH, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
   constexpr int HR = R / NH, HALF = kBlock * HR, NZ = kCells + 1;
   constexpr int TILE = kBlock * R;
-  static_assert(!LI || (D == 3 && VEC), "LDS-staged input: 3-D rows");
   constexpr int kBufWords = (D + 1) * HALF + HALF / 4;
-  constexpr int kInWords = LI ? 3 * TILE : 0;
   __shared__ uint2 sab[16];           // band [a, b] of heap node X
   __shared__ u32 zlo[NZ], zcap[NZ];   // first row and capacity of each zone's destination
   __shared__ Reorder<NZ, NH> ro;
-  __shared__ __align__(16) float lds_rows[kBufWords > kInWords ? kBufWords : kInWords];
+  __shared__ __align__(16) float lds_rows[kBufWords];
   float(&buf)[D + 1][HALF] = *reinterpret_cast<float(*)[D + 1][HALF]>(lds_rows);
   unsigned char* bz = reinterpret_cast<unsigned char*>(lds_rows + (D + 1) * HALF);
   __shared__ u32 red[kBlock / 64][2 * D];
@@ -635,29 +631,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(ScatArgs a) {
   for (i64 tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
     float v[R][D];
     u32 id[R];
-    u32 vmask;
-    if (LI && (tile + 1) * TILE <= a.n) {
-      if (tile != blockIdx.x) __syncthreads();  // the previous tile's stores have read the aliased buffer
-      const i64 t0 = tile * TILE;
-      const float4* in = reinterpret_cast<const float4*>(a.pts) + t0 * 3 / 4;
-      float4* st4 = reinterpret_cast<float4*>(lds_rows);
-      float4 f[3 * R / 4];
-#pragma unroll
-      for (int e = 0; e < 3 * R / 4; ++e) f[e] = in[e * kBlock + tid];
-#pragma unroll
-      for (int u = 0; u < R; ++u) id[u] = a.ids ? a.ids[t0 + u * kBlock + tid] : a.id_base + u32(t0 + u * kBlock + tid);
-#pragma unroll
-      for (int e = 0; e < 3 * R / 4; ++e) st4[e * kBlock + tid] = f[e];
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < R; ++u)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) v[u][c] = lds_rows[3 * (u * kBlock + tid) + c];
-      vmask = R >= 32 ? 0xffffffffu : (1u << R) - 1u;
-    } else {
-      if (LI && tile != blockIdx.x) __syncthreads();
-      vmask = load_tile<D, R, VEC>(a, tile * TILE, v, id);
-    }
+    const u32 vmask = load_tile<D, R, VEC>(a, tile * TILE, v, id);
     u32 code[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -1263,14 +1237,8 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
 }
 
 template <int D, bool VEC>
-void launch_scatter(int blocks, const ScatArgs& sc, hipStream_t stream, bool lds_in) {
+void launch_scatter(int blocks, const ScatArgs& sc, hipStream_t stream) {
   constexpr int R = D <= 4 ? 16 : 8;
-  if constexpr (D == 3 && VEC) {
-    if (lds_in) {
-      k_scatter<D, R, 2, VEC, true><<<blocks, kBlock, 0, stream>>>(sc);
-      return;
-    }
-  }
   k_scatter<D, R, 2, VEC><<<blocks, kBlock, 0, stream>>>(sc);
 }
 
@@ -1338,16 +1306,16 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   const bool vec = D == 3 && io.pts && reinterpret_cast<uintptr_t>(io.pts) % 16 == 0 &&
                    (io.ids == nullptr || reinterpret_cast<uintptr_t>(io.ids) % 16 == 0);
   switch (D) {
-    case 2: launch_scatter<2, false>(sblocks, sc, stream, t.lds_in); break;
+    case 2: launch_scatter<2, false>(sblocks, sc, stream); break;
     case 3:
-      if (vec) launch_scatter<3, true>(sblocks, sc, stream, t.lds_in);
-      else launch_scatter<3, false>(sblocks, sc, stream, t.lds_in);
+      if (vec) launch_scatter<3, true>(sblocks, sc, stream);
+      else launch_scatter<3, false>(sblocks, sc, stream);
       break;
-    case 4: launch_scatter<4, false>(sblocks, sc, stream, t.lds_in); break;
-    case 5: launch_scatter<5, false>(sblocks, sc, stream, t.lds_in); break;
-    case 6: launch_scatter<6, false>(sblocks, sc, stream, t.lds_in); break;
-    case 7: launch_scatter<7, false>(sblocks, sc, stream, t.lds_in); break;
-    default: launch_scatter<8, false>(sblocks, sc, stream, t.lds_in); break;
+    case 4: launch_scatter<4, false>(sblocks, sc, stream); break;
+    case 5: launch_scatter<5, false>(sblocks, sc, stream); break;
+    case 6: launch_scatter<6, false>(sblocks, sc, stream); break;
+    case 7: launch_scatter<7, false>(sblocks, sc, stream); break;
+    default: launch_scatter<8, false>(sblocks, sc, stream); break;
   }
   PKD_LAUNCH_CHECK();
   if (t.diag) return;  // timing diagnostic: the rest is not run

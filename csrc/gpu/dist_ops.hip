@@ -17,7 +17,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kPivotThreads = 1024;
-constexpr int kPivotLdsKeys = 12288;  // 96 KiB of keys per node in LDS; larger middles stream from L2
+constexpr int kPivotLdsKeys = 16384;  // 128 KiB of keys per node in LDS; larger middles stream from L2
 
 __device__ __forceinline__ u32 point_id(const TopPoints& p, i64 i) { return p.ids ? p.ids[i] : p.id_base + u32(i); }
 
@@ -367,7 +367,8 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
                                                              u32* __restrict__ err) {
   extern __shared__ __align__(16) u64 keys[];  // [kPivotLdsKeys]
   __shared__ u32 hist[256];
-  __shared__ u32 s_cnt, s_digit, s_rem, s_found;
+  __shared__ u32 s_cnt, s_digit, s_rem, s_found, s_bincnt;
+  __shared__ u64 s_mn[kPivotThreads / 64], s_mx[kPivotThreads / 64], s_one;
   const int j = blockIdx.x;
   const u32 h = u32((1 << level) - 1 + j);
   const int dim = mv.dim, axis = mv.axis;
@@ -392,16 +393,39 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
       if (reinterpret_cast<const u32*>(mv.g + r * mv.stride)[0] > u32(mv.cap)) atomicOr(err, 1u);
   }
   __syncthreads();
-  // 1. this node's keys into LDS
+  // 1. this node's keys into LDS (one reservation per wave, not one same-address atomic per
+  // row), with their range
+  u64 mn = ~0ull, mx = 0ull;
   for (int r = 0; r < mv.P; ++r) {
     const u32 c = mv.count(r);
-    for (u32 k = tid; k < c; k += kPivotThreads) {
-      const float* row = mv.row(r, k);
-      if (mv.node(row) == h) {
-        const u32 s = atomicAdd(&s_cnt, 1u);
-        if (s < u32(kPivotLdsKeys)) keys[s] = mv.key(row);
+    for (u32 k0 = 0; k0 < c; k0 += kPivotThreads) {  // uniform trip count: wave ballots below
+      const u32 k = k0 + tid;
+      bool mine = false;
+      u64 key = 0;
+      if (k < c) {
+        const float* row = mv.row(r, k);
+        mine = mv.node(row) == h;
+        if (mine) key = mv.key(row);
+      }
+      const u64 m = __ballot(mine);
+      if (!m) continue;
+      const int leader = __ffsll((long long)m) - 1;
+      u32 base = 0;
+      if (dev::lane() == leader) base = atomicAdd(&s_cnt, u32(__popcll(m)));
+      base = u32(__shfl(int(base), leader, 64));
+      if (mine) {
+        const u32 sidx = base + mbcnt(m);
+        if (sidx < u32(kPivotLdsKeys)) keys[sidx] = key;
+        mn = key < mn ? key : mn;
+        mx = key > mx ? key : mx;
       }
     }
+  }
+  mn = dev::wave_min_u64(mn);
+  mx = dev::wave_max_u64(mx);
+  if (dev::lane() == 0) {
+    s_mn[tid / 64] = mn;
+    s_mx[tid / 64] = mx;
   }
   __syncthreads();
   const u32 m = s_cnt;
@@ -414,28 +438,57 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
     }
     return;
   }
+  mn = s_mn[0];
+  mx = s_mx[0];
+  for (int w = 1; w < kPivotThreads / 64; ++w) {
+    mn = s_mn[w] < mn ? s_mn[w] : mn;
+    mx = s_mx[w] > mx ? s_mx[w] : mx;
+  }
   const bool in_lds = m <= u32(kPivotLdsKeys);
-  // 2. radix select, 8 bits per pass from the top
-  u64 prefix = 0;
+  // 2. radix select, 8 bits per pass from the highest bit in which the keys differ (the median
+  // bucket's keys share their top bits: those passes are skipped). Histogram adds: one per
+  // wave when all its lanes carry the same digit, else one per lane.
+  u64 prefix = mn;
   u32 rem = target;
-  for (int pass = 7; pass >= 0; --pass) {
-    const int shift = pass * 8;
-    const u64 hmask = pass == 7 ? 0ull : (~0ull << (shift + 8));
+  const u64 diff = mn ^ mx;
+  int hb = diff ? 63 - __builtin_clzll(diff) : -1;
+  prefix = hb >= 63 ? 0ull : (hb < 0 ? mn : (mn & ~((2ull << hb) - 1ull)));
+  while (hb >= 0) {
+    const int shift = hb >= 7 ? hb - 7 : 0;
+    const u32 dmask = (2u << (hb - shift)) - 1u;
+    const u64 hmask = hb >= 63 ? 0ull : ~((2ull << hb) - 1ull);
     for (int b = tid; b < 256; b += kPivotThreads) hist[b] = 0;
     __syncthreads();
+    auto add = [&](bool act, u32 d) {
+      const u64 am = __ballot(act);
+      if (!am) return;
+      const int l0 = __ffsll((long long)am) - 1;
+      const u32 d0 = u32(__shfl(int(d), l0, 64));
+      if (__ballot(act && d == d0) == am) {
+        if (dev::lane() == l0) atomicAdd(&hist[d0], u32(__popcll(am)));
+      } else if (act) {
+        atomicAdd(&hist[d], 1u);
+      }
+    };
     if (in_lds) {
-      for (u32 k = tid; k < m; k += kPivotThreads) {
-        const u64 key = keys[k];
-        if ((key & hmask) == (prefix & hmask)) atomicAdd(&hist[u32(key >> shift) & 255u], 1u);
+      for (u32 k0 = 0; k0 < m; k0 += kPivotThreads) {
+        const u32 k = k0 + tid;
+        const u64 key = k < m ? keys[k] : 0ull;
+        add(k < m && (key & hmask) == prefix, u32(key >> shift) & dmask);
       }
     } else {
       for (int r = 0; r < mv.P; ++r) {
         const u32 c = mv.count(r);
-        for (u32 k = tid; k < c; k += kPivotThreads) {
-          const float* row = mv.row(r, k);
-          if (mv.node(row) != h) continue;
-          const u64 key = mv.key(row);
-          if ((key & hmask) == (prefix & hmask)) atomicAdd(&hist[u32(key >> shift) & 255u], 1u);
+        for (u32 k0 = 0; k0 < c; k0 += kPivotThreads) {
+          const u32 k = k0 + tid;
+          bool act = false;
+          u64 key = 0;
+          if (k < c) {
+            const float* row = mv.row(r, k);
+            key = mv.key(row);
+            act = mv.node(row) == h && (key & hmask) == prefix;
+          }
+          add(act, u32(key >> shift) & dmask);
         }
       }
     }
@@ -456,14 +509,25 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
           if (rem >= c && rem < c + v[q]) {
             s_digit = u32(4 * l + q);
             s_rem = rem - c;
+            s_bincnt = v[q];
           }
           c += v[q];
         }
       }
     }
     __syncthreads();
-    prefix |= u64(s_digit) << shift;
+    prefix |= u64(s_digit & dmask) << shift;
     rem = s_rem;
+    hb = shift - 1;
+    if (s_bincnt == 1u && hb >= 0 && in_lds) {
+      // one candidate left (its key digits are distinct from every other row's): it is the pivot
+      const u64 hm = ~((2ull << hb) - 1ull);
+      for (u32 k = tid; k < m; k += kPivotThreads)
+        if ((keys[k] & hm) == prefix) s_one = keys[k];
+      __syncthreads();
+      prefix = s_one;
+      hb = -1;
+    }
     __syncthreads();
   }
   // 3. the pivot row (composite keys are unique)
@@ -556,35 +620,52 @@ __global__ __launch_bounds__(kScanThreads) void k_pack_scan(const u32* __restric
 // planar exchange is always the compact one). bm != nullptr: the leaf bitmaps of the compact
 // exchange come from the same ballots (a block's rows start on a multiple of 256, so wave w's
 // 64 rows of a chunk are exactly bitmap words 2 k and 2 k + 1 of every leaf).
+// Four 256-row sub-chunks per round: their node loads, then their rows' loads, are in flight
+// together; sub-chunks are ranked in order, so each leaf's rows stay in source-row order.
 __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32* __restrict__ node, int levels, int T,
                                                          i64 per_block, const u32* __restrict__ offsets,
                                                          float* __restrict__ out, int rs, i64 cs, u32* __restrict__ bm,
                                                          i64 bm_words) {
+  constexpr int U = 4;
   __shared__ u32 cur[64];
-  __shared__ u32 wcnt[kBlock / 64][64];
+  __shared__ u32 wcnt[U][kBlock / 64][64];
   const u32 first = u32(T - 1);
   if (threadIdx.x < T) cur[threadIdx.x] = offsets[i64(blockIdx.x) * T + threadIdx.x];
   __syncthreads();
   const i64 b0 = i64(blockIdx.x) * per_block, b1 = min(p.n, b0 + per_block);
   const int w = threadIdx.x / 64, ln = dev::lane();
   const int dim = p.dim;
-  for (i64 c0 = b0; c0 < b1; c0 += kBlock) {
-    const i64 i = c0 + threadIdx.x;
-    const u32 h = i < b1 ? (levels > 0 ? node[i] : 0u) : kTopDone;
-    const int d = (h == kTopDone || h - first >= u32(T)) ? -1 : int(h - first);
-    u32 my = 0;
-    const i64 word = (c0 + 64 * w) / 32;  // this wave's first bitmap word
-    for (int e = 0; e < T; ++e) {  // stable rank among same-destination points of the chunk
-      const u64 m = __ballot(d == e);
-      if (ln == 0) wcnt[w][e] = __popcll(m);
-      if (d == e) my = mbcnt(m);
-      if (bm && ln < 2 && word + ln < bm_words) bm[i64(e) * bm_words + word + ln] = ln == 0 ? u32(m) : u32(m >> 32);
+  for (i64 c0 = b0; c0 < b1; c0 += U * kBlock) {
+    int d[U];
+    u32 my[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 i = c0 + u * kBlock + threadIdx.x;
+      const u32 h = i < b1 ? (levels > 0 ? node[i] : 0u) : kTopDone;
+      d[u] = (h == kTopDone || h - first >= u32(T)) ? -1 : int(h - first);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      my[u] = 0;
+      const i64 word = (c0 + u * kBlock + 64 * w) / 32;  // this wave's first bitmap word
+      for (int e = 0; e < T; ++e) {  // stable rank among same-destination points of the sub-chunk
+        const u64 m = __ballot(d[u] == e);
+        if (ln == 0) wcnt[u][w][e] = __popcll(m);
+        if (d[u] == e) my[u] = mbcnt(m);
+        if (bm && ln < 2 && word + ln < bm_words && c0 + u * kBlock < b1)
+          bm[i64(e) * bm_words + word + ln] = ln == 0 ? u32(m) : u32(m >> 32);
+      }
     }
     __syncthreads();
-    if (d >= 0) {
-      u32 off = cur[d];
-      for (int v = 0; v < w; ++v) off += wcnt[v][d];
-      const i64 k = i64(off + my);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (d[u] < 0) continue;
+      const i64 i = c0 + u * kBlock + threadIdx.x;
+      u32 off = cur[d[u]];
+      for (int uu = 0; uu < u; ++uu)
+        for (int v = 0; v < kBlock / 64; ++v) off += wcnt[uu][v][d[u]];
+      for (int v = 0; v < w; ++v) off += wcnt[u][v][d[u]];
+      const i64 k = i64(off + my[u]);
       const float* r = p.pts + i * dim;
       if (cs > 0) {
         if (dim == 3) {  // one 12-B row load, three coalesced plane stores
@@ -608,7 +689,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
     __syncthreads();
     if (threadIdx.x < T) {
       u32 add = 0;
-      for (int v = 0; v < kBlock / 64; ++v) add += wcnt[v][threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        for (int v = 0; v < kBlock / 64; ++v) add += wcnt[u][v][threadIdx.x];
       cur[threadIdx.x] += add;
     }
     __syncthreads();

@@ -76,7 +76,6 @@ struct Tune {
   // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets, 3 also
   // without the scatter's global stores.
   int diag = 0;
-  bool lds_in = false;  // PKD_TOP_LDSIN (A/B): 3-D scatter tiles staged through LDS
 };
 
 size_t workspace_bytes();

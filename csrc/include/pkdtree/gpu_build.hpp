@@ -71,7 +71,6 @@ struct Tuning {
   float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
   int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
   int top_diag = 0;           // PKD_TOP_DIAG: timing diagnostics of the scatter (no tree; top4::Tune::diag)
-  bool top_lds_in = false;     // PKD_TOP_LDSIN: 3-D scatter tiles staged through LDS (A/B)
   static Tuning from_env();
 };
 

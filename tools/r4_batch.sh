@@ -5,8 +5,6 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_brute_mfma.py tests/test_gpu_top.py > $O/mfma_tests.log 2>&1 || exit 1
 timeout -k 10 200 python3 -u tools/top_diag.py 100000000 > $O/diag.log 2>&1 || exit 1
-PKD_TOP_LDSIN=1 timeout -k 10 200 python3 -u tools/top_diag.py 100000000 >> $O/diag.log 2>&1 || exit 1
-PKD_TOP_LDSIN=1 PKD_TOP_MIN_N=0 timeout -k 10 200 python3 -u tools/top_check.py --quick > $O/ldsin_check.log 2>&1 || exit 1
 PKD_BRUTE_MFMA_STATS=1 timeout -k 10 120 python3 tools/bench_query.py --queries 100 --reps 2 > $O/mfma_stats.log 2>&1 || exit 1
 timeout -k 10 120 python3 tools/bench_query.py --queries 100 > $O/mfma_bench.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
