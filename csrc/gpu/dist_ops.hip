@@ -79,6 +79,63 @@ __global__ __launch_bounds__(kBlock) void k_top_bbox(TopPoints p, i64 T, i64* __
   }
 }
 
+// 16-B loads (rows 16-B aligned): thread t reads float4s t, t + T4, ...; 4 T4 is a multiple of
+// dim, so element e of every float4 of a thread has axis (4 t + e) % dim. The < 4 floats past the
+// last whole float4 are read by thread 0.
+__global__ __launch_bounds__(kBlock) void k_top_bbox4(TopPoints p, i64 T4, i64* __restrict__ box) {
+  extern __shared__ __align__(16) u32 sb[];  // [2 * dim]
+  const int dim = p.dim;
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sb[c] = 0xffffffffu;
+  __syncthreads();
+  const i64 t = i64(blockIdx.x) * kBlock + threadIdx.x;
+  const i64 total = p.n * dim, total4 = total / 4;
+  if (t < T4 && t < total4) {
+    u32 lo[4], nhi[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo[e] = nhi[e] = 0xffffffffu;
+    const float4* in = reinterpret_cast<const float4*>(p.pts);
+    const float4 first = in[t];
+    constexpr int U = 4;
+    for (i64 q0 = t; q0 < total4; q0 += U * T4) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const i64 q = q0 + i64(u) * T4;
+        v[u] = q < total4 ? in[q] : first;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const u32 k = orderable(x[e]);
+          lo[e] = min(lo[e], k);
+          nhi[e] = min(nhi[e], ~k);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = int((4 * t + e) % dim);
+      atomicMin(&sb[c], lo[e]);
+      atomicMin(&sb[dim + c], nhi[e]);
+    }
+  }
+  if (t == 0) {
+    for (i64 f = total4 * 4; f < total; ++f) {
+      const u32 k = orderable(p.pts[f]);
+      const int c = int(f % dim);
+      atomicMin(&sb[c], k);
+      atomicMin(&sb[dim + c], ~k);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * dim; c += kBlock) {
+    if (sb[c] != 0xffffffffu)
+      atomicMin(reinterpret_cast<unsigned long long*>(box + c), (unsigned long long)sb[c]);
+  }
+}
+
 __global__ void k_top_root_cell(const i64* __restrict__ box, int dim, float* __restrict__ cells) {
   for (int c = threadIdx.x; c < dim; c += blockDim.x) {
     cells[2 * c] = from_orderable(u32(box[c]));
@@ -396,28 +453,34 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
   // 1. this node's keys into LDS (one reservation per wave, not one same-address atomic per
   // row), with their range
   u64 mn = ~0ull, mx = 0ull;
+  constexpr int U = 4;  // rows per thread per round: their loads in flight together (one block
+                        // per node walks every rank's middle rows, so rounds are latency-bound)
   for (int r = 0; r < mv.P; ++r) {
     const u32 c = mv.count(r);
-    for (u32 k0 = 0; k0 < c; k0 += kPivotThreads) {  // uniform trip count: wave ballots below
-      const u32 k = k0 + tid;
-      bool mine = false;
-      u64 key = 0;
-      if (k < c) {
-        const float* row = mv.row(r, k);
-        mine = mv.node(row) == h;
-        if (mine) key = mv.key(row);
+    for (u32 k0 = 0; k0 < c; k0 += U * kPivotThreads) {  // uniform trip count: wave ballots below
+      bool mine[U];
+      u64 key[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u32 k = k0 + u * kPivotThreads + tid;
+        const float* row = mv.row(r, k < c ? k : 0u);
+        mine[u] = k < c && mv.node(row) == h;
+        key[u] = mv.key(row);
       }
-      const u64 m = __ballot(mine);
-      if (!m) continue;
-      const int leader = __ffsll((long long)m) - 1;
-      u32 base = 0;
-      if (dev::lane() == leader) base = atomicAdd(&s_cnt, u32(__popcll(m)));
-      base = u32(__shfl(int(base), leader, 64));
-      if (mine) {
-        const u32 sidx = base + mbcnt(m);
-        if (sidx < u32(kPivotLdsKeys)) keys[sidx] = key;
-        mn = key < mn ? key : mn;
-        mx = key > mx ? key : mx;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u64 m = __ballot(mine[u]);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        u32 base = 0;
+        if (dev::lane() == leader) base = atomicAdd(&s_cnt, u32(__popcll(m)));
+        base = u32(__shfl(int(base), leader, 64));
+        if (mine[u]) {
+          const u32 sidx = base + mbcnt(m);
+          if (sidx < u32(kPivotLdsKeys)) keys[sidx] = key[u];
+          mn = key[u] < mn ? key[u] : mn;
+          mx = key[u] > mx ? key[u] : mx;
+        }
       }
     }
   }
@@ -533,9 +596,18 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
   // 3. the pivot row (composite keys are unique)
   for (int r = 0; r < mv.P; ++r) {
     const u32 c = mv.count(r);
-    for (u32 k = tid; k < c; k += kPivotThreads) {
-      const float* row = mv.row(r, k);
-      if (mv.node(row) == h && mv.key(row) == prefix) {
+    for (u32 k0 = 0; k0 < c; k0 += U * kPivotThreads) {
+      bool hit[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u32 k = k0 + u * kPivotThreads + tid;
+        const float* row = mv.row(r, k < c ? k : 0u);
+        hit[u] = k < c && mv.node(row) == h && mv.key(row) == prefix;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!hit[u]) continue;
+        const float* row = mv.row(r, k0 + u * kPivotThreads + tid);
         s_found = 1;
         pivots[h] = prefix;
         float* tr = top_rows + size_t(h) * (dim + 1);
@@ -723,6 +795,9 @@ __global__ __launch_bounds__(kBlock) void k_bm_block_sums(const u32* __restrict_
 
 // ids[recv_off[s] + k] = id_base[s] + (position of the k-th set bit of source s's bitmap):
 // the rows of a source arrive in its stable pack order, i.e. by increasing source row.
+// Words are taken lane-consecutively (word w0 + j * kBlock + tid for round j), so every round's
+// ids land in one contiguous run: each lane writes its ~4 set bits (at 1/8 density) next to
+// its neighbours' instead of walking 256 bits of its own range alone.
 __global__ __launch_bounds__(kBlock) void k_bm_ids(const u32* __restrict__ bm, int nblk, const u32* __restrict__ bsum,
                                                    BmSources src, u32* __restrict__ ids, u32* __restrict__ err) {
   constexpr int kPer = kBmWords / kBlock;
@@ -731,44 +806,53 @@ __global__ __launch_bounds__(kBlock) void k_bm_ids(const u32* __restrict__ bm, i
   const i64 last = ws > 0 ? (ws - 1) / kBmWords : 0;  // this source's last block
   if (b > last) return;
   __shared__ u32 part[kBlock / 64];
-  __shared__ u32 wtot[kBlock / 64];
-  // words of blocks before b
+  __shared__ u32 wtot[kPer][kBlock / 64];
+  // set bits in blocks before b
   u32 pre = 0;
   for (int k = threadIdx.x; k < b; k += kBlock) pre += bsum[i64(s) * nblk + k];
   for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
   if (dev::lane() == 0) part[threadIdx.x / 64] = pre;
   const u32* sb = bm + src.bm_off[s];
-  const i64 w0 = i64(b) * kBmWords + i64(threadIdx.x) * kPer;
-  u32 words[kPer], cnt = 0;
+  const i64 wb = i64(b) * kBmWords;
+  const int wv = threadIdx.x / 64;
+  u32 words[kPer], incl[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
-    words[j] = w0 + j < ws ? sb[w0 + j] : 0u;
-    cnt += u32(__popc(words[j]));
+    const i64 w = wb + j * kBlock + threadIdx.x;
+    words[j] = w < ws ? sb[w] : 0u;
   }
-  const u32 incl = dev::wave_incl_scan(cnt);
-  if (dev::lane() == 63) wtot[threadIdx.x / 64] = incl;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    incl[j] = dev::wave_incl_scan(u32(__popc(words[j])));
+    if (dev::lane() == 63) wtot[j][wv] = incl[j];
+  }
   __syncthreads();
-  u32 base = 0, before = 0;
-  for (int v = 0; v < kBlock / 64; ++v) {
-    base += part[v];
-    if (v < int(threadIdx.x / 64)) before += wtot[v];
-  }
-  u32 k = base + before + incl - cnt;  // rank of this thread's first set bit within source s
+  u32 run = 0;  // set bits of this block before round j
+  for (int v = 0; v < kBlock / 64; ++v) run += part[v];
   const i64 off = src.off[s];
   const u32 idb = src.base[s];
   const i64 cap = src.cnt[s];
+  u32 k = 0;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
+    u32 before = 0, tot = 0;
+    for (int v = 0; v < kBlock / 64; ++v) {
+      if (v < wv) before += wtot[j][v];
+      tot += wtot[j][v];
+    }
     u32 x = words[j];
+    k = run + before + incl[j] - u32(__popc(x));
+    const i64 w = wb + j * kBlock + threadIdx.x;
     while (x) {
       const int t = __ffs(int(x)) - 1;
       x &= x - 1;
-      if (i64(k) < cap) ids[off + k] = idb + u32((w0 + j) * 32 + t);
+      if (i64(k) < cap) ids[off + k] = idb + u32(w * 32 + t);
       else atomicOr(err, 8u);
       ++k;
     }
+    run += tot;
   }
-  if (b == last && threadIdx.x == kBlock - 1 && i64(k) != cap) atomicOr(err, 8u);
+  if (b == last && threadIdx.x == 0 && i64(run) != cap) atomicOr(err, 8u);
 }
 
 // pattern fill of 64-bit words; words j with (j % period) == slot get `alt` instead (the count
@@ -813,6 +897,15 @@ void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream
 void top_bbox(const TopPoints& p, i64* box, hipStream_t stream) {
   if (p.n <= 0) return;
   const int dim = p.dim;
+  if (reinterpret_cast<uintptr_t>(p.pts) % 16 == 0 && p.n * dim >= 4) {
+    // 4 T4 a multiple of dim: T4 a multiple of dim / gcd(dim, 4)
+    const i64 g = dim % 4 == 0 ? 4 : (dim % 2 == 0 ? 2 : 1), unit = dim / g;
+    const i64 want = std::min<i64>((p.n * dim) / 4, i64(2048) * kBlock);
+    const i64 T4 = std::max<i64>(unit, (want / unit) * unit);
+    k_top_bbox4<<<int((T4 + kBlock - 1) / kBlock), kBlock, size_t(2) * dim * 4, stream>>>(p, T4, box);
+    PKD_LAUNCH_CHECK();
+    return;
+  }
   // up to 2048 blocks of 8 loads in flight per thread; one LDS-reduced atomic pair per block and axis
   const i64 want = std::min<i64>(p.n * dim, i64(2048) * kBlock);
   const i64 T = std::max<i64>(dim, (want / dim) * dim);
