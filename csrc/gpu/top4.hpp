@@ -69,7 +69,7 @@ struct IO {
 };
 
 struct Tune {
-  int sample_log2 = 20;  // sample rows = 2^sample_log2 (capped at n / 4)
+  int sample_log2 = 0;  // sample rows = 2^sample_log2 (capped at n / 4); 0: by size (2^20 at 100 M)
   float z = 9.0f;        // band half-width in sample-rank standard deviations (PKD_TOP_Z)
   int scatter_blocks = 0;  // 0: by size
   // Diagnostics (PKD_TOP_DIAG; timing only, the tree is NOT built): 1 stop after the scatter,

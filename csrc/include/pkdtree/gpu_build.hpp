@@ -67,7 +67,7 @@ struct Tuning {
   // scatter pass from the AoS input, exact fix-up of the staged band rows.
   bool top = true;            // PKD_TOP=0: levels 0..3 by the exact pairs
   i64 top_min_n = 10000000;  // PKD_TOP_MIN_N: smallest build that samples its top levels (8 M: 1.18 ms sampled vs 1.16 paired; 12.5 M: 1.49 vs 1.58)
-  int top_sample_log2 = 20;   // PKD_TOP_SAMPLE: log2 of the sample rows
+  int top_sample_log2 = 0;    // PKD_TOP_SAMPLE: log2 of the sample rows (0: by size, 2^20 at 100 M)
   float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
   int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
   int top_diag = 0;           // PKD_TOP_DIAG: timing diagnostics of the scatter (no tree; top4::Tune::diag)
