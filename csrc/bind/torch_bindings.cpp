@@ -373,6 +373,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("brute") = false);
   m.def("trace_push", [](const std::string& name) { pk::trace_push(name.c_str()); }, py::arg("name"));
   m.def("trace_pop", &pk::trace_pop);
+  m.def("ab_knob", [](const std::string& name) -> py::object {
+    const char* v = pk::ab_knob(name.c_str());
+    return v ? py::object(py::str(v)) : py::object(py::none());
+  }, py::arg("name"), "Value of an A/B tuning knob: honoured only under PKD_AB=1, else None.");
   m.def("tree_dump", &tree_dump, py::arg("tree_pts"), py::arg("tree_ids"), py::arg("what") = "tree");
   m.def("point_str", &point_str, py::arg("id"), py::arg("coords"));
   m.def("invariant_violations", &invariant_violations, py::arg("tree_pts"), py::arg("tree_ids"),

@@ -2833,43 +2833,62 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 //   than 2048, 1280 or 768 (profiles/r1_level_blocks_sweep.txt).
 // * split: from level 2 (a pair boundary), 4 parts on 4 HIP streams for builds of >= 64 M
 //   points (50 M: time-neutral, 25 M: +3%, 12.5 M: +7%; profiles/r2_split_build.txt).
+const char* ab_knob(const char* name) {
+  const char* v = std::getenv(name);
+  if (v == nullptr) return nullptr;
+  const char* ab = std::getenv("PKD_AB");  // read per call: knobs are read at builder construction only
+  if (ab != nullptr && std::string(ab) == "1") return v;
+  static std::mutex mu;
+  static std::vector<std::string> noted;
+  std::lock_guard<std::mutex> lk(mu);
+  if (std::find(noted.begin(), noted.end(), name) == noted.end()) {
+    noted.emplace_back(name);
+    std::fprintf(stderr, "pkdtree: %s is an A/B knob, ignored without PKD_AB=1\n", name);
+  }
+  return nullptr;
+}
+
 Tuning Tuning::from_env() {
-  auto env_i = [](const char* k, i64 d) -> i64 {
+  auto env_i = [](const char* k, i64 d) -> i64 {  // public knobs
     const char* e = std::getenv(k);
     return e ? std::atoll(e) : d;
   };
+  auto ab_i = [](const char* k, i64 d) -> i64 {  // A/B knobs
+    const char* e = ab_knob(k);
+    return e ? std::atoll(e) : d;
+  };
   Tuning t;
-  t.implicit_ids = env_i("PKD_IMPLICIT_IDS", 1) != 0;
   const char* impl = std::getenv("PKD_SUBTREE_IMPL");
   if (impl) throw std::invalid_argument("PKD_SUBTREE_IMPL was removed: one subtree kernel ships (k_subtree_rank)");
-  t.narrow = env_i("PKD_NARROW", 1) != 0;
-  t.pairs = env_i("PKD_PAIR", 1) != 0;
-  t.triples = env_i("PKD_TRIPLE", 1) != 0;
-  t.triple_from = int(env_i("PKD_TRIPLE_FROM", 3));
-  t.atomic_ranks = int(env_i("PKD_PART_ATOMIC", -1));
-  t.atomic_ranks3 = int(env_i("PKD_PART3_ATOMIC", -1));
-  t.prefix = env_i("PKD_PART_PREFIX", 1) != 0;
-  t.tail = env_i("PKD_TAIL", 1) != 0;
   t.split = env_i("PKD_SPLIT", 1) != 0;
   t.split_trace = std::getenv("PKD_SPLIT_TRACE") != nullptr;
-  t.colgroup = int(env_i("PKD_COLGROUP", 0));
-  t.hist_div = int(std::max<i64>(1, env_i("PKD_HIST_DIV", 2)));
-  t.scan_div = int(std::max<i64>(1, env_i("PKD_SCAN_DIV", 2)));
-  const int pb = int(env_i("PKD_PAIR_BINS", kPairBins));
-  t.pair_bins = (pb >= 64 && pb <= kPairBins && (pb & (pb - 1)) == 0) ? pb : kPairBins;
-  t.level_blocks = std::max<i64>(0, env_i("PKD_LEVEL_BLOCKS", 0));
-  t.stage2_min = std::max<i64>(1, env_i("PKD_STAGE2_MIN", kRefineCap));
-  t.split_level = int(env_i("PKD_SPLIT_LEVEL", 2));
-  t.split_parts = int(env_i("PKD_SPLIT_PARTS", 4));
-  t.split_streams = int(env_i("PKD_SPLIT_STREAMS", 4));
-  t.split_min_n = env_i("PKD_SPLIT_MIN_N", i64(64) << 20);
-  t.split_min_n_3d = env_i("PKD_SPLIT_MIN_N_3D", std::getenv("PKD_SPLIT_MIN_N") ? t.split_min_n : i64(512) << 20);
   t.top = env_i("PKD_TOP", 1) != 0;
-  t.top_min_n = env_i("PKD_TOP_MIN_N", t.top_min_n);
-  t.top_sample_log2 = int(env_i("PKD_TOP_SAMPLE", t.top_sample_log2));
-  if (const char* z = std::getenv("PKD_TOP_Z")) t.top_z = float(std::atof(z));
-  t.top_blocks = int(env_i("PKD_TOP_BLOCKS", 0));
-  t.top_diag = int(env_i("PKD_TOP_DIAG", 0));
+  t.implicit_ids = ab_i("PKD_IMPLICIT_IDS", 1) != 0;
+  t.narrow = ab_i("PKD_NARROW", 1) != 0;
+  t.pairs = ab_i("PKD_PAIR", 1) != 0;
+  t.triples = ab_i("PKD_TRIPLE", 1) != 0;
+  t.triple_from = int(ab_i("PKD_TRIPLE_FROM", 3));
+  t.atomic_ranks = int(ab_i("PKD_PART_ATOMIC", -1));
+  t.atomic_ranks3 = int(ab_i("PKD_PART3_ATOMIC", -1));
+  t.prefix = ab_i("PKD_PART_PREFIX", 1) != 0;
+  t.tail = ab_i("PKD_TAIL", 1) != 0;
+  t.colgroup = int(ab_i("PKD_COLGROUP", 0));
+  t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
+  t.scan_div = int(std::max<i64>(1, ab_i("PKD_SCAN_DIV", 2)));
+  const int pb = int(ab_i("PKD_PAIR_BINS", kPairBins));
+  t.pair_bins = (pb >= 64 && pb <= kPairBins && (pb & (pb - 1)) == 0) ? pb : kPairBins;
+  t.level_blocks = std::max<i64>(0, ab_i("PKD_LEVEL_BLOCKS", 0));
+  t.stage2_min = std::max<i64>(1, ab_i("PKD_STAGE2_MIN", kRefineCap));
+  t.split_level = int(ab_i("PKD_SPLIT_LEVEL", 2));
+  t.split_parts = int(ab_i("PKD_SPLIT_PARTS", 4));
+  t.split_streams = int(ab_i("PKD_SPLIT_STREAMS", 4));
+  t.split_min_n = ab_i("PKD_SPLIT_MIN_N", i64(64) << 20);
+  t.split_min_n_3d = ab_i("PKD_SPLIT_MIN_N_3D", ab_knob("PKD_SPLIT_MIN_N") ? t.split_min_n : i64(512) << 20);
+  t.top_min_n = ab_i("PKD_TOP_MIN_N", t.top_min_n);
+  t.top_sample_log2 = int(ab_i("PKD_TOP_SAMPLE", t.top_sample_log2));
+  if (const char* z = ab_knob("PKD_TOP_Z")) t.top_z = float(std::atof(z));
+  t.top_blocks = int(ab_i("PKD_TOP_BLOCKS", 0));
+  t.top_diag = int(ab_i("PKD_TOP_DIAG", 0));
   return t;
 }
 

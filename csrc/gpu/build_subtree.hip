@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "device_utils.hpp"
+#include "pkdtree/gpu_build.hpp"
 #include "pkdtree/hip_check.hpp"
 #include "subtree.hpp"
 #include "subtree_common.hpp"
@@ -646,15 +647,15 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
             std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
   {
     static const bool wide = [] {
-      const char* e = std::getenv("PKD_SUBTREE_WIDE");
+      const char* e = ab_knob("PKD_SUBTREE_WIDE");
       return !(e && std::string(e) == "0");
     }();
     static const std::string cfg = [] {
-      const char* e = std::getenv("PKD_SUBTREE_CFG");
+      const char* e = ab_knob("PKD_SUBTREE_CFG");
       return std::string(e ? e : "");
     }();
     static const bool c1536 = [] {
-      const char* e = std::getenv("PKD_SUBTREE_1536");
+      const char* e = ab_knob("PKD_SUBTREE_1536");
       return !(e && std::string(e) == "0");
     }();
     if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);

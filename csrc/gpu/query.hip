@@ -7,6 +7,7 @@
 #include <string>
 
 #include "device_utils.hpp"
+#include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_query.hpp"
 #include "pkdtree/hip_check.hpp"
 #include "pkdtree/trace.hpp"
@@ -887,7 +888,7 @@ void launch_nn_wave(const float* P, const u32* ids, i64 n, int dim, int depth0, 
 }
 
 int traverse_mode() {  // PKD_TRAVERSE=thread: one thread per query (the older kernel)
-  const char* e = std::getenv("PKD_TRAVERSE");
+  const char* e = ab_knob("PKD_TRAVERSE");
   return e && std::string(e) == "thread" ? 1 : 0;
 }
 }  // namespace

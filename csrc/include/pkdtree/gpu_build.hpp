@@ -36,9 +36,15 @@ struct BuildOptions {
   bool allow_top = true;
 };
 
-// A/B and diagnostic knobs of the builder (PKD_* environment variables, README "Tuning"),
-// read ONCE when a builder is constructed -- never while a build is being enqueued. The
-// defaults are the measured best on MI355X (profiles/ holds the sweeps).
+// Value of an A/B knob (PKD_* variable that only exists to rerun a measured sweep): the variable
+// is honoured only under PKD_AB=1, so a stray setting cannot silently change the build. Without
+// PKD_AB=1 a set knob is ignored with a one-time note on stderr, and nullptr is returned.
+const char* ab_knob(const char* name);
+
+// Knobs of the builder (PKD_* environment variables, README "Tuning"), read ONCE when a builder
+// is constructed -- never while a build is being enqueued. The defaults are the measured best on
+// MI355X (profiles/ holds the sweeps). Public: PKD_SPLIT, PKD_TOP and the diagnostic traces;
+// every other field is an A/B knob (ab_knob, PKD_AB=1).
 struct Tuning {
   bool implicit_ids = true;   // PKD_IMPLICIT_IDS=0: the prep writes generated ids
   bool narrow = true;         // PKD_NARROW=0: full columns at high dims

@@ -104,3 +104,18 @@ def test_cpu_invariant_checker_catches_corruption():
     tp[[10, 4000]] = tp[[4000, 10]]
     ti[[10, 4000]] = ti[[4000, 10]]
     assert pk.KDTree(tp, ti).invariant_violations() > 0
+
+
+def test_ab_knobs_need_opt_in(monkeypatch, capfd):
+    """A/B tuning knobs (PKD_PAIR, PKD_TOP_Z, ...) change the build only under PKD_AB=1: a stray
+    setting is ignored with a note on stderr, so the defaults are what runs."""
+    from parallel_kd_tree_amd.ops import native as _ext
+
+    monkeypatch.delenv("PKD_AB", raising=False)
+    monkeypatch.setenv("PKD_TOP_Z", "0.5")
+    assert _ext().ab_knob("PKD_TOP_Z") is None
+    assert "PKD_TOP_Z is an A/B knob" in capfd.readouterr().err
+    monkeypatch.setenv("PKD_AB", "1")
+    assert _ext().ab_knob("PKD_TOP_Z") == "0.5"
+    monkeypatch.delenv("PKD_TOP_Z")
+    assert _ext().ab_knob("PKD_TOP_Z") is None

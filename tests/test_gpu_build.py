@@ -53,6 +53,7 @@ def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic):
     """Three levels per scatter pass (k_scan2 + k_partition3, from level 0 or 3) with zone ranks
     from wave ballots or LDS atomics (also in the pair scatters): slot for slot the CPU exact
     tree on uniform, duplicate-heavy, 2-D, 8-D and odd-depth inputs."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TAIL", "0")  # the last three levels stay triples too
     monkeypatch.setenv("PKD_TRIPLE_FROM", triple_from)
     monkeypatch.setenv("PKD_PART_ATOMIC", atomic)
@@ -84,6 +85,7 @@ def test_tail_levels(gpu_device, monkeypatch, n, dim):
     """The last three global levels in one workgroup per segment (k_tail3: bucket bins, wave
     ranking of the median bin or the radix-select fallback for heavy duplicates, LDS-staged
     leaf scatter): slot for slot the CPU exact tree."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TAIL", "1")
     b = ops.GpuTreeBuilder(n, dim)
     assert "tail" in b.describe(), b.describe()
@@ -95,6 +97,7 @@ def test_tail_levels(gpu_device, monkeypatch, n, dim):
 
 def test_tail_levels_off_equal(gpu_device, monkeypatch):
     x = pk.generate_problem(5, 3, 3_000_000).to(gpu_device)
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TAIL", "1")
     _, ti = ops.GpuTreeBuilder(3_000_000, 3).build(x)
     monkeypatch.setenv("PKD_TAIL", "0")
@@ -149,6 +152,7 @@ def test_narrow_columns_explicit_ids(gpu_device, monkeypatch):
     x = pk.generate_problem(11, dim, n)
     ids = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32) + 7
     cp, ci = ops.build_cpu(x, ids, "exact", 0, 8)
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     for narrow in ("1", "0"):
         monkeypatch.setenv("PKD_NARROW", narrow)
         b = ops.GpuTreeBuilder(n, dim, 0, 0)
@@ -163,6 +167,7 @@ def test_large_stage2_pairs_prefix_placement(gpu_device, monkeypatch, prefix):
     # prefix placement of the top pairs (per-block offsets from k_hist2p's counts) on skewed
     # data: one axis takes few distinct values, so median buckets are huge and many rows are
     # appended with cursor atomics after the certain rows; PKD_PART_PREFIX=0 is the counting pass
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_PART_PREFIX", prefix)
     x = pk.generate_problem(6, 3, 18_000_000)
     x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
@@ -249,6 +254,7 @@ def test_hipgraph_replay_equals_eager(gpu_device, n):
 def test_split_build_equals_cpu(gpu_device, monkeypatch, level, parts, streams):
     """Split build (from a pair boundary on, segment ranges on several HIP streams with their own
     histogram sets) at sizes below its default threshold: slot for slot the CPU exact tree."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
     monkeypatch.setenv("PKD_SPLIT_LEVEL", str(level))
     monkeypatch.setenv("PKD_SPLIT_PARTS", str(parts))
@@ -262,6 +268,7 @@ def test_split_build_equals_cpu(gpu_device, monkeypatch, level, parts, streams):
 def test_split_build_stage2_skewed(gpu_device, monkeypatch):
     """Split build whose parts start with second-stage levels and prefix placement (18 M
     points, split after the first pair) on skewed data."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
     x = pk.generate_problem(6, 3, 18_000_000)
     x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
@@ -271,6 +278,7 @@ def test_split_build_stage2_skewed(gpu_device, monkeypatch):
 def test_split_build_hipgraph(gpu_device, monkeypatch):
     """A split build captured into a hipGraph (fork / join events across the side streams)
     replays to the eager tree."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
     n, dim = 2_000_003, 3
     x = pk.generate_slice(9, dim, 0, n, device=gpu_device)
@@ -340,6 +348,7 @@ def test_traversal_kernels_equal_brute(gpu_device, monkeypatch, n, dim, nq, dept
     q = torch.cat([x[n:], x[: nq // 4]]).to(gpu_device)  # a quarter of the queries hit a point exactly
     pb = t.query_packed(q, "brute")
     pw = t.query_packed(q, "traverse")
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TRAVERSE", "thread")
     pt = t.query_packed(q, "traverse")
     assert torch.equal(pb, pw) and torch.equal(pb, pt)

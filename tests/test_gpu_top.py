@@ -27,6 +27,7 @@ def _same_as_cpu(x, dev, depth0=0, ids=None, expect_top=True):
 
 @pytest.fixture
 def top_always(monkeypatch):
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TOP_MIN_N", "0")
 
 
@@ -96,6 +97,7 @@ def test_top_20m_equals_pairs(gpu_device, monkeypatch):
 def test_top_band_miss_detected_and_rebuilt(gpu_device, top_always, monkeypatch):
     """Bands far too narrow (z = 0.01) miss their medians: the build must REPORT it (bit 0x20),
     never return a wrong tree silently, and KDTree.build must rebuild it exactly."""
+    monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TOP_Z", "0.01")
     x = pk.generate_problem(21, 3, 400_000)
     b = ops.GpuTreeBuilder(x.shape[0], 3, 0, 0)

@@ -82,6 +82,7 @@ for dim in args.dim:
               flush=True)
         del b0
         os.environ["PKD_SPLIT"] = "1"
+        os.environ["PKD_AB"] = "1"  # the PKD_SPLIT_* sweep knobs are A/B knobs
         if args.min_n is not None:
             os.environ["PKD_SPLIT_MIN_N"] = str(args.min_n)
         for cfg in args.cfg:

@@ -9,6 +9,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("PKD_AB", "1")  # PKD_TOP_MIN_N is an A/B knob
 os.environ.setdefault("PKD_TOP_MIN_N", "0")
 import torch  # noqa: E402
 

@@ -7,6 +7,7 @@ import os
 import sys
 import time
 
+os.environ["PKD_AB"] = "1"  # PKD_TOP_DIAG / PKD_TOP_BLOCKS are A/B knobs
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
