@@ -6,6 +6,6 @@ OUT=$1; ROUNDS=$2; VARS=$3; shift 3
 for r in $(seq 1 "$ROUNDS"); do
   for v in $VARS; do
     echo "== round $r $v" >> "$OUT"
-    env $(echo "$v" | tr , " ") PKD_SKIP_BUILD=1 timeout -k 10 150 python bench.py "$@" 2>&1 | grep -v amdgpu.ids >> "$OUT"
+    env PKD_AB=1 $(echo "$v" | tr , " ") PKD_SKIP_BUILD=1 timeout -k 10 150 python bench.py "$@" 2>&1 | grep -v amdgpu.ids >> "$OUT"
   done
 done

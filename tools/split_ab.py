@@ -29,6 +29,7 @@ knobs = sorted({kv.split("=")[0] for v in args.var for kv in v.split(":", 1)[1].
 
 
 def apply(spec):
+    os.environ["PKD_AB"] = "1"  # the variants' knobs are A/B knobs
     for k in knobs:
         os.environ.pop(k, None)
     for kv in spec.split(","):
