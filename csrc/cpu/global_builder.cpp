@@ -464,21 +464,25 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
   for (;;) {  // until no middle bucket overflows its all-gather slot
     // 1. bounding box: one allreduce(MIN) of the encoded per-rank boxes
     auto* box = static_cast<i64*>(buf(0, size_t(2 * dim) * 8));
-    fill_u64(box, 2 * dim, 0xffffffffull, s);
-    top_bbox(tp, box, s);
-    comm_.allreduce_min_i64(box, size_t(2 * dim), s);
     auto* cells = static_cast<float*>(buf(1, size_t(2 * T - 1) * dim * 2 * 4));
-    top_root_cell(box, dim, cells, s);
     auto* node = static_cast<u32*>(buf(2, size_t(std::max<i64>(n_local, 1)) * 4));
     auto* pivots = static_cast<u64*>(buf(3, size_t(std::max(T - 1, 1)) * 8));
-    fill_u64(pivots, std::max(T - 1, 1), ~0ull, s);
     top_rows = static_cast<float*>(buf(4, size_t(std::max(T - 1, 1)) * (dim + 1) * 4 + 8));  // + 8: 64-bit fill
-    fill_u64(top_rows, (i64(std::max(T - 1, 1)) * (dim + 1) + 1) / 2, 0ull, s);
     auto* err = static_cast<u32*>(buf(5, 16));
-    fill_u64(err, 2, 0ull, s);
     auto* sel = static_cast<u32*>(buf(6, size_t(kTopMaxNodes) * 4 * 4));
     u32* hist[2] = {static_cast<u32*>(buf(7, size_t(kTopBins) * 4)), static_cast<u32*>(buf(17, size_t(kTopBins) * 4))};
-    if (LL > 0) fill_u64(hist[0], kTopBins / 2, 0ull, s);
+    {  // the top phase's initial state, one launch
+      FillSegs f;
+      f.add(box, 2 * dim, 0xffffffffull);
+      f.add(pivots, std::max(T - 1, 1), ~0ull);
+      f.add(top_rows, (i64(std::max(T - 1, 1)) * (dim + 1) + 1) / 2, 0ull);
+      f.add(err, 2, 0ull);
+      if (LL > 0) f.add(hist[0], kTopBins / 2, 0ull);
+      fill_u64_multi(f, s);
+    }
+    top_bbox(tp, box, s);
+    comm_.allreduce_min_i64(box, size_t(2 * dim), s);
+    top_root_cell(box, dim, cells, s);
     // 2. top levels: level 0's histogram, then per level one fused pass (median-bucket rows
     // staged, every other row routed to its child and counted into the next level's histogram)
     // and, after the pivot, the fix-up of the staged rows

@@ -218,15 +218,18 @@ __global__ __launch_bounds__(kBlock) void k_top_select(const u32* __restrict__ h
   const int b0 = min(bins, int(threadIdx.x) * per), b1 = min(bins, b0 + per);
   u32 s = 0;
   for (int b = b0; b < b1; ++b) s += hs[b];
-  part[threadIdx.x] = s;
+  // exclusive scan of the 256 partial sums: wave scans, then the wave totals
+  __shared__ u32 wtot[kBlock / 64];
+  const u32 incl = dev::wave_incl_scan(s);
+  if (dev::lane() == 63) wtot[threadIdx.x / 64] = incl;
   __syncthreads();
-  if (threadIdx.x == 0) {  // 256 partial sums: a serial scan is cheaper than a barrier tree here
-    u32 acc = 0;
-    for (int t = 0; t < kBlock; ++t) {
-      const u32 v = part[t];
-      part[t] = acc;
-      acc += v;
-    }
+  u32 wbase = 0, acc = 0;
+  for (int w = 0; w < kBlock / 64; ++w) {
+    wbase += w < int(threadIdx.x / 64) ? wtot[w] : 0u;
+    acc += wtot[w];
+  }
+  part[threadIdx.x] = wbase + incl - s;
+  if (threadIdx.x == 0) {
     if (i64(acc) != size) atomicOr(err, 2u);
     if (size == 0) {
       sel[4 * j + 0] = 0xffffffffu;
@@ -443,11 +446,20 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
     for (int c = tid; c <= dim; c += kPivotThreads) top_rows[size_t(h) * (dim + 1) + c] = 0.0f;
     return;
   }
-  if (tid == 0) {
-    s_cnt = 0;
-    s_found = 0;
-    for (int r = 0; r < mv.P; ++r)
-      if (reinterpret_cast<const u32*>(mv.g + r * mv.stride)[0] > u32(mv.cap)) atomicOr(err, 1u);
+  __shared__ u32 s_pre[kTopMaxRanks + 1];  // rank r's middle rows: s_pre[r + 1] - s_pre[r]
+  static_assert(kTopMaxRanks == 64, "one lane per rank");
+  if (tid < 64) {  // lane r: rank r's row count (all loads in flight at once), a wave scan
+    const int r = tid;
+    const u32 raw = r < mv.P ? reinterpret_cast<const u32*>(mv.g + r * mv.stride)[0] : 0u;
+    if (raw > u32(mv.cap)) atomicOr(err, 1u);
+    const u32 c = min(raw, u32(mv.cap));
+    const u32 incl = dev::wave_incl_scan(c);
+    if (r < mv.P) s_pre[r] = incl - c;
+    if (r == mv.P - 1) s_pre[mv.P] = incl;
+    if (r == 0) {
+      s_cnt = 0;
+      s_found = 0;
+    }
   }
   __syncthreads();
   // 1. this node's keys into LDS (one reservation per wave, not one same-address atomic per
@@ -455,8 +467,10 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
   u64 mn = ~0ull, mx = 0ull;
   constexpr int U = 4;  // rows per thread per round: their loads in flight together (one block
                         // per node walks every rank's middle rows, so rounds are latency-bound)
+  // (one flat index space over all ranks with 16 rows per thread, a binary search per row for its
+  // rank, measured slower: P = 8 levels 1 / 2 48 -> 58 / 67 -> 74 us)
   for (int r = 0; r < mv.P; ++r) {
-    const u32 c = mv.count(r);
+    const u32 c = s_pre[r + 1] - s_pre[r];
     for (u32 k0 = 0; k0 < c; k0 += U * kPivotThreads) {  // uniform trip count: wave ballots below
       bool mine[U];
       u64 key[U];
@@ -464,8 +478,9 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
       for (int u = 0; u < U; ++u) {
         const u32 k = k0 + u * kPivotThreads + tid;
         const float* row = mv.row(r, k < c ? k : 0u);
-        mine[u] = k < c && mv.node(row) == h;
+        const u32 nd = mv.node(row);  // loaded unconditionally: no wait per row
         key[u] = mv.key(row);
+        mine[u] = (k < c) & (nd == h);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -595,14 +610,16 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
   }
   // 3. the pivot row (composite keys are unique)
   for (int r = 0; r < mv.P; ++r) {
-    const u32 c = mv.count(r);
+    const u32 c = s_pre[r + 1] - s_pre[r];
     for (u32 k0 = 0; k0 < c; k0 += U * kPivotThreads) {
       bool hit[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const u32 k = k0 + u * kPivotThreads + tid;
         const float* row = mv.row(r, k < c ? k : 0u);
-        hit[u] = k < c && mv.node(row) == h && mv.key(row) == prefix;
+        const u32 nd = mv.node(row);
+        const u64 kk = mv.key(row);
+        hit[u] = (k < c) & (nd == h) & (kk == prefix);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -710,11 +727,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
   for (i64 c0 = b0; c0 < b1; c0 += U * kBlock) {
     int d[U];
     u32 my[U];
+    float3 row3[U];  // dim 3: the rows are loaded with their nodes, before the ranking (the
+                     // stores below would otherwise wait on each row's load in turn)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const i64 i = c0 + u * kBlock + threadIdx.x;
       const u32 h = i < b1 ? (levels > 0 ? node[i] : 0u) : kTopDone;
       d[u] = (h == kTopDone || h - first >= u32(T)) ? -1 : int(h - first);
+      if (dim == 3) row3[u] = *reinterpret_cast<const float3*>(p.pts + (i < b1 ? i : b0) * 3);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -741,7 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
       const float* r = p.pts + i * dim;
       if (cs > 0) {
         if (dim == 3) {  // one 12-B row load, three coalesced plane stores
-          const float3 v = *reinterpret_cast<const float3*>(r);
+          const float3 v = row3[u];
           out[k] = v.x;
           out[cs + k] = v.y;
           out[2 * cs + k] = v.z;
@@ -751,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(TopPoints p, const u32*
       } else {
         float* o = out + k * rs;
         if (dim == 3) {  // one 12-B load and store per row (dwordx3) instead of three dword pairs
-          *reinterpret_cast<float3*>(o) = *reinterpret_cast<const float3*>(r);
+          *reinterpret_cast<float3*>(o) = row3[u];
         } else {
           for (int c = 0; c < dim; ++c) o[c] = r[c];
         }
@@ -865,10 +885,28 @@ __global__ void k_fill64(u64* __restrict__ p, i64 n, u64 v, int period, int slot
   }
 }
 
+// blockIdx.y: the segment
+__global__ void k_fill64_multi(FillSegs f) {
+  const int i = blockIdx.y;
+  u64* p = f.p[i];
+  const u64 v = f.v[i];
+  for (i64 j = i64(blockIdx.x) * blockDim.x + threadIdx.x; j < f.n[i]; j += i64(gridDim.x) * blockDim.x) p[j] = v;
+}
+
 int pack_blocks(i64 n) { return int(std::max<i64>(1, std::min<i64>(2048, (n + 8191) / 8192))); }
 int stream_grid(i64 n) { return int(std::max<i64>(1, std::min<i64>(512, (n + 16383) / 16384))); }
 
 }  // namespace
+
+void fill_u64_multi(const FillSegs& f, hipStream_t stream) {
+  if (f.count <= 0) return;
+  if (f.count > kFillSegs) throw std::invalid_argument("fill_u64_multi: too many segments");
+  i64 nmax = 0;
+  for (int i = 0; i < f.count; ++i) nmax = std::max(nmax, f.n[i]);
+  const int gx = int(std::max<i64>(1, std::min<i64>(64, (nmax + 255) / 256)));
+  k_fill64_multi<<<dim3(gx, f.count), 256, 0, stream>>>(f);
+  PKD_LAUNCH_CHECK();
+}
 
 void fill_u64(void* p, i64 n, u64 v, hipStream_t stream) {
   if (n <= 0) return;
@@ -963,6 +1001,7 @@ void top_fixup(const float* buf, i64 cap, int dim, int level, int axis, int next
 
 void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream) {
+  if (P < 1 || P > kTopMaxRanks) throw std::invalid_argument("top_pivot: 1 <= P <= 64 ranks");
   const size_t lds = size_t(kPivotLdsKeys) * 8;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&k_top_pivot), int(lds));
   MidView mv{gathered, i64(top_middle_words(dim, cap)), cap, P, dim, axis};

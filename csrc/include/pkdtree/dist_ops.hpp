@@ -22,6 +22,7 @@ namespace pkdtree {
 
 constexpr u32 kTopDone = 0xffffffffu;  // node index of a point that became a top-tree pivot
 constexpr int kTopMaxNodes = 32;       // nodes per top level (P <= 64)
+constexpr int kTopMaxRanks = 64;       // ranks whose middle rows one pivot block walks
 constexpr int kTopBins = 8192;         // nodes * bins per top level (LDS histogram)
 
 struct TopPoints {
@@ -43,6 +44,22 @@ struct TopSizes {
 // Device-side fills (kernels, so no host staging and graph-capturable): n 64-bit words of v;
 // the [slots][4] count matrix of top_pack with its id-base / n_local columns set.
 void fill_u64(void* p, i64 n, u64 v, hipStream_t stream);
+// Several independent fills in ONE launch (each launch of a tiny kernel costs ~5 us on the
+// chain): segment i = n[i] 64-bit words of v[i] at p[i]; count <= kFillSegs.
+constexpr int kFillSegs = 8;
+struct FillSegs {
+  u64* p[kFillSegs];
+  i64 n[kFillSegs];
+  u64 v[kFillSegs];
+  int count = 0;
+  void add(void* ptr, i64 words, u64 value) {
+    p[count] = static_cast<u64*>(ptr);
+    n[count] = words;
+    v[count] = value;
+    ++count;
+  }
+};
+void fill_u64_multi(const FillSegs& f, hipStream_t stream);
 void fill_u32(void* p, i64 n, u32 v, hipStream_t stream);
 void top_counts_init(i64* counts, int slots, i64 id_base, i64 n_local, hipStream_t stream);
 
