@@ -17,6 +17,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kPivotThreads = 1024;
+constexpr int kBboxBlocks = 512;      // grid of the bounding-box reduction
 constexpr int kPivotLdsKeys = 16384;  // 128 KiB of keys per node in LDS; larger middles stream from L2
 
 __device__ __forceinline__ u32 point_id(const TopPoints& p, i64 i) { return p.ids ? p.ids[i] : p.id_base + u32(i); }
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(kBlock) void k_top_bbox4(TopPoints p, i64 T4, i64* 
     for (int e = 0; e < 4; ++e) lo[e] = nhi[e] = 0xffffffffu;
     const float4* in = reinterpret_cast<const float4*>(p.pts);
     const float4 first = in[t];
-    constexpr int U = 4;
+    constexpr int U = 8;
     for (i64 q0 = t; q0 < total4; q0 += U * T4) {
       float4 v[U];
 #pragma unroll
@@ -938,14 +939,17 @@ void top_bbox(const TopPoints& p, i64* box, hipStream_t stream) {
   if (reinterpret_cast<uintptr_t>(p.pts) % 16 == 0 && p.n * dim >= 4) {
     // 4 T4 a multiple of dim: T4 a multiple of dim / gcd(dim, 4)
     const i64 g = dim % 4 == 0 ? 4 : (dim % 2 == 0 ? 2 : 1), unit = dim / g;
-    const i64 want = std::min<i64>((p.n * dim) / 4, i64(2048) * kBlock);
+    // 512 blocks x 8 float4 in flight per thread: the read still streams at full rate, and each
+    // box word takes 512 same-address global atomics instead of 2048 (they serialise at the
+    // memory side: 46 us for 12.5 M x 3D with 2048 blocks)
+    const i64 want = std::min<i64>((p.n * dim) / 4, i64(kBboxBlocks) * kBlock);
     const i64 T4 = std::max<i64>(unit, (want / unit) * unit);
     k_top_bbox4<<<int((T4 + kBlock - 1) / kBlock), kBlock, size_t(2) * dim * 4, stream>>>(p, T4, box);
     PKD_LAUNCH_CHECK();
     return;
   }
-  // up to 2048 blocks of 8 loads in flight per thread; one LDS-reduced atomic pair per block and axis
-  const i64 want = std::min<i64>(p.n * dim, i64(2048) * kBlock);
+  // up to kBboxBlocks blocks of 8 loads in flight per thread; one LDS-reduced atomic pair per block and axis
+  const i64 want = std::min<i64>(p.n * dim, i64(kBboxBlocks) * kBlock);
   const i64 T = std::max<i64>(dim, (want / dim) * dim);
   const int grid = int((T + kBlock - 1) / kBlock);
   k_top_bbox<<<grid, kBlock, size_t(2) * dim * 4, stream>>>(p, T, box);
