@@ -463,6 +463,16 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("top_bbox", &bbox);
+  m.def("fill_u64_multi", [](const std::vector<std::tuple<torch::Tensor, int64_t, uint64_t>>& segs) {
+    FillSegs f;
+    hipStream_t s = nullptr;
+    for (const auto& [t, words, value] : segs) {
+      TORCH_CHECK(t.is_cuda() && t.element_size() * t.numel() >= words * 8, "fill_u64_multi: segment too small");
+      s = stream_of(t);
+      f.add(t.data_ptr(), words, value);
+    }
+    fill_u64_multi(f, s);
+  });
   m.def("top_root_cell", &root_cell);
   m.def("top_route_hist", &route_hist);
   m.def("top_select", &select, pybind11::arg("hist"), pybind11::arg("level"), pybind11::arg("bins"),

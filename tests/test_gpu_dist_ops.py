@@ -41,15 +41,26 @@ def _cells(nodes_total, dim, seed):
     return c
 
 
-def test_bbox(gpu_device):
-    x = pk.generate_problem(3, 5, 123_457)
+def test_fill_u64_multi(gpu_device):
+    """Several fills in one launch: each segment gets its own value, nothing past its end is written."""
+    ts = [torch.zeros(n + 3, dtype=torch.int64, device=gpu_device) for n in (1, 6, 4096, 70_001)]
+    vals = [0xFFFFFFFF, -1 & 0xFFFFFFFFFFFFFFFF, 0, 0x123456789]
+    ops.native().fill_u64_multi([(t, t.numel() - 3, v) for t, v in zip(ts, vals)])
+    for t, v in zip(ts, vals):
+        h = t.cpu().numpy().view(np.uint64)
+        assert (h[:-3] == np.uint64(v)).all() and (h[-3:] == 0).all()
+
+
+@pytest.mark.parametrize("n,dim", [(123_457, 5), (2_000_003, 3), (1_500_001, 8)])
+def test_bbox(gpu_device, n, dim):
+    x = pk.generate_problem(3, dim, n)
     x[17, 2] = -0.0
-    box = torch.full((10,), 0xFFFFFFFF, dtype=torch.int64, device=gpu_device)
+    box = torch.full((2 * dim,), 0xFFFFFFFF, dtype=torch.int64, device=gpu_device)
     nat = ops.native()
     nat.top_bbox(x.to(gpu_device), box)
-    cells = torch.zeros(10, dtype=torch.float32, device=gpu_device)
-    nat.top_root_cell(box, 5, cells)
-    c = cells.cpu().view(5, 2)
+    cells = torch.zeros(2 * dim, dtype=torch.float32, device=gpu_device)
+    nat.top_root_cell(box, dim, cells)
+    c = cells.cpu().view(dim, 2)
     assert torch.equal(c[:, 0], x.amin(0)) and torch.equal(c[:, 1], x.amax(0))
 
 
