@@ -2826,7 +2826,10 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 // Knob defaults, with their measurements:
 // * hist_div 2: the first-level histogram's 4096-bin flush per block is its cost beyond the
 //   key read; half the blocks: 100M x 3D k_hist 130 -> 115 us.
-// * scan_div 2: k_scan's per-block histogram flush (2 x next_bins global atomics) halves and
+// * scan_div: the key sweeps run on ~1024 blocks at every size (half the partition grid from
+//   64 M points, all of it below): their per-block histogram flush (2 x next_bins global atomics)
+//   scales with blocks. 100 M x 3D: 9.12-9.18 ms vs 9.24 on 2048 blocks; 12.5 M: 1.427 vs 1.44 on
+//   512 (profiles/r4_scan_grid_ab.txt). Round 2's reading at 100 M, on pairs:
 //   the sweep stays bandwidth-bound (100M x 3D k_scan 1.57 -> 1.51 ms).
 // * level_blocks: two rounds of 4 workgroups per CU for builds >= 64 M points, one round
 //   below: at 12.5 M points (a rank's share of 100 M on 8 GPUs) 1024 blocks build 7% faster
@@ -2874,7 +2877,7 @@ Tuning Tuning::from_env() {
   t.tail = ab_i("PKD_TAIL", 1) != 0;
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
-  t.scan_div = int(std::max<i64>(1, ab_i("PKD_SCAN_DIV", 2)));
+  t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
   const int pb = int(ab_i("PKD_PAIR_BINS", kPairBins));
   t.pair_bins = (pb >= 64 && pb <= kPairBins && (pb & (pb - 1)) == 0) ? pb : kPairBins;
   t.level_blocks = std::max<i64>(0, ab_i("PKD_LEVEL_BLOCKS", 0));
@@ -2958,6 +2961,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   max_hist_ = 1;
   const i64 level_blocks =
       tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2);
+  scan_div_ = tune_.scan_div > 0 ? tune_.scan_div : int(std::max<i64>(1, level_blocks / (kLevelBlocks / 2)));
   for (int l = 0; l < lg_; ++l) {
     LevelPlan lp;
     lp.level = l;
@@ -3443,7 +3447,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             LevelArgs as = a;  // the key sweeps' own block split (their histogram flush scales with blocks)
-            as.bps = std::max(1, a.bps / tune_.scan_div);
+            as.bps = std::max(1, a.bps / scan_div_);
             k_scan<NC><<<int(segs * as.bps), kBlock, size_t(2 * lp.next_bins + 64) * 4, st>>>(as);
             PKD_LAUNCH_CHECK();
             k_pivot_both<NC><<<gs + int(segs), kBlock, 0, st>>>(a, segs, gs);
@@ -3477,7 +3481,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           constexpr int NC = decltype(nc)::value;
           if constexpr (NC > 0) {
             LevelArgs as = a;  // the scan's own block split (its histogram flush scales with blocks)
-            as.bps = std::max(1, a.bps / tune_.scan_div);
+            as.bps = std::max(1, a.bps / scan_div_);
             k_scan<NC><<<int(segs * as.bps), kBlock, lds_a, st>>>(as);
             PKD_LAUNCH_CHECK();
             k_pivot_both<NC><<<gs + int(segs), kBlock, 0, st>>>(a, segs, gs);

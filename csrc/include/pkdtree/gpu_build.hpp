@@ -59,7 +59,7 @@ struct Tuning {
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
   int colgroup = 0;           // PKD_COLGROUP: columns per load round of wide rows (0: by dim)
   int hist_div = 2;           // PKD_HIST_DIV: first-level histogram on 1/hist_div of the blocks
-  int scan_div = 2;           // PKD_SCAN_DIV: k_scan on 1/scan_div of the blocks
+  int scan_div = 0;           // PKD_SCAN_DIV: key sweeps on 1/scan_div of the blocks (0: ~1024 blocks)
   int pair_bins = 2048;       // PKD_PAIR_BINS: bins of a level a paired pass fuses
   i64 level_blocks = 0;       // PKD_LEVEL_BLOCKS: top-level partition grid (0: by n)
   i64 stage2_min = 2048;      // PKD_STAGE2_MIN: second-stage histogram above this median bucket
@@ -185,6 +185,7 @@ class GpuBuilder {
   bool narrow_ = false;  // high-dim: narrow columns + key-slot subtree (capacity nsub_ sized for it)
   int tail_ = -1;        // first of the last three global levels, built by k_tail3 (-1: none)
   int tail_items_ = 0;   // rows per thread of its 1024-thread workgroups
+  int scan_div_ = 1;     // the key sweeps run on 1 / scan_div_ of a level's partition blocks
   bool top_ = false;     // levels 0..3 by the sampled top pass (AoS input builds)
   size_t off_top_ = 0;
   // workspace offsets
