@@ -9,6 +9,6 @@ N=${1:-12500000}
 for r in 1 2; do
   for v in $VARIANTS; do
     echo "== round $r n $N $v" >> $O
-    env PKD_AB=1 PKD_SPLIT=0 $(echo "$v" | tr , " ") timeout -k 10 100 python3 tools/bench_build.py --n $N --dim 3 --steps 30 2>&1 | grep '^{' >> $O || exit 1
+    env PKD_AB=1 PKD_SPLIT=0 $(echo "$v" | tr , " ") timeout -k 10 100 python3 tools/bench_build.py --n $N --dim ${DIM:-3} --steps ${STEPS:-30} 2>&1 | grep '^{' >> $O || exit 1
   done
 done
