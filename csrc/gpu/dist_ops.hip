@@ -18,7 +18,9 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPivotThreads = 1024;
 constexpr int kBboxBlocks = 512;      // grid of the bounding-box reduction
-constexpr int kPivotLdsKeys = 16384;  // 128 KiB of keys per node in LDS; larger middles stream from L2
+// keys of a node's middle rows in LDS (+ where each came from: 12 B per row, 156 KiB); larger
+// middles stream from L2. (A 100 M-point build's middle holds ~12.2 K rows at every level.)
+constexpr int kPivotLdsKeys = 13312;
 
 __device__ __forceinline__ u32 point_id(const TopPoints& p, i64 i) { return p.ids ? p.ids[i] : p.id_base + u32(i); }
 
@@ -426,7 +428,8 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
                                                              const u32* __restrict__ sel, u64* __restrict__ pivots,
                                                              float* __restrict__ top_rows, float* __restrict__ cells,
                                                              u32* __restrict__ err) {
-  extern __shared__ __align__(16) u64 keys[];  // [kPivotLdsKeys]
+  extern __shared__ __align__(16) u64 keys[];  // [kPivotLdsKeys], then u32 locs[kPivotLdsKeys]
+  u32* locs = reinterpret_cast<u32*>(keys + kPivotLdsKeys);  // (rank << 26) | row of keys[i]
   __shared__ u32 hist[256];
   __shared__ u32 s_cnt, s_digit, s_rem, s_found, s_bincnt;
   __shared__ u64 s_mn[kPivotThreads / 64], s_mx[kPivotThreads / 64], s_one;
@@ -493,7 +496,10 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
         base = u32(__shfl(int(base), leader, 64));
         if (mine[u]) {
           const u32 sidx = base + mbcnt(m);
-          if (sidx < u32(kPivotLdsKeys)) keys[sidx] = key[u];
+          if (sidx < u32(kPivotLdsKeys)) {
+            keys[sidx] = key[u];
+            locs[sidx] = (u32(r) << 26) | (k0 + u * kPivotThreads + tid);
+          }
           mn = key[u] < mn ? key[u] : mn;
           mx = key[u] > mx ? key[u] : mx;
         }
@@ -609,8 +615,22 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
     }
     __syncthreads();
   }
-  // 3. the pivot row (composite keys are unique)
-  for (int r = 0; r < mv.P; ++r) {
+  // 3. the pivot row (composite keys are unique): from its LDS location, else by walking the rows
+  auto take = [&](const float* row) {
+    s_found = 1;
+    pivots[h] = prefix;
+    float* tr = top_rows + size_t(h) * (dim + 1);
+    for (int q = 0; q <= dim; ++q) tr[q] = row[q];
+    cl[2 * axis + 1] = row[axis];
+    cr[2 * axis] = row[axis];
+  };
+  // locations fit 26 bits of row index while every rank holds < 2^26 middle rows
+  const bool by_loc = in_lds && s_pre[mv.P] < (1u << 26);
+  if (by_loc) {
+    for (u32 k = tid; k < m; k += kPivotThreads)
+      if (keys[k] == prefix) take(mv.row(int(locs[k] >> 26), locs[k] & ((1u << 26) - 1u)));
+  }
+  for (int r = 0; r < (by_loc ? 0 : mv.P); ++r) {
     const u32 c = s_pre[r + 1] - s_pre[r];
     for (u32 k0 = 0; k0 < c; k0 += U * kPivotThreads) {
       bool hit[U];
@@ -625,13 +645,7 @@ __global__ __launch_bounds__(kPivotThreads) void k_top_pivot(MidView mv, int lev
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (!hit[u]) continue;
-        const float* row = mv.row(r, k0 + u * kPivotThreads + tid);
-        s_found = 1;
-        pivots[h] = prefix;
-        float* tr = top_rows + size_t(h) * (dim + 1);
-        for (int q = 0; q <= dim; ++q) tr[q] = row[q];
-        cl[2 * axis + 1] = row[axis];
-        cr[2 * axis] = row[axis];
+        take(mv.row(r, k0 + u * kPivotThreads + tid));
       }
     }
   }
@@ -1006,7 +1020,7 @@ void top_fixup(const float* buf, i64 cap, int dim, int level, int axis, int next
 void top_pivot(const float* gathered, int P, i64 cap, int level, int axis, int dim, const TopSizes& sizes,
                const u32* sel, u64* pivots, float* top_rows, float* cells, u32* err, hipStream_t stream) {
   if (P < 1 || P > kTopMaxRanks) throw std::invalid_argument("top_pivot: 1 <= P <= 64 ranks");
-  const size_t lds = size_t(kPivotLdsKeys) * 8;
+  const size_t lds = size_t(kPivotLdsKeys) * 12;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&k_top_pivot), int(lds));
   MidView mv{gathered, i64(top_middle_words(dim, cap)), cap, P, dim, axis};
   k_top_pivot<<<1 << level, kPivotThreads, lds, stream>>>(mv, level, sizes, sel, pivots, top_rows, cells, err);
