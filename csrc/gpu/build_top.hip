@@ -184,7 +184,17 @@ __device__ __forceinline__ u32 wave_find_small(const u32* h, int n, u32 rank, u3
 __device__ __forceinline__ void coarse_of(const u32* fine, int gs, u32* co) {
   const int t = threadIdx.x;
   u32 s = 0;
-  for (int e = 0; e < gs; ++e) s += fine[t * gs + e];
+  static_assert(kSampBins / 256 <= 64 && kResBins / 256 <= 64, "coarse_of: at most 16 16-B loads per thread");
+  if (gs % 4 == 0) {  // 16-B loads, all in flight (gs <= 64: at most 16 per thread)
+    const uint4* f4 = reinterpret_cast<const uint4*>(fine + t * gs);
+    uint4 v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = e < gs / 4 ? f4[e] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += v[e].x + v[e].y + v[e].z + v[e].w;
+  } else {
+    for (int e = 0; e < gs; ++e) s += fine[t * gs + e];
+  }
   co[t] = s;
 }
 
