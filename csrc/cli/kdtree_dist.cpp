@@ -194,6 +194,7 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
   const bool ref = o.mode == "reference";
   const bool global = o.decomp == "global";
   std::unique_ptr<GlobalBuilder> gb;
+  size_t wsb_all = 0;
   if (global) {
     gb = std::make_unique<GlobalBuilder>(rcomm, N, dim, o.pipeline_k);
   } else if (local > 0) {  // allocations outside the timed region
@@ -210,34 +211,52 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(local) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(local) * 4));
     PKD_HIP_CHECK(hipMalloc(&ws, std::max<size_t>(wsb, 256)));
+    wsb_all = wsb;
   }
   PKD_HIP_CHECK(hipEventRecord(e0, s));
   nn_init(d_res, Q, s);
   // global 1-based ids (kdtree_mpi.cpp:223)
   // (forest: the trees of this process's logical ranks one after another, one workspace; a
   // sampled-top build that reports a band miss is redone unsampled after the queries)
-  auto build_slice = [&](size_t k, bool allow_top) {
+  size_t ws_bytes = ws ? std::max<size_t>(wsb_all, 256) : 0;
+  // returns the builder that wrote the workspace's error words (the unsampled fallback has its
+  // own plan and workspace layout: the workspace is grown to it, and its error word is read)
+  std::unique_ptr<GpuBuilder> fallback;
+  auto build_slice = [&](size_t k, bool allow_top) -> GpuBuilder* {
     const Slice& sl = slices[k];
     const i64 off = sl.first - first;
-    if (sl.n <= 0) return;
-    if (ref) rbs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
-    else if (allow_top) bs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
-    else GpuBuilder(sl.n, dim, BuildOptions{o.leaf_threshold, 0, true, false})
-             .build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+    if (sl.n <= 0) return nullptr;
+    if (ref) {
+      rbs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+      return nullptr;
+    }
+    GpuBuilder* b = bs[k].get();
+    if (!allow_top) {
+      fallback = std::make_unique<GpuBuilder>(sl.n, dim, BuildOptions{o.leaf_threshold, 0, true, false});
+      if (fallback->workspace_bytes() > ws_bytes) {
+        PKD_HIP_CHECK(hipStreamSynchronize(s));
+        PKD_HIP_CHECK(hipFree(ws));
+        ws_bytes = fallback->workspace_bytes();
+        PKD_HIP_CHECK(hipMalloc(&ws, ws_bytes));
+      }
+      b = fallback.get();
+    }
+    b->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+    return b;
   };
   u32 slice_err = 0;
   if (global) {
     gb->build(d_x, local, u32(first + 1), s);
   } else if (local > 0) {
     for (size_t k = 0; k < slices.size(); ++k) {
-      build_slice(k, true);
+      GpuBuilder* wrote = build_slice(k, true);
       // the shared workspace holds one build's error words; a sampled build is checked here, on
       // this rank alone, BEFORE any collective (its rebuild must not skew the collective order)
-      if (!ref && (slices.size() > 1 || bs[k]->sampled_top())) {
-        u32 e = slices[k].n > 0 ? bs[k]->read_error(ws, s) : 0u;
-        if ((e & top4_band_miss_bit()) && bs[k]->sampled_top()) {
-          build_slice(k, false);
-          e = slices[k].n > 0 ? bs[k]->read_error(ws, s) : 0u;
+      if (wrote && (slices.size() > 1 || wrote->sampled_top())) {
+        u32 e = wrote->read_error(ws, s);
+        if ((e & top4_band_miss_bit()) && wrote->sampled_top()) {
+          wrote = build_slice(k, false);
+          e = wrote->read_error(ws, s);
         }
         slice_err |= e;
       }
@@ -249,8 +268,11 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
   if (global) {
     // routed (GlobalBuilder::query): each query searched in its home block, a MIN all-reduce
     // gives it a radius, then only in the blocks that radius reaches, a second MIN all-reduce
-    // (the top rows between blocks and the boundary rows are brute-forced)
-    gb->query(d_q, Q, d_res, s);
+    // (the top rows between blocks and the boundary rows are brute-forced); --query brute:
+    // brute force over every block of the rank, one MIN all-reduce
+    gb->query(d_q, Q, d_res, s, false,
+              o.query == "brute" ? GlobalBuilder::kQueryBrute
+                                 : (o.query == "traverse" ? GlobalBuilder::kQueryTraverse : GlobalBuilder::kQueryAuto));
   } else if (local > 0) {
     u64* d_one = nullptr;  // reference mode: each tree's search starts afresh, as on its own rank
     if (ref && slices.size() > 1) PKD_HIP_CHECK(hipMalloc(&d_one, size_t(Q) * 8));

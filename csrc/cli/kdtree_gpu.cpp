@@ -62,7 +62,8 @@ int main(int argc, char** argv) {
     PKD_HIP_CHECK(hipMalloc(&d_tree, size_t(N) * dim * 4));
     PKD_HIP_CHECK(hipMalloc(&d_ids, size_t(N) * 4));
     PKD_HIP_CHECK(hipMalloc(&d_res, size_t(Q) * 8));
-    PKD_HIP_CHECK(hipMalloc(&ws, std::max(ref ? rb.workspace_bytes() : b.workspace_bytes(), size_t(256))));
+    size_t ws_bytes = std::max(ref ? rb.workspace_bytes() : b.workspace_bytes(), size_t(256));
+    PKD_HIP_CHECK(hipMalloc(&ws, ws_bytes));
     hipEvent_t e0, e1, e2, e3;
     for (hipEvent_t* e : {&e0, &e1, &e2, &e3}) PKD_HIP_CHECK(hipEventCreate(e));
     PKD_HIP_CHECK(hipEventRecord(e0, s));
@@ -88,7 +89,14 @@ int main(int argc, char** argv) {
     u32 err0 = ref ? 0u : b.read_error(ws, s, detail);
     if ((err0 & top4_band_miss_bit()) && b.sampled_top()) {
       // a sampled top band missed its median (reported, never silent): rebuild unsampled
+      // (its plan differs, e.g. a split build's per-stream histogram sets: the workspace is
+      // grown to its size before the rebuild, never written past)
       GpuBuilder fb(N, dim, BuildOptions{o.leaf_threshold, 0, true, false});
+      if (fb.workspace_bytes() > ws_bytes) {
+        PKD_HIP_CHECK(hipFree(ws));
+        ws_bytes = fb.workspace_bytes();
+        PKD_HIP_CHECK(hipMalloc(&ws, ws_bytes));
+      }
       fb.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);
       nn_init(d_res, Q, s);
       query();

@@ -83,169 +83,12 @@ std::map<std::string, double> GlobalPhases::as_map() const {
 }
 
 // ---------------------------------------------------------------------------------------------
-namespace global_plan {
-
-void segment(i64 n_total, i64 h, i64* lo_out, i64* n_out) {
-  int l = 0;
-  while ((i64(1) << (l + 1)) - 1 <= h) ++l;  // level of heap node h
-  const i64 j = h + 1 - (i64(1) << l);
-  i64 lo = 0, m = n_total;
-  for (int b = l - 1; b >= 0; --b) {
-    if ((j >> b) & 1) {
-      lo = lo + m / 2 + 1;
-      m = std::max<i64>(0, m - m / 2 - 1);
-    } else {
-      m = m / 2;
-    }
-  }
-  *lo_out = lo;
-  *n_out = m;
-}
-
-i64 middle_cap(i64 n_total, int P, int level, int scale) {
-  const i64 expect = n_total * (i64(1) << level) / (i64(kTopBins) * P) + 1;
-  return std::min<i64>(std::max<i64>(2048, 3 * expect) * scale, std::max<i64>(n_total, 1));
-}
-
-int top_levels_for(int P, int pipeline_k) {
-  if (P < 1 || P > 64) throw std::invalid_argument("global decomposition: 1 <= P <= 64 ranks");
-  int L = 0;
-  while ((1 << L) < P) ++L;
-  const bool pow2 = (P & (P - 1)) == 0;
-  // P not a power of two: T = 2^LL leaves split over P ranks as floor / ceil(T / P); 8x more
-  // leaves than the next power of two keeps the busiest rank within ~3-9 % of the mean (P = 3:
-  // 22 / 21 of 64 instead of 6 / 5 of 16), as far as the 6-level cap allows
-  const int extra = pipeline_k >= 0 ? pipeline_k : (P == 2 ? 1 : (pow2 ? 0 : 3));
-  return std::min(6, L + extra);
-}
-
-namespace {
-// heap node between leaves a and a + 1 of the T leaves at the bottom of the top tree: their
-// lowest common ancestor
-i64 gap_node(int T, int a) {
-  i64 x = T - 1 + a, y = T + a;
-  while (x != y) {
-    x = (x - 1) / 2;
-    y = (y - 1) / 2;
-  }
-  return x;
-}
-}  // namespace
-
-Layout make_layout(i64 n_total, int P, int pipeline_k) {
-  Layout lay;
-  lay.P = P;
-  lay.LL = top_levels_for(P, pipeline_k);
-  lay.T = 1 << lay.LL;
-  const int T = lay.T;
-  lay.leaf_lo.resize(size_t(P) + 1);
-  lay.R = 0;
-  for (int r = 0; r <= P; ++r) lay.leaf_lo[size_t(r)] = int(i64(r) * T / P);
-  for (int r = 0; r < P; ++r) lay.R = std::max(lay.R, lay.leaf_lo[size_t(r) + 1] - lay.leaf_lo[size_t(r)]);
-  lay.leaf_slot.assign(size_t(T), 0);
-  lay.leaf_n.assign(size_t(T), 0);
-  lay.top_slot.assign(size_t(T - 1), -1);
-  lay.top_owner.assign(size_t(T - 1), -1);
-  // in-order walk of the top tree's fringe: leaf 0, gap 0, leaf 1, ..., leaf T - 1
-  i64 pos = 0;
-  for (int t = 0; t < T; ++t) {
-    i64 lo, n;
-    segment(n_total, T - 1 + t, &lo, &n);
-    if (n > 0 && lo != pos) throw std::logic_error("global layout: leaf slot mismatch");
-    lay.leaf_slot[size_t(t)] = pos;
-    lay.leaf_n[size_t(t)] = n;
-    pos += n;
-    if (t + 1 < T) {
-      const i64 h = gap_node(T, t);
-      segment(n_total, h, &lo, &n);
-      if (n > 0) {
-        if (lo + n / 2 != pos) throw std::logic_error("global layout: top slot mismatch");
-        lay.top_slot[size_t(h)] = pos++;
-      }
-    }
-  }
-  if (pos != n_total) throw std::logic_error("global layout: slots do not cover the tree");
-  lay.share_lo.assign(size_t(P), 0);
-  lay.share_n.assign(size_t(P), 0);
-  for (int r = 0; r < P; ++r) {
-    const int a = lay.leaf_lo[size_t(r)], b = lay.leaf_lo[size_t(r) + 1];
-    for (int t = a; t + 1 < b; ++t) lay.top_owner[size_t(gap_node(T, t))] = r;
-    lay.share_lo[size_t(r)] = lay.leaf_slot[size_t(a)];
-    lay.share_n[size_t(r)] = lay.leaf_slot[size_t(b - 1)] + lay.leaf_n[size_t(b - 1)] - lay.leaf_slot[size_t(a)];
-  }
-  return lay;
-}
-
-void share_blocks(const Layout& lay, int r, std::vector<Block>* blocks, std::vector<i64>* between_heap) {
-  blocks->clear();
-  between_heap->clear();
-  const int a = lay.leaf_lo[size_t(r)], b = lay.leaf_lo[size_t(r) + 1];
-  const i64 base = lay.share_lo[size_t(r)];
-  for (int t = a; t < b;) {
-    int s = 0;  // largest aligned power-of-two run of leaves starting at t inside [t, b)
-    while (s < lay.LL && (t % (1 << (s + 1))) == 0 && t + (1 << (s + 1)) <= b) ++s;
-    const int e = t + (1 << s);  // leaves [t, e)
-    const i64 lo = lay.leaf_slot[size_t(t)];
-    const i64 hi = lay.leaf_slot[size_t(e - 1)] + lay.leaf_n[size_t(e - 1)];
-    blocks->push_back(Block{lo - base, hi - lo, lay.LL - s, ((i64(lay.T) + t) >> s) - 1});
-    if (e < b) {
-      const i64 h = gap_node(lay.T, e - 1);
-      if (lay.top_slot[size_t(h)] >= 0) between_heap->push_back(h);
-    }
-    t = e;
-  }
-}
-
-int make_plan(const std::vector<i64>& counts, const Layout& lay, int me, Plan* plan) {
-  const int P = lay.P, T = lay.T, R = lay.R;
-  if (counts.size() != size_t(P) * T * 4) throw std::invalid_argument("make_plan: counts must be [P][T][4]");
-  auto at = [&](int src, int leaf, int f) { return counts[(size_t(src) * T + leaf) * 4 + f]; };
-  i64 errs = 0;
-  for (int src = 0; src < P; ++src)
-    for (int t = 0; t < T; ++t) errs |= at(src, t, 1);
-  if (errs & 1) return 1;  // a middle bucket overflowed its all-gather slot: retry larger
-  if (errs & 2) throw std::runtime_error("global top levels: histogram totals disagree with the tree geometry");
-  // every rank checks every leaf's total: a failure raises on all ranks together
-  for (int t = 0; t < T; ++t) {
-    i64 got = 0;
-    for (int src = 0; src < P; ++src) got += at(src, t, 0);
-    if (got != lay.leaf_n[size_t(t)])
-      throw std::runtime_error("global exchange: top-level leaf " + std::to_string(t) + " would receive " +
-                               std::to_string(got) + " points for a subtree of " +
-                               std::to_string(lay.leaf_n[size_t(t)]));
-  }
-  plan->leaf_start.assign(size_t(T) + 1, 0);
-  for (int t = 0; t < T; ++t) plan->leaf_start[size_t(t) + 1] = plan->leaf_start[size_t(t)] + at(me, t, 0);
-  plan->send_rows.assign(size_t(R), std::vector<i64>(size_t(P), 0));
-  plan->send_off.assign(size_t(R), std::vector<i64>(size_t(P), 0));
-  plan->recv_rows.assign(size_t(R), std::vector<i64>(size_t(P), 0));
-  const int my_a = lay.leaf_lo[size_t(me)], my_cnt = lay.leaf_lo[size_t(me) + 1] - my_a;
-  for (int j = 0; j < R; ++j) {
-    for (int q = 0; q < P; ++q) {
-      const int t = lay.leaf_lo[size_t(q)] + j;
-      if (t < lay.leaf_lo[size_t(q) + 1]) {
-        plan->send_rows[size_t(j)][size_t(q)] = at(me, t, 0);
-        plan->send_off[size_t(j)][size_t(q)] = plan->leaf_start[size_t(t)];
-      }
-    }
-    if (j < my_cnt)
-      for (int p = 0; p < P; ++p) plan->recv_rows[size_t(j)][size_t(p)] = at(p, my_a + j, 0);
-  }
-  plan->src_base.resize(size_t(P));
-  plan->src_n.resize(size_t(P));
-  for (int p = 0; p < P; ++p) {
-    plan->src_base[size_t(p)] = at(p, 0, 2);
-    plan->src_n[size_t(p)] = at(p, 0, 3);
-  }
-  return 0;
-}
-
-}  // namespace global_plan
 
 // ---------------------------------------------------------------------------------------------
 struct GlobalBuilder::Leaf {
   i64 n;
   int depth;
+  bool top;
   std::unique_ptr<GpuBuilder> b;
 };
 
@@ -298,18 +141,20 @@ void* GlobalBuilder::buf(int slot, size_t bytes) {
   return b.first;
 }
 
-GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth) {
+GpuBuilder& GlobalBuilder::leaf_builder(i64 n, int depth, bool allow_top) {
   for (auto& l : leaves_)
-    if (l->n == n && l->depth == depth) return *l->b;
+    if (l->n == n && l->depth == depth && l->top == allow_top) return *l->b;
   auto l = std::make_unique<Leaf>();
   l->n = n;
   l->depth = depth;
+  l->top = allow_top;
   // no split build inside a distributed build: its side streams plus the caller's and the
   // communication stream would exceed the 4 hardware queues, and RCCL's kernels would queue
   // behind partition passes
-  // sampled top levels from the received columns at >= 10 M points (a band miss, ~1e-18 per build,
-  // reports error bit 0x20: the build fails loudly, it is never wrong)
-  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false, true});
+  // sampled top levels from the received columns at >= 10 M points (a band miss reports error
+  // bit 0x20; build() then rebuilds that leaf with allow_top = false from the same columns,
+  // which a sampled build reads without clobbering)
+  l->b = std::make_unique<GpuBuilder>(n, dim_, BuildOptions{0, depth, false, allow_top});
   leaves_.push_back(std::move(l));
   return *leaves_.back()->b;
 }
@@ -337,7 +182,7 @@ u32 GlobalBuilder::read_error(hipStream_t stream) const {
   return (w[0] & 8u) | w[1];  // the compact exchange's bitmap check | the leaf builds' error words
 }
 
-i64 GlobalBuilder::query(const float* queries, i64 Q, u64* out, hipStream_t s, bool count_work) {
+i64 GlobalBuilder::query(const float* queries, i64 Q, u64* out, hipStream_t s, bool count_work, int method) {
   if (Q <= 0) return 0;
   const int dim = dim_;
   std::vector<global_plan::Block> all;
@@ -348,7 +193,7 @@ i64 GlobalBuilder::query(const float* queries, i64 Q, u64* out, hipStream_t s, b
     if (b.n > 0) bl.push_back(b);
   const int nb = int(bl.size());
   if (nb > kRqMaxBlocks) throw std::runtime_error("GlobalBuilder::query: more than 64 blocks");
-  const bool routed = dim <= 16;
+  const bool routed = method == kQueryTraverse || (method == kQueryAuto && dim <= 16);
   auto* counts = static_cast<u32*>(buf(301, size_t(std::max(nb, 1)) * 4));
   nn_init(out, Q, s);
   // the top rows between this rank's blocks, and on rank 0 the boundary top rows: brute force
@@ -612,6 +457,7 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
   auto* send = static_cast<float*>(buf(10, 0));
   auto* bm = static_cast<u32*>(buf(12, 0));
   auto* err = static_cast<u32*>(buf(5, 16));
+  auto* leaf_err = static_cast<u32*>(buf(260, size_t(std::max(mine, 1)) * 4));  // each leaf's own error word
   // the top nodes between my leaves are replicated rows: straight into my share
   {
     TopPlacement pl{};
@@ -703,12 +549,44 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
       if (planar_) b.build_columns(recv[size_t(j)], tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s, leaf_cell);
       else b.build(recv[size_t(j)], lids[size_t(j)], 0, tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s);
       or_error_word(b.error_word(leaf_ws_), err + 1, s);  // the leaves share one workspace
+      PKD_HIP_CHECK(hipMemcpyAsync(leaf_err + j, b.error_word(leaf_ws_), 4, hipMemcpyDeviceToDevice, s));
     }
     if (profile_) PKD_HIP_CHECK(hipEventRecord(ev(round_ev(j, kLeafEnd)), s));
   }
   // the send buffers are rewritten by the next build: the caller's stream waits for the rounds
   PKD_HIP_CHECK(hipEventRecord(packed_, comm_stream_));
   PKD_HIP_CHECK(hipStreamWaitEvent(s, packed_, 0));
+  // A sampled leaf whose band missed its median (error bit 0x20) is rebuilt locally without
+  // sampling, from its received columns (intact: the sampled top reads them into the
+  // workspace's own). No collective is involved, so the ranks stay in step. One host wait per
+  // build, after everything is enqueued, and only when some leaf sampled its top levels.
+  bool any_top = false;
+  for (int j = 0; j < mine; ++j) any_top = any_top || (lb[size_t(j)] && lb[size_t(j)]->sampled_top());
+  if (any_top) {
+    comm_.wait(s, "leaf band check");
+    std::vector<u32> le(size_t(mine), 0u);
+    PKD_HIP_CHECK(hipMemcpy(le.data(), leaf_err, size_t(mine) * 4, hipMemcpyDeviceToHost));
+    bool redo = false;
+    for (int j = 0; j < mine; ++j)
+      if (lb[size_t(j)] && lb[size_t(j)]->sampled_top() && (le[size_t(j)] & top4_band_miss_bit())) redo = true;
+    if (redo) {
+      PKD_HIP_CHECK(hipMemsetAsync(err + 1, 0, 4, s));
+      for (int j = 0; j < mine; ++j) {
+        GpuBuilder* b = lb[size_t(j)];
+        if (!b) continue;
+        if (b->sampled_top() && (le[size_t(j)] & top4_band_miss_bit())) {
+          const int t = my_a + j;
+          GpuBuilder& fb = leaf_builder(lay_.leaf_n[size_t(t)], LL, false);
+          ensure_leaf_workspace(fb.workspace_bytes());
+          const i64 a = lay_.leaf_slot[size_t(t)] - lay_.share_lo[size_t(me)];
+          const float* leaf_cell = static_cast<const float*>(bufs_[1].first) + size_t(T - 1 + t) * dim * 2;
+          fb.build_columns(recv[size_t(j)], tree_pts_ + a * dim, tree_ids_ + a, leaf_ws_, s, leaf_cell);
+          PKD_HIP_CHECK(hipMemcpyAsync(leaf_err + j, fb.error_word(leaf_ws_), 4, hipMemcpyDeviceToDevice, s));
+        }
+        or_error_word(leaf_err + j, err + 1, s);
+      }
+    }
+  }
   if (profile_) {
     PKD_HIP_CHECK(hipEventRecord(ev(kEvEnd), s));
     last_ = info;
@@ -719,35 +597,11 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
 // Loopback communicator: ranks are threads; every collective stages through the host.
 namespace {
 
-struct Shared {
-  explicit Shared(int n) : size(n), slots(size_t(n)), sbytes(size_t(n)), soff(size_t(n)) {}
-  int size;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  long generation = 0;
-  std::vector<std::vector<char>> slots;            // each rank's staged bytes
-  std::vector<std::vector<size_t>> sbytes, soff;   // alltoallv: each rank's send layout
-
-  // A rank that fails stops arriving: the others give up after a deadline instead of hanging.
-  void barrier() {
-    std::unique_lock<std::mutex> lk(mu);
-    const long gen = generation;
-    if (++arrived == size) {
-      arrived = 0;
-      ++generation;
-      cv.notify_all();
-    } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; })) {
-      throw std::runtime_error("loopback communicator: a rank did not reach the barrier within 120 s");
-    }
-  }
-};
-
 class ThreadComm final : public Comm {
  public:
-  ThreadComm(std::shared_ptr<Shared> sh, int rank) : sh_(std::move(sh)), rank_(rank) {}
+  ThreadComm(std::shared_ptr<loopback::Hub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
   int rank() const override { return rank_; }
-  int size() const override { return sh_->size; }
+  int size() const override { return hub_->size(); }
 
   void allreduce_sum_u32(u32* buf, size_t count, hipStream_t s) override {
     reduce<u32>(buf, count, s, [](u32 a, u32 b) { return a + b; });
@@ -756,61 +610,52 @@ class ThreadComm final : public Comm {
     reduce<i64>(buf, count, s, [](i64 a, i64 b) { return std::min(a, b); });
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    stage(send, bytes, s);
-    std::vector<char> out(bytes * size_t(size()));
-    for (int r = 0; r < size(); ++r) std::memcpy(out.data() + size_t(r) * bytes, sh_->slots[size_t(r)].data(), bytes);
-    sh_->barrier();  // every rank has read every slot
+    const std::vector<char> mine = to_host(send, bytes, s);
+    std::vector<char> out;
+    hub_->allgather(rank_, mine.data(), bytes, &out);
     if (bytes) PKD_HIP_CHECK(hipMemcpy(recv, out.data(), out.size(), hipMemcpyHostToDevice));
   }
   void alltoallv(const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off, hipStream_t s) override {
-    size_t total = 0;
-    for (int p = 0; p < size(); ++p) total = std::max(total, send_off[p] + send_bytes[p]);
-    sh_->sbytes[size_t(rank_)].assign(send_bytes, send_bytes + size());
-    sh_->soff[size_t(rank_)].assign(send_off, send_off + size());
-    stage(send, total, s);
+    size_t total = 0, rtotal = 0;
     for (int p = 0; p < size(); ++p) {
-      const size_t n = sh_->sbytes[size_t(p)][size_t(rank_)];
-      if (n != recv_bytes[p]) throw std::runtime_error("loopback alltoallv: size mismatch");
-      if (n)
-        PKD_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + recv_off[p],
-                                sh_->slots[size_t(p)].data() + sh_->soff[size_t(p)][size_t(rank_)], n,
-                                hipMemcpyHostToDevice));
+      total = std::max(total, send_off[p] + send_bytes[p]);
+      rtotal = std::max(rtotal, recv_off[p] + recv_bytes[p]);
     }
-    sh_->barrier();
+    const std::vector<char> mine = to_host(send, total, s);
+    std::vector<char> in(rtotal);
+    hub_->alltoallv(rank_, mine.data(), send_bytes, send_off, in.data(), recv_bytes, recv_off);
+    for (int p = 0; p < size(); ++p)  // only the received ranges: the rest of recv is not ours
+      if (recv_bytes[p])
+        PKD_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + recv_off[p], in.data() + recv_off[p], recv_bytes[p],
+                                hipMemcpyHostToDevice));
   }
 
  private:
   template <class T, class F>
   void reduce(T* buf, size_t count, hipStream_t s, F f) {
-    stage(buf, count * sizeof(T), s);
-    std::vector<T> acc(count);
-    std::memcpy(acc.data(), sh_->slots[0].data(), count * sizeof(T));
-    for (int r = 1; r < size(); ++r) {
-      const T* v = reinterpret_cast<const T*>(sh_->slots[size_t(r)].data());
-      for (size_t i = 0; i < count; ++i) acc[i] = f(acc[i], v[i]);
-    }
-    sh_->barrier();
+    const std::vector<char> mine = to_host(buf, count * sizeof(T), s);
+    std::vector<T> acc;
+    hub_->reduce<T>(rank_, reinterpret_cast<const T*>(mine.data()), count, f, &acc);
     if (count) PKD_HIP_CHECK(hipMemcpy(buf, acc.data(), count * sizeof(T), hipMemcpyHostToDevice));
   }
-  // my bytes -> my host slot; every slot is readable after the barrier
-  void stage(const void* dev, size_t bytes, hipStream_t s) {
+  // the device bytes, after everything enqueued on s before this collective
+  static std::vector<char> to_host(const void* dev, size_t bytes, hipStream_t s) {
     PKD_HIP_CHECK(hipStreamSynchronize(s));
-    auto& v = sh_->slots[size_t(rank_)];
-    v.resize(bytes);
+    std::vector<char> v(bytes);
     if (bytes) PKD_HIP_CHECK(hipMemcpy(v.data(), dev, bytes, hipMemcpyDeviceToHost));
-    sh_->barrier();
+    return v;
   }
-  std::shared_ptr<Shared> sh_;
+  std::shared_ptr<loopback::Hub> hub_;
   int rank_;
 };
 
 }  // namespace
 
 std::vector<std::unique_ptr<Comm>> make_thread_comms(int size) {
-  auto sh = std::make_shared<Shared>(size);
+  auto hub = std::make_shared<loopback::Hub>(size);
   std::vector<std::unique_ptr<Comm>> out;
-  for (int r = 0; r < size; ++r) out.push_back(std::make_unique<ThreadComm>(sh, r));
+  for (int r = 0; r < size; ++r) out.push_back(std::make_unique<ThreadComm>(hub, r));
   return out;
 }
 

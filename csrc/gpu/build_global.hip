@@ -3245,6 +3245,7 @@ void GpuBuilder::run_top(const float* pts, const float* in_cols, const u32* ids,
   tt.z = tune_.top_z;
   tt.scatter_blocks = tune_.top_blocks;
   tt.diag = tune_.top_diag;
+  tt.salt = top_salt_++;
   {
     TraceRange trt("pkd.top4");
     top4::run(g, io, tt, stream);

@@ -308,6 +308,7 @@ struct SampArgs {
   u32* gpart;  // [gather blocks][2 kLevels]: per-block min / max key of each level's axis
   u32* zero;   // the state and histograms, zeroed here as well (no kernel of their own)
   i64 zwords;
+  u32 salt;    // per-build: the sample positions (and so a band miss) are never fixed by the input
 };
 
 __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_samp_gather(SampArgs a) {
     const int kc = k < a.S ? k : a.S - 1;
     const i64 w0 = (i64(kc) * a.n) / a.S, w1 = (i64(kc + 1) * a.n) / a.S;
     const u32 win = u32(max<i64>(1, w1 - w0));
-    const i64 r = w0 + i64(mix32(u32(kc) * 0x9e3779b9u + 0x7f4a7c15u) % win);
+    const i64 r = w0 + i64(mix32(u32(kc) * 0x9e3779b9u + 0x7f4a7c15u + mix32(a.salt)) % win);
 #pragma unroll
     for (int j = 0; j < kLevels; ++j) v[u][j] = a.pts ? a.pts[r * a.dim + a.ax[j]] : a.in_cols[a.ax[j] * a.in_ncol + r];
   }
@@ -1279,7 +1280,7 @@ void run(const Geom& g, const IO& io, const Tune& t, hipStream_t stream) {
   const i64 zwords = i64(L.zero_end - L.state) / 4;
   const int gblocks = (S + kBlock * kGatherRows - 1) / (kBlock * kGatherRows);
   SampArgs sa{io.pts, io.in_cols, io.in_ncol, D, n, S, {g.axis[0], g.axis[1], g.axis[2], g.axis[3]}, skey, gpart,
-              reinterpret_cast<u32*>(ws + L.state), zwords};
+              reinterpret_cast<u32*>(ws + L.state), zwords, t.salt};
   k_samp_gather<<<gblocks, kBlock, 0, stream>>>(sa);
   PKD_LAUNCH_CHECK();
   const int hblocks = std::max(1, std::min(kSampBlocks, S / (kHistThreads * 4)));

@@ -1,4 +1,6 @@
 // Exact 1-NN kernels (see gpu_query.hpp).
+#include <map>
+#include <mutex>
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -488,11 +490,44 @@ bool mfma_brute_enabled() {  // PKD_BRUTE_MFMA=0: the VALU brute force for every
   return !(e && std::string(e) == "0");
 }
 
+namespace {
+// The MFMA brute force's scratch (~330 KB): one persistent buffer per (device, stream), made on
+// first use and kept (calls on one stream are ordered, so they may share it; calls on different
+// streams get their own). No allocator call per batch. A first use inside a graph capture takes
+// a stream-ordered allocation instead (hipMalloc is not capturable).
+struct MfScratchKey {
+  int dev;
+  hipStream_t stream;
+  bool operator<(const MfScratchKey& o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
+};
+mf::Scratch* mf_scratch(hipStream_t stream, bool* transient) {
+  static std::mutex mu;
+  static std::map<MfScratchKey, mf::Scratch*> cache;
+  int dev = 0;
+  PKD_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(MfScratchKey{dev, stream});
+  *transient = false;
+  if (it != cache.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  PKD_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+  mf::Scratch* s = nullptr;
+  if (cs != hipStreamCaptureStatusNone) {
+    PKD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&s), sizeof(mf::Scratch), stream));
+    *transient = true;
+    return s;
+  }
+  PKD_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s), sizeof(mf::Scratch)));
+  cache[MfScratchKey{dev, stream}] = s;
+  return s;
+}
+}  // namespace
+
 void launch_brute_mfma(const float* pts, const u32* ids, u32 id_base, i64 n, int dim, const float* queries, i64 nq,
                        u64* out, hipStream_t stream) {
   using namespace mf;
-  Scratch* s = nullptr;
-  PKD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&s), sizeof(Scratch), stream));
+  bool transient = false;
+  Scratch* s = mf_scratch(stream, &transient);
   const size_t lds = size_t(kQB) * (dim + 8) * 2 + size_t((dim + 3) & ~3) * 4 + size_t(kQB) * 16;
   const int kg = dim % 64 == 0 ? 4 : (dim % 32 == 0 ? 2 : 1);  // k-steps per load group
   auto pass = [&](int mode, int grid, int nqb) {
@@ -539,7 +574,7 @@ void launch_brute_mfma(const float* pts, const u32* ids, u32 id_base, i64 n, int
                    (long long)b0, nqb, mx, double(sum) / nqb, ov);
     }
   }
-  PKD_HIP_CHECK(hipFreeAsync(s, stream));
+  if (transient) PKD_HIP_CHECK(hipFreeAsync(s, stream));
 }
 
 // Batched exact NN, one WAVE per query: the top of the implicit tree is walked by the whole

@@ -76,6 +76,7 @@ struct Tune {
   // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets, 3 also
   // without the scatter's global stores.
   int diag = 0;
+  u32 salt = 0;  // sample positions are a hash of (row window, salt): the builder varies it per build
 };
 
 size_t workspace_bytes();

@@ -17,13 +17,13 @@
 #include <hip/hip_runtime.h>
 
 #include "pkdtree/common.hpp"
+#include "pkdtree/global_plan.hpp"  // kTopBins
 
 namespace pkdtree {
 
 constexpr u32 kTopDone = 0xffffffffu;  // node index of a point that became a top-tree pivot
 constexpr int kTopMaxNodes = 32;       // nodes per top level (P <= 64)
 constexpr int kTopMaxRanks = 64;       // ranks whose middle rows one pivot block walks
-constexpr int kTopBins = 8192;         // nodes * bins per top level (LDS histogram)
 
 struct TopPoints {
   const float* pts;  // [n][dim]

@@ -31,8 +31,9 @@ struct BuildOptions {
   // off for its leaf builds: their streams plus its communication stream would exceed the
   // hardware queues (GPU_MAX_HW_QUEUES = 4), and RCCL's kernels would queue behind partitions.
   bool allow_split = true;
-  // Sampled top levels allowed (AoS-input builds of >= Tuning::top_min_n points). Off for the
-  // distributed builder's leaf builds: they start from received SoA columns.
+  // Sampled top levels allowed (builds of >= Tuning::top_min_n points, from AoS input or from
+  // caller-owned SoA columns such as the distributed builder's received leaves). A band miss
+  // (error bit top4_band_miss_bit()) is redone by a builder with allow_top = false.
   bool allow_top = true;
 };
 
@@ -187,6 +188,7 @@ class GpuBuilder {
   int tail_items_ = 0;   // rows per thread of its 1024-thread workgroups
   int scan_div_ = 1;     // the key sweeps run on 1 / scan_div_ of a level's partition blocks
   bool top_ = false;     // levels 0..3 by the sampled top pass (AoS input builds)
+  mutable u32 top_salt_ = 0;  // per-build salt of the sample positions: a miss is never input-determined
   size_t off_top_ = 0;
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,

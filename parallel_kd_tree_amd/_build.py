@@ -27,7 +27,7 @@ BIN = ROOT / "bin"
 ARCH = os.environ.get("PKD_OFFLOAD_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
-CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp", "cpu/tree_io.cpp"]
+CORE_CPU = ["cpu/generator.cpp", "cpu/cpu_tree.cpp", "cpu/protocol.cpp", "cpu/tree_io.cpp", "cpu/global_plan.cpp"]
 CORE_HIP = ["gpu/build_global.hip", "gpu/build_top.hip", "gpu/build_subtree.hip", "gpu/build_reference.hip", "gpu/query.hip",
             "gpu/dist_ops.hip", "gpu/generator.hip"]
 HOST_HIP = ["cpu/global_builder.cpp", "cpu/tree_io_device.cpp"]  # host C++ on the HIP runtime (no device code)

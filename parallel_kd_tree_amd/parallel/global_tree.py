@@ -185,7 +185,8 @@ class DistTree:
                     full[s] = self.top_rows[i].to(dev)
         return full[:, :self.dim].contiguous(), full[:, self.dim].contiguous().view(torch.int32)
 
-    def query_packed(self, queries: torch.Tensor, method: str = "auto", routed: bool = True) -> torch.Tensor:
+    def query_packed(self, queries: torch.Tensor, method: str = "auto", routed: bool = True,
+                     count_work: bool = False) -> torch.Tensor:
         """Exact NN over the whole distributed tree, packed (d2 << 32 | id), on every rank.
 
         routed (default): queries are replicated on every rank (as in kdtree_mpi.cpp:234-243),
@@ -199,7 +200,9 @@ class DistTree:
              all-reduce gives the answer.
         The top rows between blocks and the boundary rows are brute-forced (<= 63 rows).
         routed=False: every rank searches every query in all its blocks (one MIN all-reduce).
-        ``self.last_query_work`` holds this rank's (query, block) searches of the last call."""
+        ``self.last_query_work`` holds this rank's (query, block) searches of the last call (the
+        native routed search counts them only with ``count_work=True``: two extra device-to-host
+        reads and communicator waits; -1 otherwise)."""
         dev = self.tree_pts.device
         q = queries.to(dev, torch.float32).contiguous()
         Q = q.shape[0]
@@ -207,8 +210,8 @@ class DistTree:
         if native is not None and routed and method == "auto":
             # the native routed search (GlobalBuilder::query): home block, MIN all-reduce, reach
             # blocks, MIN all-reduce -- device lists, no per-block Python loop
-            packed, work = native.query(q, True)
-            self.last_query_work = int(work)
+            packed, work = native.query(q, bool(count_work))
+            self.last_query_work = int(work) if count_work else -1
             return packed
         packed = torch.full((Q,), ops.query.INF_PACKED, dtype=torch.int64, device=dev)
         blocks = [b for b in self.blocks if b[1] > 0]

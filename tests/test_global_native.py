@@ -178,3 +178,16 @@ def test_native_global_loopback_dupes_20m_p8(gpu_device, native):
     x = torch.randint(0, 3, (20_000_000, 3), generator=g).float()
     scale, radix = _loopback_equal(native, x, 8, 0, with_radix=True)
     assert scale == 1 and radix
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,k", [(2, 0), (4, 1)])
+def test_native_global_leaf_band_miss_rebuilt(gpu_device, native, monkeypatch, P, k):
+    """Leaves that sample their top levels (PKD_TOP_MIN_N=0) with bands far too narrow
+    (z = 0.01) miss their medians: each such leaf is rebuilt locally without sampling from its
+    received columns (no collective), so the build reports no error and the tree is exact."""
+    monkeypatch.setenv("PKD_AB", "1")
+    monkeypatch.setenv("PKD_TOP_MIN_N", "0")
+    monkeypatch.setenv("PKD_TOP_Z", "0.01")
+    x = pk.generate_problem(31 + P, 3, 300_000 * P)
+    _loopback_equal(native, x, P, k)

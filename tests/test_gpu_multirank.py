@@ -167,7 +167,7 @@ def _routed(rank, world, n, dim, nq):
     b = NativeGlobalBuilder(n, dim, dev, timeout_s=60)
     t = b.build(full[first:first + cnt].to(dev), id_base=first + 1)
     q = full[n:].to(dev)
-    d2, ids = ops.unpack(t.query_packed(q))
+    d2, ids = ops.unpack(t.query_packed(q, count_work=True))
     work = t.last_query_work
     d2a, _ = ops.unpack(t.query_packed(q, routed=False))
     assert torch.equal(d2, d2a)
