@@ -355,6 +355,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<RefBuilder>(m, "ReferenceBuilder")
       .def(py::init<int64_t, int64_t, int64_t>(), py::arg("n"), py::arg("dim"), py::arg("depth0") = 0)
       .def("build", &RefBuilder::build, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("id_base") = 0)
+      .def("read_ties", [](RefBuilder& b) {
+        TORCH_CHECK(b.ws.defined(), "read_ties: no build yet");
+        return int64_t(b.b.read_ties(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream()));
+      })
       .def_property_readonly("sorted_levels", [](const RefBuilder& b) { return b.b.sorted_levels(); })
       .def_property_readonly("global_levels", [](const RefBuilder& b) { return b.b.global_levels(); })
       .def_property_readonly("workspace_bytes", [](const RefBuilder& b) { return int64_t(b.b.workspace_bytes()); });

@@ -51,6 +51,7 @@
 #include <vector>
 
 #include "cli_common.hpp"
+#include "ref_fallback.hpp"
 #include "pkdtree/generator.hpp"
 #include "pkdtree/global_builder.hpp"
 #include "pkdtree/gpu_build.hpp"
@@ -226,8 +227,9 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
     const Slice& sl = slices[k];
     const i64 off = sl.first - first;
     if (sl.n <= 0) return nullptr;
-    if (ref) {
-      rbs[k]->build(d_x + off * dim, nullptr, u32(sl.first + 1), d_tree + off * dim, d_ids + off, ws, s);
+    if (ref) {  // (ties: this rank's tree from the CPU std::sort builder, before any collective)
+      cli::build_reference_checked(*rbs[k], d_x + off * dim, sl.n, dim, u32(sl.first + 1), d_tree + off * dim,
+                                   d_ids + off, ws, s, "kdtree_dist");
       return nullptr;
     }
     GpuBuilder* b = bs[k].get();

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "cli_common.hpp"
+#include "ref_fallback.hpp"
 #include "pkdtree/generator.hpp"
 #include "pkdtree/gpu_build.hpp"
 #include "pkdtree/gpu_generator.hpp"
@@ -69,7 +70,7 @@ int main(int argc, char** argv) {
     PKD_HIP_CHECK(hipEventRecord(e0, s));
     if (o.host_gen) PKD_HIP_CHECK(hipMemcpyAsync(d_x, x.data(), total * 4, hipMemcpyHostToDevice, s));
     PKD_HIP_CHECK(hipEventRecord(e1, s));
-    if (ref) rb.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);  // reference point IDs are 1..N
+    if (ref) cli::build_reference_checked(rb, d_x, N, dim, 1u, d_tree, d_ids, ws, s, "kdtree_gpu");  // IDs 1..N
     else b.build(d_x, nullptr, 1u, d_tree, d_ids, ws, s);
     PKD_HIP_CHECK(hipEventRecord(e2, s));
     const float* d_q = d_x + size_t(N) * dim;

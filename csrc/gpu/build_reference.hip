@@ -1,26 +1,40 @@
-// Reference-mode builder on the GPU: the reference's own (quirky) tree.
+// Reference-mode builder on the GPU: the reference's own (quirky) tree, by SELECTION.
 //
 // build_tree_rec (kdtree_sequential.cpp:30-66, kdtree_mpi.cpp:60-100) sorts only the FIRST
-// n - 1 points of every subrange on the node's axis (:46-48), takes list[n/2] as the median
-// and recurses on [0, n/2) and [n/2 + 1, n): the last point of a subrange keeps its slot, so
-// the tree violates the kd invariant and depends on array positions, not only
-// on point sets. Level-synchronous reproduction on a u32 permutation (rows never move; the
-// output rows are gathered once at the end):
-//   * levels whose segments exceed the LDS finish (kFinCap rows): a segmented LSD radix sort of
-//     every segment's first n - 1 positions on the level's 32-bit orderable key, four 8-bit
-//     passes. Tiles never cross a segment (host-computed from the implicit geometry), so a pass
-//     is: per-tile digit histograms laid out segment by segment, digit-major inside a segment
-//     (k_rs_hist); ONE exclusive scan over them gives every (segment, digit, tile) its output
-//     offset (k_scan_*); a stable scatter ranks each wave's items by ballot matching of the
-//     digit bits (k_rs_scatter). The last position of every segment and the finished medians
-//     are never touched, and four passes bring the result back into the same buffer.
-//   * then one workgroup per segment (<= kFinCap rows) finishes all remaining levels in LDS:
-//     per level every sortable row's rank inside its sub-segment is counted against the other
-//     rows (stable: position breaks ties), rows move to their ranks, sub-segments split.
-// The sorts are stable (ties keep their previous order) while std::sort is not, so the tree
-// equals the reference's exactly when no two points of a segment share a key on its axis --
-// always true for tie-free data, usually true for the reference generator at
-// small N. Exact mode (gpu_build.hpp) is the fast path; this one is a parity mode.
+// n - 1 points of every subrange on the node's axis (:46-48), takes list[n/2] as the median and
+// recurses on [0, n/2) and [n/2 + 1, n). Nothing needs a sort to reproduce that:
+// with m = n / 2 and ranks taken among the n - 1 sortable rows of the segment,
+//   * the median is rank m (n = 2: no sortable rank m, the untouched last row is the median);
+//   * the left child [0, m) holds ranks 0 .. m - 1, and ITS last row (which the next level
+//     leaves out of its sort) is rank m - 1, the left maximum;
+//   * the right child [m + 1, n) holds ranks m + 1 .. n - 2 followed by the parent's last row,
+//     which stays the right child's last row.
+// So every level is an exact rank-m selection per segment with the invariant "the segment's
+// last position holds its excluded row": rows never need a full order, only the left maximum
+// and the median need exact places. Level-synchronous, on a u32 permutation of the input rows:
+//   global levels (segments > kFinCap rows), per level:
+//     k_ref_keys      the level's key of every sortable row (gathered through the permutation)
+//                     and each segment's key range
+//     k_ref_hist      a value-linear histogram of each segment's keys over its range
+//     k_ref_select    the buckets b1 <= b2 holding ranks m - 1 and m
+//     k_ref_part      every sortable row moves once: left of b1 / inside [b1, b2] / right of b2,
+//                     with wave ballots and one reservation per zone and chunk; the last row
+//                     keeps its slot; the left zone's maximum and the right zone's minimum are
+//                     kept (composite (key, row))
+//     k_ref_refine    one workgroup per segment: exact (key, row) ranks m - 1 and m inside the
+//                     middle zone (MSD radix select), the middle rows placed around them
+//   k_ref_finish      one workgroup per segment of <= kFinCap rows finishes all remaining levels
+//                     in LDS: each sub-segment's sortable rows ranked through a per-sub-segment
+//                     bucket histogram (buckets = the sub-segment's own slot range) and exact
+//                     comparisons inside a bucket, then moved to their ranks
+//   k_ref_gather      output rows through the final permutation.
+// Ties. std::sort is unstable, so when equal keys meet where the tree is decided the reference
+// binary's tree depends on its library's sort internals. Exactly three adjacent-rank pairs of a
+// segment decide its tree: (m - 1, m) and (m, m + 1) pick the median and the two child sets,
+// (m - 2, m - 1) picks the left child's excluded last row; the order of every other row is
+// re-sorted by the next level anyway. A tie on any of those pairs is COUNTED (ties_word()): the
+// tree is then the (key, row)-ordered one, which may differ from the binary's, and callers fall
+// back to the CPU std::sort builder (kdtree_gpu / kdtree_dist --mode reference, KDTree.build).
 #include <algorithm>
 #include <stdexcept>
 
@@ -33,157 +47,25 @@ namespace pkdtree {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTile = 4096;      // sortable rows per radix tile (4 waves x 16 x 64)
-constexpr int kFinCap = 2048;    // largest segment the LDS finish takes
-constexpr int kScanChunk = kBlock * 16;
+constexpr int kFinCap = 2048;     // largest segment the LDS finish takes
+constexpr int kFinThreads = 256;  // its workgroup: kFinCap / kFinThreads rows per thread
+constexpr int kFinItems = kFinCap / kFinThreads;
+constexpr int kItems = 8;         // rows per thread per partition chunk
+constexpr int kChunk = kBlock * kItems;
+constexpr int kRefineCap = 4096;  // middle rows selected in LDS (more: streamed from global)
 
-int grid_for(i64 n) { return int(std::min<i64>(8192, std::max<i64>(1, (n + kBlock - 1) / kBlock))); }
+struct RefSeg {
+  u32 lo, n;              // slot range of the segment
+  u32 kmin, kmax;         // orderable key range of its sortable rows on the level's axis
+  u32 b1, b2;             // buckets of ranks m - 1 and m
+  u32 L, M;               // sortable rows below b1 / inside [b1, b2]
+  u32 cur[3];             // zone cursors of the partition
+  u32 pad;
+  u64 left_max;           // largest composite of the left zone (0: empty)
+  u64 right_min;          // smallest composite of the right zone (~0: empty)
+};
 
-__global__ __launch_bounds__(kBlock) void k_ref_init(u32* __restrict__ perm, i64 n) {
-  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += i64(gridDim.x) * kBlock) perm[p] = u32(p);
-}
-
-using Tile = ReferenceBuilder::Tile;
-
-// sort keys of the level's sortable positions (every tile's rows)
-__global__ __launch_bounds__(kBlock) void k_ref_keys(const float* __restrict__ pts, int dim, int axis,
-                                                     const u32* __restrict__ perm, const Tile* __restrict__ tiles,
-                                                     u32* __restrict__ keys) {
-  const Tile t = tiles[blockIdx.x];
-  for (u32 e = threadIdx.x; e < t.len; e += kBlock) {
-    const u32 p = t.pos0 + e;
-    keys[p] = orderable(pts[i64(perm[p]) * dim + axis]);
-  }
-}
-
-// per-tile digit histogram -> cnt[ent0 + digit * tseg + trel]
-__global__ __launch_bounds__(kBlock) void k_rs_hist(const u32* __restrict__ keys, const Tile* __restrict__ tiles,
-                                                    int shift, u32* __restrict__ cnt) {
-  __shared__ u32 h[256];
-  const Tile t = tiles[blockIdx.x];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  for (u32 e = threadIdx.x; e < t.len; e += kBlock) atomicAdd(&h[(keys[t.pos0 + e] >> shift) & 255u], 1u);
-  __syncthreads();
-  cnt[size_t(t.ent0) + size_t(threadIdx.x) * t.tseg + t.trel] = h[threadIdx.x];
-}
-
-// exclusive scan of n words in place: chunk sums, a scan of the sums, chunk scans + base
-__global__ __launch_bounds__(kBlock) void k_scan_sums(const u32* __restrict__ v, i64 n, u32* __restrict__ sums) {
-  __shared__ u32 red[kBlock / 64];
-  const i64 c0 = i64(blockIdx.x) * kScanChunk;
-  u32 s = 0;
-  for (int k = 0; k < 16; ++k) {
-    const i64 i = c0 + i64(k) * kBlock + threadIdx.x;
-    if (i < n) s += v[i];
-  }
-  s = dev::wave_incl_scan(s);
-  if (dev::lane() == 63) red[threadIdx.x / 64] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-// one block: exclusive scan of m block sums (m <= kBlock * 16)
-__global__ __launch_bounds__(kBlock) void k_scan_top(u32* __restrict__ sums, int m) {
-  __shared__ u32 ws[kBlock / 64];
-  u32 loc[16];
-  u32 s = 0;
-  for (int k = 0; k < 16; ++k) {
-    const int i = threadIdx.x * 16 + k;
-    loc[k] = i < m ? sums[i] : 0u;
-    s += loc[k];
-  }
-  const u32 incl = dev::wave_incl_scan(s);
-  if (dev::lane() == 63) ws[threadIdx.x / 64] = incl;
-  __syncthreads();
-  u32 base = 0;
-  for (int w = 0; w < int(threadIdx.x / 64); ++w) base += ws[w];
-  u32 run = base + incl - s;
-  for (int k = 0; k < 16; ++k) {
-    const int i = threadIdx.x * 16 + k;
-    if (i < m) sums[i] = run;
-    run += loc[k];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_apply(u32* __restrict__ v, i64 n, const u32* __restrict__ sums) {
-  __shared__ u32 ws[kBlock / 64];
-  const i64 c0 = i64(blockIdx.x) * kScanChunk;
-  u32 loc[16];
-  u32 s = 0;
-  for (int k = 0; k < 16; ++k) {  // thread t owns 16 consecutive words
-    const i64 i = c0 + i64(threadIdx.x) * 16 + k;
-    loc[k] = i < n ? v[i] : 0u;
-    s += loc[k];
-  }
-  const u32 incl = dev::wave_incl_scan(s);
-  if (dev::lane() == 63) ws[threadIdx.x / 64] = incl;
-  __syncthreads();
-  u32 base = sums[blockIdx.x];
-  for (int w = 0; w < int(threadIdx.x / 64); ++w) base += ws[w];
-  u32 run = base + incl - s;
-  for (int k = 0; k < 16; ++k) {
-    const i64 i = c0 + i64(threadIdx.x) * 16 + k;
-    if (i < n) v[i] = run;
-    run += loc[k];
-  }
-}
-
-// stable scatter of one tile: wave w owns tile rows [w * 1024, (w + 1) * 1024); item i of lane
-// l is row w * 1024 + i * 64 + l, so (w, i, l) is the input order. Lanes with equal digits are
-// matched by 8 ballots; a digit's running count per wave lives in LDS.
-__global__ __launch_bounds__(kBlock) void k_rs_scatter(const u32* __restrict__ kin, const u32* __restrict__ vin,
-                                                       u32* __restrict__ kout, u32* __restrict__ vout,
-                                                       const Tile* __restrict__ tiles, int shift,
-                                                       const u32* __restrict__ off) {
-  __shared__ u32 wc[kBlock / 64][256];
-  const Tile t = tiles[blockIdx.x];
-  const int w = threadIdx.x / 64, ln = dev::lane();
-  for (int d = threadIdx.x; d < 4 * 256; d += kBlock) (&wc[0][0])[d] = 0u;
-  __syncthreads();
-  const u64 lt = (u64(1) << ln) - 1ull;
-  u32 kk[16], vv[16], rk[16];
-  for (int i = 0; i < 16; ++i) {
-    const u32 e = u32(w) * 1024u + u32(i) * 64u + u32(ln);
-    const bool valid = e < t.len;
-    const u32 key = valid ? kin[t.pos0 + e] : 0u;
-    kk[i] = key;
-    vv[i] = valid ? vin[t.pos0 + e] : 0u;
-    const u32 d = (key >> shift) & 255u;
-    u64 m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const u64 bb = __ballot((d >> b) & 1u);
-      m &= ((d >> b) & 1u) ? bb : ~bb;
-    }
-    u32 base = 0;
-    if (valid) base = wc[w][d];
-    rk[i] = base + u32(__popcll(m & lt));
-    if (valid && (m & lt) == 0ull) wc[w][d] = base + u32(__popcll(m));  // the group's first lane
-  }
-  __syncthreads();
-  {  // wave prefix per digit
-    const int d = threadIdx.x;
-    u32 s = 0;
-    for (int ww = 0; ww < kBlock / 64; ++ww) {
-      const u32 c = wc[ww][d];
-      wc[ww][d] = s;
-      s += c;
-    }
-  }
-  __syncthreads();
-  for (int i = 0; i < 16; ++i) {
-    const u32 e = u32(w) * 1024u + u32(i) * 64u + u32(ln);
-    if (e >= t.len) continue;
-    const u32 d = (kk[i] >> shift) & 255u;
-    const u32 pos = t.seg_lo + (off[size_t(t.ent0) + size_t(d) * t.tseg + t.trel] - t.rows_before) + wc[w][d] + rk[i];
-    kout[pos] = kk[i];
-    vout[pos] = vv[i];
-  }
-}
-
-// (lo, n) of segment j of level l of the implicit tree over n rows
-__device__ __forceinline__ void seg_geometry(i64 n, int l, i64 j, i64* lo_out, i64* n_out) {
+__host__ __device__ inline void seg_geometry(i64 n, int l, i64 j, i64* lo_out, i64* n_out) {
   i64 lo = 0, m = n;
   for (int b = l - 1; b >= 0; --b) {
     if ((j >> b) & 1) {
@@ -198,16 +80,369 @@ __device__ __forceinline__ void seg_geometry(i64 n, int l, i64 j, i64* lo_out, i
   *n_out = m;
 }
 
-// One workgroup per segment of level lf (<= kFinCap rows): every remaining level in LDS.
-__global__ __launch_bounds__(kBlock) void k_ref_finish(const float* __restrict__ pts, int dim, int depth0,
-                                                       u32* __restrict__ perm, i64 n, int lf, int levels) {
+// Value-linear bucket of an orderable key over [kmin, kmax] (integer arithmetic, monotone).
+__device__ __forceinline__ u32 ref_bucket(u32 k, u32 kmin, u32 kmax, u32 B) {
+  const u64 span = u64(kmax - kmin) + 1ull;
+  const u64 b = (u64(k - kmin) * B) / span;
+  return u32(b < B ? b : B - 1);
+}
+
+__device__ __forceinline__ u64 comp(u32 key, u32 row) { return (u64(key) << 32) | row; }
+
+__global__ __launch_bounds__(kBlock) void k_ref_init(u32* __restrict__ perm, i64 n) {
+  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += i64(gridDim.x) * kBlock) perm[p] = u32(p);
+}
+
+// Segment descriptors of level l (geometry, cleared ranges and cursors) and a zeroed histogram.
+__global__ __launch_bounds__(kBlock) void k_ref_seg_init(RefSeg* __restrict__ seg, i64 S, i64 n_total, int l,
+                                                         u32* __restrict__ hist, i64 hwords) {
+  for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < hwords; i += i64(gridDim.x) * kBlock) hist[i] = 0u;
+  for (i64 s = i64(blockIdx.x) * kBlock + threadIdx.x; s < S; s += i64(gridDim.x) * kBlock) {
+    i64 lo = 0, m = 0;
+    seg_geometry(n_total, l, s, &lo, &m);
+    RefSeg r{};
+    r.lo = u32(lo);
+    r.n = u32(m);
+    r.kmin = 0xffffffffu;
+    r.kmax = 0u;
+    r.left_max = 0ull;
+    r.right_min = ~0ull;
+    seg[s] = r;
+  }
+}
+
+// The sortable rows [lo, lo + n - 1) of segment s, split over bps blocks.
+__device__ __forceinline__ void block_part(const RefSeg& r, int part, int bps, u32* b0, u32* b1) {
+  const u32 sortable = r.n > 0 ? r.n - 1 : 0u;
+  const u32 per = (sortable + u32(bps) - 1) / u32(bps);
+  *b0 = min(sortable, u32(part) * per);
+  *b1 = min(sortable, *b0 + per);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ref_keys(const float* __restrict__ pts, int dim, int axis,
+                                                     const u32* __restrict__ perm, RefSeg* __restrict__ seg, int bps,
+                                                     u32* __restrict__ keys) {
+  const i64 s = blockIdx.x / bps;
+  const int part = blockIdx.x % bps;
+  const RefSeg r = seg[s];
+  u32 b0, b1;
+  block_part(r, part, bps, &b0, &b1);
+  u32 mn = 0xffffffffu, mx = 0u;
+  constexpr int U = 4;  // gathers in flight per thread
+  for (u32 e0 = b0; e0 < b1; e0 += kBlock * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32 e = e0 + u32(u * kBlock) + threadIdx.x;
+      v[u] = e < b1 ? pts[i64(perm[r.lo + e]) * dim + axis] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32 e = e0 + u32(u * kBlock) + threadIdx.x;
+      if (e < b1) {
+        const u32 k = orderable(v[u]);
+        keys[r.lo + e] = k;
+        mn = min(mn, k);
+        mx = max(mx, k);
+      }
+    }
+  }
+  mn = dev::wave_min_u32(mn);
+  mx = dev::wave_max_u32(mx);
+  if (dev::lane() == 0 && mn <= mx) {
+    atomicMin(&seg[s].kmin, mn);
+    atomicMax(&seg[s].kmax, mx);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ref_hist(const u32* __restrict__ keys, const RefSeg* __restrict__ seg,
+                                                     int bps, int B, u32* __restrict__ hist) {
+  extern __shared__ u32 h[];
+  const i64 s = blockIdx.x / bps;
+  const int part = blockIdx.x % bps;
+  const RefSeg r = seg[s];
+  for (int b = threadIdx.x; b < B; b += kBlock) h[b] = 0u;
+  __syncthreads();
+  u32 b0, b1;
+  block_part(r, part, bps, &b0, &b1);
+  for (u32 e = b0 + threadIdx.x; e < b1; e += kBlock)
+    atomicAdd(&h[ref_bucket(keys[r.lo + e], r.kmin, r.kmax, u32(B))], 1u);
+  __syncthreads();
+  u32* out = hist + s * i64(B);
+  for (int b = threadIdx.x; b < B; b += kBlock)
+    if (h[b]) atomicAdd(&out[b], h[b]);
+}
+
+// Bucket holding the rank-th element of h[0, B) (B <= 4096; one wave): *below = rows before it.
+__device__ __forceinline__ u32 wave_find(const u32* h, int B, u32 rank, u32* below) {
+  const int per = (B + 63) / 64, ln = dev::lane();
+  u32 s = 0;
+  for (int i = 0; i < per; ++i) {
+    const int b = ln * per + i;
+    s += b < B ? h[b] : 0u;
+  }
+  const u32 incl = dev::wave_incl_scan(s), excl = incl - s;
+  const u64 m = __ballot(rank >= excl && rank < incl);
+  if (!m) {
+    *below = __shfl(incl, 63, 64);
+    return u32(B);
+  }
+  const int src = __ffsll((long long)m) - 1;
+  u32 bin = 0, bel = 0;
+  if (ln == src) {
+    u32 c = excl;
+    int b = ln * per;
+    while (b + 1 < ln * per + per && b + 1 < B && rank >= c + h[b]) c += h[b++];
+    bin = u32(b);
+    bel = c;
+  }
+  *below = u32(__shfl(int(bel), src, 64));
+  return u32(__shfl(int(bin), src, 64));
+}
+
+__global__ __launch_bounds__(64) void k_ref_select(RefSeg* __restrict__ seg, int B, const u32* __restrict__ hist,
+                                                   u32* __restrict__ err) {
+  const i64 s = blockIdx.x;
+  const RefSeg r = seg[s];
+  if (r.n < 3) return;  // (global segments always hold more than kFinCap rows)
+  const u32 m = r.n / 2;
+  const u32* h = hist + s * i64(B);
+  u32 L = 0, below2 = 0;
+  const u32 b1 = wave_find(h, B, m - 1, &L);
+  const u32 b2 = wave_find(h, B, m, &below2);
+  if (dev::lane() == 0) {
+    if (b1 >= u32(B) || b2 >= u32(B)) {
+      atomicOr(err, 1u);
+      return;
+    }
+    u32 M = below2 + h[b2] - L;
+    seg[s].b1 = b1;
+    seg[s].b2 = b2;
+    seg[s].L = L;
+    seg[s].M = M;
+  }
+}
+
+// Every sortable row once: zone 0 (bucket < b1) -> [lo, lo + L), zone 1 -> [lo + L, lo + L + M)
+// with its composite in midc, zone 2 -> [lo + L + M, lo + n - 1); the last row keeps its slot.
+__global__ __launch_bounds__(kBlock) void k_ref_part(const u32* __restrict__ keys, const u32* __restrict__ src,
+                                                     u32* __restrict__ dst, u64* __restrict__ midc,
+                                                     RefSeg* __restrict__ seg, int bps, int B) {
+  __shared__ u32 wc[kBlock / 64][3];
+  __shared__ u32 zb[kBlock / 64][3];
+  __shared__ u64 red[kBlock / 64][2];
+  const i64 s = blockIdx.x / bps;
+  const int part = blockIdx.x % bps;
+  const RefSeg r = seg[s];
+  const int w = threadIdx.x / 64, ln = dev::lane();
+  if (part == 0 && threadIdx.x == 0 && r.n > 0) dst[r.lo + r.n - 1] = src[r.lo + r.n - 1];
+  u32 b0, b1;
+  block_part(r, part, bps, &b0, &b1);
+  u64 lmax = 0ull, rmin = ~0ull;
+  for (u32 c0 = b0; c0 < b1; c0 += kChunk) {
+    u32 key[kItems], row[kItems], z[kItems], rk[kItems];
+    u32 cnt[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const u32 e = c0 + u32(w * 64 * kItems + i * 64 + ln);
+      const bool valid = e < b1;
+      key[i] = valid ? keys[r.lo + e] : 0u;
+      row[i] = valid ? src[r.lo + e] : 0u;
+      const u32 b = ref_bucket(key[i], r.kmin, r.kmax, u32(B));
+      z[i] = !valid ? 3u : (b < r.b1 ? 0u : (b <= r.b2 ? 1u : 2u));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const u64 mq = __ballot(z[i] == u32(q));
+        if (z[i] == u32(q)) rk[i] = cnt[q] + dev::mbcnt(mq);
+        cnt[q] += u32(__popcll(mq));
+      }
+      const u64 cp = comp(key[i], row[i]);
+      if (z[i] == 0u) lmax = cp > lmax ? cp : lmax;
+      if (z[i] == 2u) rmin = cp < rmin ? cp : rmin;
+    }
+    if (ln < 3) wc[w][ln] = cnt[ln];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      const int q = threadIdx.x;
+      u32 t = 0;
+      for (int k = 0; k < kBlock / 64; ++k) t += wc[k][q];
+      u32 base = t ? atomicAdd(&seg[s].cur[q], t) : 0u;
+      for (int k = 0; k < kBlock / 64; ++k) {
+        zb[k][q] = base;
+        base += wc[k][q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      if (z[i] > 2u) continue;
+      const u32 off = zb[w][z[i]] + rk[i];
+      const u32 pos = r.lo + (z[i] == 0u ? 0u : (z[i] == 1u ? r.L : r.L + r.M)) + off;
+      dst[pos] = row[i];
+      if (z[i] == 1u) midc[pos] = comp(key[i], row[i]);
+    }
+    __syncthreads();  // wc / zb are rewritten by the next chunk
+  }
+  lmax = dev::wave_max_u64(lmax);
+  rmin = dev::wave_min_u64(rmin);
+  if (ln == 0) {
+    red[w][0] = lmax;
+    red[w][1] = rmin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) {
+      lmax = red[k][0] > lmax ? red[k][0] : lmax;
+      rmin = red[k][1] < rmin ? red[k][1] : rmin;
+    }
+    if (lmax) atomicMax((unsigned long long*)&seg[s].left_max, (unsigned long long)lmax);
+    if (rmin != ~0ull) atomicMin((unsigned long long*)&seg[s].right_min, (unsigned long long)rmin);
+  }
+}
+
+// rank-th smallest (0-based) of the composites visited by each(f): MSD radix select, 8-bit
+// digits below the highest bit in which the candidates differ (every thread of the block calls
+// it and visits its share).
+template <class Each>
+__device__ u64 block_select(Each each, u32 rank) {
+  __shared__ __align__(16) u32 hist[256];
+  __shared__ u64 rmn[kBlock / 64], rmx[kBlock / 64];
+  __shared__ u32 info[2];
+  u64 mn = ~0ull, mx = 0ull;
+  each([&](u64 v) {
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  });
+  mn = dev::wave_min_u64(mn);
+  mx = dev::wave_max_u64(mx);
+  __syncthreads();
+  if (dev::lane() == 0) {
+    rmn[threadIdx.x / 64] = mn;
+    rmx[threadIdx.x / 64] = mx;
+  }
+  __syncthreads();
+  mn = rmn[0];
+  mx = rmx[0];
+  for (int k = 1; k < kBlock / 64; ++k) {
+    mn = rmn[k] < mn ? rmn[k] : mn;
+    mx = rmx[k] > mx ? rmx[k] : mx;
+  }
+  const u64 diff = mn ^ mx;
+  if (!diff) return mn;
+  int hb = 63 - __builtin_clzll(diff);
+  u64 prefix = hb >= 63 ? 0ull : (mn & ~((2ull << hb) - 1ull));
+  while (hb >= 0) {
+    const int sh = hb >= 7 ? hb - 7 : 0;
+    const u32 dmask = (2u << (hb - sh)) - 1u;
+    const u64 himask = hb >= 63 ? 0ull : ~((2ull << hb) - 1ull);
+    __syncthreads();
+    hist[threadIdx.x] = 0u;
+    __syncthreads();
+    each([&](u64 v) {
+      if ((v & himask) == prefix) atomicAdd(&hist[u32(v >> sh) & dmask], 1u);
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      u32 below = 0;
+      const u32 b = wave_find(hist, 256, rank, &below);
+      if (threadIdx.x == 0) {
+        info[0] = b;
+        info[1] = below;
+      }
+    }
+    __syncthreads();
+    prefix |= u64(info[0] & dmask) << sh;
+    rank -= info[1];
+    hb = sh - 1;
+  }
+  return prefix;
+}
+
+// One workgroup per segment: ranks m - 1 and m inside the middle zone, the middle rows placed
+// around them (left of the left maximum / right of the median), the median written to both
+// permutation buffers (its slot is final), and the three deciding pairs checked for ties.
+__global__ __launch_bounds__(kBlock) void k_ref_refine(const RefSeg* __restrict__ seg, const u64* __restrict__ midc,
+                                                       u32* __restrict__ dst, u32* __restrict__ other,
+                                                       u32* __restrict__ ties) {
+  __shared__ u64 buf[kRefineCap];
+  __shared__ u32 cl, cr;
+  __shared__ u64 rpred[kBlock / 64], rsucc[kBlock / 64];
+  const RefSeg r = seg[blockIdx.x];
+  if (r.n < 3) return;
+  const u32 m = r.n / 2, L = r.L, M = r.M;
+  const u32 base = r.lo + L;
+  const bool in_lds = M <= u32(kRefineCap);
+  if (in_lds)
+    for (u32 e = threadIdx.x; e < M; e += kBlock) buf[e] = midc[base + e];
+  if (threadIdx.x == 0) {
+    cl = 0;
+    cr = 0;
+  }
+  __syncthreads();
+  auto each = [&](auto f) {
+    if (in_lds) {
+      for (u32 e = threadIdx.x; e < M; e += kBlock) f(buf[e]);
+    } else {
+      for (u32 e = threadIdx.x; e < M; e += kBlock) f(midc[base + e]);
+    }
+  };
+  const u64 c1 = block_select(each, m - 1 - L);
+  const u64 c2 = block_select(each, m - L);
+  u64 pred = r.left_max, succ = r.right_min;  // ranks m - 2 and m + 1 (0 / ~0: none)
+  each([&](u64 v) {
+    if (v < c1) pred = v > pred ? v : pred;
+    if (v > c2) succ = v < succ ? v : succ;
+  });
+  pred = dev::wave_max_u64(pred);
+  succ = dev::wave_min_u64(succ);
+  if (dev::lane() == 0) {
+    rpred[threadIdx.x / 64] = pred;
+    rsucc[threadIdx.x / 64] = succ;
+  }
+  __syncthreads();
+  // place: [lo + L, lo + m - 1) left of c1, lo + m - 1 = c1, lo + m = c2, (lo + m, lo + L + M) right of c2
+  each([&](u64 v) {
+    u32 pos;
+    if (v < c1) pos = base + atomicAdd(&cl, 1u);
+    else if (v == c1) pos = r.lo + m - 1;
+    else if (v == c2) pos = r.lo + m;
+    else pos = r.lo + m + 1 + atomicAdd(&cr, 1u);
+    dst[pos] = u32(v);
+    if (v == c2) other[pos] = u32(v);  // the median's slot is final: both buffers
+  });
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < kBlock / 64; ++k) {
+      pred = rpred[k] > pred ? rpred[k] : pred;
+      succ = rsucc[k] < succ ? rsucc[k] : succ;
+    }
+    const u32 k1 = u32(c1 >> 32), k2 = u32(c2 >> 32);
+    bool tie = k1 == k2;
+    if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;       // rank m - 2 vs the left's last
+    if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;  // rank m + 1 vs the median
+    if (tie) atomicAdd(ties, 1u);
+  }
+}
+
+// One workgroup per segment of level lf (<= kFinCap rows): every remaining level in LDS. Each
+// sub-segment [sl, sl + sn) with sn >= 3 ranks its sortable rows (all but its last slot) by
+// (key, slot): buckets are the sub-segment's own slots [sl, sl + sn - 1), value-linear over its
+// key range, so one block scan serves every sub-segment; rows move to sl + rank.
+__global__ __launch_bounds__(kFinThreads) void k_ref_finish(const float* __restrict__ pts, int dim, int depth0,
+                                                            u32* __restrict__ perm, i64 n_total, int lf, int levels,
+                                                            u32* __restrict__ ties) {
   __shared__ u32 P[2][kFinCap], K[kFinCap];
-  __shared__ unsigned short SL[kFinCap], SN[kFinCap];
-  i64 lo = 0, m = 0;
-  seg_geometry(n, lf, blockIdx.x, &lo, &m);
-  if (m <= 1) return;
-  const int M = int(m);
-  for (int p = threadIdx.x; p < M; p += kBlock) {
+  __shared__ u32 H[kFinCap + 1];
+  __shared__ u32 smin[kFinCap], smax[kFinCap];
+  u32* tk = smin;  // bucket-ordered keys: smin / smax are dead once the buckets are known
+  __shared__ unsigned short tp[kFinCap], SL[kFinCap], SN[kFinCap];
+  __shared__ u32 wsum[kFinThreads / 64];
+  i64 lo64 = 0, m64 = 0;
+  seg_geometry(n_total, lf, blockIdx.x, &lo64, &m64);
+  if (m64 <= 1) return;
+  const int M = int(m64);
+  const u32 lo = u32(lo64);
+  const int tid = threadIdx.x;
+  for (int p = tid; p < M; p += kFinThreads) {
     P[0][p] = perm[lo + p];
     SL[p] = 0;
     SN[p] = (unsigned short)M;
@@ -216,28 +451,129 @@ __global__ __launch_bounds__(kBlock) void k_ref_finish(const float* __restrict__
   __syncthreads();
   for (int l = lf; l < levels; ++l) {
     const int axis = (depth0 + l) % dim;
-    for (int p = threadIdx.x; p < M; p += kBlock) {
-      const int sl = SL[p], sn = SN[p];
-      if (sn >= 2 && p != sl + sn - 1) K[p] = orderable(pts[i64(P[cur][p]) * dim + axis]);
+    // 1. keys of the sortable rows, sub-segment key ranges, empty histogram
+    for (int p = tid; p < M; p += kFinThreads) {
+      smin[p] = 0xffffffffu;
+      smax[p] = 0u;
+    }
+    for (int p = tid; p <= M; p += kFinThreads) H[p] = 0u;
+    __syncthreads();
+    u32 key[kFinItems], slot[kFinItems];
+    bool srt[kFinItems];
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      srt[i] = false;
+      key[i] = 0;
+      if (p < M) {
+        const int sl = SL[p], sn = SN[p];
+        srt[i] = sn >= 3 && p != sl + sn - 1;
+        if (srt[i]) {
+          key[i] = orderable(pts[i64(P[cur][p]) * dim + axis]);
+          atomicMin(&smin[sl], key[i]);
+          atomicMax(&smax[sl], key[i]);
+        }
+      }
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < M; p += kBlock) {
-      const int sl = SL[p], sn = SN[p];
-      int dst = p;
-      if (sn >= 2 && p != sl + sn - 1) {
-        const u32 kp = K[p];
-        int r = 0;
-        for (int q = sl; q < sl + sn - 1; ++q) {
-          const u32 kq = K[q];
-          r += (kq < kp || (kq == kp && q < p)) ? 1 : 0;
-        }
-        dst = sl + r;
+    // 2. bucket counts (bucket = a slot of the sub-segment's sortable range)
+    u32 bk[kFinItems];
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      bk[i] = 0;
+      slot[i] = 0;
+      if (srt[i]) {
+        const int sl = SL[p], sn = SN[p];
+        bk[i] = u32(sl) + ref_bucket(key[i], smin[sl], smax[sl], u32(sn - 1));
+        slot[i] = atomicAdd(&H[bk[i]], 1u);
       }
-      P[cur ^ 1][dst] = P[cur][p];
+    }
+    __syncthreads();
+    // 3. exclusive scan of H[0, M) (H[M] = total)
+    {
+      constexpr int C = kFinItems;
+      u32 x[C], s = 0;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int b = tid * C + j;
+        x[j] = b < M ? H[b] : 0u;
+        s += x[j];
+      }
+      const u32 incl = dev::wave_incl_scan(s);
+      if (dev::lane() == 63) wsum[tid / 64] = incl;
+      __syncthreads();
+      u32 run = incl - s;
+      for (int w = 0; w < tid / 64; ++w) run += wsum[w];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int b = tid * C + j;
+        if (b < M) H[b] = run;
+        run += x[j];
+      }
+      if (tid == kFinThreads - 1) H[M] = run;
+    }
+    __syncthreads();
+    // 4. rows in bucket order; rank = rows of the sub-segment in lower buckets (+ the bucket's
+    // smaller rows below)
+    u32 rank[kFinItems], st[kFinItems], cnt[kFinItems];
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      rank[i] = 0;
+      st[i] = 0;
+      cnt[i] = 0;
+      if (srt[i]) {
+        const int sl = SL[p];
+        st[i] = H[bk[i]];
+        cnt[i] = H[bk[i] + 1] - st[i];
+        rank[i] = st[i] - H[sl];
+        tk[st[i] + slot[i]] = key[i];
+        tp[st[i] + slot[i]] = (unsigned short)p;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      for (u32 j = 0; j < cnt[i]; ++j) {
+        const u32 q = st[i] + j;
+        const u32 kq = tk[q];
+        rank[i] += (kq < key[i] || (kq == key[i] && int(tp[q]) < p)) ? 1u : 0u;
+      }
+    }
+    // 5. move: sortable rows to sl + rank, the others stay
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      if (p >= M) continue;
+      const int np = srt[i] ? int(SL[p]) + int(rank[i]) : p;
+      P[cur ^ 1][np] = P[cur][p];
+      K[np] = key[i];
     }
     __syncthreads();
     cur ^= 1;
-    for (int p = threadIdx.x; p < M; p += kBlock) {  // sub-segments of the next level
+    // 6. ties on the deciding pairs of every sub-segment (checked by its first slot's thread),
+    // then the next level's sub-segments
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      if (p >= M) continue;
+      const int sl = SL[p], sn = SN[p];
+      if (p == sl && sn >= 3) {
+        const int m = sn / 2;
+        const u32* kk = K + sl;
+        bool tie = kk[m - 1] == kk[m];
+        if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
+        if (m + 1 <= sn - 2 && kk[m] == kk[m + 1]) tie = true;
+        if (tie) atomicAdd(ties, 1u);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = tid + i * kFinThreads;
+      if (p >= M) continue;
       const int sl = SL[p], sn = SN[p];
       if (sn <= 1) continue;
       const int mid = sl + sn / 2;
@@ -253,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_finish(const float* __restrict__
     }
     __syncthreads();
   }
-  for (int p = threadIdx.x; p < M; p += kBlock) perm[lo + p] = P[cur][p];
+  for (int p = tid; p < M; p += kFinThreads) perm[lo + p] = P[cur][p];
 }
 
 __global__ __launch_bounds__(kBlock) void k_ref_gather(const float* __restrict__ pts, const u32* __restrict__ ids,
@@ -267,20 +603,11 @@ __global__ __launch_bounds__(kBlock) void k_ref_gather(const float* __restrict__
 }
 
 size_t align_up(size_t v) { return (v + 255) / 256 * 256; }
-
-void host_geometry(i64 n, int l, i64 j, i64* lo_out, i64* n_out) {
-  i64 lo = 0, m = n;
-  for (int b = l - 1; b >= 0; --b) {
-    if ((j >> b) & 1) {
-      lo = lo + m / 2 + 1;
-      m = m - m / 2 - 1;
-    } else {
-      m = m / 2;
-    }
-    if (m < 0) m = 0;
-  }
-  *lo_out = lo;
-  *n_out = m;
+int grid_for(i64 n) { return int(std::min<i64>(8192, std::max<i64>(1, (n + kBlock - 1) / kBlock))); }
+int pow2_floor(i64 v) {
+  int p = 1;
+  while (i64(p) * 2 <= v) p *= 2;
+  return p;
 }
 
 }  // namespace
@@ -290,35 +617,17 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   levels_ = 0;
   while ((n_ >> levels_) >= 2) ++levels_;  // the largest segment of level l has n >> l rows
-  // global levels: while the largest segment exceeds the LDS finish
-  lfin_ = 0;
+  lfin_ = 0;  // global levels: while the largest segment exceeds the LDS finish
   while (lfin_ < levels_ && (n_ >> lfin_) > kFinCap) ++lfin_;
-  level_tile0_.push_back(0);
+  i64 max_segs = 1, max_hist = 1;
   for (int l = 0; l < lfin_; ++l) {
-    const i64 segs = i64(1) << l;
-    u32 rows_before = 0;
-    for (i64 j = 0; j < segs; ++j) {
-      i64 lo = 0, m = 0;
-      host_geometry(n_, l, j, &lo, &m);
-      if (m < 2) continue;
-      const i64 sortable = m - 1;  // the last row of the segment keeps its slot
-      const u32 ts = u32((sortable + kTile - 1) / kTile);
-      const u32 t0 = u32(tiles_.size() - size_t(level_tile0_.back()));
-      for (u32 k = 0; k < ts; ++k) {
-        Tile t{};
-        t.pos0 = u32(lo + i64(k) * kTile);
-        t.len = u32(std::min<i64>(kTile, sortable - i64(k) * kTile));
-        t.seg_lo = u32(lo);
-        t.rows_before = rows_before;
-        t.ent0 = 256u * t0;
-        t.tseg = ts;
-        t.trel = k;
-        tiles_.push_back(t);
-      }
-      rows_before += u32(sortable);
-    }
-    level_tile0_.push_back(i64(tiles_.size()));
-    max_tiles_ = std::max<i64>(max_tiles_, level_tile0_[size_t(l + 1)] - level_tile0_[size_t(l)]);
+    RefLevel p;
+    p.segs = i64(1) << l;
+    p.bins = std::max(64, std::min(2048, pow2_floor(std::max<i64>(1, (n_ >> l) / 8))));
+    p.bps = int(std::max<i64>(1, std::min<i64>(2048 / p.segs, ((n_ >> l) + kChunk - 1) / kChunk)));
+    plan_.push_back(p);
+    max_segs = std::max(max_segs, p.segs);
+    max_hist = std::max(max_hist, p.segs * p.bins);
   }
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -329,15 +638,21 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
   const size_t nn = size_t(std::max<i64>(n_, 1));
   off_perm_[0] = take(nn * 4);
   off_perm_[1] = take(nn * 4);
-  off_key_[0] = take(nn * 4);
-  off_key_[1] = take(nn * 4);
-  off_tiles_ = take(tiles_.size() * sizeof(Tile));
-  const i64 ents = 256 * max_tiles_;
-  off_cnt_ = take(size_t(ents) * 4);
-  off_sums_ = take(size_t((ents + kScanChunk - 1) / kScanChunk + 1) * 4);
-  if ((ents + kScanChunk - 1) / kScanChunk > i64(kBlock) * 16)
-    throw std::invalid_argument("pkdtree: reference builder scan too large");
+  off_keys_ = take(nn * 4);
+  off_midc_ = take(lfin_ > 0 ? nn * 8 : 8);
+  off_hist_ = take(size_t(max_hist) * 4);
+  off_segs_ = take(size_t(max_segs) * sizeof(RefSeg));
+  off_words_ = take(16);  // [0] ties, [1] error
   ws_bytes_ = off;
+}
+
+u32 ReferenceBuilder::read_ties(const void* workspace, hipStream_t stream) const {
+  u32 w[4] = {0, 0, 0, 0};
+  if (n_ == 0) return 0;
+  PKD_HIP_CHECK(hipMemcpyAsync(w, static_cast<const char*>(workspace) + off_words_, 16, hipMemcpyDeviceToHost, stream));
+  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  if (w[1]) throw std::runtime_error("pkdtree: reference build inconsistency (histogram select)");
+  return w[0];
 }
 
 void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, float* out_pts, u32* out_ids,
@@ -345,44 +660,42 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
   if (n_ == 0) return;
   char* ws = static_cast<char*>(workspace);
   u32* perm[2] = {reinterpret_cast<u32*>(ws + off_perm_[0]), reinterpret_cast<u32*>(ws + off_perm_[1])};
-  u32* key[2] = {reinterpret_cast<u32*>(ws + off_key_[0]), reinterpret_cast<u32*>(ws + off_key_[1])};
-  Tile* tiles = reinterpret_cast<Tile*>(ws + off_tiles_);
-  u32* cnt = reinterpret_cast<u32*>(ws + off_cnt_);
-  u32* sums = reinterpret_cast<u32*>(ws + off_sums_);
-  if (!tiles_.empty())
-    PKD_HIP_CHECK(hipMemcpyAsync(tiles, tiles_.data(), tiles_.size() * sizeof(Tile), hipMemcpyHostToDevice, stream));
+  u32* keys = reinterpret_cast<u32*>(ws + off_keys_);
+  u64* midc = reinterpret_cast<u64*>(ws + off_midc_);
+  u32* hist = reinterpret_cast<u32*>(ws + off_hist_);
+  RefSeg* segs = reinterpret_cast<RefSeg*>(ws + off_segs_);
+  u32* words = reinterpret_cast<u32*>(ws + off_words_);
+  PKD_HIP_CHECK(hipMemsetAsync(words, 0, 16, stream));
   const int g = grid_for(n_);
   k_ref_init<<<g, kBlock, 0, stream>>>(perm[0], n_);
   PKD_LAUNCH_CHECK();
+  int cur = 0;
   for (int l = 0; l < lfin_; ++l) {
+    const RefLevel& p = plan_[size_t(l)];
     const int axis = (depth0_ + l) % dim_;
-    const Tile* lt = tiles + level_tile0_[size_t(l)];
-    const int nt = int(level_tile0_[size_t(l + 1)] - level_tile0_[size_t(l)]);
-    if (nt == 0) continue;
-    const i64 ents = 256 * i64(nt);
-    const int chunks = int((ents + kScanChunk - 1) / kScanChunk);
-    k_ref_keys<<<nt, kBlock, 0, stream>>>(pts, dim_, axis, perm[0], lt, key[0]);
+    const int S = int(p.segs), grid = S * p.bps;
+    const i64 hw = p.segs * p.bins;
+    k_ref_seg_init<<<int(std::min<i64>(1024, (std::max<i64>(hw, p.segs) + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
+        segs, p.segs, n_, l, hist, hw);
     PKD_LAUNCH_CHECK();
-    for (int pass = 0; pass < 4; ++pass) {  // 8-bit digits, LSD; four passes end in buffer 0
-      const int in = pass & 1, shift = 8 * pass;
-      k_rs_hist<<<nt, kBlock, 0, stream>>>(key[in], lt, shift, cnt);
-      PKD_LAUNCH_CHECK();
-      k_scan_sums<<<chunks, kBlock, 0, stream>>>(cnt, ents, sums);
-      PKD_LAUNCH_CHECK();
-      k_scan_top<<<1, kBlock, 0, stream>>>(sums, chunks);
-      PKD_LAUNCH_CHECK();
-      k_scan_apply<<<chunks, kBlock, 0, stream>>>(cnt, ents, sums);
-      PKD_LAUNCH_CHECK();
-      k_rs_scatter<<<nt, kBlock, 0, stream>>>(key[in], perm[in], key[in ^ 1], perm[in ^ 1], lt, shift, cnt);
-      PKD_LAUNCH_CHECK();
-    }
+    k_ref_keys<<<grid, kBlock, 0, stream>>>(pts, dim_, axis, perm[cur], segs, p.bps, keys);
+    PKD_LAUNCH_CHECK();
+    k_ref_hist<<<grid, kBlock, size_t(p.bins) * 4, stream>>>(keys, segs, p.bps, p.bins, hist);
+    PKD_LAUNCH_CHECK();
+    k_ref_select<<<S, 64, 0, stream>>>(segs, p.bins, hist, words + 1);
+    PKD_LAUNCH_CHECK();
+    k_ref_part<<<grid, kBlock, 0, stream>>>(keys, perm[cur], perm[cur ^ 1], midc, segs, p.bps, p.bins);
+    PKD_LAUNCH_CHECK();
+    k_ref_refine<<<S, kBlock, 0, stream>>>(segs, midc, perm[cur ^ 1], perm[cur], words);
+    PKD_LAUNCH_CHECK();
+    cur ^= 1;
   }
   if (lfin_ < levels_) {
-    const i64 segs = i64(1) << lfin_;
-    k_ref_finish<<<int(segs), kBlock, 0, stream>>>(pts, dim_, depth0_, perm[0], n_, lfin_, levels_);
+    const i64 segs_f = i64(1) << lfin_;
+    k_ref_finish<<<int(segs_f), kFinThreads, 0, stream>>>(pts, dim_, depth0_, perm[cur], n_, lfin_, levels_, words);
     PKD_LAUNCH_CHECK();
   }
-  k_ref_gather<<<g, kBlock, 0, stream>>>(pts, ids, id_base, dim_, perm[0], n_, out_pts, out_ids);
+  k_ref_gather<<<g, kBlock, 0, stream>>>(pts, ids, id_base, dim_, perm[cur], n_, out_pts, out_ids);
   PKD_LAUNCH_CHECK();
 }
 

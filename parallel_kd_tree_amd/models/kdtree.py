@@ -58,9 +58,8 @@ class KDTree:
             t = cls(tp, ti, depth0, mode)
             t._err = b.error_words()  # this build's error words (device copy, stream-ordered)
             return t
-        if points.is_cuda:  # reference mode on the GPU
-            b = ops.reference_builder(points.shape[0], points.shape[1], depth0, points.device)
-            tp, ti = b.build(points, ids, id_base)
+        if points.is_cuda:  # reference mode on the GPU (CPU std::sort builder where ties decide)
+            tp, ti, _ = ops.build_reference_gpu_checked(points, ids, id_base, depth0)
             return cls(tp, ti, depth0, mode)
         else:
             cpu_ids = ids

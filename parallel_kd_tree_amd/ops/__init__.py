@@ -27,7 +27,8 @@ def native_path() -> str:
     return native().__file__
 
 
-from .build import (GpuTreeBuilder, ReferenceTreeBuilder, build_cpu, build_gpu, build_gpu_checked, check_unique_ids,  # noqa: E402
+from .build import (GpuTreeBuilder, ReferenceTreeBuilder, build_cpu, build_gpu, build_gpu_checked, check_unique_ids,
+                    build_reference_gpu_checked,  # noqa: E402
                     gpu_builder, reference_builder)
 from .query import nn_gpu, unpack, finalize, nn_cpu  # noqa: E402
 

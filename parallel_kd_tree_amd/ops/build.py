@@ -99,7 +99,7 @@ class GpuTreeBuilder:
 
 class ReferenceTreeBuilder:
     """Reference-mode builder on the GPU (csrc/gpu/build_reference.hip): the reference's own
-    tree (first n - 1 points sorted per segment), one segmented radix sort per level."""
+    tree (first n - 1 points sorted per segment), by per-level rank selection."""
 
     def __init__(self, n: int, dim: int, depth0: int = 0):
         self._b = native().ReferenceBuilder(int(n), int(dim), int(depth0))
@@ -107,6 +107,15 @@ class ReferenceTreeBuilder:
 
     def build(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0):
         return tuple(self._b.build(points.contiguous(), ids, int(id_base)))
+
+    def read_ties(self) -> int:
+        """Segments of the last build whose tree equal keys decided (there the reference's
+        unstable std::sort decides: the tree may differ from the binary's). Synchronises."""
+        return int(self._b.read_ties())
+
+    @property
+    def global_levels(self) -> int:
+        return int(self._b.global_levels)
 
 
 _builders: dict = {}
@@ -171,6 +180,27 @@ def check_unique_ids(ids: Optional[torch.Tensor]) -> None:
         return
     if torch.unique(ids.reshape(-1)).numel() != ids.numel():
         raise ValueError("point ids must be distinct")
+
+
+def build_reference_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
+                                depth0: int = 0):
+    """The reference tree on the GPU; if equal keys decided any segment (std::sort is unstable,
+    so there the reference binary's tree is its library's choice), the tree is rebuilt by the
+    CPU std::sort builder, which mirrors the binary, with a warning. Returns (tree_pts,
+    tree_ids, ties). Synchronises."""
+    import warnings
+    points = points.contiguous()
+    b = reference_builder(points.shape[0], points.shape[1], depth0, points.device)
+    tp, ti = b.build(points, ids, id_base)
+    ties = b.read_ties()
+    if ties:
+        warnings.warn(f"reference mode: {ties} segment(s) of this input are decided by equal keys, where the "
+                      "reference's unstable std::sort picks the order; using the CPU std::sort builder",
+                      RuntimeWarning, stacklevel=2)
+        cids = ids if ids is not None else (torch.arange(points.shape[0], dtype=torch.int64) + id_base).to(torch.int32)
+        cp, ci = build_cpu(points.cpu(), cids.cpu(), "reference", depth0, 1)
+        tp, ti = cp.to(points.device), ci.to(points.device)
+    return tp, ti, ties
 
 
 def build_cpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, mode: str = "exact", depth0: int = 0,

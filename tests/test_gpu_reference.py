@@ -31,10 +31,54 @@ def tie_free(n, dim, seed):
                                    (100_000, 3), (30_000, 8), (20_000, 16)])
 def test_reference_tree_equals_cpu(gpu_device, n, dim):
     x = tie_free(n, dim, n + dim)
-    tp, ti = ops.ReferenceTreeBuilder(n, dim).build(x.to(gpu_device), None, 1)
+    b = ops.ReferenceTreeBuilder(n, dim)
+    tp, ti = b.build(x.to(gpu_device), None, 1)
     cp, ci = ops.build_cpu(x, (torch.arange(n) + 1).to(torch.int32), "reference", 0, 1)
+    assert b.read_ties() == 0, "tie-free data reported a deciding tie"
     assert torch.equal(ti.cpu(), ci), "GPU reference tree differs from the CPU reference tree"
     assert torch.equal(tp.cpu(), cp)
+
+
+@pytest.mark.parametrize("n,dim", [(1_000_003, 3), (600_000, 2), (300_000, 5)])
+def test_reference_selection_large_tie_free(gpu_device, n, dim):
+    """Several device-wide selection levels (segments > 2048 rows: middle-zone refine, left
+    maximum to the left segment's last slot, the last row kept) then the LDS finish."""
+    x = tie_free(n, dim, 7 * n + dim)
+    b = ops.ReferenceTreeBuilder(n, dim)
+    assert b.global_levels >= 8
+    tp, ti = b.build(x.to(gpu_device), None, 1)
+    cp, ci = ops.build_cpu(x, (torch.arange(n) + 1).to(torch.int32), "reference", 0, 1)
+    assert b.read_ties() == 0
+    assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+
+
+@pytest.mark.parametrize("n,vals", [(50_000, 7), (200_000, 1000), (3_001, 3)])
+def test_reference_ties_detected_and_rebuilt(gpu_device, n, vals):
+    """Heavy duplicates: equal keys decide segments (where std::sort's order is its library's
+    business). The GPU build must COUNT them, and KDTree.build(mode='reference') must then return
+    the CPU std::sort builder's tree (the reference binary's), with a warning -- never a tree that
+    silently differs."""
+    g = torch.Generator().manual_seed(n + vals)
+    x = torch.randint(0, vals, (n, 3), generator=g).float()
+    b = ops.ReferenceTreeBuilder(n, 3)
+    b.build(x.to(gpu_device), None, 1)
+    assert b.read_ties() > 0
+    with pytest.warns(RuntimeWarning, match="std::sort"):
+        t = pk.KDTree.build(x.to(gpu_device), id_base=1, mode="reference")
+    cp, ci = ops.build_cpu(x, (torch.arange(n) + 1).to(torch.int32), "reference", 0, 1)
+    assert torch.equal(t.tree_ids.cpu(), ci) and torch.equal(t.tree_pts.cpu(), cp)
+
+
+def test_kdtree_gpu_reference_ties_fall_back_to_cpu():
+    """The reference generator at 3 M points (~22.5 M distinct values per axis) puts
+    equal keys on deciding ranks: kdtree_gpu --mode reference notes it on stderr and prints the
+    CPU std::sort builder's answers, i.e. kdtree_sequential --mode reference's."""
+    g = _run([BIN / "kdtree_gpu", "--mode", "reference", 11, 2, 3_000_000])
+    c = _run([BIN / "kdtree_sequential", "--mode", "reference", 11, 2, 3_000_000])
+    assert g.returncode == 0 and c.returncode == 0, g.stderr + c.stderr
+    assert "CPU std::sort builder" in g.stderr
+    strip = lambda out: [l for l in out.splitlines() if not l.startswith("elapsed time")]  # noqa: E731
+    assert strip(g.stdout) == strip(c.stdout)
 
 
 def test_reference_tree_is_not_exact(gpu_device):

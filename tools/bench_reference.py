@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
-"""Reference-mode GPU build (csrc/gpu/build_reference.hip: the reference's own tree, every
-segment's first n-1 rows sorted per level by segmented LSD radix passes) against the exact
-builder, same points, warm timings. Usage: bench_reference.py [--n 10000000 ...] [--dim 3]"""
+"""Reference-mode GPU build (csrc/gpu/build_reference.hip: the reference's own tree by per-level
+rank selection, tie-checked) against the exact builder, same points, warm timings. Usage: bench_reference.py [--n 10000000 ...] [--dim 3]"""
 import argparse
 import json
 import os
@@ -39,4 +38,5 @@ for n in args.n:
     ref_ms = timed(lambda: rb.build(x, None, 1))
     exact_ms = timed(lambda: eb.build(x, None, 1))
     print(json.dumps({"n": n, "dim": args.dim, "reference_ms": round(ref_ms, 3), "exact_ms": round(exact_ms, 3),
-                      "global_levels": rb._b.global_levels, "sorted_levels": rb._b.sorted_levels}), flush=True)
+                      "global_levels": rb._b.global_levels, "sorted_levels": rb._b.sorted_levels,
+                      "ties": rb.read_ties()}), flush=True)
