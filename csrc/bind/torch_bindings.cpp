@@ -336,10 +336,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("split_streams", [](const Builder& b) { return b.b.split_streams(); })
       .def("describe", [](const Builder& b) { return b.b.describe(); })
       .def_property_readonly("sampled_top", [](const Builder& b) { return b.b.sampled_top(); })
+      .def_property_readonly("sampled", [](const Builder& b) { return b.b.sampled(); })
       .def_property_readonly("column_stride", [](const Builder& b) { return int64_t(b.b.column_stride()); })
       .def("top_band_report", [](Builder& b) {  // per top node: band rows, rank in the median's bin, staged rows
         TORCH_CHECK(b.ws.defined(), "no build yet");
         const auto v = b.b.top_band_report(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());
+        return std::vector<int64_t>(v.begin(), v.end());
+      })
+      .def("g3_report", [](Builder& b) {  // last sampled triple: level, then 25 words per segment
+        TORCH_CHECK(b.ws.defined(), "no build yet");
+        const auto v = b.b.g3_report(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());
         return std::vector<int64_t>(v.begin(), v.end());
       })
       .def("error_words", [](Builder& b) {  // view of the workspace's 4 error words (int32)

@@ -254,9 +254,9 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
       GpuBuilder* wrote = build_slice(k, true);
       // the shared workspace holds one build's error words; a sampled build is checked here, on
       // this rank alone, BEFORE any collective (its rebuild must not skew the collective order)
-      if (wrote && (slices.size() > 1 || wrote->sampled_top())) {
+      if (wrote && (slices.size() > 1 || wrote->sampled())) {
         u32 e = wrote->read_error(ws, s);
-        if ((e & top4_band_miss_bit()) && wrote->sampled_top()) {
+        if ((e & top4_band_miss_bit()) && wrote->sampled()) {
           wrote = build_slice(k, false);
           e = wrote->read_error(ws, s);
         }
@@ -314,7 +314,7 @@ int run_rank(int rank, int P, int R, Config cfg, const cli::Options& o, const st
   const float gen = float(std::chrono::duration<double, std::milli>(g1 - g0).count());
   // the build's device error word rides along (MAX over ranks: non-zero iff any rank failed)
   u32 berr = global ? gb->read_error(s) : slice_err;
-  if (!global && !ref && slices.size() == 1 && local > 0 && !bs[0]->sampled_top()) berr = bs[0]->read_error(ws, s);
+  if (!global && !ref && slices.size() == 1 && local > 0 && !bs[0]->sampled()) berr = bs[0]->read_error(ws, s);
   float* d_t = nullptr;
   PKD_HIP_CHECK(hipMalloc(&d_t, 4 * sizeof(float)));
   const float ht[4] = {gen, bld, qry, float(berr & 0xFFFFFFu) + (berr >> 24 ? 1.0f : 0.0f)};

@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
     PKD_HIP_CHECK(hipStreamSynchronize(s));
     u32 detail[3] = {0, 0, 0};
     u32 err0 = ref ? 0u : b.read_error(ws, s, detail);
-    if ((err0 & top4_band_miss_bit()) && b.sampled_top()) {
+    if ((err0 & top4_band_miss_bit()) && b.sampled()) {
       // a sampled top band missed its median (reported, never silent): rebuild unsampled
       // (its plan differs, e.g. a split build's per-stream histogram sets: the workspace is
       // grown to its size before the rebuild, never written past)

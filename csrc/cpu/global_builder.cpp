@@ -558,23 +558,23 @@ void GlobalBuilder::build(const float* pts, i64 n_local, u32 id_base, hipStream_
   PKD_HIP_CHECK(hipStreamWaitEvent(s, packed_, 0));
   // A sampled leaf whose band missed its median (error bit 0x20) is rebuilt locally without
   // sampling, from its received columns (intact: the sampled top reads them into the
-  // workspace's own). No collective is involved, so the ranks stay in step. One host wait per
+  // workspace's own, and a leaf with sampled triples only builds on a copy). No collective is involved, so the ranks stay in step. One host wait per
   // build, after everything is enqueued, and only when some leaf sampled its top levels.
   bool any_top = false;
-  for (int j = 0; j < mine; ++j) any_top = any_top || (lb[size_t(j)] && lb[size_t(j)]->sampled_top());
+  for (int j = 0; j < mine; ++j) any_top = any_top || (lb[size_t(j)] && lb[size_t(j)]->sampled());
   if (any_top) {
     comm_.wait(s, "leaf band check");
     std::vector<u32> le(size_t(mine), 0u);
     PKD_HIP_CHECK(hipMemcpy(le.data(), leaf_err, size_t(mine) * 4, hipMemcpyDeviceToHost));
     bool redo = false;
     for (int j = 0; j < mine; ++j)
-      if (lb[size_t(j)] && lb[size_t(j)]->sampled_top() && (le[size_t(j)] & top4_band_miss_bit())) redo = true;
+      if (lb[size_t(j)] && lb[size_t(j)]->sampled() && (le[size_t(j)] & top4_band_miss_bit())) redo = true;
     if (redo) {
       PKD_HIP_CHECK(hipMemsetAsync(err + 1, 0, 4, s));
       for (int j = 0; j < mine; ++j) {
         GpuBuilder* b = lb[size_t(j)];
         if (!b) continue;
-        if (b->sampled_top() && (le[size_t(j)] & top4_band_miss_bit())) {
+        if (b->sampled() && (le[size_t(j)] & top4_band_miss_bit())) {
           const int t = my_a + j;
           GpuBuilder& fb = leaf_builder(lay_.leaf_n[size_t(t)], LL, false);
           ensure_leaf_workspace(fb.workspace_bytes());

@@ -2392,6 +2392,925 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
 }
 
 // =====================================================================================
+// Sampled triples (G3). A triple (levels l, l+1, l+2 in one row-moving pass) otherwise needs the
+// exact pivots of l and l+1 BEFORE its scatter: two key sweeps over every row (k_scan 8 B,
+// k_scan2 12 B) and six small launches. Here those pivots are estimated from a sample first and
+// made exact afterwards over the few rows the estimate could not place (SURVEY.md §5.8's
+// "sample -> splitters -> exact fix-up", as the sampled top levels do for levels 0..3):
+//   k_g3_sample<1>  (segments x blocks) stratified sample of each segment (one 64-row run per
+//                   window): histograms of the children's keys on axis l+1 (the child from level
+//                   l's exact median bucket b*; inside b*, against the bucket's middle);
+//   k_g3_band<1>    per segment: each child's band [a, b] on axis l+1 holding its median with z
+//                   standard deviations of the sample rank to spare, and its estimated pivot;
+//   k_g3_sample<2>  the grandchildren's keys on axis l+2 (grandchild by the estimated pivot);
+//   k_g3_band<2>    their bands; the segment's staging regions (one per tag, sized from the
+//                   sample's band counts), the great-grandchildren's histogram bucketing;
+//   k_g3_part       every row ONCE: certain at all three levels (outside b*, outside its child's
+//                   band, outside its grandchild's band) -> straight into its great-grandchild
+//                   (8 zones, fused level-(l+3) histogram); otherwise into the staging region of
+//                   the level that could not place it (tag 0: b*, 1 + c: child band, 3 + g:
+//                   grandchild band);
+//   k_g3_res<0>     per segment: level l's median among the b* rows (b* holds rank n/2), written
+//                   out; the b* rows routed on (appended to a child / grandchild band region, or
+//                   inserted after their great-grandchild's certain rows);
+//   k_g3_res<1>     per child: its median's rank inside its band (exact counts of the rows left
+//                   of the band), found by a band histogram and a select over the median's bin,
+//                   written out; the band rows routed on;
+//   k_g3_res<2>     per grandchild: the same; every row is now in its great-grandchild.
+// Traffic per three levels: 16 + 16 B per row plus the sample and the staged rows, instead of
+// 8 + 12 + 16 + 16 B. A band that misses its median, or a region that overflows, marks the
+// segment bad and sets the sampled-levels error bit (top4_band_miss_bit()): the caller rebuilds
+// unsampled. A bad segment still leaves level l+3 consistent (its histograms are recounted from
+// the slots), so the remaining levels run to completion without faults. Replaces
+// build_tree_rec's std::sort of three levels (kdtree_sequential.cpp:30-66).
+constexpr int kG3Bins = 1024;      // sample histogram bins per node
+constexpr int kG3ResBins = 2048;   // band-row histogram bins of a resolve workgroup
+constexpr int kG3Cand = 2048;      // candidates of a median's bin selected in LDS
+constexpr int kG3Run = 64;         // sample rows per window (one wave's coalesced run)
+constexpr int kG3SampU = 4;        // windows per wave per sample iteration (loads in flight)
+constexpr int kG3Threads = 512;    // resolve workgroups
+constexpr int kG3Gg = 8;           // great-grandchildren of a segment
+
+struct G3Seg {
+  u32 a1[2], b1[2];  // children's bands on axis l+1 (orderable keys, inclusive)
+  u32 a2[4], b2[4];  // grandchildren's bands on axis l+2
+  u32 p1[2];         // children's estimated pivots (orderable; the second sample pass routes by them)
+  u32 tot[2];        // samples per child
+  u32 bsamp[6];      // samples inside each band (children, grandchildren)
+  u32 off[8];        // staging region of tag t: stage rows [lo + off[t], lo + off[t] + cap[t])
+  u32 cap[8];
+  u32 ins[8];        // staged rows inserted per great-grandchild (after its certain rows)
+  u32 bad;           // a band missed or a region overflowed: the segment's subtree is invalid
+  u32 pad[7];
+  // the pass's zone cursors, one 64-B line each (every block of the segment reserves on them once
+  // per chunk): zc[gg][0] certain rows placed per great-grandchild (its first slots), zc[8 + t][0]
+  // rows staged per tag t (may exceed cap: overflow)
+  u32 zc[16][16];
+};
+
+struct G3Args {
+  G3Seg* g3;       // per level-l segment (level-relative index)
+  u32* shist;      // sample histograms [segment][6][kG3Bins] (level-relative)
+  float* stage;    // staging columns (NCOL, stride ncol); a segment's regions lie in its [lo, lo + n)
+  i64 seg0;        // level-relative index of the launch's first segment
+  int axis2, axis3;
+  int bins3;       // level l+3 bins (0: l+3 is not a histogrammed global level)
+  u32* hist3;      // level l+3 histograms [8 * segs][bins3] (launch-relative)
+  int sample_div;  // one run of kG3Run rows per window of kG3Run * sample_div rows
+  int sblocks;     // sample blocks per segment
+  float z;         // band half-width in standard deviations of the sample rank
+  u32 salt;        // per build: the sample positions (so a miss) are never fixed by the input
+};
+
+__device__ __forceinline__ u32 g3_mix(u32 x) {  // murmur3 finaliser
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ void g3_bad(u32* err, G3Seg* gs) {
+  atomicOr(&gs->bad, 1u);
+  atomicOr(err, top4::kErrBit);
+}
+
+// Edges of level l's median bucket b* on its axis (the cell's range when the bucketing is flat).
+__device__ __forceinline__ void g3_bstar_edges(const LevelArgs& a, i64 h, float* e_lo, float* e_hi) {
+  const BucketParams prm = a.params[h];
+  const u32 bstar = a.state[h].bstar;
+  const float* cell = a.cells + h * 2 * a.dim;
+  *e_lo = cell[2 * a.axis];
+  *e_hi = cell[2 * a.axis + 1];
+  if (prm.scale > 0.0f) {
+    *e_lo = prm.lo + float(bstar) / prm.scale;
+    *e_hi = prm.lo + float(bstar + 1) / prm.scale;
+  }
+}
+
+__device__ __forceinline__ float g3_lo_of(u32 A) { return A ? from_orderable(A) : -INFINITY; }
+__device__ __forceinline__ float g3_hi_of(u32 B) { return B != 0xffffffffu ? from_orderable(B) : INFINITY; }
+
+// Range on axis `ax` of descendant (depth, idx) of a segment (depth 1: child idx; 2: grandchild;
+// 3: great-grandchild), from the segment's cell narrowed by b*'s edges and the bands that are
+// known (pass the band arrays, or nullptr for the ones not known yet). Any monotone bucketing is
+// correct: this only sets a histogram's resolution.
+__device__ __forceinline__ void g3_range(const float* cell, int ax, int axis, int ax1, int ax2, float e_lo,
+                                         float e_hi, int depth, int idx, const u32* a1, const u32* b1,
+                                         const u32* a2, const u32* b2, float* lo_out, float* hi_out) {
+  float lo = cell[2 * ax], hi = cell[2 * ax + 1];
+  const int s0 = idx >> (depth - 1);
+  if (ax == axis) {
+    if (s0 == 0) hi = fminf(hi, e_hi);
+    else lo = fmaxf(lo, e_lo);
+  }
+  if (depth >= 2 && ax == ax1 && a1 != nullptr) {
+    const int s1 = (idx >> (depth - 2)) & 1;
+    if (s1 == 0) hi = fminf(hi, g3_hi_of(b1[s0]));
+    else lo = fmaxf(lo, g3_lo_of(a1[s0]));
+  }
+  if (depth == 3 && ax == ax2 && a2 != nullptr) {
+    const int gi = idx >> 1;
+    if ((idx & 1) == 0) hi = fminf(hi, g3_hi_of(b2[gi]));
+    else lo = fmaxf(lo, g3_lo_of(a2[gi]));
+  }
+  if (!(hi >= lo)) hi = lo;
+  *lo_out = lo;
+  *hi_out = hi;
+}
+
+// Sample-histogram bucketing of node k of a segment (0, 1: children on axis l+1; 2 + g:
+// grandchildren on axis l+2). Sampler and band kernel compute the same one.
+__device__ __forceinline__ BucketParams g3_node_params(const LevelArgs& a, const G3Args& g, const G3Seg* gs, i64 h,
+                                                       int k) {
+  float e_lo, e_hi, lo, hi;
+  g3_bstar_edges(a, h, &e_lo, &e_hi);
+  const float* cell = a.cells + h * 2 * a.dim;
+  if (k < 2)
+    g3_range(cell, a.next_axis, a.axis, a.next_axis, g.axis2, e_lo, e_hi, 1, k, nullptr, nullptr, nullptr, nullptr,
+             &lo, &hi);
+  else
+    g3_range(cell, g.axis2, a.axis, a.next_axis, g.axis2, e_lo, e_hi, 2, k - 2, gs->a1, gs->b1, nullptr, nullptr,
+             &lo, &hi);
+  return make_params(lo, hi, kG3Bins);
+}
+
+// Sample pass PASS (1: children, 2: grandchildren), grid segs x sblocks.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_g3_sample(LevelArgs a, G3Args g) {
+  constexpr int NN = PASS == 1 ? 2 : 4;
+  __shared__ u32 hs[NN * kG3Bins];
+  __shared__ BucketParams pn[NN];
+  __shared__ u32 p1[2];
+  const i64 s = blockIdx.x / g.sblocks;
+  const int part = blockIdx.x % g.sblocks;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const G3Seg* gs = g.g3 + g.seg0 + s;
+  for (int i = threadIdx.x; i < NN * kG3Bins; i += kBlock) hs[i] = 0u;
+  if (threadIdx.x < NN) pn[threadIdx.x] = g3_node_params(a, g, gs, h, PASS == 1 ? int(threadIdx.x) : 2 + int(threadIdx.x));
+  if (PASS == 2 && threadIdx.x < 2) p1[threadIdx.x] = gs->p1[threadIdx.x];
+  __syncthreads();
+  if (n > 0) {
+    const BucketParams prm = a.params[h];
+    const u32 bstar = a.state[h].bstar;
+    float e_lo, e_hi;
+    g3_bstar_edges(a, h, &e_lo, &e_hi);
+    const float emid = 0.5f * (e_lo + e_hi);
+    const i64 nc = a.ncol;
+    const float* c0 = a.src + i64(a.axis) * nc + lo;
+    const float* c1 = a.src + i64(a.next_axis) * nc + lo;
+    const float* c2 = a.src + i64(g.axis2) * nc + lo;
+    const i64 W = i64(kG3Run) * g.sample_div;
+    const i64 nwin = (n + W - 1) / W;
+    const i64 w0 = nwin * part / g.sblocks, w1 = nwin * (part + 1) / g.sblocks;
+    const int w = threadIdx.x / 64, ln = dev::lane();
+    const u32 sseed = g3_mix(g.salt * 0x9e3779b9u + u32(g.seg0 + s));
+    for (i64 r0 = w0 + i64(w) * kG3SampU; r0 < w1; r0 += i64(kBlock / 64) * kG3SampU) {
+      float k0[kG3SampU], k1[kG3SampU], k2[kG3SampU];
+      bool v[kG3SampU];
+#pragma unroll
+      for (int u = 0; u < kG3SampU; ++u) {  // the windows' runs (all loads in flight together)
+        const i64 r = r0 + u;
+        const i64 wb = r * W, wl = min(W, n - wb);
+        const i64 span = wl > kG3Run ? wl - kG3Run + 1 : 1;
+        const i64 e = wb + i64(g3_mix(u32(r) ^ sseed) % u32(span)) + ln;
+        v[u] = r < w1 && e < wb + wl;
+        const i64 ei = v[u] ? e : 0;
+        k0[u] = c0[ei];
+        k1[u] = c1[ei];
+        k2[u] = PASS == 2 ? c2[ei] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kG3SampU; ++u) {
+        if (!v[u]) continue;
+        const u32 b = bucket_of(k0[u], prm, a.bins);
+        const u32 c = b != bstar ? (b < bstar ? 0u : 1u) : (k0[u] < emid ? 0u : 1u);
+        if (PASS == 1) {
+          atomicAdd(&hs[c * kG3Bins + bucket_of(k1[u], pn[c], kG3Bins)], 1u);
+        } else {
+          const u32 gi = 2 * c + (orderable(k1[u]) < p1[c] ? 0u : 1u);
+          atomicAdd(&hs[gi * kG3Bins + bucket_of(k2[u], pn[gi], kG3Bins)], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  u32* out = g.shist + (g.seg0 + s) * 6 * kG3Bins + (PASS == 1 ? 0 : 2 * kG3Bins);
+  for (int i = threadIdx.x; i < NN * kG3Bins; i += kBlock) {
+    const u32 x = hs[i];
+    if (x) atomicAdd(&out[i], x);
+  }
+}
+
+// One wave: the bin of a kG3Bins histogram holding the rank-th element (kG3Bins when
+// rank >= total); *below = elements before that bin, *total = all.
+__device__ __forceinline__ u32 g3_wave_find(const u32* h, u32 rank, u32* below, u32* total) {
+  constexpr int per = kG3Bins / 64;
+  const int ln = dev::lane();
+  u32 v[per], sum = 0;
+#pragma unroll
+  for (int i = 0; i < per; ++i) {
+    v[i] = h[ln * per + i];
+    sum += v[i];
+  }
+  const u32 incl = dev::wave_incl_scan(sum), excl = incl - sum;
+  *total = u32(__shfl(int(incl), 63, 64));
+  const u64 m = __ballot(rank >= excl && rank < incl);
+  if (!m) {
+    *below = *total;
+    return u32(kG3Bins);
+  }
+  const int src = __ffsll((long long)m) - 1;
+  u32 bin = 0, bel = excl;
+  if (ln == src) {
+    int i = 0;
+    while (i + 1 < per && rank >= bel + v[i]) bel += v[i++];
+    bin = u32(ln * per + i);
+  }
+  *below = u32(__shfl(int(bel), src, 64));
+  return u32(__shfl(int(bin), src, 64));
+}
+
+// Keys just below / above every value of bin b of a value-linear bucketing (a margin for the
+// bucketing's rounding), as in top4.
+__device__ __forceinline__ u32 g3_key_below(BucketParams p, u32 b) {
+  const float e = p.lo + float(b) / p.scale;
+  return orderable(e - (fabsf(e) * 1e-5f + float(kG3Bins) / p.scale * 1e-6f));
+}
+__device__ __forceinline__ u32 g3_key_above(BucketParams p, u32 b) {
+  const float e = p.lo + float(b + 1) / p.scale;
+  return orderable(e + (fabsf(e) * 1e-5f + float(kG3Bins) / p.scale * 1e-6f));
+}
+
+// One wave: the band of a node from its sample histogram: inclusive [*A, *B] of orderable keys,
+// the estimated pivot, the samples of the band's bins and all samples.
+__device__ __forceinline__ void g3_band(const u32* hb, BucketParams p, float z, u32* A, u32* B, u32* P, u32* bs,
+                                        u32* tot) {
+  u32 below = 0, c = 0;
+  (void)g3_wave_find(hb, 0, &below, &c);
+  *tot = c;
+  *A = 0u;
+  *B = 0xffffffffu;
+  *P = orderable(p.lo);
+  *bs = c;
+  if (c == 0 || !(p.scale > 0.0f)) return;  // no resolution: the whole range is the band
+  const u32 half = u32(ceilf(z * sqrtf(float(c)) * 0.5f)) + 2u;
+  const u32 rm = c / 2, rlo = rm > half ? rm - half : 0u, rhi = min(c - 1, rm + half);
+  u32 t = 0, bel_lo = 0, bel_hi = 0;
+  const u32 bl = g3_wave_find(hb, rlo, &bel_lo, &t);
+  const u32 bm = g3_wave_find(hb, rm, &below, &t);
+  const u32 bh = g3_wave_find(hb, rhi, &bel_hi, &t);
+  const bool open_lo = rlo == 0 || bl == 0, open_hi = rhi >= c - 1 || bh >= u32(kG3Bins - 1);
+  *A = open_lo ? 0u : g3_key_below(p, bl);
+  *B = open_hi ? 0xffffffffu : g3_key_above(p, bh);
+  *P = orderable(p.lo + (float(bm) + 0.5f) / p.scale);
+  *bs = (open_hi ? c : bel_hi + hb[bh]) - (open_lo ? 0u : bel_lo);
+}
+
+// Bands from the sample histograms (one workgroup per segment). PASS 1: children; PASS 2:
+// grandchildren, then the staging layout, the counters, provisional cells of the 14 nodes below
+// (exact ones replace them as the medians are found; a bad segment keeps them), the
+// great-grandchildren's bucketing and their zeroed level-(l+3) histograms.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_g3_band(LevelArgs a, G3Args g) {
+  __shared__ BucketParams pn[4];
+  __shared__ u32 sa1[2], sb1[2], sa2[4], sb2[4], sbs[6], stot[2];
+  const i64 s = blockIdx.x, h = a.heap0 + s;
+  const i64 n = a.seg_n[h];
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  const u32* hsamp = g.shist + (g.seg0 + s) * 6 * kG3Bins;
+  const int w = threadIdx.x / 64, ln = dev::lane(), tid = threadIdx.x;
+  const int D = a.dim;
+  if (PASS == 1) {
+    if (tid < 2) pn[tid] = g3_node_params(a, g, gs, h, tid);
+    __syncthreads();
+    if (w < 2) {
+      u32 A, B, P, bs, tot;
+      g3_band(hsamp + w * kG3Bins, pn[w], g.z, &A, &B, &P, &bs, &tot);
+      if (ln == 0) {
+        gs->a1[w] = A;
+        gs->b1[w] = B;
+        gs->p1[w] = P;
+        gs->bsamp[w] = bs;
+        gs->tot[w] = tot;
+      }
+    }
+    return;
+  }
+  if (tid < 4) pn[tid] = g3_node_params(a, g, gs, h, 2 + tid);
+  if (tid < 2) {
+    sa1[tid] = gs->a1[tid];
+    sb1[tid] = gs->b1[tid];
+    sbs[tid] = gs->bsamp[tid];
+    stot[tid] = gs->tot[tid];
+  }
+  __syncthreads();
+  {
+    u32 A, B, P, bs, tot;
+    g3_band(hsamp + (2 + w) * kG3Bins, pn[w], g.z, &A, &B, &P, &bs, &tot);
+    if (ln == 0) {
+      gs->a2[w] = A;
+      gs->b2[w] = B;
+      gs->bsamp[2 + w] = bs;
+      sa2[w] = A;
+      sb2[w] = B;
+      sbs[2 + w] = bs;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {  // staging layout: the band regions first, tag 0 (b*'s rows, counted exactly) last
+    const u32 mid = a.state[h].cnt_mid;
+    const u32 ctot = stot[0] + stot[1];
+    const float scale = float(n) / float(max(1u, ctot));
+    u32 cap[7];
+    for (int t = 1; t <= 2; ++t) cap[t] = u32(fminf(float(sbs[t - 1]) * scale * 1.5f + 2048.0f, float(n)));
+    for (int t = 3; t <= 6; ++t)  // + the rows the resolves append: b*'s and some of the child band's
+      cap[t] = u32(fminf(float(sbs[t - 1]) * scale * 1.5f + 2048.0f + float(mid) + 0.5f * float(cap[1 + (t - 3) / 2]),
+                         float(n)));
+    u64 off = 0;
+    for (int t = 1; t <= 6; ++t) {
+      gs->off[t] = u32(off);
+      off += cap[t];
+    }
+    const bool fits = off + mid <= u64(n);
+    for (int t = 1; t <= 6; ++t) gs->cap[t] = fits ? cap[t] : 0u;
+    gs->off[0] = u32(n) - mid;
+    gs->cap[0] = fits ? mid : 0u;
+    gs->off[7] = 0u;
+    gs->cap[7] = 0u;
+    gs->bad = fits ? 0u : 1u;
+    if (!fits) atomicOr(a.err, top4::kErrBit);
+  }
+  if (tid < 8) {
+    gs->zc[8 + (tid)][0] = 0u;
+    gs->zc[tid][0] = 0u;
+    gs->ins[tid] = 0u;
+  }
+  if (g.bins3 > 0)
+    for (int i = tid; i < kG3Gg * g.bins3; i += kBlock) g.hist3[(kG3Gg * s) * g.bins3 + i] = 0u;
+  float e_lo, e_hi;
+  g3_bstar_edges(a, h, &e_lo, &e_hi);
+  const float* cell = a.cells + h * 2 * D;
+  for (int e = tid; e < 14 * D; e += kBlock) {  // (node, axis) per thread
+    const int k = 1 + e / D, c = e % D;
+    const int depth = k < 3 ? 1 : (k < 7 ? 2 : 3);
+    const int idx = k - ((1 << depth) - 1);
+    float lo, hi;
+    g3_range(cell, c, a.axis, a.next_axis, g.axis2, e_lo, e_hi, depth, idx, sa1, sb1, sa2, sb2, &lo, &hi);
+    const i64 hk = k < 3 ? 2 * h + k : (k < 7 ? 4 * h + k : 8 * h + k);
+    a.cells[hk * 2 * D + 2 * c] = lo;
+    a.cells[hk * 2 * D + 2 * c + 1] = hi;
+    if (depth == 3 && c == g.axis3 && g.bins3 > 0) a.params[hk] = make_params(lo, hi, g.bins3);
+  }
+}
+
+// The pass: every row once; 8 great-grandchild zones + the 7 staging regions. Zone ranks as in
+// k_partition3: LDS atomics (ATOM) or wave ballots.
+template <int NCOL, int KI, bool ATOM>
+__global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
+  constexpr int kItems = KI;
+  constexpr int kCh = kBlock * KI;
+  constexpr int NZ = 15;  // 0..7 great-grandchild, 8 + t staging tag t
+  constexpr int D = NCOL - 1;
+  constexpr int W = kBlock / 64;
+  static_assert(kItems % 4 == 0, "16-B row loads take 4 rows per item group");
+  extern __shared__ __align__(16) u32 nh[];  // [8 * bins3]
+  __shared__ u32 wcnt[W][16];
+  __shared__ u32 wbase[W][16];
+  __shared__ u32 gcnt[ATOM ? 1 : NZ][64];
+  __shared__ BucketParams ggp[8];
+  __shared__ i64 glo[8], gn[8];
+  __shared__ u32 roff[8], rcap[8];
+  __shared__ u32 ba1[2], bb1[2], ba2[4], bb2[4];
+  __shared__ u32 sbad;
+  const i64 s = blockIdx.x / a.bps;
+  const int part = blockIdx.x % a.bps;
+  const i64 h = a.heap0 + s;
+  const i64 lo = a.seg_lo[h], n = a.seg_n[h];
+  const int nb3 = g.bins3;
+  const bool fuse = nb3 > 0;
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  if (fuse)
+    for (int b = threadIdx.x; b < kG3Gg * nb3; b += kBlock) nh[b] = 0;
+  const i64 gg0 = 8 * h + 7;
+  if (threadIdx.x < W * 16) (&wcnt[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x < 8) {
+    const int t = int(threadIdx.x);
+    if (fuse) ggp[t] = a.params[gg0 + t];
+    glo[t] = a.seg_lo[gg0 + t];
+    gn[t] = a.seg_n[gg0 + t];
+    roff[t] = gs->off[t];
+    rcap[t] = gs->cap[t];
+  }
+  if (threadIdx.x < 2) {
+    ba1[threadIdx.x] = gs->a1[threadIdx.x];
+    bb1[threadIdx.x] = gs->b1[threadIdx.x];
+  }
+  if (threadIdx.x < 4) {
+    ba2[threadIdx.x] = gs->a2[threadIdx.x];
+    bb2[threadIdx.x] = gs->b2[threadIdx.x];
+  }
+  if (threadIdx.x == 0) sbad = 0u;
+  const i64 per = (n + a.bps - 1) / a.bps;
+  const i64 b0 = min(n, i64(part) * per), b1 = min(n, b0 + per);
+  const u32 bstar = a.state[h].bstar;
+  const BucketParams prm = a.params[h];
+  __syncthreads();
+  const float* __restrict__ src = a.src;
+  float* __restrict__ dst = a.dst;
+  float* __restrict__ stg = g.stage;
+  const i64 nc = a.ncol;
+  const int axis = a.axis, ax1 = a.next_axis, ax2 = g.axis2, ax3 = g.axis3;
+  const int w = threadIdx.x / 64;
+  auto classify = [&](float k0, float k1, float k2, bool valid) -> u32 {
+    if (!valid) return 15u;
+    const u32 b = bucket_of(k0, prm, a.bins);
+    if (b == bstar) return 8u;  // tag 0
+    const u32 c = b < bstar ? 0u : 1u;
+    const u32 o1 = orderable(k1);
+    if (o1 >= ba1[c] && o1 <= bb1[c]) return 9u + c;  // tag 1 + c
+    const u32 gi = 2 * c + (o1 > bb1[c] ? 1u : 0u);
+    const u32 o2 = orderable(k2);
+    if (o2 >= ba2[gi] && o2 <= bb2[gi]) return 11u + gi;  // tag 3 + gi
+    return 2 * gi + (o2 > bb2[gi] ? 1u : 0u);
+  };
+  const i64 cstart = ((lo + b0) & ~i64(3)) - lo;
+  for (i64 c0 = cstart; c0 < b1; c0 += kCh) {
+    float row[kItems][NCOL];
+    bool vld[kItems];
+#pragma unroll
+    for (int gq = 0; gq < kItems / 4; ++gq) {
+      const i64 e4 = c0 + (i64(gq) * kBlock + threadIdx.x) * 4;
+      const i64 p4 = lo + (e4 < b1 ? e4 : cstart);
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) {
+        const float4 v = *reinterpret_cast<const float4*>(src + i64(c) * nc + p4);
+        row[4 * gq + 0][c] = v.x;
+        row[4 * gq + 1][c] = v.y;
+        row[4 * gq + 2][c] = v.z;
+        row[4 * gq + 3][c] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vld[4 * gq + j] = e4 + j >= b0 && e4 + j < b1;
+    }
+    u32 zone_pre[kItems];
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      float k0 = row[i][0], k1 = row[i][0], k2 = row[i][0], k3 = row[i][0];
+#pragma unroll
+      for (int c = 1; c < D; ++c) {
+        k0 = c == axis ? row[i][c] : k0;
+        k1 = c == ax1 ? row[i][c] : k1;
+        k2 = c == ax2 ? row[i][c] : k2;
+        k3 = c == ax3 ? row[i][c] : k3;
+      }
+      const u32 q = classify(k0, k1, k2, vld[i]);
+      if constexpr (ATOM) {
+        zone_pre[i] = (q << 16) | atomicAdd(&wcnt[w][q], 1u);
+      } else {
+        u32 my = 0;
+#pragma unroll
+        for (int z = 0; z < NZ; ++z) {
+          const u64 m = __ballot(q == u32(z));
+          if (dev::lane() == 0) gcnt[z][i * 4 + w] = __popcll(m);
+          if (q == u32(z)) my = mbcnt(m);
+        }
+        zone_pre[i] = (q << 16) | my;
+      }
+      if (fuse && q < 8u) atomicAdd(&nh[q * u32(nb3) + bucket_of(k3, ggp[q], nb3)], 1u);
+    }
+    __syncthreads();
+    if constexpr (!ATOM) {
+      for (int z = w; z < NZ; z += W) {  // wave w scans zones w, w + 4, ...
+        const int ln = dev::lane();
+        const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
+        const u32 incl = dev::wave_incl_scan(v);
+        const u32 tot = __shfl(incl, 63, 64);
+        u32 base = 0;
+        if (ln == 0 && tot) base = atomicAdd(&gs->zc[z][0], tot);
+        base = __shfl(base, 0, 64);
+        gcnt[z][ln] = base + incl - v;
+      }
+    } else if (threadIdx.x < NZ) {  // zone z's waves, scanned, reserved once per chunk
+      const int z = int(threadIdx.x);
+      u32 c[W], tot = 0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        c[k] = wcnt[k][z];
+        tot += c[k];
+      }
+      u32 base = tot ? atomicAdd(&gs->zc[z][0], tot) : 0u;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        wbase[k][z] = base;
+        base += c[k];
+        wcnt[k][z] = 0;
+      }
+    }
+    if (ATOM && threadIdx.x >= NZ && threadIdx.x < NZ + W) wcnt[threadIdx.x - NZ][15] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+      const u32 zi = zone_pre[i] >> 16;
+      if (zi >= u32(NZ)) continue;
+      const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
+      i64 d = -1;
+      float* out = dst;
+      if (zi < 8u) {
+        if (i64(off) < gn[zi]) d = glo[zi] + off;
+      } else if (off < rcap[zi - 8]) {
+        d = lo + roff[zi - 8] + off;
+        out = stg;
+      }
+      if (d < 0) {
+        sbad = 1u;
+        continue;
+      }
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = row[i][c];
+    }
+    if (!ATOM) __syncthreads();  // the next chunk rewrites gcnt
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && sbad) g3_bad(a.err, gs);
+  if (fuse) {
+    u32* hn = g.hist3 + (kG3Gg * s) * nb3;
+    for (int b = threadIdx.x; b < kG3Gg * nb3; b += kBlock) {
+      const u32 v = nh[b];
+      if (v) atomicAdd(&hn[b], v);
+    }
+  }
+}
+
+// rank-th smallest (0-based) of the composites that each(f) visits (every thread of the NT calls
+// it and visits its share): MSD radix select on 8-bit digits below the highest bit in which the
+// candidates differ.
+template <int NT, class Each>
+__device__ u64 g3_block_select(Each each, u32 rank) {
+  __shared__ __align__(16) u32 hist[256];
+  __shared__ u64 rmn[NT / 64], rmx[NT / 64];
+  __shared__ u32 info[2];
+  u64 mn = ~0ull, mx = 0ull;
+  each([&](u64 v) {
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  });
+  mn = dev::wave_min_u64(mn);
+  mx = dev::wave_max_u64(mx);
+  __syncthreads();
+  if (dev::lane() == 0) {
+    rmn[threadIdx.x / 64] = mn;
+    rmx[threadIdx.x / 64] = mx;
+  }
+  __syncthreads();
+  mn = rmn[0];
+  mx = rmx[0];
+  for (int k = 1; k < NT / 64; ++k) {
+    mn = rmn[k] < mn ? rmn[k] : mn;
+    mx = rmx[k] > mx ? rmx[k] : mx;
+  }
+  const u64 diff = mn ^ mx;
+  if (!diff) return mn;
+  int hb = 63 - __builtin_clzll(diff);
+  u64 prefix = hb >= 63 ? 0ull : (mn & ~((2ull << hb) - 1ull));
+  while (hb >= 0) {
+    const int sh = hb >= 7 ? hb - 7 : 0;
+    const u32 dmask = (2u << (hb - sh)) - 1u;
+    const u64 himask = hb >= 63 ? 0ull : ~((2ull << hb) - 1ull);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0u;
+    __syncthreads();
+    each([&](u64 v) {
+      if ((v & himask) == prefix) atomicAdd(&hist[u32(v >> sh) & dmask], 1u);
+    });
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x;
+      u32 v4[4], s4 = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v4[q] = hist[4 * l + q];
+        s4 += v4[q];
+      }
+      const u32 incl = dev::wave_incl_scan(s4);
+      u32 c = incl - s4;
+      if (rank >= c && rank < incl) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (rank >= c && rank < c + v4[q]) {
+            info[0] = u32(4 * l + q);
+            info[1] = c;
+          }
+          c += v4[q];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= u64(info[0] & dmask) << sh;
+    rank -= info[1];
+    hb = sh - 1;
+  }
+  return prefix;
+}
+
+// Resolve of one node: LEVEL 0 the segment (over b*'s rows), 1 a child, 2 a grandchild (over
+// its band rows). Grid: segments x nodes per segment.
+template <int NCOL, int LEVEL>
+__global__ __launch_bounds__(kG3Threads) void k_g3_res(LevelArgs a, G3Args g) {
+  constexpr int NT = kG3Threads;
+  constexpr int D = NCOL - 1;
+  constexpr int NODES = LEVEL == 0 ? 1 : (LEVEL == 1 ? 2 : 4);  // nodes of this level per segment
+  constexpr int NG = 8 / NODES;                                  // great-grandchildren below a node
+  constexpr int R = 4;                                           // rows per thread per move chunk
+  __shared__ u32 hres[kG3ResBins];
+  __shared__ u64 cand[kG3Cand];
+  __shared__ u32 h3[NG * kTripleBins];
+  __shared__ u32 lc[16], lbase[16], ssum[NT / 64];
+  __shared__ u32 ccnt, sbin, srank, scnt, sbad, sok, sm, st_, incomplete;
+  __shared__ BucketParams bp;
+  const i64 s = blockIdx.x / NODES;
+  const int x = int(blockIdx.x % NODES);
+  const i64 h = a.heap0 + s;
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  const i64 n = a.seg_n[h];
+  const int tid = threadIdx.x;
+  const int nb3 = g.bins3;
+  const i64 nc = a.ncol;
+  const int ax = LEVEL == 0 ? a.axis : (LEVEL == 1 ? a.next_axis : g.axis2);
+  const i64 hn = LEVEL == 0 ? h : (LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x);  // the node
+  const int tag = LEVEL == 0 ? 0 : (LEVEL == 1 ? 1 + x : 3 + x);
+  const int fg = NG * x;               // its first great-grandchild (among the segment's eight)
+  const i64 gg0 = 8 * h + 7 + fg;
+  float* __restrict__ stg = g.stage;
+  const i64 lo = a.seg_lo[h];
+  const i64 nn = a.seg_n[hn], nlo = a.seg_lo[hn];
+  for (int i = tid; i < NG * nb3; i += NT) h3[i] = 0u;
+  if (tid < 16) lc[tid] = 0u;
+  if (tid == 0) {  // the node's median: its rank among the staged rows, from exact counts of the rows left of them
+    ccnt = 0u;
+    sbad = 0u;
+    u32 ok = n > 0 && gs->bad == 0u;
+    const u32 m = gs->zc[8 + (tag)][0];
+    i64 left = 0;
+    if (LEVEL == 0) {
+      const SegState st = a.state[h];
+      left = st.cnt_less;
+      ok = ok && m == st.cnt_mid;
+    } else if (LEVEL == 1) {  // certain and resolved rows of the child's left grandchild
+      left = i64(gs->zc[4 * x][0]) + gs->zc[4 * x + 1][0] + gs->ins[4 * x] + gs->ins[4 * x + 1] + gs->zc[8 + (3 + 2 * x)][0];
+    } else {
+      left = i64(gs->zc[2 * x][0]) + gs->ins[2 * x];
+    }
+    const i64 tt = nn / 2 - left;
+    const bool hit = m <= gs->cap[tag] && tt >= 0 && tt < i64(m);
+    if (ok && !hit) sbad = 1u;  // a band missed its median
+    sok = ok && hit;
+    sm = m;
+    st_ = u32(tt);
+  }
+  __syncthreads();  // (every counter read before this workgroup moves rows)
+  const bool ok = sok != 0u;
+  const u32 m = sm, t = st_;
+  const i64 r0 = lo + gs->off[tag];  // the node's staged rows: stage rows [r0, r0 + m)
+  auto key_at = [&](u32 e) { return stg[i64(ax) * nc + r0 + e]; };
+  auto id_at = [&](u32 e) { return reinterpret_cast<const u32*>(stg)[i64(D) * nc + r0 + e]; };
+  u64 piv = 0;
+  if (ok) {
+    // the median's bin (LEVEL 0: all of b* is the candidate set)
+    u32 bin = 0, cnt_bin = m, rank = t;
+    if (LEVEL > 0) {
+      if (tid == 0) {
+        const float* cl = a.cells + hn * 2 * D;
+        const u32 A = LEVEL == 1 ? gs->a1[x] : gs->a2[x], B = LEVEL == 1 ? gs->b1[x] : gs->b2[x];
+        const float flo = fmaxf(g3_lo_of(A), cl[2 * ax]);
+        const float fhi = fminf(g3_hi_of(B), cl[2 * ax + 1]);
+        bp = make_params(flo, fhi > flo ? fhi : flo, kG3ResBins);
+      }
+      for (int i = tid; i < kG3ResBins; i += NT) hres[i] = 0u;
+      __syncthreads();
+      const BucketParams p = bp;
+      for (u32 e0 = 0; e0 < m; e0 += NT * 8) {
+        float k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const u32 e = e0 + u * NT + tid;
+          k[u] = key_at(e < m ? e : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + u * NT + tid < m) atomicAdd(&hres[bucket_of(k[u], p, kG3ResBins)], 1u);
+      }
+      __syncthreads();
+      constexpr int per = kG3ResBins / NT;  // bins per thread, one block scan
+      u32 v[per], sum = 0;
+#pragma unroll
+      for (int i = 0; i < per; ++i) {
+        v[i] = hres[tid * per + i];
+        sum += v[i];
+      }
+      const u32 incl = dev::wave_incl_scan(sum);
+      if (dev::lane() == 63) ssum[tid / 64] = incl;
+      __syncthreads();
+      u32 ex = incl - sum;
+      for (int k2 = 0; k2 < tid / 64; ++k2) ex += ssum[k2];
+      if (t >= ex && t < ex + sum) {
+        u32 c = ex;
+        int i = 0;
+        while (i + 1 < per && t >= c + v[i]) c += v[i++];
+        sbin = u32(tid * per + i);
+        srank = t - c;
+        scnt = v[i];
+      }
+      __syncthreads();
+      bin = sbin;
+      rank = srank;
+      cnt_bin = scnt;
+    }
+    // the bin's composites into LDS (streamed from the stage when they do not fit)
+    const bool fits = cnt_bin <= u32(kG3Cand);
+    const BucketParams p = bp;
+    if (fits) {
+      for (u32 e0 = 0; e0 < m; e0 += NT) {
+        const u32 e = e0 + tid;
+        bool mine = false;
+        u64 ck = 0;
+        if (e < m) {
+          const float kf = key_at(e);
+          mine = LEVEL == 0 || bucket_of(kf, p, kG3ResBins) == bin;
+          if (mine) ck = composite_key(kf, id_at(e));
+        }
+        const u64 bm = __ballot(mine);
+        if (!bm) continue;
+        const int leader = __ffsll((long long)bm) - 1;
+        u32 base = 0;
+        if (dev::lane() == leader) base = atomicAdd(&ccnt, u32(__popcll(bm)));
+        base = u32(__shfl(int(base), leader, 64));
+        if (mine) cand[base + mbcnt(bm)] = ck;
+      }
+      __syncthreads();
+    }
+    piv = g3_block_select<NT>(
+        [&](auto f) {
+          if (fits) {
+            for (u32 e = tid; e < cnt_bin; e += NT) f(cand[e]);
+          } else {
+            for (u32 e = tid; e < m; e += NT) {
+              const float kf = key_at(e);
+              if (LEVEL == 0 || bucket_of(kf, p, kG3ResBins) == bin) f(composite_key(kf, id_at(e)));
+            }
+          }
+        },
+        rank);
+    // the node's children's cells: its cell split at the pivot
+    const float pk = from_orderable(u32(piv >> 32));
+    const float* cl = a.cells + hn * 2 * D;
+    for (int q = tid; q < 2 * D; q += NT) {
+      const float v0 = cl[q];
+      a.cells[(2 * hn + 1) * 2 * D + q] = q == 2 * ax + 1 ? pk : v0;
+      a.cells[(2 * hn + 2) * 2 * D + q] = q == 2 * ax ? pk : v0;
+    }
+  }
+  // the staged rows move on: the median to its output slot; code 0..NG-1 a great-grandchild
+  // (inserted after its certain rows), 8 + t the staging region of tag t (appended), 15 nothing
+  const int axis = a.axis, ax1 = a.next_axis, ax2 = g.axis2, ax3 = g.axis3;
+  u32 A1[2], B1[2], A2[4], B2[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    A1[i] = gs->a1[i];
+    B1[i] = gs->b1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    A2[i] = gs->a2[i];
+    B2[i] = gs->b2[i];
+  }
+  auto dest = [&](const float* row) -> u32 {
+    float k0 = row[0], k1 = row[0], k2 = row[0];
+#pragma unroll
+    for (int c = 1; c < D; ++c) {
+      k0 = c == axis ? row[c] : k0;
+      k1 = c == ax1 ? row[c] : k1;
+      k2 = c == ax2 ? row[c] : k2;
+    }
+    const u32 id = __float_as_uint(row[D]);
+    const u64 ck = composite_key(LEVEL == 0 ? k0 : (LEVEL == 1 ? k1 : k2), id);
+    if (ck == piv) {
+      const i64 mpos = nlo + nn / 2;
+#pragma unroll
+      for (int c = 0; c < D; ++c) a.out_pts[mpos * D + c] = row[c];
+      a.out_ids[mpos] = id;
+      return 15u;
+    }
+    const u32 side = ck < piv ? 0u : 1u;
+    if (LEVEL == 2) return side;
+    u32 gi;
+    if (LEVEL == 0) {
+      const u32 o1 = orderable(k1);
+      if (o1 >= A1[side] && o1 <= B1[side]) return 9u + side;
+      gi = 2 * side + (o1 > B1[side] ? 1u : 0u);
+    } else {
+      gi = 2 * u32(x) + side;
+    }
+    const u32 o2 = orderable(k2);
+    if (o2 >= A2[gi] && o2 <= B2[gi]) return 11u + gi;
+    return 2 * gi + (o2 > B2[gi] ? 1u : 0u) - u32(fg);
+  };
+  if (ok) {
+    for (u32 e0 = 0; e0 < m; e0 += NT * R) {
+      float row[R][NCOL];
+      u32 code[R], rk[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const u32 e = e0 + u * NT + tid;
+        const u32 ei = e < m ? e : 0;
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) row[u][c] = stg[i64(c) * nc + r0 + ei];
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        code[u] = e0 + u * NT + tid < m ? dest(row[u]) : 15u;
+        rk[u] = code[u] < 15u ? atomicAdd(&lc[code[u]], 1u) : 0u;
+      }
+      __syncthreads();
+      if (tid < 15) {  // one reservation per destination per chunk
+        const u32 c = lc[tid];
+        if (c) lbase[tid] = atomicAdd(tid < 8 ? &gs->ins[fg + tid] : &gs->zc[8 + (tid - 8)][0], c);
+        lc[tid] = 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const u32 cd = code[u];
+        if (cd >= 15u) continue;
+        const u32 q = lbase[cd] + rk[u];
+        float* out = a.dst;
+        i64 d = -1;
+        if (cd < 8u) {
+          const i64 gq = gg0 + cd;
+          const i64 pos = i64(gs->zc[fg + cd][0]) + q;
+          if (pos < a.seg_n[gq]) {
+            d = a.seg_lo[gq] + pos;
+            if (nb3 > 0) {
+              float k3 = row[u][0];
+#pragma unroll
+              for (int c = 1; c < D; ++c) k3 = c == ax3 ? row[u][c] : k3;
+              atomicAdd(&h3[cd * nb3 + bucket_of(k3, a.params[gq], nb3)], 1u);
+            }
+          }
+        } else if (q < gs->cap[cd - 8u]) {
+          d = lo + gs->off[cd - 8u] + q;
+          out = stg;
+        }
+        if (d < 0) {
+          sbad = 1u;
+          continue;
+        }
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = row[u][c];
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && sbad) g3_bad(a.err, gs);
+  if (nb3 <= 0) return;
+  u32* hn3 = g.hist3 + (kG3Gg * s + fg) * nb3;
+  if (LEVEL < 2) {  // the inserted rows' level-(l+3) counts
+    for (int i = tid; i < NG * nb3; i += NT)
+      if (h3[i]) atomicAdd(&hn3[i], h3[i]);
+    return;
+  }
+  // LEVEL 2 is the last writer of its two great-grandchildren: complete -> add the counts;
+  // otherwise (this or an earlier step failed) recount them from their slots, so the levels after
+  // stay consistent for a build that will be redone anyway
+  if (tid == 0) incomplete = 0u;
+  __syncthreads();
+  if (tid < NG) {
+    const u32 placed = atomicAdd(&gs->zc[fg + tid][0], 0u) + atomicAdd(&gs->ins[fg + tid], 0u);
+    if (i64(placed) != a.seg_n[gg0 + tid]) atomicOr(&incomplete, 1u);
+  }
+  __syncthreads();
+  if (!incomplete) {
+    for (int i = tid; i < NG * nb3; i += NT)
+      if (h3[i]) atomicAdd(&hn3[i], h3[i]);
+    return;
+  }
+  if (tid == 0 && n > 0) g3_bad(a.err, gs);
+  for (int i = tid; i < NG * nb3; i += NT) h3[i] = 0u;
+  __syncthreads();
+  for (int k = 0; k < NG; ++k) {
+    const i64 gq = gg0 + k;
+    const BucketParams p3 = a.params[gq];
+    const float* col = a.dst + i64(ax3) * nc + a.seg_lo[gq];
+    for (i64 e = tid; e < a.seg_n[gq]; e += NT) atomicAdd(&h3[k * nb3 + bucket_of(col[e], p3, nb3)], 1u);
+  }
+  __syncthreads();
+  for (int i = tid; i < NG * nb3; i += NT) hn3[i] = h3[i];
+}
+
+// =====================================================================================
 // Tail levels: the last three global levels of a segment (<= 16 Ki rows) in ONE workgroup.
 // The segment's rows stay where the previous scatter put them; every row is read once per
 // level (only that level's key column, coalesced, one row per lane per item) and once more
@@ -2754,7 +3673,7 @@ void k_tail3(TailArgs a) {
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       if (path[i] < kMed) {
-        stage[path[i]] = v[i];
+        stage[path[i] + u32(shift)] = v[i];  // stage index = column row - alo: 16-B groups align
       } else if (path[i] != kDead) {  // a tail median: straight to its output slot
         const int k = int(path[i] & 15u);
         const i64 slot = nlo[k] + nn[k] / 2;
@@ -2764,8 +3683,25 @@ void k_tail3(TailArgs a) {
     }
     __syncthreads();
     const auto dr = col(a.dst, c);
-#pragma unroll 4
-    for (int p = tid; p < n; p += T) __builtin_amdgcn_raw_buffer_store_b32(stage[p], dr, u32(p + shift) * 4u, 0, 0);
+    // 16-B stores of the aligned groups of 4 rows inside the segment (a quarter of the store
+    // and LDS-read instructions of one word per lane); the <= 2 edge groups word by word (their
+    // other words belong to neighbouring segments)
+    using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+    const int ng = (n + shift + 3) >> 2;
+#pragma unroll 2
+    for (int q = tid; q < ng; q += T) {
+      const int j0 = 4 * q;
+      if (j0 >= shift && j0 + 3 < n + shift) {
+        const u32x4 v4 = *reinterpret_cast<const u32x4*>(stage + j0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4, dr, u32(j0) * 4u, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = j0 + e;
+          if (j >= shift && j < n + shift) __builtin_amdgcn_raw_buffer_store_b32(stage[j], dr, u32(j) * 4u, 0, 0);
+        }
+      }
+    }
     __syncthreads();
     tail_stamp(a, 14 + c);
   }
@@ -2892,6 +3828,11 @@ Tuning Tuning::from_env() {
   if (const char* z = ab_knob("PKD_TOP_Z")) t.top_z = float(std::atof(z));
   t.top_blocks = int(ab_i("PKD_TOP_BLOCKS", 0));
   t.top_diag = int(ab_i("PKD_TOP_DIAG", 0));
+  t.g3 = ab_i("PKD_G3", t.g3 ? 1 : 0) != 0;
+  t.g3_min_segs = int(std::max<i64>(1, ab_i("PKD_G3_MIN_SEGS", t.g3_min_segs)));
+  t.g3_min_rows = std::max<i64>(4096, ab_i("PKD_G3_MIN_ROWS", t.g3_min_rows));
+  t.g3_sample = std::max<i64>(1024, ab_i("PKD_G3_SAMPLE", t.g3_sample));
+  if (const char* z = ab_knob("PKD_G3_Z")) t.g3_z = float(std::atof(z));
   return t;
 }
 
@@ -3030,6 +3971,22 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     l = next;
   }
   if (tail_ > 0) levels_[size_t(tail_ - 1)].next_bins = 0;  // k_tail3 bins its levels itself
+  // Sampled triples: full-column rows in registers, segments many and large enough (the fix-up
+  // kernels run one workgroup per node; the staging regions must fit a segment), and level l's
+  // median bucket exact from the fused histogram alone (no second stage).
+  i64 g3_segs = 0;
+  for (int l = 0; l < lg_; ++l) {
+    LevelPlan& lp = levels_[size_t(l)];
+    if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= 8 && !lp.stage2 &&
+          lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
+      continue;
+    lp.g3 = true;
+    lp.g3_div = int(std::max<i64>(1, lp.nmax / tune_.g3_sample));
+    const i64 windows = std::max<i64>(1, lp.nmax / (64 * i64(lp.g3_div)));
+    lp.g3_sblocks = int(std::max<i64>(1, std::min<i64>(2048 / lp.segs, windows / 64)));
+    g3_ = true;
+    g3_segs = std::max(g3_segs, lp.segs);
+  }
   for (size_t l = 0; l < levels_.size(); ++l) {
     max_bins_ = std::max(max_bins_, levels_[l].bins);
     max_hist_ = std::max<i64>(max_hist_, levels_[l].segs * levels_[l].bins);
@@ -3058,6 +4015,11 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
   off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
   if (top_) off_top_ = take(top4::workspace_bytes());
+  if (g3_) {
+    off_stage_ = take(colbytes);
+    off_g3_ = take(size_t(g3_segs) * sizeof(G3Seg));
+    off_g3_hist_ = take(size_t(g3_segs) * 6 * kG3Bins * 4);
+  }
   {
     const Tuning& sc = tune_;
     const int L = sc.split_level;
@@ -3106,7 +4068,7 @@ std::string GpuBuilder::describe() const {
     os << "\n  L" << lp.level << " segs=" << lp.segs << " nmax=" << lp.nmax << " bins=" << lp.bins
        << " next_bins=" << lp.next_bins << " bps=" << lp.bps << " axis=" << lp.axis << (lp.stage2 ? " stage2" : "")
        << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "") << (lp.tail ? " tail" : "")
-       << (lp.sampled ? " sampled" : "");
+       << (lp.sampled ? " sampled" : "") << (lp.g3 ? " g3" : "");
   return os.str();
 }
 
@@ -3120,6 +4082,32 @@ u32 GpuBuilder::read_error(const void* workspace, hipStream_t stream, u32* detai
     detail[2] = e[3];
   }
   return e[0];
+}
+
+std::vector<u32> GpuBuilder::g3_report(const void* workspace, hipStream_t stream) const {
+  std::vector<u32> out;
+  int last = -1;
+  for (const auto& lp : levels_)
+    if (lp.g3) last = lp.level;
+  if (last < 0 || n_ == 0) return out;
+  const i64 segs = levels_[size_t(last)].segs;
+  std::vector<G3Seg> g(static_cast<size_t>(segs));
+  std::vector<i64> sn(static_cast<size_t>(segs));
+  const char* ws = static_cast<const char*>(workspace);
+  PKD_HIP_CHECK(hipMemcpyAsync(g.data(), ws + off_g3_, size_t(segs) * sizeof(G3Seg), hipMemcpyDeviceToHost, stream));
+  PKD_HIP_CHECK(hipMemcpyAsync(sn.data(), ws + off_seg_n_ + size_t(segs - 1) * 8, size_t(segs) * 8,
+                               hipMemcpyDeviceToHost, stream));
+  PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  out.push_back(u32(last));
+  for (i64 s = 0; s < segs; ++s) {
+    const G3Seg& q = g[size_t(s)];
+    out.push_back(u32(sn[size_t(s)]));
+    for (int t = 0; t < 7; ++t) out.push_back(q.zc[8 + t][0]);
+    for (int z = 0; z < 8; ++z) out.push_back(q.zc[z][0]);
+    for (int z = 0; z < 8; ++z) out.push_back(q.ins[z]);
+    out.push_back(q.bad);
+  }
+  return out;
 }
 
 float* GpuBuilder::soa_input(void* workspace) const {
@@ -3281,6 +4269,13 @@ void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* 
     run_top(nullptr, cols, nullptr, 0, out_pts, out_ids, ws, stream);
     return;
   }
+  if (g3_ && !top_ && cols != reinterpret_cast<float*>(ws + off_cols_a_)) {
+    // a sampled triple may miss (error bit top4_band_miss_bit()): its rebuild reads the caller's
+    // columns again, so the levels run on a copy instead of clobbering them
+    PKD_HIP_CHECK(hipMemcpyAsync(ws + off_cols_a_, cols, size_t(dim_ + 1) * size_t(ncol_) * 4, hipMemcpyDeviceToDevice,
+                                 stream));
+    cols = reinterpret_cast<float*>(ws + off_cols_a_);
+  }
   if (root_cell) {  // the caller's box of the points: no bounding-box pass over the columns
     k_cell_root<<<1, 64, 0, stream>>>(root_cell, dim_, reinterpret_cast<float*>(ws + off_cells_),
                                       reinterpret_cast<BucketParams*>(ws + off_params_), opt_.depth0 % dim_,
@@ -3303,6 +4298,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
                             u32 id_base, const float* in_rows, i64 in_rs, float* cols_a, int first_level,
                             bool root_ready) const {
   const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
+  const u32 g3_salt = g3_ ? g3_salt_++ : 0u;  // this build's sample positions (sampled triples)
   float* colsA = cols_a ? cols_a : reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
@@ -3429,6 +4425,51 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         PKD_LAUNCH_CHECK();
       }
       const int grid = int(segs * a.bps);
+      if (lp.g3) {
+        const LevelPlan& lr = levels_[size_t(l + 2)];
+        G3Args ga;
+        ga.g3 = reinterpret_cast<G3Seg*>(ws + off_g3_);
+        ga.shist = reinterpret_cast<u32*>(ws + off_g3_hist_);
+        ga.stage = reinterpret_cast<float*>(ws + off_stage_);
+        ga.seg0 = i64(part) * segs;
+        ga.axis2 = lr.axis;
+        ga.axis3 = (opt_.depth0 + l + 3) % dim_;
+        ga.bins3 = lr.next_bins;
+        ga.hist3 = l + 3 < lg_ ? hist_of(l + 3) : nullptr;
+        ga.sample_div = lp.g3_div;
+        ga.sblocks = lp.g3_sblocks;
+        ga.z = tune_.g3_z;
+        ga.salt = g3_salt * 0x9e3779b9u + u32(l);
+        zero_u32(ga.shist + ga.seg0 * 6 * kG3Bins, segs * 6 * kG3Bins, st);
+        const int sgrid = int(segs * lp.g3_sblocks);
+        k_g3_sample<1><<<sgrid, kBlock, 0, st>>>(a, ga);
+        PKD_LAUNCH_CHECK();
+        k_g3_band<1><<<int(segs), kBlock, 0, st>>>(a, ga);
+        PKD_LAUNCH_CHECK();
+        k_g3_sample<2><<<sgrid, kBlock, 0, st>>>(a, ga);
+        PKD_LAUNCH_CHECK();
+        k_g3_band<2><<<int(segs), kBlock, 0, st>>>(a, ga);
+        PKD_LAUNCH_CHECK();
+        with_ncol(dim_, [&](auto nc) {
+          constexpr int NC = decltype(nc)::value;
+          if constexpr (NC >= 3) {
+            constexpr int KI = NC <= 5 ? 8 : 4;
+            const size_t lds3 = size_t(std::max(1, kG3Gg * ga.bins3)) * 4;
+            if (atomic_ranks(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
+            else k_g3_part<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ga);
+            PKD_LAUNCH_CHECK();
+            k_g3_res<NC, 0><<<int(segs), kG3Threads, 0, st>>>(a, ga);
+            PKD_LAUNCH_CHECK();
+            k_g3_res<NC, 1><<<int(2 * segs), kG3Threads, 0, st>>>(a, ga);
+            PKD_LAUNCH_CHECK();
+            k_g3_res<NC, 2><<<int(4 * segs), kG3Threads, 0, st>>>(a, ga);
+            PKD_LAUNCH_CHECK();
+          }
+        });
+        std::swap(src, dst);
+        l += 3;
+        continue;
+      }
       if (lp.triple) {
         const LevelPlan& lq = levels_[size_t(l + 1)];
         const LevelPlan& lr = levels_[size_t(l + 2)];

@@ -80,11 +80,15 @@ __host__ __device__ inline void seg_geometry(i64 n, int l, i64 j, i64* lo_out, i
   *n_out = m;
 }
 
-// Value-linear bucket of an orderable key over [kmin, kmax] (integer arithmetic, monotone).
+// Value-linear bucket of an orderable key over [kmin, kmax]: float(k - kmin) * B / (span + 1),
+// truncated. Conversion, multiplication by a positive constant and truncation are all monotone,
+// so any key order is kept (ranks stay exact) and no 64-bit division is needed.
+__device__ __forceinline__ float ref_scale(u32 kmin, u32 kmax, u32 B) { return float(B) / (float(kmax - kmin) + 1.0f); }
+__device__ __forceinline__ u32 ref_bucket_s(u32 k, u32 kmin, float scale, u32 B) {
+  return min(u32(float(k - kmin) * scale), B - 1);
+}
 __device__ __forceinline__ u32 ref_bucket(u32 k, u32 kmin, u32 kmax, u32 B) {
-  const u64 span = u64(kmax - kmin) + 1ull;
-  const u64 b = (u64(k - kmin) * B) / span;
-  return u32(b < B ? b : B - 1);
+  return ref_bucket_s(k, kmin, ref_scale(kmin, kmax, B), B);
 }
 
 __device__ __forceinline__ u64 comp(u32 key, u32 row) { return (u64(key) << 32) | row; }
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_init(u32* __restrict__ perm, i64
 __global__ __launch_bounds__(kBlock) void k_ref_seg_init(RefSeg* __restrict__ seg, i64 S, i64 n_total, int l,
                                                          u32* __restrict__ hist, i64 hwords) {
   for (i64 i = i64(blockIdx.x) * kBlock + threadIdx.x; i < hwords; i += i64(gridDim.x) * kBlock) hist[i] = 0u;
-  for (i64 s = i64(blockIdx.x) * kBlock + threadIdx.x; s < S; s += i64(gridDim.x) * kBlock) {
+  for (i64 s = i64(blockIdx.x) * kBlock + threadIdx.x; seg != nullptr && s < S; s += i64(gridDim.x) * kBlock) {
     i64 lo = 0, m = 0;
     seg_geometry(n_total, l, s, &lo, &m);
     RefSeg r{};
@@ -200,26 +204,49 @@ __device__ __forceinline__ u32 wave_find(const u32* h, int B, u32 rank, u32* bel
   return u32(__shfl(int(bin), src, 64));
 }
 
-__global__ __launch_bounds__(64) void k_ref_select(RefSeg* __restrict__ seg, int B, const u32* __restrict__ hist,
-                                                   u32* __restrict__ err) {
+// One workgroup per segment: the buckets of ranks m - 1 and m (every thread sums B / 256
+// consecutive buckets, one block scan, the owning threads walk their buckets).
+__global__ __launch_bounds__(kBlock) void k_ref_select(RefSeg* __restrict__ seg, int B, const u32* __restrict__ hist,
+                                                       u32* __restrict__ err) {
+  __shared__ u32 wsum[kBlock / 64];
   const i64 s = blockIdx.x;
   const RefSeg r = seg[s];
   if (r.n < 3) return;  // (global segments always hold more than kFinCap rows)
   const u32 m = r.n / 2;
   const u32* h = hist + s * i64(B);
-  u32 L = 0, below2 = 0;
-  const u32 b1 = wave_find(h, B, m - 1, &L);
-  const u32 b2 = wave_find(h, B, m, &below2);
-  if (dev::lane() == 0) {
-    if (b1 >= u32(B) || b2 >= u32(B)) {
+  const int per = B >= kBlock ? B / kBlock : 1;
+  const int t = threadIdx.x, b0 = t * per;
+  u32 c = 0;
+  if (b0 < B)
+    for (int i = 0; i < per; ++i) c += h[b0 + i];
+  const u32 incl = dev::wave_incl_scan(c);
+  if (dev::lane() == 63) wsum[t / 64] = incl;
+  __syncthreads();
+  u32 ex = incl - c;
+  for (int w = 0; w < t / 64; ++w) ex += wsum[w];
+  __shared__ u32 res[4];  // b1, L, b2, rows up to the end of b2
+  if (t < 4) res[t] = 0xffffffffu;
+  __syncthreads();
+  for (int q = 0; q < 2; ++q) {
+    const u32 rank = m - 1 + u32(q);
+    if (c > 0 && rank >= ex && rank < ex + c) {
+      u32 below = ex;
+      int b = b0;
+      while (rank >= below + h[b]) below += h[b++];
+      res[2 * q] = u32(b);
+      res[2 * q + 1] = q == 0 ? below : below + h[b];
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (res[0] >= u32(B) || res[2] >= u32(B) || res[3] < res[1]) {
       atomicOr(err, 1u);
       return;
     }
-    u32 M = below2 + h[b2] - L;
-    seg[s].b1 = b1;
-    seg[s].b2 = b2;
-    seg[s].L = L;
-    seg[s].M = M;
+    seg[s].b1 = res[0];
+    seg[s].L = res[1];
+    seg[s].b2 = res[2];
+    seg[s].M = res[3] - res[1];
   }
 }
 
@@ -602,6 +629,529 @@ __global__ __launch_bounds__(kBlock) void k_ref_gather(const float* __restrict__
   }
 }
 
+// ---- row path (dim <= 8): rows move as SoA columns (dim coordinates + the input row index),
+// so a level reads its keys contiguously and the medians go straight to the output -------------
+// cols(c, p): column c of slot p; column dim holds the input row index bits.
+struct RowCols {
+  float* c;
+  i64 ncol;
+  __device__ __forceinline__ float& at(int col, u32 p) const { return c[i64(col) * ncol + p]; }
+};
+
+// Block-wide min / max (every thread calls it; red: LDS [kBlock / 64][2]); valid in thread 0.
+__device__ __forceinline__ void block_minmax(u32* mn, u32* mx, u32 (*red)[2]) {
+  u32 a = dev::wave_min_u32(*mn), b = dev::wave_max_u32(*mx);
+  __syncthreads();
+  if (dev::lane() == 0) {
+    red[threadIdx.x / 64][0] = a;
+    red[threadIdx.x / 64][1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k < kBlock / 64; ++k) {
+      a = min(a, red[k][0]);
+      b = max(b, red[k][1]);
+    }
+  *mn = a;
+  *mx = b;
+}
+
+// AoS input -> SoA columns; the key range of level 0's sortable rows [0, n - 1).
+__global__ __launch_bounds__(kBlock) void k_rr_prep(const float* __restrict__ pts, i64 n, int dim, int axis0,
+                                                    RowCols out, RefSeg* __restrict__ seg0) {
+  __shared__ u32 red[kBlock / 64][2];
+  u32 mn = 0xffffffffu, mx = 0u;
+  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += i64(gridDim.x) * kBlock) {
+    for (int c = 0; c < dim; ++c) {
+      const float v = pts[p * dim + c];
+      out.at(c, u32(p)) = v;
+      if (c == axis0 && p + 1 < n) {
+        mn = min(mn, orderable(v));
+        mx = max(mx, orderable(v));
+      }
+    }
+    out.at(dim, u32(p)) = __uint_as_float(u32(p));
+  }
+  block_minmax(&mn, &mx, red);
+  if (threadIdx.x == 0 && seg0 && mn <= mx) {
+    atomicMin(&seg0->kmin, mn);
+    atomicMax(&seg0->kmax, mx);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const RefSeg* __restrict__ seg, int bps,
+                                                    int B, u32* __restrict__ hist) {
+  extern __shared__ u32 h[];
+  const i64 s = blockIdx.x / bps;
+  const int part = blockIdx.x % bps;
+  const RefSeg r = seg[s];
+  for (int b = threadIdx.x; b < B; b += kBlock) h[b] = 0u;
+  __syncthreads();
+  u32 b0, b1;
+  block_part(r, part, bps, &b0, &b1);
+  const float sc = ref_scale(r.kmin, r.kmax, u32(B));
+  const float* kc = src.c + i64(axis) * src.ncol + r.lo;
+  constexpr int U = 4;
+  for (u32 e0 = b0; e0 < b1; e0 += kBlock * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32 e = e0 + u32(u * kBlock) + threadIdx.x;
+      v[u] = kc[e < b1 ? e : b0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32 e = e0 + u32(u * kBlock) + threadIdx.x;
+      if (e < b1) atomicAdd(&h[ref_bucket_s(orderable(v[u]), r.kmin, sc, u32(B))], 1u);
+    }
+  }
+  __syncthreads();
+  u32* out = hist + s * i64(B);
+  for (int b = threadIdx.x; b < B; b += kBlock)
+    if (h[b]) atomicAdd(&out[b], h[b]);
+}
+
+// Per-block partials of a row-path partition (no same-address atomics across blocks): the
+// children's next-axis ranges and the zones' extreme composites, reduced by k_rr_refine.
+struct PartPartial {
+  u32 lmn, lmx, rmn, rmx;
+  u64 lmax, rmin;
+};
+
+// The row-path partition: as k_ref_part, moving every column; the children's key ranges on the
+// next level's axis are collected (left zone -> left child, right zone and the last row -> right
+// child; the middle rows' share is added by k_rr_refine).
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_rr_part(RowCols src, RowCols dst, int axis, int naxis,
+                                                    RefSeg* __restrict__ seg, int bps, int B,
+                                                    PartPartial* __restrict__ partials) {
+  constexpr int kI = NC <= 5 ? 8 : 4;  // rows per thread per chunk
+  __shared__ u32 wc[kBlock / 64][3];
+  __shared__ u32 zb[kBlock / 64][3];
+  __shared__ u64 red[kBlock / 64][2];
+  __shared__ u32 red2[kBlock / 64][2];
+  const i64 s = blockIdx.x / bps;
+  const int part = blockIdx.x % bps;
+  const RefSeg r = seg[s];
+  const int w = threadIdx.x / 64, ln = dev::lane();
+  u32 lmn = 0xffffffffu, lmx = 0u, rmn = 0xffffffffu, rmx = 0u;  // children's next-axis ranges
+  if (part == 0 && threadIdx.x == 0 && r.n > 0) {  // the last row keeps its slot (the right child's last)
+    const u32 p = r.lo + r.n - 1;
+    for (int c = 0; c < NC; ++c) dst.at(c, p) = src.at(c, p);
+    rmn = rmx = orderable(src.at(naxis, p));
+  }
+  u32 b0, b1;
+  block_part(r, part, bps, &b0, &b1);
+  const float sc = ref_scale(r.kmin, r.kmax, u32(B));
+  u64 lmax = 0ull, rmin = ~0ull;
+  constexpr int kCh = kBlock * kI;
+  for (u32 c0 = b0; c0 < b1; c0 += kCh) {
+    float v[kI][NC];
+    u32 z[kI], rk[kI];
+    u32 cnt[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < kI; ++i) {
+      const u32 e = c0 + u32(w * 64 * kI + i * 64 + ln);
+      const bool valid = e < b1;
+      const u32 pe = r.lo + (valid ? e : b0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) v[i][c] = src.at(c, pe);
+      float kf = v[i][0], nf = v[i][0];
+#pragma unroll
+      for (int c = 1; c < NC - 1; ++c) {
+        kf = c == axis ? v[i][c] : kf;
+        nf = c == naxis ? v[i][c] : nf;
+      }
+      const u32 key = orderable(kf);
+      const u32 b = ref_bucket_s(key, r.kmin, sc, u32(B));
+      z[i] = !valid ? 3u : (b < r.b1 ? 0u : (b <= r.b2 ? 1u : 2u));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const u64 mq = __ballot(z[i] == u32(q));
+        if (z[i] == u32(q)) rk[i] = cnt[q] + dev::mbcnt(mq);
+        cnt[q] += u32(__popcll(mq));
+      }
+      const u64 cp = comp(key, __float_as_uint(v[i][NC - 1]));
+      const u32 nk = orderable(nf);
+      if (z[i] == 0u) {
+        lmax = cp > lmax ? cp : lmax;
+        lmn = min(lmn, nk);
+        lmx = max(lmx, nk);
+      }
+      if (z[i] == 2u) {
+        rmin = cp < rmin ? cp : rmin;
+        rmn = min(rmn, nk);
+        rmx = max(rmx, nk);
+      }
+    }
+    if (ln < 3) wc[w][ln] = cnt[ln];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      const int q = threadIdx.x;
+      u32 t = 0;
+      for (int k = 0; k < kBlock / 64; ++k) t += wc[k][q];
+      u32 base = t ? atomicAdd(&seg[s].cur[q], t) : 0u;
+      for (int k = 0; k < kBlock / 64; ++k) {
+        zb[k][q] = base;
+        base += wc[k][q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kI; ++i) {
+      if (z[i] > 2u) continue;
+      const u32 pos = r.lo + (z[i] == 0u ? 0u : (z[i] == 1u ? r.L : r.L + r.M)) + zb[w][z[i]] + rk[i];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst.at(c, pos) = v[i][c];
+    }
+    __syncthreads();  // wc / zb are rewritten by the next chunk
+  }
+  block_minmax(&lmn, &lmx, red2);
+  block_minmax(&rmn, &rmx, red2);
+  lmax = dev::wave_max_u64(lmax);
+  rmin = dev::wave_min_u64(rmin);
+  if (ln == 0) {
+    red[w][0] = lmax;
+    red[w][1] = rmin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) {
+      lmax = red[k][0] > lmax ? red[k][0] : lmax;
+      rmin = red[k][1] < rmin ? red[k][1] : rmin;
+    }
+    partials[blockIdx.x] = PartPartial{lmn, lmx, rmn, rmx, lmax, rmin};
+  }
+}
+
+// Row-path refine (one workgroup per segment): the partition's block partials are reduced; the
+// middle zone is copied to the same slots of src (dead there since the partition), then every
+// middle row is read from src and written to its place in dst; the median row goes straight to
+// the output; the children's next-axis ranges are stored (this workgroup is their only writer).
+// Middle zones of <= 64 rows (the deep levels) are ranked by one wave without a barrier.
+__global__ __launch_bounds__(kBlock) void k_rr_refine(RowCols src, RowCols dst, int dim, int axis, int naxis,
+                                                      const RefSeg* __restrict__ seg, RefSeg* __restrict__ nseg,
+                                                      const PartPartial* __restrict__ partials, int bps,
+                                                      const u32* __restrict__ ids, u32 id_base,
+                                                      float* __restrict__ out_pts, u32* __restrict__ out_ids,
+                                                      u32* __restrict__ ties) {
+  __shared__ u64 buf[kRefineCap];
+  __shared__ u32 cl, cr;
+  __shared__ u64 r64[kBlock / 64][3];
+  __shared__ u32 red2[kBlock / 64][2];
+  __shared__ u64 sc1, sc2;
+  const RefSeg r = seg[blockIdx.x];
+  if (r.n < 3) return;
+  const u32 m = r.n / 2, L = r.L, M = r.M;
+  const u32 base = r.lo + L;
+  const int NC = dim + 1;
+  const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
+  // the partition's partials
+  u32 lmn = 0xffffffffu, lmx = 0u, rmn = 0xffffffffu, rmx = 0u;
+  u64 pred = 0ull, succ = ~0ull;  // left zone max / right zone min so far
+  for (int k = tid; k < bps; k += kBlock) {
+    const PartPartial q = partials[i64(blockIdx.x) * bps + k];
+    lmn = min(lmn, q.lmn);
+    lmx = max(lmx, q.lmx);
+    rmn = min(rmn, q.rmn);
+    rmx = max(rmx, q.rmx);
+    pred = q.lmax > pred ? q.lmax : pred;
+    succ = q.rmin < succ ? q.rmin : succ;
+  }
+  const bool in_lds = M <= u32(kRefineCap);
+  for (u32 e = tid; e < M; e += kBlock) {
+    const u32 p = base + e;
+    float key = 0.0f;
+    u32 row = 0;
+    for (int c = 0; c < NC; ++c) {
+      const float v = dst.at(c, p);
+      src.at(c, p) = v;
+      if (c == axis) key = v;
+      if (c == dim) row = __float_as_uint(v);
+    }
+    if (in_lds) buf[e] = comp(orderable(key), row);
+  }
+  if (tid == 0) {
+    cl = 0;
+    cr = 0;
+  }
+  __syncthreads();
+  auto val = [&](u32 e) -> u64 {
+    return in_lds ? buf[e] : comp(orderable(src.at(axis, base + e)), __float_as_uint(src.at(dim, base + e)));
+  };
+  u64 c1, c2;
+  if (M <= 64) {  // one wave: ranks by comparison, no barrier
+    if (w == 0) {
+      const u64 v = ln < int(M) ? buf[ln] : ~0ull;
+      u32 rk = 0;
+      for (u32 j = 0; j < M; ++j) rk += dev::shfl_u64(v, int(j)) < v ? 1u : 0u;
+      const u64 m1 = __ballot(ln < int(M) && rk == m - 1 - L), m2 = __ballot(ln < int(M) && rk == m - L);
+      const u64 a1 = dev::shfl_u64(v, __ffsll((long long)m1) - 1), a2 = dev::shfl_u64(v, __ffsll((long long)m2) - 1);
+      if (ln == 0) {
+        sc1 = a1;
+        sc2 = a2;
+      }
+    }
+    __syncthreads();
+    c1 = sc1;
+    c2 = sc2;
+  } else {
+    auto each = [&](auto f) {
+      for (u32 e = tid; e < M; e += kBlock) f(val(e));
+    };
+    c1 = block_select(each, m - 1 - L);
+    u64 nx = ~0ull;  // rank m is the successor of rank m - 1
+    each([&](u64 v) {
+      if (v > c1) nx = v < nx ? v : nx;
+    });
+    nx = dev::wave_min_u64(nx);
+    if (ln == 0) r64[w][0] = nx;
+    __syncthreads();
+    c2 = r64[0][0];
+    for (int k = 1; k < kBlock / 64; ++k) c2 = r64[k][0] < c2 ? r64[k][0] : c2;
+  }
+  for (u32 e = tid; e < M; e += kBlock) {
+    const u32 p = base + e;
+    const u64 v = val(e);
+    const u32 nk = orderable(src.at(naxis, p));
+    if (v < c1) pred = v > pred ? v : pred;
+    if (v > c2) succ = v < succ ? v : succ;
+    if (v == c2) {  // the median: its slot is final
+      const u32 slot = r.lo + m, row = u32(v);
+      for (int c = 0; c < dim; ++c) out_pts[i64(slot) * dim + c] = src.at(c, p);
+      out_ids[slot] = ids ? ids[row] : id_base + row;
+      continue;
+    }
+    u32 pos;
+    if (v < c1) pos = base + atomicAdd(&cl, 1u);
+    else if (v == c1) pos = r.lo + m - 1;
+    else pos = r.lo + m + 1 + atomicAdd(&cr, 1u);
+    for (int c = 0; c < NC; ++c) dst.at(c, pos) = src.at(c, p);
+    if (v <= c1) {
+      lmn = min(lmn, nk);
+      lmx = max(lmx, nk);
+    } else {
+      rmn = min(rmn, nk);
+      rmx = max(rmx, nk);
+    }
+  }
+  block_minmax(&lmn, &lmx, red2);
+  block_minmax(&rmn, &rmx, red2);
+  pred = dev::wave_max_u64(pred);
+  succ = dev::wave_min_u64(succ);
+  if (ln == 0) {
+    r64[w][1] = pred;
+    r64[w][2] = succ;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 0; k < kBlock / 64; ++k) {
+      pred = r64[k][1] > pred ? r64[k][1] : pred;
+      succ = r64[k][2] < succ ? r64[k][2] : succ;
+    }
+    if (nseg) {
+      nseg[2 * blockIdx.x].kmin = lmn;
+      nseg[2 * blockIdx.x].kmax = lmx;
+      nseg[2 * blockIdx.x + 1].kmin = rmn;
+      nseg[2 * blockIdx.x + 1].kmax = rmx;
+    }
+    const u32 k1 = u32(c1 >> 32), k2 = u32(c2 >> 32);
+    bool tie = k1 == k2;
+    if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;
+    if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;
+    if (tie) atomicAdd(ties, 1u);
+  }
+}
+
+// Row-path LDS finish: the segment's columns are loaded once (X[c][local row]); slots hold
+// local row indices, keys are read through them, and every slot's row is written to the
+// output at the end. Thread t owns the kFinItems consecutive slots from t * kFinItems, so a
+// sub-segment's key range takes one LDS atomic per run of a thread's slots, not one per row.
+__global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim, int depth0, i64 n_total, int lf,
+                                                           int levels, const u32* __restrict__ ids, u32 id_base,
+                                                           float* __restrict__ out_pts, u32* __restrict__ out_ids,
+                                                           u32* __restrict__ ties) {
+  extern __shared__ float X[];  // [dim + 1][kFinCap]
+  __shared__ unsigned short P[2][kFinCap];
+  __shared__ u32 H[kFinCap + 1];
+  __shared__ u32 smin[kFinCap], smax[kFinCap];
+  __shared__ unsigned short tp[kFinCap], SL[kFinCap], SN[kFinCap];
+  __shared__ u32 wsum[kFinThreads / 64];
+  u32* tk = smin;  // bucket-ordered keys (smin / smax are dead once the buckets are known)
+  u32* K = smax;   // sorted keys of the level, for the tie checks
+  i64 lo64 = 0, m64 = 0;
+  seg_geometry(n_total, lf, blockIdx.x, &lo64, &m64);
+  if (m64 <= 0) return;
+  const int M = int(m64);
+  const u32 lo = u32(lo64);
+  const int tid = threadIdx.x, p0 = tid * kFinItems;
+  for (int c = 0; c <= dim; ++c)
+    for (int p = tid; p < M; p += kFinThreads) X[c * kFinCap + p] = src.at(c, lo + u32(p));
+  for (int p = tid; p < M; p += kFinThreads) {
+    P[0][p] = (unsigned short)p;
+    SL[p] = 0;
+    SN[p] = (unsigned short)M;
+    smin[p] = 0xffffffffu;
+    smax[p] = 0u;
+  }
+  int cur = 0;
+  __syncthreads();
+  for (int l = lf; l < levels; ++l) {
+    const int axis = (depth0 + l) % dim;
+    const float* xk = X + axis * kFinCap;
+    for (int p = tid; p <= M; p += kFinThreads) H[p] = 0u;
+    u32 key[kFinItems], slot[kFinItems], bk[kFinItems];
+    bool srt[kFinItems];
+    {
+      u32 rmn = 0xffffffffu, rmx = 0u;
+      int rs = -1;  // the current run's sub-segment start
+#pragma unroll
+      for (int i = 0; i < kFinItems; ++i) {
+        const int p = p0 + i;
+        srt[i] = false;
+        key[i] = 0;
+        if (p < M) {
+          const int sl = SL[p], sn = SN[p];
+          srt[i] = sn >= 3 && p != sl + sn - 1;
+          if (srt[i]) {
+            key[i] = orderable(xk[P[cur][p]]);
+            if (sl != rs) {
+              if (rs >= 0) {
+                atomicMin(&smin[rs], rmn);
+                atomicMax(&smax[rs], rmx);
+              }
+              rs = sl;
+              rmn = 0xffffffffu;
+              rmx = 0u;
+            }
+            rmn = min(rmn, key[i]);
+            rmx = max(rmx, key[i]);
+          }
+        }
+      }
+      if (rs >= 0) {
+        atomicMin(&smin[rs], rmn);
+        atomicMax(&smax[rs], rmx);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      bk[i] = 0;
+      slot[i] = 0;
+      if (srt[i]) {
+        const int sl = SL[p], sn = SN[p];
+        const u32 kmn = smin[sl];
+        bk[i] = u32(sl) + ref_bucket_s(key[i], kmn, ref_scale(kmn, smax[sl], u32(sn - 1)), u32(sn - 1));
+        slot[i] = atomicAdd(&H[bk[i]], 1u);
+      }
+    }
+    __syncthreads();
+    {  // exclusive scan of H[0, M): thread t owns H[t * kFinItems, + kFinItems); H[M] = total
+      u32 x[kFinItems], sum = 0;
+#pragma unroll
+      for (int j = 0; j < kFinItems; ++j) {
+        x[j] = p0 + j < M ? H[p0 + j] : 0u;
+        sum += x[j];
+      }
+      const u32 incl = dev::wave_incl_scan(sum);
+      if (dev::lane() == 63) wsum[tid / 64] = incl;
+      __syncthreads();
+      u32 run = incl - sum;
+      for (int w = 0; w < tid / 64; ++w) run += wsum[w];
+#pragma unroll
+      for (int j = 0; j < kFinItems; ++j) {
+        if (p0 + j < M) H[p0 + j] = run;
+        run += x[j];
+      }
+      if (tid == kFinThreads - 1) H[M] = run;
+    }
+    __syncthreads();
+    u32 rank[kFinItems], st[kFinItems], cnt[kFinItems];
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      rank[i] = 0;
+      st[i] = 0;
+      cnt[i] = 0;
+      if (srt[i]) {
+        st[i] = H[bk[i]];
+        cnt[i] = H[bk[i] + 1] - st[i];
+        rank[i] = st[i] - H[SL[p]];
+        tk[st[i] + slot[i]] = key[i];
+        tp[st[i] + slot[i]] = (unsigned short)p;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      for (u32 j = 0; j < cnt[i]; ++j) {
+        const u32 q = st[i] + j;
+        const u32 kq = tk[q];
+        rank[i] += (kq < key[i] || (kq == key[i] && int(tp[q]) < p)) ? 1u : 0u;
+      }
+    }
+    __syncthreads();  // tk (= smin) is read above; K (= smax) is written below
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      if (p >= M) continue;
+      const int np = srt[i] ? int(SL[p]) + int(rank[i]) : p;
+      P[cur ^ 1][np] = P[cur][p];
+      K[np] = key[i];
+    }
+    __syncthreads();
+    cur ^= 1;
+    // ties on the deciding pairs of every sub-segment (checked by its first slot's thread),
+    // then the next level's sub-segments; their key-range words are reset at their heads
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      if (p >= M) continue;
+      const int sl = SL[p], sn = SN[p];
+      if (p == sl && sn >= 3) {
+        const int m = sn / 2;
+        const u32* kk = K + sl;
+        bool tie = kk[m - 1] == kk[m];
+        if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
+        if (m + 1 <= sn - 2 && kk[m] == kk[m + 1]) tie = true;
+        if (tie) atomicAdd(ties, 1u);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      if (p >= M) continue;
+      smin[p] = 0xffffffffu;
+      smax[p] = 0u;
+      const int sl = SL[p], sn = SN[p];
+      if (sn <= 1) continue;
+      const int mid = sl + sn / 2;
+      if (p < mid) {
+        SN[p] = (unsigned short)(sn / 2);
+      } else if (p == mid) {
+        SL[p] = (unsigned short)mid;
+        SN[p] = 1;
+      } else {
+        SL[p] = (unsigned short)(mid + 1);
+        SN[p] = (unsigned short)(sn - sn / 2 - 1);
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < M * dim; e += kFinThreads) {  // rows out: consecutive threads, consecutive floats
+    const int p = e / dim, c = e - p * dim;
+    out_pts[i64(lo + u32(p)) * dim + c] = X[c * kFinCap + P[cur][p]];
+  }
+  for (int p = tid; p < M; p += kFinThreads) {
+    const u32 row = __float_as_uint(X[dim * kFinCap + P[cur][p]]);
+    out_ids[lo + u32(p)] = ids ? ids[row] : id_base + row;
+  }
+}
+
 size_t align_up(size_t v) { return (v + 255) / 256 * 256; }
 int grid_for(i64 n) { return int(std::min<i64>(8192, std::max<i64>(1, (n + kBlock - 1) / kBlock))); }
 int pow2_floor(i64 v) {
@@ -615,6 +1165,7 @@ int pow2_floor(i64 v) {
 ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim), depth0_(depth0) {
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
+  rows_ = dim <= 8;  // rows move as SoA columns; above, only a permutation (keys gathered per level)
   levels_ = 0;
   while ((n_ >> levels_) >= 2) ++levels_;  // the largest segment of level l has n >> l rows
   lfin_ = 0;  // global levels: while the largest segment exceeds the LDS finish
@@ -623,8 +1174,11 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
   for (int l = 0; l < lfin_; ++l) {
     RefLevel p;
     p.segs = i64(1) << l;
-    p.bins = std::max(64, std::min(2048, pow2_floor(std::max<i64>(1, (n_ >> l) / 8))));
+    // about 8 rows per bucket, so the middle zone (the buckets of ranks m - 1 and m) fits the
+    // refine's LDS; the histogram pass runs on 1/8 of the partition's blocks (fewer flushes)
+    p.bins = std::max(64, std::min(rows_ ? 16384 : 2048, pow2_floor(std::max<i64>(1, (n_ >> l) / 8))));
     p.bps = int(std::max<i64>(1, std::min<i64>(2048 / p.segs, ((n_ >> l) + kChunk - 1) / kChunk)));
+    p.hbps = int(std::max<i64>(1, std::min<i64>(p.bps, 256 / p.segs)));
     plan_.push_back(p);
     max_segs = std::max(max_segs, p.segs);
     max_hist = std::max(max_hist, p.segs * p.bins);
@@ -636,12 +1190,19 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
     return o;
   };
   const size_t nn = size_t(std::max<i64>(n_, 1));
-  off_perm_[0] = take(nn * 4);
-  off_perm_[1] = take(nn * 4);
-  off_keys_ = take(nn * 4);
-  off_midc_ = take(lfin_ > 0 ? nn * 8 : 8);
+  ncol_ = i64(std::max<size_t>(64, (nn + 63) / 64 * 64));
+  if (rows_) {
+    off_perm_[0] = take(size_t(dim + 1) * size_t(ncol_) * 4);  // SoA columns (ping)
+    off_perm_[1] = take(size_t(dim + 1) * size_t(ncol_) * 4);  // (pong)
+    off_keys_ = take(size_t(std::max<i64>(2048, max_segs)) * sizeof(PartPartial));  // partition partials
+  } else {
+    off_perm_[0] = take(nn * 4);
+    off_perm_[1] = take(nn * 4);
+    off_keys_ = take(nn * 4);
+    off_midc_ = take(lfin_ > 0 ? nn * 8 : 8);
+  }
   off_hist_ = take(size_t(max_hist) * 4);
-  off_segs_ = take(size_t(max_segs) * sizeof(RefSeg));
+  off_segs_ = take(2 * size_t(max_segs) * sizeof(RefSeg));
   off_words_ = take(16);  // [0] ties, [1] error
   ws_bytes_ = off;
 }
@@ -659,14 +1220,70 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
                              void* workspace, hipStream_t stream) const {
   if (n_ == 0) return;
   char* ws = static_cast<char*>(workspace);
-  u32* perm[2] = {reinterpret_cast<u32*>(ws + off_perm_[0]), reinterpret_cast<u32*>(ws + off_perm_[1])};
-  u32* keys = reinterpret_cast<u32*>(ws + off_keys_);
-  u64* midc = reinterpret_cast<u64*>(ws + off_midc_);
   u32* hist = reinterpret_cast<u32*>(ws + off_hist_);
-  RefSeg* segs = reinterpret_cast<RefSeg*>(ws + off_segs_);
+  i64 max_segs = 1;
+  for (const RefLevel& p : plan_) max_segs = std::max(max_segs, p.segs);
+  RefSeg* segs[2] = {reinterpret_cast<RefSeg*>(ws + off_segs_), reinterpret_cast<RefSeg*>(ws + off_segs_) + max_segs};
   u32* words = reinterpret_cast<u32*>(ws + off_words_);
   PKD_HIP_CHECK(hipMemsetAsync(words, 0, 16, stream));
   const int g = grid_for(n_);
+  auto seg_init = [&](RefSeg* sg, const RefLevel& p, int l, i64 hw) {
+    k_ref_seg_init<<<int(std::min<i64>(1024, (std::max<i64>(hw, p.segs) + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
+        sg, p.segs, n_, l, hist, hw);
+    PKD_LAUNCH_CHECK();
+  };
+  if (rows_) {
+    auto* partials = reinterpret_cast<PartPartial*>(ws + off_keys_);
+    RowCols cols[2] = {{reinterpret_cast<float*>(ws + off_perm_[0]), ncol_},
+                       {reinterpret_cast<float*>(ws + off_perm_[1]), ncol_}};
+    const int NC = dim_ + 1;
+    if (lfin_ > 0) seg_init(segs[0], plan_[0], 0, 0);
+    k_rr_prep<<<std::min(g, 1024), kBlock, 0, stream>>>(pts, n_, dim_, depth0_ % dim_, cols[0],
+                                                        lfin_ > 0 ? segs[0] : nullptr);
+    PKD_LAUNCH_CHECK();
+    int cur = 0;
+    for (int l = 0; l < lfin_; ++l) {
+      const RefLevel& p = plan_[size_t(l)];
+      const int axis = (depth0_ + l) % dim_, naxis = (depth0_ + l + 1) % dim_;
+      const int S = int(p.segs);
+      RefSeg* sg = segs[l & 1];
+      RefSeg* nsg = l + 1 < lfin_ ? segs[(l + 1) & 1] : nullptr;
+      // the next level's descriptors (its key ranges are filled by this level's moves) and this
+      // level's histogram, zeroed
+      if (nsg) seg_init(nsg, plan_[size_t(l + 1)], l + 1, p.segs * p.bins);
+      else {
+        k_ref_seg_init<<<int(std::min<i64>(1024, (p.segs * p.bins + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
+            nullptr, 0, n_, l, hist, p.segs * p.bins);
+        PKD_LAUNCH_CHECK();
+      }
+      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_hist), p.bins * 4);
+      k_rr_hist<<<S * p.hbps, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, p.hbps, p.bins, hist);
+      PKD_LAUNCH_CHECK();
+      k_ref_select<<<S, kBlock, 0, stream>>>(sg, p.bins, hist, words + 1);
+      PKD_LAUNCH_CHECK();
+      switch (NC) {
+#define PKD_RR(N) \
+  case N: k_rr_part<N><<<S * p.bps, kBlock, 0, stream>>>(cols[cur], cols[cur ^ 1], axis, naxis, sg, p.bps, p.bins, partials); break;
+        PKD_RR(2) PKD_RR(3) PKD_RR(4) PKD_RR(5) PKD_RR(6) PKD_RR(7) PKD_RR(8) default: PKD_RR(9)
+#undef PKD_RR
+      }
+      PKD_LAUNCH_CHECK();
+      k_rr_refine<<<S, kBlock, 0, stream>>>(cols[cur], cols[cur ^ 1], dim_, axis, naxis, sg, nsg, partials, p.bps,
+                                            ids, id_base, out_pts, out_ids, words);
+      PKD_LAUNCH_CHECK();
+      cur ^= 1;
+    }
+    const i64 segs_f = i64(1) << lfin_;
+    const size_t lds = size_t(NC) * kFinCap * 4;
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_finish), int(lds));
+    k_rr_finish<<<int(segs_f), kFinThreads, lds, stream>>>(cols[cur], dim_, depth0_, n_, lfin_, levels_, ids, id_base,
+                                                           out_pts, out_ids, words);
+    PKD_LAUNCH_CHECK();
+    return;
+  }
+  u32* perm[2] = {reinterpret_cast<u32*>(ws + off_perm_[0]), reinterpret_cast<u32*>(ws + off_perm_[1])};
+  u32* keys = reinterpret_cast<u32*>(ws + off_keys_);
+  u64* midc = reinterpret_cast<u64*>(ws + off_midc_);
   k_ref_init<<<g, kBlock, 0, stream>>>(perm[0], n_);
   PKD_LAUNCH_CHECK();
   int cur = 0;
@@ -674,19 +1291,16 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
     const RefLevel& p = plan_[size_t(l)];
     const int axis = (depth0_ + l) % dim_;
     const int S = int(p.segs), grid = S * p.bps;
-    const i64 hw = p.segs * p.bins;
-    k_ref_seg_init<<<int(std::min<i64>(1024, (std::max<i64>(hw, p.segs) + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
-        segs, p.segs, n_, l, hist, hw);
+    seg_init(segs[0], p, l, p.segs * p.bins);
+    k_ref_keys<<<grid, kBlock, 0, stream>>>(pts, dim_, axis, perm[cur], segs[0], p.bps, keys);
     PKD_LAUNCH_CHECK();
-    k_ref_keys<<<grid, kBlock, 0, stream>>>(pts, dim_, axis, perm[cur], segs, p.bps, keys);
+    k_ref_hist<<<grid, kBlock, size_t(p.bins) * 4, stream>>>(keys, segs[0], p.bps, p.bins, hist);
     PKD_LAUNCH_CHECK();
-    k_ref_hist<<<grid, kBlock, size_t(p.bins) * 4, stream>>>(keys, segs, p.bps, p.bins, hist);
+    k_ref_select<<<S, kBlock, 0, stream>>>(segs[0], p.bins, hist, words + 1);
     PKD_LAUNCH_CHECK();
-    k_ref_select<<<S, 64, 0, stream>>>(segs, p.bins, hist, words + 1);
+    k_ref_part<<<grid, kBlock, 0, stream>>>(keys, perm[cur], perm[cur ^ 1], midc, segs[0], p.bps, p.bins);
     PKD_LAUNCH_CHECK();
-    k_ref_part<<<grid, kBlock, 0, stream>>>(keys, perm[cur], perm[cur ^ 1], midc, segs, p.bps, p.bins);
-    PKD_LAUNCH_CHECK();
-    k_ref_refine<<<S, kBlock, 0, stream>>>(segs, midc, perm[cur ^ 1], perm[cur], words);
+    k_ref_refine<<<S, kBlock, 0, stream>>>(segs[0], midc, perm[cur ^ 1], perm[cur], words);
     PKD_LAUNCH_CHECK();
     cur ^= 1;
   }

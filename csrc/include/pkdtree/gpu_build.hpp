@@ -31,9 +31,10 @@ struct BuildOptions {
   // off for its leaf builds: their streams plus its communication stream would exceed the
   // hardware queues (GPU_MAX_HW_QUEUES = 4), and RCCL's kernels would queue behind partitions.
   bool allow_split = true;
-  // Sampled top levels allowed (builds of >= Tuning::top_min_n points, from AoS input or from
-  // caller-owned SoA columns such as the distributed builder's received leaves). A band miss
-  // (error bit top4_band_miss_bit()) is redone by a builder with allow_top = false.
+  // Sampled levels allowed: the top levels (builds of >= Tuning::top_min_n points, from AoS input
+  // or from caller-owned SoA columns such as the distributed builder's received leaves) and the
+  // sampled triples. A band miss (error bit top4_band_miss_bit(), GpuBuilder::sampled() builds
+  // only) is redone by a builder with allow_top = false.
   bool allow_top = true;
 };
 
@@ -78,6 +79,14 @@ struct Tuning {
   float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
   int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
   int top_diag = 0;           // PKD_TOP_DIAG: timing diagnostics of the scatter (no tree; top4::Tune::diag)
+  // Sampled triples (build_global.hip, k_g3_*): a triple's pivots of levels l and l+1 estimated
+  // from a sample instead of two key sweeps, made exact over the staged band rows.
+  bool g3 = false;            // PKD_G3=1: sampled triples (off until they beat the exact sweeps)
+  int g3_min_segs = 128;      // PKD_G3_MIN_SEGS: first triple level that samples (segments; the
+                              //   per-segment fix-up kernels need many segments to fill the chip)
+  i64 g3_min_rows = 65536;    // PKD_G3_MIN_ROWS: smallest segment a sampled triple starts from
+  i64 g3_sample = 65536;      // PKD_G3_SAMPLE: sample rows per segment (64-row runs)
+  float g3_z = 6.0f;          // PKD_G3_Z: band half-width in sample-rank standard deviations
   static Tuning from_env();
 };
 
@@ -94,6 +103,9 @@ struct LevelPlan {
   bool triple = false;  // this level and the next two are moved by ONE fused partition pass
   bool tail = false;    // this level and the next two: one workgroup per segment (k_tail3)
   bool sampled = false; // built by the sampled top levels (top4::run)
+  bool g3 = false;      // a triple whose pivots of this level and the next are sampled (k_g3_*)
+  int g3_div = 1;       // its sample: one 64-row run per 64 * g3_div rows
+  int g3_sblocks = 1;   // sample blocks per segment
 };
 
 struct SplitStreams;  // side HIP streams + fork / join events of a split build
@@ -108,9 +120,16 @@ class GpuBuilder {
   int global_levels() const { return lg_; }
   // Levels 0..3 built by the sampled top pass (AoS input builds; see top4.hpp).
   bool sampled_top() const { return top_; }
+  // Any level built from a sample (the top levels or a sampled triple): a build's error word
+  // may then carry top4_band_miss_bit(), and the build must be redone with allow_top = false.
+  bool sampled() const { return top_ || g3_; }
   // Diagnostic: per top node {band rows, rank inside the median's fine bin, rows staged at
   // the node} of the last build on `workspace` (synchronises).
   std::vector<u32> top_band_report(const void* workspace, hipStream_t stream) const;
+  // Diagnostic: the last sampled triple of the last build on `workspace` (synchronises): its
+  // level, then per segment {rows, rows staged per tag 0..6, certain rows per great-grandchild
+  // 0..7, staged rows inserted per great-grandchild 0..7, bad} (25 words). Empty without one.
+  std::vector<u32> g3_report(const void* workspace, hipStream_t stream) const;
   int subtree_max() const { return nsub_; }
   // Split build (0 parts: off): from level split_level() on, the 2^split_level segments are
   // built as split_parts() independent parts on split_streams() HIP streams.
@@ -190,6 +209,9 @@ class GpuBuilder {
   bool top_ = false;     // levels 0..3 by the sampled top pass (AoS input builds)
   mutable u32 top_salt_ = 0;  // per-build salt of the sample positions: a miss is never input-determined
   size_t off_top_ = 0;
+  bool g3_ = false;           // some triple is sampled
+  mutable u32 g3_salt_ = 0;
+  size_t off_stage_ = 0, off_g3_ = 0, off_g3_hist_ = 0;  // staging columns, per-segment state, sample histograms
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,
@@ -204,8 +226,8 @@ class GpuBuilder {
   std::shared_ptr<SplitStreams> split_;
 };
 
-// Error-word bit of the sampled top levels: a band missed its median (the build is invalid and
-// must be redone with BuildOptions::allow_top = false).
+// Error-word bit of the sampled levels (top levels, sampled triples): a band missed its median
+// (the build is invalid and must be redone with BuildOptions::allow_top = false).
 constexpr u32 top4_band_miss_bit() { return 0x20u; }
 
 // Subtree kernel capacity for a dimension (largest power of two whose LDS image fits).

@@ -30,10 +30,11 @@ class ReferenceBuilder {
  private:
   struct RefLevel {
     i64 segs;
-    int bins, bps;
+    int bins, bps, hbps;  // histogram buckets per segment, partition / histogram blocks per segment
   };
-  i64 n_;
+  i64 n_, ncol_ = 0;
   int dim_, depth0_, levels_ = 0, lfin_ = 0;
+  bool rows_ = false;  // dim <= 8: rows move as SoA columns (else a permutation, keys gathered)
   std::vector<RefLevel> plan_;
   size_t off_perm_[2] = {0, 0}, off_keys_ = 0, off_midc_ = 0, off_hist_ = 0, off_segs_ = 0, off_words_ = 0,
          ws_bytes_ = 0;

@@ -21,7 +21,7 @@ class GpuTreeBuilder:
     (benchmarks, rebuilds of a streaming index) allocate nothing.
     """
 
-    TOP_BAND_MISS = 0x20  # error bit: a sampled top band missed its median (rebuild unsampled)
+    TOP_BAND_MISS = 0x20  # error bit: a sampled band (top levels or a triple) missed its median: rebuild unsampled
 
     def __init__(self, n: int, dim: int, depth0: int = 0, subtree_max: int = 0, allow_top: bool = True):
         self._b = native().GpuBuilder(int(n), int(dim), int(depth0), int(subtree_max), bool(allow_top))
@@ -62,11 +62,26 @@ class GpuTreeBuilder:
         """Levels 0..3 come from the sampled top pass (csrc/gpu/top4.hpp)."""
         return bool(self._b.sampled_top)
 
+    @property
+    def sampled(self) -> bool:
+        """Some levels come from a sample (the top pass or a sampled triple): the error word may
+        carry TOP_BAND_MISS, and such a build is redone unsampled (build_gpu_checked)."""
+        return bool(self._b.sampled)
+
     def top_band_report(self):
         """Per top node (heap 0..14) of the last build: (band rows, rank inside the median's
         fine bin, rows the scatter staged at the node). Synchronises."""
         v = list(self._b.top_band_report())
         return [tuple(v[3 * i:3 * i + 3]) for i in range(len(v) // 3)]
+
+    def g3_report(self):
+        """The last sampled triple of the last build (synchronises): (level, per-segment rows
+        [n, staged per tag 0..6, certain per great-grandchild 0..7, inserted per great-grandchild
+        0..7, bad]); None without a sampled triple."""
+        v = list(self._b.g3_report())
+        if not v:
+            return None
+        return v[0], [v[1 + 25 * i:26 + 25 * i] for i in range((len(v) - 1) // 25)]
 
     def read_error(self) -> int:
         """Sticky device error word of the last build (0 = ok). Synchronises."""
@@ -162,7 +177,7 @@ def build_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor] = None, 
     points = points.contiguous()
     b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
     tp, ti = b.build(points, ids, id_base)
-    if b.sampled_top and (b.read_error() & GpuTreeBuilder.TOP_BAND_MISS):
+    if b.sampled and (b.read_error() & GpuTreeBuilder.TOP_BAND_MISS):
         key = ("unsampled", points.shape[0], points.shape[1], depth0, subtree_max, points.device)
         fb = _builders.get(key)
         if fb is None:
