@@ -1883,14 +1883,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
       if constexpr (ATOM) {
         zone_pre[i] = (zi << 16) | atomicAdd(&wcnt[w][zi], 1u);
       } else {
-        u32 my = 0;
-#pragma unroll
-        for (int z = 0; z < NZ; ++z) {
-          const u64 m = __ballot(zi == u32(z));
-          if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
-          if (zi == u32(z)) my = mbcnt(m);
-        }
-        zone_pre[i] = (zi << 16) | my;
+        zone_pre[i] = (zi << 16) | dev::wave_zone_rank<NZ>(zi, &gcnt[0][i * 4 + w], 64);
       }
       if (fuse && q < 6 && q != 1 && q != 4) {
         const u32 g = (q / 3) * 2 + (q % 3 == 2 ? 1u : 0u);
@@ -2306,14 +2299,7 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
       if constexpr (ATOM) {
         zone_pre[i] = (q << 16) | atomicAdd(&wcnt[w][q], 1u);
       } else {
-        u32 my = 0;
-#pragma unroll
-        for (int z = 0; z < NZ; ++z) {
-          const u64 m = __ballot(q == u32(z));
-          if (ln == 0) gcnt[z][i * 4 + w] = __popcll(m);
-          if (q == u32(z)) my = mbcnt(m);
-        }
-        zone_pre[i] = (q << 16) | my;
+        zone_pre[i] = (q << 16) | dev::wave_zone_rank<NZ>(q, &gcnt[0][i * 4 + w], 64);
       }
       const u32 zz = q % 3;
       if (fuse && q < u32(NZ) && zz != 1) {
@@ -2460,6 +2446,10 @@ struct G3Args {
   int sblocks;     // sample blocks per segment
   float z;         // band half-width in standard deviations of the sample rank
   u32 salt;        // per build: the sample positions (so a miss) are never fixed by the input
+  // multi-block resolve (k_g3_m*): per-node state, band histograms, median-bin candidates
+  struct G3Node* nodes;     // [segment][6]
+  u32* mhist;               // [segment][6][kG3ResBins]
+  u64* cand;                // [segment][6][kG3MCand]
 };
 
 __device__ __forceinline__ u32 g3_mix(u32 x) {  // murmur3 finaliser
@@ -2750,6 +2740,8 @@ __global__ __launch_bounds__(kBlock) void k_g3_band(LevelArgs a, G3Args g) {
   }
   if (g.bins3 > 0)
     for (int i = tid; i < kG3Gg * g.bins3; i += kBlock) g.hist3[(kG3Gg * s) * g.bins3 + i] = 0u;
+  if (g.mhist != nullptr)  // the multi-block resolve's band histograms
+    for (int i = tid; i < 6 * kG3ResBins; i += kBlock) g.mhist[(g.seg0 + s) * 6 * kG3ResBins + i] = 0u;
   float e_lo, e_hi;
   g3_bstar_edges(a, h, &e_lo, &e_hi);
   const float* cell = a.cells + h * 2 * D;
@@ -2870,14 +2862,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
       if constexpr (ATOM) {
         zone_pre[i] = (q << 16) | atomicAdd(&wcnt[w][q], 1u);
       } else {
-        u32 my = 0;
-#pragma unroll
-        for (int z = 0; z < NZ; ++z) {
-          const u64 m = __ballot(q == u32(z));
-          if (dev::lane() == 0) gcnt[z][i * 4 + w] = __popcll(m);
-          if (q == u32(z)) my = mbcnt(m);
-        }
-        zone_pre[i] = (q << 16) | my;
+        zone_pre[i] = (q << 16) | dev::wave_zone_rank<NZ>(q, &gcnt[0][i * 4 + w], 64);
       }
       if (fuse && q < 8u) atomicAdd(&nh[q * u32(nb3) + bucket_of(k3, ggp[q], nb3)], 1u);
     }
@@ -3308,6 +3293,413 @@ __global__ __launch_bounds__(kG3Threads) void k_g3_res(LevelArgs a, G3Args g) {
   }
   __syncthreads();
   for (int i = tid; i < NG * nb3; i += NT) hn3[i] = h3[i];
+}
+
+// Multi-block resolve of levels l+1 and l+2 (sampled triples of few, large segments, e.g. the
+// 16 segments of level 4: one workgroup per node would leave most CUs idle while it streams its
+// band rows three times). Each step runs on K blocks per node and meets the next one at a
+// kernel boundary:
+//   k_g3_mh  band-row histogram (LDS, flushed to the node's global histogram);
+//   k_g3_ms  per node: the median's rank among its band rows (exact counts), its bin;
+//   k_g3_mc  the bin's composites appended to the node's candidate list;
+//   k_g3_mp  per node: the exact pivot (radix select), the children's cells;
+//   k_g3_mr  every band row routed on (the median out, appends / inserts by per-chunk reservation);
+//   k_g3_fin per great-grandchild: complete, or (a failed segment) its histogram recounted.
+constexpr int kG3MCand = 4096;  // candidates of a node's median bin (multi-block resolve)
+
+struct G3Node {  // per node of a multi-block resolve: [segment][slot], slot 0-1 children, 2-5 grandchildren
+  u32 ok, m, t, bin, rank, cnt, ccnt, pad;
+  unsigned long long piv;
+};
+
+// The node's exact median rank among its staged rows (thread 0 only): *ok false if the segment is
+// bad or the band missed (then *miss).
+template <int LEVEL>
+__device__ __forceinline__ void g3_node_rank(const LevelArgs& a, const G3Seg* gs, i64 h, int x, bool* ok, bool* miss,
+                                             u32* m_out, u32* t_out) {
+  const int tag = LEVEL == 0 ? 0 : (LEVEL == 1 ? 1 + x : 3 + x);
+  const i64 hn = LEVEL == 0 ? h : (LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x);
+  const i64 n = a.seg_n[h], nn = a.seg_n[hn];
+  bool good = n > 0 && gs->bad == 0u;
+  const u32 m = gs->zc[8 + tag][0];
+  i64 left = 0;
+  if (LEVEL == 0) {
+    const SegState st = a.state[h];
+    left = st.cnt_less;
+    good = good && m == st.cnt_mid;
+  } else if (LEVEL == 1) {  // certain and resolved rows of the child's left grandchild
+    left = i64(gs->zc[4 * x][0]) + gs->zc[4 * x + 1][0] + gs->ins[4 * x] + gs->ins[4 * x + 1] + gs->zc[8 + 3 + 2 * x][0];
+  } else {
+    left = i64(gs->zc[2 * x][0]) + gs->ins[2 * x];
+  }
+  const i64 tt = nn / 2 - left;
+  const bool hit = m <= gs->cap[tag] && tt >= 0 && tt < i64(m);
+  *miss = good && !hit;
+  *ok = good && hit;
+  *m_out = m;
+  *t_out = u32(tt);
+}
+
+// Bucketing of a node's band rows: its band, narrowed by its exact cell.
+template <int LEVEL>
+__device__ __forceinline__ BucketParams g3_res_params(const LevelArgs& a, const G3Seg* gs, i64 hn, int x, int ax) {
+  const float* cl = a.cells + hn * 2 * a.dim;
+  const u32 A = LEVEL == 1 ? gs->a1[x] : gs->a2[x], B = LEVEL == 1 ? gs->b1[x] : gs->b2[x];
+  const float flo = fmaxf(g3_lo_of(A), cl[2 * ax]);
+  const float fhi = fminf(g3_hi_of(B), cl[2 * ax + 1]);
+  return make_params(flo, fhi > flo ? fhi : flo, kG3ResBins);
+}
+
+template <int LEVEL>
+__global__ __launch_bounds__(kBlock) void k_g3_mh(LevelArgs a, G3Args g, int K) {
+  constexpr int NODES = LEVEL == 1 ? 2 : 4;
+  __shared__ u32 hres[kG3ResBins];
+  __shared__ BucketParams bp;
+  __shared__ u32 sm, sgo;
+  const i64 s = blockIdx.x / (NODES * K);
+  const int x = int(blockIdx.x / K % NODES), part = int(blockIdx.x % K);
+  const i64 h = a.heap0 + s;
+  const G3Seg* gs = g.g3 + g.seg0 + s;
+  const int ax = LEVEL == 1 ? a.next_axis : g.axis2;
+  const i64 hn = LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x;
+  const int tag = LEVEL == 1 ? 1 + x : 3 + x;
+  for (int i = threadIdx.x; i < kG3ResBins; i += kBlock) hres[i] = 0u;
+  if (threadIdx.x == 0) {
+    sgo = a.seg_n[h] > 0 && gs->bad == 0u;
+    sm = min(gs->zc[8 + tag][0], gs->cap[tag]);
+    bp = g3_res_params<LEVEL>(a, gs, hn, x, ax);
+  }
+  __syncthreads();
+  if (!sgo) return;
+  const u32 m = sm, per = (m + u32(K) - 1) / u32(K);
+  const u32 e0 = min(m, u32(part) * per), e1 = min(m, e0 + per);
+  const float* kc = g.stage + i64(ax) * a.ncol + a.seg_lo[h] + gs->off[tag];
+  const BucketParams p = bp;
+  for (u32 b0 = e0; b0 < e1; b0 += kBlock * 8) {
+    float k[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const u32 e = b0 + u * kBlock + threadIdx.x;
+      k[u] = kc[e < e1 ? e : e0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + u * kBlock + threadIdx.x < e1) atomicAdd(&hres[bucket_of(k[u], p, kG3ResBins)], 1u);
+  }
+  __syncthreads();
+  u32* out = g.mhist + ((g.seg0 + s) * 6 + (LEVEL == 1 ? 0 : 2) + x) * kG3ResBins;
+  for (int i = threadIdx.x; i < kG3ResBins; i += kBlock)
+    if (hres[i]) atomicAdd(&out[i], hres[i]);
+}
+
+template <int LEVEL>
+__global__ __launch_bounds__(kBlock) void k_g3_ms(LevelArgs a, G3Args g) {
+  constexpr int NODES = LEVEL == 1 ? 2 : 4;
+  __shared__ u32 ssum[kBlock / 64], sok, sm, st_, sbin, srank, scnt;
+  const i64 s = blockIdx.x / NODES;
+  const int x = int(blockIdx.x % NODES), slot = (LEVEL == 1 ? 0 : 2) + x;
+  const i64 h = a.heap0 + s;
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  G3Node* nd = g.nodes + (g.seg0 + s) * 6 + slot;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    bool ok, miss;
+    u32 m, t;
+    g3_node_rank<LEVEL>(a, gs, h, x, &ok, &miss, &m, &t);
+    if (miss) g3_bad(a.err, gs);
+    sok = ok;
+    sm = m;
+    st_ = t;
+    sbin = 0xffffffffu;
+  }
+  __syncthreads();
+  const u32 t = st_;
+  if (sok) {
+    const u32* hb = g.mhist + ((g.seg0 + s) * 6 + slot) * kG3ResBins;
+    constexpr int per = kG3ResBins / kBlock;
+    u32 v[per], sum = 0;
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      v[i] = hb[tid * per + i];
+      sum += v[i];
+    }
+    const u32 incl = dev::wave_incl_scan(sum);
+    if (dev::lane() == 63) ssum[tid / 64] = incl;
+    __syncthreads();
+    u32 ex = incl - sum;
+    for (int k2 = 0; k2 < tid / 64; ++k2) ex += ssum[k2];
+    if (t >= ex && t < ex + sum) {
+      u32 c = ex;
+      int i = 0;
+      while (i + 1 < per && t >= c + v[i]) c += v[i++];
+      sbin = u32(tid * per + i);
+      srank = t - c;
+      scnt = v[i];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const bool ok = sok && sbin != 0xffffffffu;
+    if (sok && !ok) g3_bad(a.err, gs);  // (the histogram does not hold the rank: inconsistent)
+    nd->ok = ok;
+    nd->m = sm;
+    nd->t = t;
+    nd->bin = sbin;
+    nd->rank = srank;
+    nd->cnt = scnt;
+    nd->ccnt = 0u;
+  }
+}
+
+template <int NCOL, int LEVEL>
+__global__ __launch_bounds__(kBlock) void k_g3_mc(LevelArgs a, G3Args g, int K) {
+  constexpr int NODES = LEVEL == 1 ? 2 : 4;
+  constexpr int D = NCOL - 1;
+  __shared__ BucketParams bp;
+  __shared__ G3Node snd;
+  const i64 s = blockIdx.x / (NODES * K);
+  const int x = int(blockIdx.x / K % NODES), part = int(blockIdx.x % K), slot = (LEVEL == 1 ? 0 : 2) + x;
+  const i64 h = a.heap0 + s;
+  const G3Seg* gs = g.g3 + g.seg0 + s;
+  G3Node* nd = g.nodes + (g.seg0 + s) * 6 + slot;
+  const int ax = LEVEL == 1 ? a.next_axis : g.axis2;
+  const i64 hn = LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x;
+  const int tag = LEVEL == 1 ? 1 + x : 3 + x;
+  if (threadIdx.x == 0) {
+    snd = *nd;
+    bp = g3_res_params<LEVEL>(a, gs, hn, x, ax);
+  }
+  __syncthreads();
+  if (!snd.ok || snd.cnt > u32(kG3MCand)) return;  // (too many: the select streams them instead)
+  const u32 m = snd.m, per = (m + u32(K) - 1) / u32(K);
+  const u32 e0 = min(m, u32(part) * per), e1 = min(m, e0 + per);
+  const i64 r0 = a.seg_lo[h] + gs->off[tag];
+  const float* kc = g.stage + i64(ax) * a.ncol + r0;
+  const u32* ic = reinterpret_cast<const u32*>(g.stage) + i64(D) * a.ncol + r0;
+  u64* cand = g.cand + ((g.seg0 + s) * 6 + slot) * kG3MCand;
+  const BucketParams p = bp;
+  for (u32 b0 = e0; b0 < e1; b0 += kBlock) {  // uniform trip count: ballots below
+    const u32 e = b0 + threadIdx.x;
+    bool mine = false;
+    float kf = 0.0f;
+    if (e < e1) {
+      kf = kc[e];
+      mine = bucket_of(kf, p, kG3ResBins) == snd.bin;
+    }
+    const u64 bm = __ballot(mine);
+    if (!bm) continue;
+    const int leader = __ffsll((long long)bm) - 1;
+    u32 base = 0;
+    if (dev::lane() == leader) base = atomicAdd(&nd->ccnt, u32(__popcll(bm)));
+    base = u32(__shfl(int(base), leader, 64));
+    if (mine) cand[base + mbcnt(bm)] = composite_key(kf, ic[e]);
+  }
+}
+
+template <int NCOL, int LEVEL>
+__global__ __launch_bounds__(kG3Threads) void k_g3_mp(LevelArgs a, G3Args g) {
+  constexpr int NT = kG3Threads;
+  constexpr int NODES = LEVEL == 1 ? 2 : 4;
+  constexpr int D = NCOL - 1;
+  __shared__ G3Node snd;
+  __shared__ BucketParams bp;
+  const i64 s = blockIdx.x / NODES;
+  const int x = int(blockIdx.x % NODES), slot = (LEVEL == 1 ? 0 : 2) + x;
+  const i64 h = a.heap0 + s;
+  const G3Seg* gs = g.g3 + g.seg0 + s;
+  G3Node* nd = g.nodes + (g.seg0 + s) * 6 + slot;
+  const int ax = LEVEL == 1 ? a.next_axis : g.axis2;
+  const i64 hn = LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x;
+  const int tag = LEVEL == 1 ? 1 + x : 3 + x;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    snd = *nd;
+    bp = g3_res_params<LEVEL>(a, gs, hn, x, ax);
+  }
+  __syncthreads();
+  if (!snd.ok) return;
+  const u32 m = snd.m, cnt = snd.cnt, bin = snd.bin;
+  const bool fits = cnt <= u32(kG3MCand);
+  const i64 r0 = a.seg_lo[h] + gs->off[tag];
+  const float* kc = g.stage + i64(ax) * a.ncol + r0;
+  const u32* ic = reinterpret_cast<const u32*>(g.stage) + i64(D) * a.ncol + r0;
+  const u64* cand = g.cand + ((g.seg0 + s) * 6 + slot) * kG3MCand;
+  const BucketParams p = bp;
+  const u64 piv = g3_block_select<NT>(
+      [&](auto f) {
+        if (fits) {
+          for (u32 e = tid; e < cnt; e += NT) f(cand[e]);
+        } else {
+          for (u32 e = tid; e < m; e += NT) {
+            const float kf = kc[e];
+            if (bucket_of(kf, p, kG3ResBins) == bin) f(composite_key(kf, ic[e]));
+          }
+        }
+      },
+      snd.rank);
+  if (tid == 0) nd->piv = piv;
+  const float pk = from_orderable(u32(piv >> 32));
+  const float* cl = a.cells + hn * 2 * D;
+  for (int q = tid; q < 2 * D; q += NT) {
+    const float v0 = cl[q];
+    a.cells[(2 * hn + 1) * 2 * D + q] = q == 2 * ax + 1 ? pk : v0;
+    a.cells[(2 * hn + 2) * 2 * D + q] = q == 2 * ax ? pk : v0;
+  }
+}
+
+template <int NCOL, int LEVEL>
+__global__ __launch_bounds__(kBlock) void k_g3_mr(LevelArgs a, G3Args g, int K) {
+  constexpr int NT = kBlock;
+  constexpr int D = NCOL - 1;
+  constexpr int NODES = LEVEL == 1 ? 2 : 4;
+  constexpr int NG = 8 / NODES;
+  constexpr int R = 4;
+  __shared__ u32 h3[NG * kTripleBins];
+  __shared__ u32 lc[16], lbase[16], sbad;
+  __shared__ G3Node snd;
+  const i64 s = blockIdx.x / (NODES * K);
+  const int x = int(blockIdx.x / K % NODES), part = int(blockIdx.x % K), slot = (LEVEL == 1 ? 0 : 2) + x;
+  const i64 h = a.heap0 + s;
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  const int tid = threadIdx.x;
+  const int nb3 = g.bins3;
+  const i64 nc = a.ncol;
+  const i64 hn = LEVEL == 1 ? 2 * h + 1 + x : 4 * h + 3 + x;
+  const int tag = LEVEL == 1 ? 1 + x : 3 + x;
+  const int fg = NG * x;
+  const i64 gg0 = 8 * h + 7 + fg;
+  float* __restrict__ stg = g.stage;
+  const i64 lo = a.seg_lo[h];
+  const i64 nn = a.seg_n[hn], nlo = a.seg_lo[hn];
+  for (int i = tid; i < NG * nb3; i += NT) h3[i] = 0u;
+  if (tid < 16) lc[tid] = 0u;
+  if (tid == 0) {
+    snd = g.nodes[(g.seg0 + s) * 6 + slot];
+    sbad = 0u;
+  }
+  __syncthreads();
+  if (!snd.ok) return;
+  const u64 piv = snd.piv;
+  const u32 m = snd.m, per = (m + u32(K) - 1) / u32(K);
+  const u32 e0 = min(m, u32(part) * per), e1 = min(m, e0 + per);
+  const i64 r0 = lo + gs->off[tag];
+  const int ax1 = a.next_axis, ax2 = g.axis2, ax3 = g.axis3;
+  u32 A2[4], B2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    A2[i] = gs->a2[i];
+    B2[i] = gs->b2[i];
+  }
+  auto dest = [&](const float* row) -> u32 {
+    float k1 = row[0], k2 = row[0];
+#pragma unroll
+    for (int c = 1; c < D; ++c) {
+      k1 = c == ax1 ? row[c] : k1;
+      k2 = c == ax2 ? row[c] : k2;
+    }
+    const u32 id = __float_as_uint(row[D]);
+    const u64 ck = composite_key(LEVEL == 1 ? k1 : k2, id);
+    if (ck == piv) {
+      const i64 mpos = nlo + nn / 2;
+#pragma unroll
+      for (int c = 0; c < D; ++c) a.out_pts[mpos * D + c] = row[c];
+      a.out_ids[mpos] = id;
+      return 15u;
+    }
+    const u32 side = ck < piv ? 0u : 1u;
+    if (LEVEL == 2) return side;
+    const u32 gi = 2 * u32(x) + side;
+    const u32 o2 = orderable(k2);
+    if (o2 >= A2[gi] && o2 <= B2[gi]) return 11u + gi;
+    return 2 * gi + (o2 > B2[gi] ? 1u : 0u) - u32(fg);
+  };
+  for (u32 b0 = e0; b0 < e1; b0 += NT * R) {
+    float row[R][NCOL];
+    u32 code[R], rk[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const u32 e = b0 + u * NT + tid;
+      const u32 ei = e < e1 ? e : e0;
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) row[u][c] = stg[i64(c) * nc + r0 + ei];
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      code[u] = b0 + u * NT + tid < e1 ? dest(row[u]) : 15u;
+      rk[u] = code[u] < 15u ? atomicAdd(&lc[code[u]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (tid < 15) {  // one reservation per destination per chunk
+      const u32 c = lc[tid];
+      if (c) lbase[tid] = atomicAdd(tid < 8 ? &gs->ins[fg + tid] : &gs->zc[tid][0], c);
+      lc[tid] = 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const u32 cd = code[u];
+      if (cd >= 15u) continue;
+      const u32 q = lbase[cd] + rk[u];
+      float* out = a.dst;
+      i64 d = -1;
+      if (cd < 8u) {
+        const i64 gq = gg0 + cd;
+        const i64 pos = i64(gs->zc[fg + cd][0]) + q;
+        if (pos < a.seg_n[gq]) {
+          d = a.seg_lo[gq] + pos;
+          if (nb3 > 0) {
+            float k3 = row[u][0];
+#pragma unroll
+            for (int c = 1; c < D; ++c) k3 = c == ax3 ? row[u][c] : k3;
+            atomicAdd(&h3[cd * nb3 + bucket_of(k3, a.params[gq], nb3)], 1u);
+          }
+        }
+      } else if (q < gs->cap[cd - 8u]) {
+        d = lo + gs->off[cd - 8u] + q;
+        out = stg;
+      }
+      if (d < 0) {
+        sbad = 1u;
+        continue;
+      }
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = row[u][c];
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (tid == 0 && sbad) g3_bad(a.err, gs);
+  if (nb3 <= 0) return;
+  u32* hn3 = g.hist3 + (kG3Gg * s + fg) * nb3;
+  for (int i = tid; i < NG * nb3; i += NT)
+    if (h3[i]) atomicAdd(&hn3[i], h3[i]);
+}
+
+// One workgroup per great-grandchild after a multi-block resolve: every row placed, or (a failed
+// segment) its level-(l+3) histogram recounted from its slots.
+__global__ __launch_bounds__(kBlock) void k_g3_fin(LevelArgs a, G3Args g) {
+  __shared__ u32 h3[kTripleBins];
+  __shared__ u32 incomplete;
+  const i64 s = blockIdx.x / kG3Gg;
+  const int k = int(blockIdx.x % kG3Gg);
+  const i64 h = a.heap0 + s;
+  G3Seg* gs = g.g3 + g.seg0 + s;
+  const i64 gq = 8 * h + 7 + k;
+  const int nb3 = g.bins3;
+  if (threadIdx.x == 0) {
+    incomplete = i64(gs->zc[k][0]) + gs->ins[k] != a.seg_n[gq];
+    if (incomplete && a.seg_n[h] > 0) g3_bad(a.err, gs);
+  }
+  __syncthreads();
+  if (!incomplete || nb3 <= 0) return;
+  for (int i = threadIdx.x; i < nb3; i += kBlock) h3[i] = 0u;
+  __syncthreads();
+  const BucketParams p3 = a.params[gq];
+  const float* col = a.dst + i64(g.axis3) * a.ncol + a.seg_lo[gq];
+  for (i64 e = threadIdx.x; e < a.seg_n[gq]; e += kBlock) atomicAdd(&h3[bucket_of(col[e], p3, nb3)], 1u);
+  __syncthreads();
+  u32* out = g.hist3 + (kG3Gg * s + k) * nb3;
+  for (int i = threadIdx.x; i < nb3; i += kBlock) out[i] = h3[i];
 }
 
 // =====================================================================================
@@ -3832,6 +4224,9 @@ Tuning Tuning::from_env() {
   t.g3_min_segs = int(std::max<i64>(1, ab_i("PKD_G3_MIN_SEGS", t.g3_min_segs)));
   t.g3_min_rows = std::max<i64>(4096, ab_i("PKD_G3_MIN_ROWS", t.g3_min_rows));
   t.g3_sample = std::max<i64>(1024, ab_i("PKD_G3_SAMPLE", t.g3_sample));
+  t.g3_div_min = int(std::max<i64>(1, ab_i("PKD_G3_DIV_MIN", t.g3_div_min)));
+  t.g3_multi_below = std::max<i64>(1, ab_i("PKD_G3_MULTI_BELOW", t.g3_multi_below));
+  t.g3_sample_blocks = std::max<i64>(1, ab_i("PKD_G3_SAMPLE_BLOCKS", t.g3_sample_blocks));
   if (const char* z = ab_knob("PKD_G3_Z")) t.g3_z = float(std::atof(z));
   return t;
 }
@@ -3974,16 +4369,24 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   // Sampled triples: full-column rows in registers, segments many and large enough (the fix-up
   // kernels run one workgroup per node; the staging regions must fit a segment), and level l's
   // median bucket exact from the fused histogram alone (no second stage).
-  i64 g3_segs = 0;
+  i64 g3_segs = 0, g3_multi_segs = 0;
   for (int l = 0; l < lg_; ++l) {
     LevelPlan& lp = levels_[size_t(l)];
     if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= 8 && !lp.stage2 &&
           lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
       continue;
     lp.g3 = true;
-    lp.g3_div = int(std::max<i64>(1, lp.nmax / tune_.g3_sample));
+    // sample rows per segment: g3_sample, or 1 / 24 of a larger segment (the staged fraction falls
+    // as 1 / sqrt(sample) while the sample's own reads grow linearly)
+    const i64 want = std::max<i64>(tune_.g3_sample, lp.nmax / 24);
+    lp.g3_div = int(std::max<i64>(tune_.g3_div_min, lp.nmax / want));
     const i64 windows = std::max<i64>(1, lp.nmax / (64 * i64(lp.g3_div)));
-    lp.g3_sblocks = int(std::max<i64>(1, std::min<i64>(2048 / lp.segs, windows / 64)));
+    lp.g3_sblocks = int(std::max<i64>(1, std::min<i64>(tune_.g3_sample_blocks / lp.segs, windows / 64)));
+    if (lp.segs < tune_.g3_multi_below) {  // few nodes: K blocks each for the resolve of levels l+1, l+2
+      lp.g3_k1 = int(std::max<i64>(2, 1024 / (2 * lp.segs)));
+      lp.g3_k2 = int(std::max<i64>(2, 1024 / (4 * lp.segs)));
+      g3_multi_segs = std::max(g3_multi_segs, lp.segs);
+    }
     g3_ = true;
     g3_segs = std::max(g3_segs, lp.segs);
   }
@@ -4019,6 +4422,11 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     off_stage_ = take(colbytes);
     off_g3_ = take(size_t(g3_segs) * sizeof(G3Seg));
     off_g3_hist_ = take(size_t(g3_segs) * 6 * kG3Bins * 4);
+    if (g3_multi_segs > 0) {
+      off_g3_nodes_ = take(size_t(g3_multi_segs) * 6 * sizeof(G3Node));
+      off_g3_mhist_ = take(size_t(g3_multi_segs) * 6 * kG3ResBins * 4);
+      off_g3_cand_ = take(size_t(g3_multi_segs) * 6 * kG3MCand * 8);
+    }
   }
   {
     const Tuning& sc = tune_;
@@ -4440,6 +4848,10 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         ga.sblocks = lp.g3_sblocks;
         ga.z = tune_.g3_z;
         ga.salt = g3_salt * 0x9e3779b9u + u32(l);
+        const bool multi = lp.g3_k1 > 1;
+        ga.nodes = multi ? reinterpret_cast<G3Node*>(ws + off_g3_nodes_) : nullptr;
+        ga.mhist = multi ? reinterpret_cast<u32*>(ws + off_g3_mhist_) : nullptr;
+        ga.cand = multi ? reinterpret_cast<u64*>(ws + off_g3_cand_) : nullptr;
         zero_u32(ga.shist + ga.seg0 * 6 * kG3Bins, segs * 6 * kG3Bins, st);
         const int sgrid = int(segs * lp.g3_sblocks);
         k_g3_sample<1><<<sgrid, kBlock, 0, st>>>(a, ga);
@@ -4460,10 +4872,26 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             PKD_LAUNCH_CHECK();
             k_g3_res<NC, 0><<<int(segs), kG3Threads, 0, st>>>(a, ga);
             PKD_LAUNCH_CHECK();
-            k_g3_res<NC, 1><<<int(2 * segs), kG3Threads, 0, st>>>(a, ga);
-            PKD_LAUNCH_CHECK();
-            k_g3_res<NC, 2><<<int(4 * segs), kG3Threads, 0, st>>>(a, ga);
-            PKD_LAUNCH_CHECK();
+            if (lp.g3_k1 > 1) {  // few large segments: every step of levels l+1, l+2 on K blocks per node
+              const int k1 = lp.g3_k1, k2 = lp.g3_k2;
+              k_g3_mh<1><<<int(2 * segs * k1), kBlock, 0, st>>>(a, ga, k1);
+              k_g3_ms<1><<<int(2 * segs), kBlock, 0, st>>>(a, ga);
+              k_g3_mc<NC, 1><<<int(2 * segs * k1), kBlock, 0, st>>>(a, ga, k1);
+              k_g3_mp<NC, 1><<<int(2 * segs), kG3Threads, 0, st>>>(a, ga);
+              k_g3_mr<NC, 1><<<int(2 * segs * k1), kBlock, 0, st>>>(a, ga, k1);
+              k_g3_mh<2><<<int(4 * segs * k2), kBlock, 0, st>>>(a, ga, k2);
+              k_g3_ms<2><<<int(4 * segs), kBlock, 0, st>>>(a, ga);
+              k_g3_mc<NC, 2><<<int(4 * segs * k2), kBlock, 0, st>>>(a, ga, k2);
+              k_g3_mp<NC, 2><<<int(4 * segs), kG3Threads, 0, st>>>(a, ga);
+              k_g3_mr<NC, 2><<<int(4 * segs * k2), kBlock, 0, st>>>(a, ga, k2);
+              k_g3_fin<<<int(kG3Gg * segs), kBlock, 0, st>>>(a, ga);
+              PKD_LAUNCH_CHECK();
+            } else {
+              k_g3_res<NC, 1><<<int(2 * segs), kG3Threads, 0, st>>>(a, ga);
+              PKD_LAUNCH_CHECK();
+              k_g3_res<NC, 2><<<int(4 * segs), kG3Threads, 0, st>>>(a, ga);
+              PKD_LAUNCH_CHECK();
+            }
           }
         });
         std::swap(src, dst);

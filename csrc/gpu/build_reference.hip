@@ -48,7 +48,8 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kFinCap = 2048;     // largest segment the LDS finish takes
-constexpr int kFinThreads = 256;  // its workgroup: kFinCap / kFinThreads rows per thread
+constexpr int kFinThreads = 1024;  // its workgroup: kFinCap / kFinThreads rows per thread (1024: the per-level
+                                   // barrier / LDS-latency chains are 4x shorter than with 256 threads)
 constexpr int kFinItems = kFinCap / kFinThreads;
 constexpr int kItems = 8;         // rows per thread per partition chunk
 constexpr int kChunk = kBlock * kItems;
@@ -450,6 +451,27 @@ __global__ __launch_bounds__(kBlock) void k_ref_refine(const RefSeg* __restrict_
   }
 }
 
+// LDS min / max of a key into smin[sl] / smax[sl] (every lane calls it): the lanes that share
+// the first active lane's sub-segment -- all of them at the first finish levels, where a few
+// sub-segments span the block -- combine with wave reductions and one atomic pair; the others
+// issue their own.
+__device__ __forceinline__ void seg_minmax(u32* smin, u32* smax, int sl, bool act, u32 key) {
+  const u64 am = __ballot(act);
+  if (!am) return;
+  const int leader = __ffsll((long long)am) - 1;
+  const int lsl = __shfl(sl, leader, 64);
+  const bool same = act && sl == lsl;
+  const u32 wmn = dev::wave_min_u32(same ? key : 0xffffffffu), wmx = dev::wave_max_u32(same ? key : 0u);
+  if (dev::lane() == leader) {
+    atomicMin(&smin[lsl], wmn);
+    atomicMax(&smax[lsl], wmx);
+  }
+  if (act && !same) {
+    atomicMin(&smin[sl], key);
+    atomicMax(&smax[sl], key);
+  }
+}
+
 // One workgroup per segment of level lf (<= kFinCap rows): every remaining level in LDS. Each
 // sub-segment [sl, sl + sn) with sn >= 3 ranks its sortable rows (all but its last slot) by
 // (key, slot): buckets are the sub-segment's own slots [sl, sl + sn - 1), value-linear over its
@@ -492,15 +514,14 @@ __global__ __launch_bounds__(kFinThreads) void k_ref_finish(const float* __restr
       const int p = tid + i * kFinThreads;
       srt[i] = false;
       key[i] = 0;
+      int sl = 0;
       if (p < M) {
-        const int sl = SL[p], sn = SN[p];
+        const int sn = SN[p];
+        sl = SL[p];
         srt[i] = sn >= 3 && p != sl + sn - 1;
-        if (srt[i]) {
-          key[i] = orderable(pts[i64(P[cur][p]) * dim + axis]);
-          atomicMin(&smin[sl], key[i]);
-          atomicMax(&smax[sl], key[i]);
-        }
+        if (srt[i]) key[i] = orderable(pts[i64(P[cur][p]) * dim + axis]);
       }
+      seg_minmax(smin, smax, sl, srt[i], key[i]);
     }
     __syncthreads();
     // 2. bucket counts (bucket = a slot of the sub-segment's sortable range)
@@ -829,28 +850,125 @@ __global__ __launch_bounds__(kBlock) void k_rr_part(RowCols src, RowCols dst, in
 // middle row is read from src and written to its place in dst; the median row goes straight to
 // the output; the children's next-axis ranges are stored (this workgroup is their only writer).
 // Middle zones of <= 64 rows (the deep levels) are ranked by one wave without a barrier.
+// Middle zones of <= 64 rows (every segment of the deep levels): one wave per segment, four per
+// block, no barrier. Each lane holds one middle row (loads before stores: in place), ranks it
+// against the others by shuffles and writes it to its final place.
+template <int NC>
+__device__ __forceinline__ void rr_refine_wave(const RefSeg& r, i64 s, RowCols dst, int axis, int naxis,
+                                               RefSeg* __restrict__ nseg, const PartPartial* __restrict__ partials,
+                                               int bps, const u32* __restrict__ ids, u32 id_base,
+                                               float* __restrict__ out_pts, u32* __restrict__ out_ids,
+                                               u32* __restrict__ ties) {
+  constexpr int D = NC - 1;
+  const int ln = dev::lane();
+  const u32 m = r.n / 2, L = r.L, M = r.M;
+  u32 lmn = 0xffffffffu, lmx = 0u, rmn = 0xffffffffu, rmx = 0u;
+  u64 pred = 0ull, succ = ~0ull;
+  for (int k = ln; k < bps; k += 64) {
+    const PartPartial q = partials[s * bps + k];
+    lmn = min(lmn, q.lmn);
+    lmx = max(lmx, q.lmx);
+    rmn = min(rmn, q.rmn);
+    rmx = max(rmx, q.rmx);
+    pred = q.lmax > pred ? q.lmax : pred;
+    succ = q.rmin < succ ? q.rmin : succ;
+  }
+  const bool in = ln < int(M);
+  const u32 p = r.lo + L + (in ? u32(ln) : 0u);
+  float v[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) v[c] = dst.at(c, p);
+  float kf = v[0], nf = v[0];
+#pragma unroll
+  for (int c = 1; c < D; ++c) {
+    kf = c == axis ? v[c] : kf;
+    nf = c == naxis ? v[c] : nf;
+  }
+  const u32 row = __float_as_uint(v[D]);
+  const u64 ck = in ? comp(orderable(kf), row) : ~0ull;
+  u32 rk = 0;
+  for (u32 j = 0; j < M; ++j) rk += dev::shfl_u64(ck, int(j)) < ck ? 1u : 0u;
+  // rank among the middle rows: < m - 1 - L left of c1, == m - 1 - L c1, == m - L the median
+  const u32 r1 = m - 1 - L, r2 = m - L;
+  const u32 nk = orderable(nf);
+  if (in) {
+    if (rk == r2) {
+      const u32 slot = r.lo + m;
+#pragma unroll
+      for (int c = 0; c < D; ++c) out_pts[i64(slot) * D + c] = v[c];
+      out_ids[slot] = ids ? ids[row] : id_base + row;
+    } else {
+      const u32 pos = rk < r1 ? r.lo + L + rk : (rk == r1 ? r.lo + m - 1 : r.lo + m + 1 + (rk - r2 - 1));
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst.at(c, pos) = v[c];
+    }
+    if (rk <= r1) {
+      lmn = min(lmn, nk);
+      lmx = max(lmx, nk);
+    } else if (rk > r2) {
+      rmn = min(rmn, nk);
+      rmx = max(rmx, nk);
+    }
+    if (rk < r1) pred = ck > pred ? ck : pred;
+    if (rk > r2) succ = ck < succ ? ck : succ;
+  }
+  const u64 c1 = dev::shfl_u64(ck, __ffsll((long long)__ballot(in && rk == r1)) - 1);
+  const u64 c2 = dev::shfl_u64(ck, __ffsll((long long)__ballot(in && rk == r2)) - 1);
+  lmn = dev::wave_min_u32(lmn);
+  lmx = dev::wave_max_u32(lmx);
+  rmn = dev::wave_min_u32(rmn);
+  rmx = dev::wave_max_u32(rmx);
+  pred = dev::wave_max_u64(pred);
+  succ = dev::wave_min_u64(succ);
+  if (ln == 0) {
+    if (nseg) {
+      nseg[2 * s].kmin = lmn;
+      nseg[2 * s].kmax = lmx;
+      nseg[2 * s + 1].kmin = rmn;
+      nseg[2 * s + 1].kmax = rmx;
+    }
+    const u32 k1 = u32(c1 >> 32), k2 = u32(c2 >> 32);
+    bool tie = k1 == k2;
+    if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;
+    if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;
+    if (tie) atomicAdd(ties, 1u);
+  }
+}
+
+// Blocks [0, gsm): four segments each, one wave per segment whose middle zone holds <= 64 rows;
+// blocks [gsm, gsm + S): one segment each, the larger middle zones.
+template <int NC>
 __global__ __launch_bounds__(kBlock) void k_rr_refine(RowCols src, RowCols dst, int dim, int axis, int naxis,
                                                       const RefSeg* __restrict__ seg, RefSeg* __restrict__ nseg,
                                                       const PartPartial* __restrict__ partials, int bps,
                                                       const u32* __restrict__ ids, u32 id_base,
                                                       float* __restrict__ out_pts, u32* __restrict__ out_ids,
-                                                      u32* __restrict__ ties) {
+                                                      u32* __restrict__ ties, int S, int gsm) {
+  if (int(blockIdx.x) < gsm) {
+    const i64 sw = i64(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+    if (sw >= S) return;
+    const RefSeg r = seg[sw];
+    if (r.n < 3 || r.M > 64u) return;
+    rr_refine_wave<NC>(r, sw, dst, axis, naxis, nseg, partials, bps, ids, id_base, out_pts, out_ids, ties);
+    return;
+  }
   __shared__ u64 buf[kRefineCap];
   __shared__ u32 cl, cr;
   __shared__ u64 r64[kBlock / 64][3];
   __shared__ u32 red2[kBlock / 64][2];
   __shared__ u64 sc1, sc2;
-  const RefSeg r = seg[blockIdx.x];
-  if (r.n < 3) return;
+  const i64 sb = i64(blockIdx.x) - gsm;
+  const RefSeg r = seg[sb];
+  if (r.n < 3 || r.M <= 64u) return;
   const u32 m = r.n / 2, L = r.L, M = r.M;
   const u32 base = r.lo + L;
-  const int NC = dim + 1;
+  (void)dim;  // (NC = dim + 1)
   const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
   // the partition's partials
   u32 lmn = 0xffffffffu, lmx = 0u, rmn = 0xffffffffu, rmx = 0u;
   u64 pred = 0ull, succ = ~0ull;  // left zone max / right zone min so far
   for (int k = tid; k < bps; k += kBlock) {
-    const PartPartial q = partials[i64(blockIdx.x) * bps + k];
+    const PartPartial q = partials[sb * bps + k];
     lmn = min(lmn, q.lmn);
     lmx = max(lmx, q.lmx);
     rmn = min(rmn, q.rmn);
@@ -950,10 +1068,10 @@ __global__ __launch_bounds__(kBlock) void k_rr_refine(RowCols src, RowCols dst, 
       succ = r64[k][2] < succ ? r64[k][2] : succ;
     }
     if (nseg) {
-      nseg[2 * blockIdx.x].kmin = lmn;
-      nseg[2 * blockIdx.x].kmax = lmx;
-      nseg[2 * blockIdx.x + 1].kmin = rmn;
-      nseg[2 * blockIdx.x + 1].kmax = rmx;
+      nseg[2 * sb].kmin = lmn;
+      nseg[2 * sb].kmax = lmx;
+      nseg[2 * sb + 1].kmin = rmn;
+      nseg[2 * sb + 1].kmax = rmx;
     }
     const u32 k1 = u32(c1 >> 32), k2 = u32(c2 >> 32);
     bool tie = k1 == k2;
@@ -965,8 +1083,8 @@ __global__ __launch_bounds__(kBlock) void k_rr_refine(RowCols src, RowCols dst, 
 
 // Row-path LDS finish: the segment's columns are loaded once (X[c][local row]); slots hold
 // local row indices, keys are read through them, and every slot's row is written to the
-// output at the end. Thread t owns the kFinItems consecutive slots from t * kFinItems, so a
-// sub-segment's key range takes one LDS atomic per run of a thread's slots, not one per row.
+// output at the end. Thread t owns the kFinItems consecutive slots from t * kFinItems; a
+// sub-segment's key range is combined per wave before its LDS atomics (seg_minmax).
 __global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim, int depth0, i64 n_total, int lf,
                                                            int levels, const u32* __restrict__ ids, u32 id_base,
                                                            float* __restrict__ out_pts, u32* __restrict__ out_ids,
@@ -1002,37 +1120,19 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim,
     for (int p = tid; p <= M; p += kFinThreads) H[p] = 0u;
     u32 key[kFinItems], slot[kFinItems], bk[kFinItems];
     bool srt[kFinItems];
-    {
-      u32 rmn = 0xffffffffu, rmx = 0u;
-      int rs = -1;  // the current run's sub-segment start
 #pragma unroll
-      for (int i = 0; i < kFinItems; ++i) {
-        const int p = p0 + i;
-        srt[i] = false;
-        key[i] = 0;
-        if (p < M) {
-          const int sl = SL[p], sn = SN[p];
-          srt[i] = sn >= 3 && p != sl + sn - 1;
-          if (srt[i]) {
-            key[i] = orderable(xk[P[cur][p]]);
-            if (sl != rs) {
-              if (rs >= 0) {
-                atomicMin(&smin[rs], rmn);
-                atomicMax(&smax[rs], rmx);
-              }
-              rs = sl;
-              rmn = 0xffffffffu;
-              rmx = 0u;
-            }
-            rmn = min(rmn, key[i]);
-            rmx = max(rmx, key[i]);
-          }
-        }
+    for (int i = 0; i < kFinItems; ++i) {
+      const int p = p0 + i;
+      srt[i] = false;
+      key[i] = 0;
+      int sl = 0;
+      if (p < M) {
+        const int sn = SN[p];
+        sl = SL[p];
+        srt[i] = sn >= 3 && p != sl + sn - 1;
+        if (srt[i]) key[i] = orderable(xk[P[cur][p]]);
       }
-      if (rs >= 0) {
-        atomicMin(&smin[rs], rmn);
-        atomicMax(&smax[rs], rmx);
-      }
+      seg_minmax(smin, smax, sl, srt[i], key[i]);
     }
     __syncthreads();
 #pragma unroll
@@ -1268,8 +1368,18 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
 #undef PKD_RR
       }
       PKD_LAUNCH_CHECK();
-      k_rr_refine<<<S, kBlock, 0, stream>>>(cols[cur], cols[cur ^ 1], dim_, axis, naxis, sg, nsg, partials, p.bps,
-                                            ids, id_base, out_pts, out_ids, words);
+      {  // middle zones of <= 64 rows by one wave each (4 per block), the rest by a block each
+        const int gsm = (S + kBlock / 64 - 1) / (kBlock / 64);
+        switch (NC) {
+#define PKD_RF(N)                                                                                                      \
+  case N:                                                                                                              \
+    k_rr_refine<N><<<gsm + S, kBlock, 0, stream>>>(cols[cur], cols[cur ^ 1], dim_, axis, naxis, sg, nsg, partials,     \
+                                                   p.bps, ids, id_base, out_pts, out_ids, words, S, gsm);              \
+    break;
+          PKD_RF(2) PKD_RF(3) PKD_RF(4) PKD_RF(5) PKD_RF(6) PKD_RF(7) PKD_RF(8) default: PKD_RF(9)
+#undef PKD_RF
+        }
+      }
       PKD_LAUNCH_CHECK();
       cur ^= 1;
     }

@@ -74,6 +74,22 @@ __device__ __forceinline__ u64 wave_max_u64(u64 v) {
   return v;
 }
 
+// Multi-split rank of a wave's lanes by zone q (< 16; callers use 15 for "no zone"): this lane's
+// rank among the lanes of its zone, lower lanes first, from 4 bit-sliced ballots instead of one
+// ballot per zone; lane z < NZ stores zone z's count to cnt[z * stride] (one LDS store per wave
+// instead of one single-lane store per zone). All 64 lanes must call it.
+template <int NZ>
+__device__ __forceinline__ u32 wave_zone_rank(u32 q, u32* cnt, int stride) {
+  static_assert(NZ <= 16, "4-bit zones");
+  const u64 b0 = __ballot(q & 1u), b1 = __ballot(q & 2u), b2 = __ballot(q & 4u), b3 = __ballot(q & 8u);
+  auto same = [&](u32 z) {
+    return ((z & 1u) ? b0 : ~b0) & ((z & 2u) ? b1 : ~b1) & ((z & 4u) ? b2 : ~b2) & ((z & 8u) ? b3 : ~b3);
+  };
+  const u32 ln = u32(lane());
+  if (ln < u32(NZ)) cnt[ln * u32(stride)] = u32(__popcll(same(ln)));
+  return mbcnt(same(q));
+}
+
 // Bucketing used by every histogram/partition pair. Monotone non-decreasing in x, so the
 // bucket order never contradicts the key order; identical inputs give identical buckets
 // in every kernel (-ffp-contract=off, no FMA possible in this expression).

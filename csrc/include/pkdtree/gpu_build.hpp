@@ -76,17 +76,26 @@ struct Tuning {
   bool top = true;            // PKD_TOP=0: levels 0..3 by the exact pairs
   i64 top_min_n = 10000000;  // PKD_TOP_MIN_N: smallest build that samples its top levels (8 M: 1.18 ms sampled vs 1.16 paired; 12.5 M: 1.49 vs 1.58)
   int top_sample_log2 = 0;    // PKD_TOP_SAMPLE: log2 of the sample rows (0: by size, 2^20 at 100 M)
-  float top_z = 9.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
+  // z: a miss is detected and rebuilt unsampled (+1 build), so z only has to make that rare:
+  // P(|N(0,1)| > 6) = 2e-9 per node x 15 nodes; 100M x 3D top staging 6% -> 4% of the rows.
+  float top_z = 6.0f;         // PKD_TOP_Z: band half-width in sample-rank standard deviations
   int top_blocks = 0;         // PKD_TOP_BLOCKS: scatter grid (0: by size)
   int top_diag = 0;           // PKD_TOP_DIAG: timing diagnostics of the scatter (no tree; top4::Tune::diag)
   // Sampled triples (build_global.hip, k_g3_*): a triple's pivots of levels l and l+1 estimated
   // from a sample instead of two key sweeps, made exact over the staged band rows.
-  bool g3 = false;            // PKD_G3=1: sampled triples (off until they beat the exact sweeps)
-  int g3_min_segs = 128;      // PKD_G3_MIN_SEGS: first triple level that samples (segments; the
-                              //   per-segment fix-up kernels need many segments to fill the chip)
-  i64 g3_min_rows = 65536;    // PKD_G3_MIN_ROWS: smallest segment a sampled triple starts from
+  // 100M x 3D (profiles/r5_g3_ab.txt): 9.147 ms exact, 8.946 sampled at level 7 (781 k-row
+  // segments, 8% of the rows staged); sampling the level-10 triple too (98 k rows) costs more
+  // than its sweeps (9.233), as does the level-7 triple of 12.5 M (1.447 vs 1.433).
+  bool g3 = true;             // PKD_G3=0: every triple by its exact key sweeps
+  int g3_min_segs = 16;       // PKD_G3_MIN_SEGS: first triple level that samples (segments; below
+                              //   128 the fix-up of levels l+1, l+2 runs on several blocks per node)
+  i64 g3_min_rows = 262144;   // PKD_G3_MIN_ROWS: smallest segment a sampled triple starts from
   i64 g3_sample = 65536;      // PKD_G3_SAMPLE: sample rows per segment (64-row runs)
-  float g3_z = 6.0f;          // PKD_G3_Z: band half-width in sample-rank standard deviations
+  int g3_div_min = 1;         // PKD_G3_DIV_MIN: the sample holds at most 1 / g3_div_min of a segment
+  i64 g3_multi_below = 128;   // PKD_G3_MULTI_BELOW: triples of fewer segments resolve on several blocks per node
+  i64 g3_sample_blocks = 2048;  // PKD_G3_SAMPLE_BLOCKS: grid of a sample pass (all segments)
+  float g3_z = 5.0f;          // PKD_G3_Z: band half-width in sample-rank standard deviations (5: a miss in
+                              //   ~1 of 2000 100M builds, i.e. +5 us expected; staged 8.0% -> 6.8%)
   static Tuning from_env();
 };
 
@@ -106,6 +115,7 @@ struct LevelPlan {
   bool g3 = false;      // a triple whose pivots of this level and the next are sampled (k_g3_*)
   int g3_div = 1;       // its sample: one 64-row run per 64 * g3_div rows
   int g3_sblocks = 1;   // sample blocks per segment
+  int g3_k1 = 0, g3_k2 = 0;  // blocks per node of the multi-block resolve of levels +1 / +2 (0: one)
 };
 
 struct SplitStreams;  // side HIP streams + fork / join events of a split build
@@ -212,6 +222,7 @@ class GpuBuilder {
   bool g3_ = false;           // some triple is sampled
   mutable u32 g3_salt_ = 0;
   size_t off_stage_ = 0, off_g3_ = 0, off_g3_hist_ = 0;  // staging columns, per-segment state, sample histograms
+  size_t off_g3_nodes_ = 0, off_g3_mhist_ = 0, off_g3_cand_ = 0;  // multi-block resolve
   // workspace offsets
   size_t off_cols_a_ = 0, off_cols_b_ = 0, off_seg_lo_ = 0, off_seg_n_ = 0, off_state_ = 0,
          off_params_ = 0, off_cells_ = 0, off_hist0_ = 0, off_hist1_ = 0, off_bbox_ = 0, off_err_ = 0, off_hist2_ = 0, off_bcnt_ = 0,

@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, nargs="+", default=[100_000_000, 12_500_000])
 ap.add_argument("--dim", type=int, default=3)
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--reps", type=int, default=1, help="rounds over the sets (interleaved, median reported)")
 ap.add_argument("--sets", nargs="+", default=["PKD_G3=0", ""],
                 help="knob sets, each 'K=V,K=V' ('' = defaults)")
 args = ap.parse_args()
@@ -27,7 +28,8 @@ os.environ["PKD_AB"] = "1"
 for n in args.n:
     x = pk.uniform_points(n, args.dim, seed=1, device=dev)
     ref = None
-    for ks in args.sets:
+    times = {ks: [] for ks in args.sets}
+    for ks in [k for _ in range(args.reps) for k in args.sets]:
         kv = dict(p.split("=", 1) for p in ks.split(",") if p)
         old = {k: os.environ.get(k) for k in kv}
         os.environ.update(kv)
@@ -51,6 +53,7 @@ for n in args.n:
             b.build(x, None, 0, tp, ti)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        times[ks].append(ms)
         rep = b.g3_report()
         staged = None
         if rep is not None:
@@ -62,5 +65,10 @@ for n in args.n:
         print(json.dumps({"n": n, "dim": args.dim, "set": ks or "default", "ms": round(ms, 3), "err": err,
                           "same_as_first": same, "g3": " g3" in b.describe(), "staged": staged}), flush=True)
         del b
+    if args.reps > 1:
+        for ks, v in times.items():
+            v = sorted(v)
+            print(json.dumps({"n": n, "dim": args.dim, "set": ks or "default", "median_ms": round(v[len(v) // 2], 3),
+                              "all_ms": [round(t, 3) for t in v]}), flush=True)
     del x, ref, tp, ti
     torch.cuda.empty_cache()
