@@ -4227,6 +4227,8 @@ Tuning Tuning::from_env() {
   t.g3_div_min = int(std::max<i64>(1, ab_i("PKD_G3_DIV_MIN", t.g3_div_min)));
   t.g3_multi_below = std::max<i64>(1, ab_i("PKD_G3_MULTI_BELOW", t.g3_multi_below));
   t.g3_sample_blocks = std::max<i64>(1, ab_i("PKD_G3_SAMPLE_BLOCKS", t.g3_sample_blocks));
+  t.g3_min_n = std::max<i64>(0, ab_i("PKD_G3_MIN_N", t.g3_min_n));
+  t.g3_max_dim = int(ab_i("PKD_G3_MAX_DIM", t.g3_max_dim));
   if (const char* z = ab_knob("PKD_G3_Z")) t.g3_z = float(std::atof(z));
   return t;
 }
@@ -4372,8 +4374,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   i64 g3_segs = 0, g3_multi_segs = 0;
   for (int l = 0; l < lg_; ++l) {
     LevelPlan& lp = levels_[size_t(l)];
-    if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= 8 && !lp.stage2 &&
-          lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
+    if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= std::min(8, tune_.g3_max_dim) &&
+          !lp.stage2 && n_ >= tune_.g3_min_n && lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
       continue;
     lp.g3 = true;
     // sample rows per segment: g3_sample, or 1 / 24 of a larger segment (the staged fraction falls

@@ -81,15 +81,26 @@ __host__ __device__ inline void seg_geometry(i64 n, int l, i64 j, i64* lo_out, i
   *n_out = m;
 }
 
-// Value-linear bucket of an orderable key over [kmin, kmax]: float(k - kmin) * B / (span + 1),
-// truncated. Conversion, multiplication by a positive constant and truncation are all monotone,
-// so any key order is kept (ranks stay exact) and no 64-bit division is needed.
-__device__ __forceinline__ float ref_scale(u32 kmin, u32 kmax, u32 B) { return float(B) / (float(kmax - kmin) + 1.0f); }
-__device__ __forceinline__ u32 ref_bucket_s(u32 k, u32 kmin, float scale, u32 B) {
-  return min(u32(float(k - kmin) * scale), B - 1);
+// Value-linear bucket of an orderable key's float value over [value(kmin), value(kmax)]:
+// (x - lo) * B / span, clamped and truncated. Subtraction, multiplication by a positive constant
+// (no FMA: -ffp-contract=off), clamping and truncation are all monotone, so any key order is kept
+// and ranks stay exact. Buckets linear in the key's BIT PATTERN instead would crowd the rows of
+// any range spanning several binary exponents (every cell around 0) into a few buckets, whose
+// select then streams thousands of rows (a 10 M build's refines and LDS finish: 2-5x slower).
+struct RefBk {
+  float lo, scale;
+};
+__device__ __forceinline__ RefBk ref_scale(u32 kmin, u32 kmax, u32 B) {
+  const float lo = from_orderable(kmin), span = from_orderable(kmax) - lo;
+  return RefBk{lo, (span > 0.0f && span < INFINITY) ? float(B) / span : 0.0f};
 }
+__device__ __forceinline__ u32 ref_bucket_v(float x, RefBk p, u32 B) {
+  const float t = fminf(fmaxf((x - p.lo) * p.scale, 0.0f), float(B - 1));
+  return u32(t);
+}
+__device__ __forceinline__ u32 ref_bucket_s(u32 k, RefBk p, u32 B) { return ref_bucket_v(from_orderable(k), p, B); }
 __device__ __forceinline__ u32 ref_bucket(u32 k, u32 kmin, u32 kmax, u32 B) {
-  return ref_bucket_s(k, kmin, ref_scale(kmin, kmax, B), B);
+  return ref_bucket_s(k, ref_scale(kmin, kmax, B), B);
 }
 
 __device__ __forceinline__ u64 comp(u32 key, u32 row) { return (u64(key) << 32) | row; }
@@ -710,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const
   __syncthreads();
   u32 b0, b1;
   block_part(r, part, bps, &b0, &b1);
-  const float sc = ref_scale(r.kmin, r.kmax, u32(B));
+  const RefBk sc = ref_scale(r.kmin, r.kmax, u32(B));
   const float* kc = src.c + i64(axis) * src.ncol + r.lo;
   constexpr int U = 4;
   for (u32 e0 = b0; e0 < b1; e0 += kBlock * U) {
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const u32 e = e0 + u32(u * kBlock) + threadIdx.x;
-      if (e < b1) atomicAdd(&h[ref_bucket_s(orderable(v[u]), r.kmin, sc, u32(B))], 1u);
+      if (e < b1) atomicAdd(&h[ref_bucket_v(v[u], sc, u32(B))], 1u);
     }
   }
   __syncthreads();
@@ -763,7 +774,7 @@ __global__ __launch_bounds__(kBlock) void k_rr_part(RowCols src, RowCols dst, in
   }
   u32 b0, b1;
   block_part(r, part, bps, &b0, &b1);
-  const float sc = ref_scale(r.kmin, r.kmax, u32(B));
+  const RefBk sc = ref_scale(r.kmin, r.kmax, u32(B));
   u64 lmax = 0ull, rmin = ~0ull;
   constexpr int kCh = kBlock * kI;
   for (u32 c0 = b0; c0 < b1; c0 += kCh) {
@@ -784,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_rr_part(RowCols src, RowCols dst, in
         nf = c == naxis ? v[i][c] : nf;
       }
       const u32 key = orderable(kf);
-      const u32 b = ref_bucket_s(key, r.kmin, sc, u32(B));
+      const u32 b = ref_bucket_v(kf, sc, u32(B));
       z[i] = !valid ? 3u : (b < r.b1 ? 0u : (b <= r.b2 ? 1u : 2u));
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -1143,7 +1154,7 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim,
       if (srt[i]) {
         const int sl = SL[p], sn = SN[p];
         const u32 kmn = smin[sl];
-        bk[i] = u32(sl) + ref_bucket_s(key[i], kmn, ref_scale(kmn, smax[sl], u32(sn - 1)), u32(sn - 1));
+        bk[i] = u32(sl) + ref_bucket_s(key[i], ref_scale(kmn, smax[sl], u32(sn - 1)), u32(sn - 1));
         slot[i] = atomicAdd(&H[bk[i]], 1u);
       }
     }

@@ -90,6 +90,10 @@ struct Tuning {
   int g3_min_segs = 16;       // PKD_G3_MIN_SEGS: first triple level that samples (segments; below
                               //   128 the fix-up of levels l+1, l+2 runs on several blocks per node)
   i64 g3_min_rows = 262144;   // PKD_G3_MIN_ROWS: smallest segment a sampled triple starts from
+  i64 g3_min_n = i64(32) << 20;  // PKD_G3_MIN_N: smallest build that samples triples (12.5 M: 1.406 ms
+                                 //   without, 1.434 with the 16-segment level-4 triple sampled)
+  int g3_max_dim = 3;         // PKD_G3_MAX_DIM: widest rows that sample triples (100M x 8D: 20.72 ms
+                              //   exact, 21.01 sampled: 36-B rows make the staging dearer)
   i64 g3_sample = 65536;      // PKD_G3_SAMPLE: sample rows per segment (64-row runs)
   int g3_div_min = 1;         // PKD_G3_DIV_MIN: the sample holds at most 1 / g3_div_min of a segment
   i64 g3_multi_below = 128;   // PKD_G3_MULTI_BELOW: triples of fewer segments resolve on several blocks per node

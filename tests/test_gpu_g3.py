@@ -19,6 +19,8 @@ pytestmark = pytest.mark.gpu
 def g3_small(monkeypatch):
     monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_G3_MIN_SEGS", "4")
+    monkeypatch.setenv("PKD_G3_MIN_N", "0")
+    monkeypatch.setenv("PKD_G3_MAX_DIM", "8")
     monkeypatch.setenv("PKD_G3_MIN_ROWS", "4096")
     monkeypatch.setenv("PKD_G3_SAMPLE", "8192")
     importlib.import_module("parallel_kd_tree_amd.ops.build")._builders.clear()
