@@ -4300,102 +4300,112 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   const i64 level_blocks =
       tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2);
   scan_div_ = tune_.scan_div > 0 ? tune_.scan_div : int(std::max<i64>(1, level_blocks / (kLevelBlocks / 2)));
-  for (int l = 0; l < lg_; ++l) {
-    LevelPlan lp;
-    lp.level = l;
-    lp.segs = i64(1) << l;
-    lp.nmax = n_ >> l;
-    lp.bins = global_bins(lp.nmax);
-    lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
-    // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
-    // 256 CUs) while segments are few; one block per segment below that.
-    // rows per block-chunk of the partition kernel used for this dim (runtime-dim rows are
-    // wide, so their blocks take 1024-row chunks and more blocks share a segment)
-    const i64 chunk = dim <= 8 ? i64(kChunk) : i64(kBlock) * 4;
-    lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + chunk - 1) / chunk)));
-    lp.axis = (opt.depth0 + l) % dim;
-    // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
-    lp.stage2 = lp.nmax / lp.bins > tune_.stage2_min;
-    if (lp.stage2) max_hist2_ = std::max<i64>(max_hist2_, lp.segs * kBins2);
-    levels_.push_back(lp);
-    max_bins_ = std::max(max_bins_, lp.bins);
-    max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
-  }
-  // Levels l, l+1, l+2 move in ONE fused scatter pass (a triple) when rows fit the register
-  // path and neither l+1 nor l+2 needs a second-stage histogram (their median buckets are
-  // narrowed by the two key sweeps k_scan / k_scan2 and k_refine alone); otherwise l and l+1
-  // pair up. A triple never straddles the split level of a split build.
-  const bool pairs = dim <= 8 && tune_.pairs;
-  const bool may_split = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
-  auto cap_bins = [&](int l, int cap) {  // level l's bins, fused into the previous pass's LDS
-    if (l >= lg_) return;
-    LevelPlan& g = levels_[size_t(l)];
-    g.bins = std::min(g.bins, cap);
-    levels_[size_t(l - 1)].next_bins = g.bins;
-  };
-  // The last three global levels: one workgroup per segment (k_tail3) when a segment fits its
-  // 1024 threads x 8 / 12 / 16 rows (always, below the subtree capacity of 2048) and rows fit
-  // registers (dim <= 8, full columns).
-  // (A split build's parts start at split_level: the tail may not begin above it.)
-  const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
-  if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - 3 >= tune_.split_level)) {
-    const i64 nl = (n_ >> (lg_ - 3)) + 3;  // + the 16-B alignment shift of the segment start
-    tail_items_ = nl <= 8 * 1024 ? 8 : (nl <= 12 * 1024 ? 12 : (nl <= 16 * 1024 ? 16 : 0));
-    if (tail_items_ > 0) {
-      tail_ = lg_ - 3;
-      for (int l = tail_; l < lg_; ++l) levels_[size_t(l)].tail = true;
-    }
-  }
-  const int lgrp = tail_ >= 0 ? tail_ : lg_;  // levels the pairs / triples cover
-  const int lfirst = top_ ? top4::kLevels : 0;
-  if (top_)
-    for (int l = 0; l < top4::kLevels; ++l) levels_[size_t(l)].sampled = true;
-  for (int l = lfirst; pairs && l + 1 < lgrp;) {
-    // (four levels left: two pairs, not a triple and a lone level, whose single-level pass moves
-    // every row for one level: 100M x 8D level 13 alone took 1.7 ms)
-    const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && lgrp - l != 4 &&
-                     !levels_[size_t(l + 1)].stage2 && !levels_[size_t(l + 2)].stage2;
-    int next = l + (tri ? 3 : 2);
-    if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
-    if (next - l == 3) {
-      levels_[size_t(l)].triple = true;
-      cap_bins(l + 2, tune_.pair_bins);   // k_scan2: 4 grandchild histograms in LDS
-      cap_bins(l + 3, kTripleBins);       // k_partition3: 8 great-grandchild histograms in LDS
-    } else if (next - l == 2) {
-      levels_[size_t(l)].pair = true;
-      cap_bins(l + 2, tune_.pair_bins);   // the pair's scatter fuses 4 grandchild histograms in LDS
-    }
-    l = next;
-  }
-  if (tail_ > 0) levels_[size_t(tail_ - 1)].next_bins = 0;  // k_tail3 bins its levels itself
-  // Sampled triples: full-column rows in registers, segments many and large enough (the fix-up
-  // kernels run one workgroup per node; the staging regions must fit a segment), and level l's
-  // median bucket exact from the fused histogram alone (no second stage).
+  // The level plan: with the sampled top (levels 0..3 by top4::run, pairing from level 4) for the
+  // AoS / caller-column entry points, and without it for the entry points that start at level 0
+  // (build_rows, build_from_soa, strided or row-id input): there levels 0..3 pair up as usual.
   i64 g3_segs = 0, g3_multi_segs = 0;
-  for (int l = 0; l < lg_; ++l) {
-    LevelPlan& lp = levels_[size_t(l)];
-    if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= std::min(8, tune_.g3_max_dim) &&
-          !lp.stage2 && n_ >= tune_.g3_min_n && lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
-      continue;
-    lp.g3 = true;
-    // sample rows per segment: g3_sample, or 1 / 24 of a larger segment (the staged fraction falls
-    // as 1 / sqrt(sample) while the sample's own reads grow linearly)
-    const i64 want = std::max<i64>(tune_.g3_sample, lp.nmax / 24);
-    lp.g3_div = int(std::max<i64>(tune_.g3_div_min, lp.nmax / want));
-    const i64 windows = std::max<i64>(1, lp.nmax / (64 * i64(lp.g3_div)));
-    lp.g3_sblocks = int(std::max<i64>(1, std::min<i64>(tune_.g3_sample_blocks / lp.segs, windows / 64)));
-    if (lp.segs < tune_.g3_multi_below) {  // few nodes: K blocks each for the resolve of levels l+1, l+2
-      lp.g3_k1 = int(std::max<i64>(2, 1024 / (2 * lp.segs)));
-      lp.g3_k2 = int(std::max<i64>(2, 1024 / (4 * lp.segs)));
-      g3_multi_segs = std::max(g3_multi_segs, lp.segs);
+  auto make_plan = [&](bool with_top) {
+    std::vector<LevelPlan> lv;
+    for (int l = 0; l < lg_; ++l) {
+      LevelPlan lp;
+      lp.level = l;
+      lp.segs = i64(1) << l;
+      lp.nmax = n_ >> l;
+      lp.bins = global_bins(lp.nmax);
+      lp.next_bins = (l + 1 < lg_) ? global_bins(n_ >> (l + 1)) : 0;
+      // 2048 blocks per level (a whole number of rounds at 2 or 4 resident blocks per CU on
+      // 256 CUs) while segments are few; one block per segment below that.
+      // rows per block-chunk of the partition kernel used for this dim (runtime-dim rows are
+      // wide, so their blocks take 1024-row chunks and more blocks share a segment)
+      const i64 chunk = dim <= 8 ? i64(kChunk) : i64(kBlock) * 4;
+      lp.bps = int(std::max<i64>(1, std::min<i64>(level_blocks / lp.segs, (lp.nmax + chunk - 1) / chunk)));
+      lp.axis = (opt.depth0 + l) % dim;
+      // expected middle zone nmax / bins larger than the LDS refine: split the median bucket
+      lp.stage2 = lp.nmax / lp.bins > tune_.stage2_min;
+      if (lp.stage2) max_hist2_ = std::max<i64>(max_hist2_, lp.segs * kBins2);
+      lv.push_back(lp);
+      max_bins_ = std::max(max_bins_, lp.bins);
+      max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
     }
-    g3_ = true;
-    g3_segs = std::max(g3_segs, lp.segs);
-  }
-  for (size_t l = 0; l < levels_.size(); ++l) {
-    max_bins_ = std::max(max_bins_, levels_[l].bins);
-    max_hist_ = std::max<i64>(max_hist_, levels_[l].segs * levels_[l].bins);
-  }
+    // Levels l, l+1, l+2 move in ONE fused scatter pass (a triple) when rows fit the register
+    // path and neither l+1 nor l+2 needs a second-stage histogram (their median buckets are
+    // narrowed by the two key sweeps k_scan / k_scan2 and k_refine alone); otherwise l and l+1
+    // pair up. A triple never straddles the split level of a split build.
+    const bool pairs = dim <= 8 && tune_.pairs;
+    const bool may_split = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
+    auto cap_bins = [&](int l, int cap) {  // level l's bins, fused into the previous pass's LDS
+      if (l >= lg_) return;
+      LevelPlan& g = lv[size_t(l)];
+      g.bins = std::min(g.bins, cap);
+      lv[size_t(l - 1)].next_bins = g.bins;
+    };
+    // The last three global levels: one workgroup per segment (k_tail3) when a segment fits its
+    // 1024 threads x 8 / 12 / 16 rows (always, below the subtree capacity of 2048) and rows fit
+    // registers (dim <= 8, full columns).
+    // (A split build's parts start at split_level: the tail may not begin above it.)
+    const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
+    if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - 3 >= tune_.split_level)) {
+      const i64 nl = (n_ >> (lg_ - 3)) + 3;  // + the 16-B alignment shift of the segment start
+      tail_items_ = nl <= 8 * 1024 ? 8 : (nl <= 12 * 1024 ? 12 : (nl <= 16 * 1024 ? 16 : 0));
+      if (tail_items_ > 0) {
+        tail_ = lg_ - 3;
+        for (int l = tail_; l < lg_; ++l) lv[size_t(l)].tail = true;
+      }
+    }
+    const int lgrp = tail_ >= 0 ? tail_ : lg_;  // levels the pairs / triples cover
+    const int lfirst = with_top ? top4::kLevels : 0;
+    if (with_top)
+      for (int l = 0; l < top4::kLevels; ++l) lv[size_t(l)].sampled = true;
+    for (int l = lfirst; pairs && l + 1 < lgrp;) {
+      // (four levels left: two pairs, not a triple and a lone level, whose single-level pass moves
+      // every row for one level: 100M x 8D level 13 alone took 1.7 ms)
+      const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && lgrp - l != 4 &&
+                       !lv[size_t(l + 1)].stage2 && !lv[size_t(l + 2)].stage2;
+      int next = l + (tri ? 3 : 2);
+      if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
+      if (next - l == 3) {
+        lv[size_t(l)].triple = true;
+        cap_bins(l + 2, tune_.pair_bins);   // k_scan2: 4 grandchild histograms in LDS
+        cap_bins(l + 3, kTripleBins);       // k_partition3: 8 great-grandchild histograms in LDS
+      } else if (next - l == 2) {
+        lv[size_t(l)].pair = true;
+        cap_bins(l + 2, tune_.pair_bins);   // the pair's scatter fuses 4 grandchild histograms in LDS
+      }
+      l = next;
+    }
+    if (tail_ > 0) lv[size_t(tail_ - 1)].next_bins = 0;  // k_tail3 bins its levels itself
+    // Sampled triples: full-column rows in registers, segments many and large enough (the fix-up
+    // kernels run one workgroup per node; the staging regions must fit a segment), and level l's
+    // median bucket exact from the fused histogram alone (no second stage).
+    for (int l = 0; l < lg_; ++l) {
+      LevelPlan& lp = lv[size_t(l)];
+      if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= std::min(8, tune_.g3_max_dim) &&
+            !lp.stage2 && n_ >= tune_.g3_min_n && lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
+        continue;
+      lp.g3 = true;
+      // sample rows per segment: g3_sample, or 1 / 24 of a larger segment (the staged fraction falls
+      // as 1 / sqrt(sample) while the sample's own reads grow linearly)
+      const i64 want = std::max<i64>(tune_.g3_sample, lp.nmax / 24);
+      lp.g3_div = int(std::max<i64>(tune_.g3_div_min, lp.nmax / want));
+      const i64 windows = std::max<i64>(1, lp.nmax / (64 * i64(lp.g3_div)));
+      lp.g3_sblocks = int(std::max<i64>(1, std::min<i64>(tune_.g3_sample_blocks / lp.segs, windows / 64)));
+      if (lp.segs < tune_.g3_multi_below) {  // few nodes: K blocks each for the resolve of levels l+1, l+2
+        lp.g3_k1 = int(std::max<i64>(2, 1024 / (2 * lp.segs)));
+        lp.g3_k2 = int(std::max<i64>(2, 1024 / (4 * lp.segs)));
+        g3_multi_segs = std::max(g3_multi_segs, lp.segs);
+      }
+      g3_ = true;
+      g3_segs = std::max(g3_segs, lp.segs);
+    }
+    return lv;
+  };
+  levels_ = make_plan(top_);
+  if (top_) levels_nt_ = make_plan(false);
+  for (const auto* plan : {&levels_, &levels_nt_})
+    for (const LevelPlan& lp : *plan) {
+      max_bins_ = std::max(max_bins_, lp.bins);
+      max_hist_ = std::max<i64>(max_hist_, lp.segs * lp.bins);
+    }
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -4417,7 +4427,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   off_bbox_ = take(size_t(2 * dim) * 4 * (1 + kMaxBoxParts));  // final box + per-block partials
   off_err_ = take(16);
   i64 max_grid = 1;
-  for (const auto& lp : levels_) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
+  for (const auto* plan : {&levels_, &levels_nt_})
+    for (const LevelPlan& lp : *plan) max_grid = std::max<i64>(max_grid, lp.segs * lp.bps);
   off_bcnt_ = take(size_t(max_grid) * 4 * 4 * 2);  // per-block counts + bases (prefix placement)
   if (top_) off_top_ = take(top4::workspace_bytes());
   if (g3_) {
@@ -4563,7 +4574,8 @@ void GpuBuilder::prep_and_run(const float* pts, int rs, bool ids_in_row, const u
     const int g = int(std::min<i64>(2048, std::max<i64>(1, (n_ / 16 + kBlock - 1) / kBlock)));
     // generated ids are synthesised by the first pair's kernels instead of written here
     // (-4 B written and -4 B read per point); the first level must be a pair for that
-    const bool implicit = ids == nullptr && lg_ >= 2 && (levels_[0].pair || levels_[0].triple) && tune_.implicit_ids;
+    const std::vector<LevelPlan>& plan0 = top_ ? levels_nt_ : levels_;  // (this entry starts at level 0)
+    const bool implicit = ids == nullptr && lg_ >= 2 && (plan0[0].pair || plan0[0].triple) && tune_.implicit_ids;
     k_prep3v<<<g, kBlock, 0, stream>>>(pts, ids, id_base, colsA, n_, ncol_, part, implicit ? 0 : 1);
     PKD_LAUNCH_CHECK();
     k_bbox_reduce<<<2 * dim_, kBlock, 0, stream>>>(part, g, dim_, bbox);
@@ -4689,7 +4701,7 @@ void GpuBuilder::build_columns(float* cols, float* out_pts, u32* out_ids, void* 
   if (root_cell) {  // the caller's box of the points: no bounding-box pass over the columns
     k_cell_root<<<1, 64, 0, stream>>>(root_cell, dim_, reinterpret_cast<float*>(ws + off_cells_),
                                       reinterpret_cast<BucketParams*>(ws + off_params_), opt_.depth0 % dim_,
-                                      lg_ > 0 ? levels_[0].bins : 1);
+                                      lg_ > 0 ? (top_ ? levels_nt_ : levels_)[0].bins : 1);
     PKD_LAUNCH_CHECK();
     run_levels(out_pts, out_ids, ws, stream, false, 0, nullptr, 0, cols, 0, true);
     return;
@@ -4709,6 +4721,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
                             bool root_ready) const {
   const int narrow_k = in_rows ? lg_ : 0;  // key columns of the narrow layout
   const u32 g3_salt = g3_ ? g3_salt_++ : 0u;  // this build's sample positions (sampled triples)
+  // levels 0..3 already built by the sampled top, or the plan that pairs them from level 0
+  const std::vector<LevelPlan>& levels = (top_ && first_level == 0) ? levels_nt_ : levels_;
   float* colsA = cols_a ? cols_a : reinterpret_cast<float*>(ws + off_cols_a_);
   float* colsB = reinterpret_cast<float*>(ws + off_cols_b_);
   i64* seg_lo = reinterpret_cast<i64*>(ws + off_seg_lo_);
@@ -4725,7 +4739,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   PKD_LAUNCH_CHECK();
   const int axis0 = opt_.depth0 % dim_;
   if (first_level == 0 && !root_ready) {
-    k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels_[0].bins : 1);
+    k_root<<<1, 64, 0, stream>>>(bbox, dim_, cells, params, axis0, lg_ > 0 ? levels[0].bins : 1);
     PKD_LAUNCH_CHECK();
   }
 
@@ -4746,20 +4760,20 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
                        float*& src, float*& dst) {
     auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
       if (base > 0 && l == base)
-        return hist[l & 1] + size_t(part) * size_t(levels_[size_t(l)].segs / nparts) * size_t(levels_[size_t(l)].bins);
+        return hist[l & 1] + size_t(part) * size_t(levels[size_t(l)].segs / nparts) * size_t(levels[size_t(l)].bins);
       return hs.h[(l - base) & 1];
     };
     // A part's kernels run next to split_streams_ - 1 others: its blocks per segment scale by
     // parts / streams so the concurrent grids together match the unsplit level's grid.
     auto bps_of = [&](int l) -> int {
-      const LevelPlan& lp = levels_[size_t(l)];
+      const LevelPlan& lp = levels[size_t(l)];
       if (nparts == 1) return lp.bps;
       const i64 chunk = dim_ <= 8 ? i64(kChunk) : i64(kBlock) * 4;
       const i64 want = i64(lp.bps) * nparts / std::max(1, split_streams_);
       return int(std::max<i64>(1, std::min<i64>(want, (lp.nmax + chunk - 1) / chunk)));
     };
     auto level_args = [&](int l) {
-      const LevelPlan& lp = levels_[size_t(l)];
+      const LevelPlan& lp = levels[size_t(l)];
       LevelArgs a;
       a.src = src;
       a.dst = dst;
@@ -4814,7 +4828,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
                                               "pkd.level8", "pkd.level9", "pkd.level10", "pkd.level11+"};
     const int lend = tail_ >= 0 ? std::min(l1, tail_) : l1;
     for (int l = l0; l < lend;) {
-      const LevelPlan& lp = levels_[size_t(l)];
+      const LevelPlan& lp = levels[size_t(l)];
       const i64 segs = lp.segs / nparts;  // this part's segments at level l
       TraceRange trl(kLevelNames[std::min(l, 11)]);  // a pair's range carries its first level
       LevelArgs a = level_args(l);
@@ -4836,7 +4850,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       }
       const int grid = int(segs * a.bps);
       if (lp.g3) {
-        const LevelPlan& lr = levels_[size_t(l + 2)];
+        const LevelPlan& lr = levels[size_t(l + 2)];
         G3Args ga;
         ga.g3 = reinterpret_cast<G3Seg*>(ws + off_g3_);
         ga.shist = reinterpret_cast<u32*>(ws + off_g3_hist_);
@@ -4901,8 +4915,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         continue;
       }
       if (lp.triple) {
-        const LevelPlan& lq = levels_[size_t(l + 1)];
-        const LevelPlan& lr = levels_[size_t(l + 2)];
+        const LevelPlan& lq = levels[size_t(l + 1)];
+        const LevelPlan& lr = levels[size_t(l + 2)];
         const i64 segs1 = lq.segs / nparts, segs2 = lr.segs / nparts;
         const int gs = int((segs + 3) / 4), gs1 = int((segs1 + 3) / 4);
         LevelArgs b = level_args(l + 1);
@@ -4945,7 +4959,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
         continue;
       }
       if (lp.pair) {
-        const LevelPlan& lq = levels_[size_t(l + 1)];
+        const LevelPlan& lq = levels[size_t(l + 1)];
         const i64 segs1 = lq.segs / nparts;
         const size_t lds_a = size_t(2 * lp.next_bins + 64) * 4;
         const int gs = int((segs + 3) / 4);
@@ -5024,7 +5038,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
     }
     if (tail_ >= 0 && l1 == lg_) {  // the last three levels of this part's segments
       TraceRange trt("pkd.tail");
-      const LevelPlan& lp = levels_[size_t(tail_)];
+      const LevelPlan& lp = levels[size_t(tail_)];
       const i64 segs = lp.segs / nparts;
       TailArgs ta{src, dst, ncol_, seg_lo, seg_n, cells, lp.segs - 1 + i64(part) * segs, tail_, opt_.depth0,
                   out_pts, out_ids, err, tail_stamp_buffer()};

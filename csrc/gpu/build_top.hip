@@ -44,6 +44,7 @@ constexpr int kHistThreads = 1024;   // workgroup of the LDS histogram kernels
 constexpr int kSampBlocks = 64;
 constexpr int kResBlocks = 256;
 constexpr int kSmallCap = 4096;      // rows of a median's bin selected in LDS
+constexpr i64 kStreamCap = i64(1) << 20;  // staged rows a one-workgroup select over the arena may stream
 constexpr u32 kMed = 0x80000000u;    // tag of a median row: kMed | node
 constexpr int kMaxParts = 2048;      // scatter blocks (one bounding-box partial each)
 constexpr int kMaxSampleLog2 = 21;
@@ -1040,8 +1041,14 @@ __global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
         rank);
   } else {
     // heavy duplicates: the bin holds more rows than LDS takes; select over the staging arena
-    // (every pass streams the staged rows: slow, but exact for any input)
+    // (every pass streams the staged rows: exact, but one workgroup per node streaming a large
+    // arena up to 8 times would take longer than the unsampled build; above kStreamCap staged
+    // rows the miss bit is reported instead, and the build is redone without sampling)
     const i64 staged = st->cursor[kCells];
+    if (staged > kStreamCap) {
+      if (threadIdx.x == 0) report(a.err, 0x200au, u32(X), cnt);
+      return;
+    }
     const u32 A = st->a[X], B = st->b[X];
     const dev::BucketParams bp = st->bparam[X];
     const int axj = a.ax[j];

@@ -211,7 +211,8 @@ class GpuBuilder {
   Tuning tune_;
   int lg_ = 0;      // number of global levels
   int nsub_ = 0;    // LDS subtree capacity
-  std::vector<LevelPlan> levels_;
+  std::vector<LevelPlan> levels_;     // the plan (from level 4 when the top levels are sampled)
+  std::vector<LevelPlan> levels_nt_;  // top_ only: the plan of the entry points that start at level 0
   i64 heap_nodes_ = 0;  // nodes of levels 0..lg_
   int max_bins_ = 0;
   i64 max_hist_ = 0;

@@ -127,3 +127,50 @@ def test_top_from_columns(gpu_device, top_always, n, dim, depth0):
     assert b.read_error() == 0
     cp, ci = ops.build_cpu(x, ids, "exact", depth0, 8)
     assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+
+
+@pytest.mark.parametrize("entry", ["rows", "soa"])
+def test_top_builder_level0_entry_points(gpu_device, top_always, entry):
+    """A builder that samples its top for AoS input still builds rows-with-ids and SoA input from
+    level 0 (its second level plan pairs levels 0..3 there); trees equal the CPU exact tree."""
+    n, dim = 300_000, 3
+    x = pk.generate_problem(55, dim, n)
+    ids = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32) + 1
+    b = ops.GpuTreeBuilder(n, dim, 0, 0)
+    assert b.sampled_top
+    if entry == "rows":
+        rows = torch.cat([x, ids.view(torch.float32).unsqueeze(1)], dim=1).to(gpu_device)
+        tp, ti = b.build_rows(rows)
+    else:
+        cols = b.soa_input(gpu_device)
+        cols[:dim, :n] = x.t().to(gpu_device)
+        cols[dim, :n] = ids.to(gpu_device).view(torch.float32)
+        tp, ti = b.build_from_soa(gpu_device)
+    torch.cuda.synchronize()
+    assert b.read_error() == 0
+    cp, ci = ops.build_cpu(x, ids, "exact", 0, 8)
+    assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+
+
+def test_top_heavy_duplicates_large_is_bounded(gpu_device):
+    """12 M points with 2 distinct values per axis: a median's bin holds millions of staged rows.
+    Rather than one workgroup per node streaming that arena on every select pass, the sampled top
+    reports a miss and build_gpu_checked redoes the build unsampled: exact and bounded in time."""
+    import time
+    torch.manual_seed(1)
+    n = 12_000_000
+    x = torch.randint(0, 2, (n, 3), device=gpu_device).float()
+    importlib.import_module("parallel_kd_tree_amd.ops.build")._builders.clear()
+    ops.build_gpu_checked(x)  # (warm: kernels loaded, builders made)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tp, ti, b = ops.build_gpu_checked(x)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert b.read_error() == 0 and not b.sampled_top  # the unsampled rebuild's builder
+    t = pk.KDTree(tp, ti)
+    assert t.invariant_violations() == 0
+    seen = torch.zeros(n, dtype=torch.int32, device=gpu_device)
+    seen.index_add_(0, ti.long(), torch.ones_like(ti))
+    assert bool((seen == 1).all())
+    assert dt < 2.0, dt
