@@ -4304,6 +4304,13 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   // AoS / caller-column entry points, and without it for the entry points that start at level 0
   // (build_rows, build_from_soa, strided or row-id input): there levels 0..3 pair up as usual.
   i64 g3_segs = 0, g3_multi_segs = 0;
+  // A triple from level l may be sampled (k_g3_*): rows in registers, a large build, many large
+  // segments. Level l's own median bucket is taken from the fused histogram as is (a second stage
+  // is skipped: its rows are the staged tag-0 rows, ranked exactly by k_g3_res<0>).
+  auto g3_ok = [&](const LevelPlan& lp) {
+    return tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= std::min(8, tune_.g3_max_dim) &&
+           n_ >= tune_.g3_min_n && lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows;
+  };
   auto make_plan = [&](bool with_top) {
     std::vector<LevelPlan> lv;
     for (int l = 0; l < lg_; ++l) {
@@ -4359,8 +4366,9 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     for (int l = lfirst; pairs && l + 1 < lgrp;) {
       // (four levels left: two pairs, not a triple and a lone level, whose single-level pass moves
       // every row for one level: 100M x 8D level 13 alone took 1.7 ms)
+      // (a sampled triple needs no histogram of levels l+1, l+2, so their second stages do not matter)
       const bool tri = tune_.triples && l >= tune_.triple_from && l + 2 < lgrp && lgrp - l != 4 &&
-                       !lv[size_t(l + 1)].stage2 && !lv[size_t(l + 2)].stage2;
+                       ((!lv[size_t(l + 1)].stage2 && !lv[size_t(l + 2)].stage2) || g3_ok(lv[size_t(l)]));
       int next = l + (tri ? 3 : 2);
       if (may_split && l < tune_.split_level && tune_.split_level < next) next = tune_.split_level;  // a pass ends there
       if (next - l == 3) {
@@ -4379,9 +4387,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     // median bucket exact from the fused histogram alone (no second stage).
     for (int l = 0; l < lg_; ++l) {
       LevelPlan& lp = lv[size_t(l)];
-      if (!(lp.triple && tune_.g3 && opt.allow_top && !narrow_ && dim >= 2 && dim <= std::min(8, tune_.g3_max_dim) &&
-            !lp.stage2 && n_ >= tune_.g3_min_n && lp.segs >= tune_.g3_min_segs && lp.nmax >= tune_.g3_min_rows))
-        continue;
+      if (!(lp.triple && g3_ok(lp))) continue;
       lp.g3 = true;
       // sample rows per segment: g3_sample, or 1 / 24 of a larger segment (the staged fraction falls
       // as 1 / sqrt(sample) while the sample's own reads grow linearly)
@@ -4841,7 +4847,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       }
       k_select<<<int(segs), kBlock, 0, st>>>(a);
       PKD_LAUNCH_CHECK();
-      if (lp.stage2) {
+      if (lp.stage2 && !lp.g3) {
         zero_u32(a.hist2, segs * kBins2, st);
         k_hist2<<<int(segs * a.bps), kBlock, 0, st>>>(a);
         PKD_LAUNCH_CHECK();

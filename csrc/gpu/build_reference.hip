@@ -711,8 +711,12 @@ __global__ __launch_bounds__(kBlock) void k_rr_prep(const float* __restrict__ pt
   }
 }
 
+// Histogram of a level's sortable keys: every block's LDS histogram is STORED (all B bins,
+// coalesced) -- straight into the segment's histogram when the segment has one block, else into
+// per-block partials that k_rr_hred sums. (Flushing with global atomics cost ~4 M atomics a level:
+// 256 blocks x 16 Ki bins; 30 us of a 10 M level's 36.)
 __global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const RefSeg* __restrict__ seg, int bps,
-                                                    int B, u32* __restrict__ hist) {
+                                                    int B, u32* __restrict__ out) {
   extern __shared__ u32 h[];
   const i64 s = blockIdx.x / bps;
   const int part = blockIdx.x % bps;
@@ -738,9 +742,20 @@ __global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const
     }
   }
   __syncthreads();
-  u32* out = hist + s * i64(B);
-  for (int b = threadIdx.x; b < B; b += kBlock)
-    if (h[b]) atomicAdd(&out[b], h[b]);
+  u32* o = out + i64(blockIdx.x) * B;  // (block = segment when bps == 1)
+  for (int b = threadIdx.x; b < B; b += kBlock) o[b] = h[b];
+}
+
+// Segment histograms from the blocks' partials: one thread per (segment, bin).
+__global__ __launch_bounds__(kBlock) void k_rr_hred(const u32* __restrict__ part, int bps, int B, i64 total,
+                                                    u32* __restrict__ hist) {
+  const i64 i = i64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= total) return;
+  const i64 s = i / B, b = i % B;
+  const u32* p = part + (s * bps) * B + b;
+  u32 sum = 0;
+  for (int k = 0; k < bps; ++k) sum += p[i64(k) * B];
+  hist[i] = sum;
 }
 
 // Per-block partials of a row-path partition (no same-address atomics across blocks): the
@@ -1313,6 +1328,13 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
     off_midc_ = take(lfin_ > 0 ? nn * 8 : 8);
   }
   off_hist_ = take(size_t(max_hist) * 4);
+  {  // the row path's per-block histogram partials
+    i64 hp = 1;
+    if (rows_)
+      for (const RefLevel& p : plan_)
+        if (p.hbps > 1) hp = std::max(hp, p.segs * p.hbps * p.bins);
+    off_hpart_ = take(size_t(hp) * 4);
+  }
   off_segs_ = take(2 * size_t(max_segs) * sizeof(RefSeg));
   off_words_ = take(16);  // [0] ties, [1] error
   ws_bytes_ = off;
@@ -1359,16 +1381,19 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
       const int S = int(p.segs);
       RefSeg* sg = segs[l & 1];
       RefSeg* nsg = l + 1 < lfin_ ? segs[(l + 1) & 1] : nullptr;
-      // the next level's descriptors (its key ranges are filled by this level's moves) and this
-      // level's histogram, zeroed
-      if (nsg) seg_init(nsg, plan_[size_t(l + 1)], l + 1, p.segs * p.bins);
-      else {
-        k_ref_seg_init<<<int(std::min<i64>(1024, (p.segs * p.bins + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(
-            nullptr, 0, n_, l, hist, p.segs * p.bins);
-        PKD_LAUNCH_CHECK();
-      }
+      // the next level's descriptors (its key ranges are filled by this level's moves); this
+      // level's histogram is stored whole below (no zeroing)
+      if (nsg) seg_init(nsg, plan_[size_t(l + 1)], l + 1, 0);
       ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_hist), p.bins * 4);
-      k_rr_hist<<<S * p.hbps, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, p.hbps, p.bins, hist);
+      if (p.hbps == 1) {
+        k_rr_hist<<<S, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, 1, p.bins, hist);
+      } else {
+        u32* hpart = reinterpret_cast<u32*>(ws + off_hpart_);
+        k_rr_hist<<<S * p.hbps, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, p.hbps, p.bins, hpart);
+        PKD_LAUNCH_CHECK();
+        const i64 tot = p.segs * p.bins;
+        k_rr_hred<<<int((tot + kBlock - 1) / kBlock), kBlock, 0, stream>>>(hpart, p.hbps, p.bins, tot, hist);
+      }
       PKD_LAUNCH_CHECK();
       k_ref_select<<<S, kBlock, 0, stream>>>(sg, p.bins, hist, words + 1);
       PKD_LAUNCH_CHECK();

@@ -37,7 +37,7 @@ class ReferenceBuilder {
   bool rows_ = false;  // dim <= 8: rows move as SoA columns (else a permutation, keys gathered)
   std::vector<RefLevel> plan_;
   size_t off_perm_[2] = {0, 0}, off_keys_ = 0, off_midc_ = 0, off_hist_ = 0, off_segs_ = 0, off_words_ = 0,
-         ws_bytes_ = 0;
+         off_hpart_ = 0, ws_bytes_ = 0;
 };
 
 }  // namespace pkdtree

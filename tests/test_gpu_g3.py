@@ -158,3 +158,15 @@ def test_g3_default_40m_equals_unsampled(gpu_device):
     torch.cuda.synchronize()
     assert b.read_error() == 0 and b0.read_error() == 0
     assert torch.equal(ti, ti0) and torch.equal(tp, tp0)
+
+
+@pytest.mark.parametrize("multi", ["1", "1024"])
+def test_g3_across_second_stage_levels(gpu_device, g3_small, monkeypatch, multi):
+    """Levels whose median bucket would take a second-stage histogram (the 1 B build's levels 4-7)
+    still sample their triples: level l's bucket rows are ranked exactly among the staged rows,
+    levels l+1 and l+2 need no histogram at all (PKD_STAGE2_MIN pushes the second stage down to
+    this size)."""
+    monkeypatch.setenv("PKD_STAGE2_MIN", "4")
+    monkeypatch.setenv("PKD_G3_MULTI_BELOW", multi)
+    b = _same_as_cpu(pk.generate_problem(99, 3, 2_000_000), gpu_device)
+    assert " stage2" in b.describe(), b.describe()
