@@ -3759,12 +3759,17 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
   return before + incl - v;
 }
 
-template <int D, int ITEMS, int WPE>
+// SLIM (D >= 3): two key register sets (level 2's keys reuse level 0's, loaded when level 2
+// starts) and no id registers (a row's id is read from its column only where a key equals the
+// pivot key or the row is a median-bin candidate): 32 fewer registers per 16 items, so the
+// 16-item shape of the 1 B build spills 120 instead of 212 bytes per lane (the 12-item one none).
+template <int D, int ITEMS, int WPE, bool SLIM = false>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
-  // columns kept in registers: every column for D < 3, else the three levels' key columns
-  constexpr int KC = D < 3 ? D : 3;
+  static_assert(!SLIM || D >= 3, "slim registers need three distinct level axes");
+  // columns kept in registers: every column for D < 3, else the three levels' key columns (SLIM: two sets)
+  constexpr int KC = D < 3 ? D : (SLIM ? 2 : 3);
   constexpr u32 kDead = 0xffffffffu, kMed = 0x80000000u;  // absent row / median of tail node (low bits)
   static_assert(ITEMS % 4 == 0, "16-B groups of 4 rows");
   static_assert(CAP >= NB, "the stage buffer holds the bins");
@@ -3808,7 +3813,7 @@ void k_tail3(TailArgs a) {
 #pragma unroll
   for (int t = 0; t < 3; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
   float xs[KC][ITEMS];
-  u32 ids[ITEMS];
+  u32 ids[SLIM ? 1 : ITEMS];
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const auto r = col(a.src, D < 3 ? k : axis_of[k]);
@@ -3819,15 +3824,19 @@ void k_tail3(TailArgs a) {
       for (int j = 0; j < 4; ++j) xs[k][4 * g + j] = __uint_as_float(v[j]);
     }
   }
-  {
-    const auto r = col(a.src, D);
+  const auto rid = col(a.src, D);
+  if constexpr (!SLIM) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const auto v = ld4(r, g);
+      const auto v = ld4(rid, g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) ids[4 * g + j] = v[j];
     }
   }
+  auto id_of = [&](int i) -> u32 {  // item i's id: a register, or (SLIM) one dword load
+    if constexpr (SLIM) return __builtin_amdgcn_raw_buffer_load_b32(rid, vo + u32(i % 4) * 4u, u32(i / 4 * T * 16), 0);
+    else return ids[i];
+  };
   if (tid < 15) {  // node k (heap order: 0 = h, 1-2 children, 3-6 grandchildren, 7-14 leaves)
     const int lev = tid >= 7 ? 3 : (tid >= 3 ? 2 : (tid >= 1 ? 1 : 0));
     const i64 hk = (h + 1) * (i64(1) << lev) - 1 + (tid - ((1 << lev) - 1));
@@ -3853,7 +3862,16 @@ void k_tail3(TailArgs a) {
     const int S = 1 << t, B = NB >> t, lgB = 12 - t;
     static_assert(NB == 4096, "lgB");
     const int axis = axis_of[t];
-    const int kx = D < 3 ? axis : t;  // register set of this level's keys
+    const int kx = D < 3 ? axis : (SLIM ? (t & 1) : t);  // register set of this level's keys
+    if (SLIM && t == 2) {  // level 2's keys into level 0's (dead) registers
+      const auto r = col(a.src, axis);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const auto v = ld4(r, g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xs[0][4 * g + j] = __uint_as_float(v[j]);
+      }
+    }
     for (int b = tq; b < NB; b += T) bins[b] = 0;
     if (tq < 4) {
       ccnt[tq] = 0;
@@ -3910,7 +3928,7 @@ void k_tail3(TailArgs a) {
         const u32 k = atomicAdd(&ccnt[sp], 1u);
         if (k < u32(kTailCand)) {
           ckey[sp][k] = orderable(xs[kx][i]);
-          cid[sp][k] = ids[i];
+          cid[sp][k] = id_of(i);
         }
       }
     }
@@ -3944,7 +3962,7 @@ void k_tail3(TailArgs a) {
         for (int i = 0; i < ITEMS; ++i) {
           const u32 sp = path[i] >> lgB;
           if (path[i] < kMed && path[i] == sbst[sp]) {
-            const u64 ck = (u64(orderable(xs[kx][i])) << 32) | u64(ids[i]);
+            const u64 ck = (u64(orderable(xs[kx][i])) << 32) | u64(id_of(i));
             if (((ck ^ spiv[sp]) & known) == 0) atomicAdd(&bins[sp * 256 + u32((ck >> sh) & 255u)], 1u);
           }
         }
@@ -3983,8 +4001,13 @@ void k_tail3(TailArgs a) {
       if (path[i] >= kMed) continue;
       const u32 sp = path[i] >> lgB;
       const u64 pv = spiv[sp];
-      const u64 ck = (u64(orderable(xs[kx][i])) << 32) | u64(ids[i]);
-      path[i] = ck == pv ? (kMed | u32(S - 1 + sp)) : 2 * sp + (ck > pv ? 1u : 0u);
+      const u32 ok = orderable(xs[kx][i]), pk = u32(pv >> 32);
+      if (ok != pk) {  // the key decides (the id is read only on a key tie with the pivot)
+        path[i] = 2 * sp + (ok > pk ? 1u : 0u);
+      } else {
+        const u64 ck = (u64(ok) << 32) | u64(id_of(i));
+        path[i] = ck == pv ? (kMed | u32(S - 1 + sp)) : 2 * sp + (ck > pv ? 1u : 0u);
+      }
     }
     if (tq < 2 * S) {  // children cells: the pivot key bounds the split axis
       const int sp = tq / 2, side = tq & 1;
@@ -4016,9 +4039,10 @@ void k_tail3(TailArgs a) {
   const int grp = tid / 16;
   if (tid < kGroups * 8) gcnt[tid] = 0;
   __syncthreads();
-  u32 pos[ITEMS];
+  // (leaf << 24) | rank among the 16-lane group's rows of that leaf, in place of the leaf index
 #pragma unroll
-  for (int i = 0; i < ITEMS; ++i) pos[i] = path[i] < kMed ? atomicAdd(&gcnt[grp * 8 + path[i]], 1u) : 0u;
+  for (int i = 0; i < ITEMS; ++i)
+    if (path[i] < kMed) path[i] = (path[i] << 24) | atomicAdd(&gcnt[grp * 8 + path[i]], 1u);
   __syncthreads();
   if (tid < 8) {
     const u32 first = u32(nlo[7 + tid] - lo);
@@ -4032,20 +4056,20 @@ void k_tail3(TailArgs a) {
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i)
-    if (path[i] < kMed) path[i] = pos[i] + gbase[grp][path[i]];
+    if (path[i] < kMed) path[i] = (path[i] & 0xffffffu) + gbase[grp][path[i] >> 24];
   tail_stamp(a, 13);
 #pragma unroll
   for (int c = 0; c <= D; ++c) {
     // column c: from registers (a level's keys or the ids), else loaded
     int kreg = -1;
 #pragma unroll
-    for (int k = 0; k < KC; ++k)
-      if ((D < 3 ? k : axis_of[k]) == c) kreg = k;
+    for (int k = 0; k < KC; ++k)  // (SLIM: set 0 holds level 2's keys by now, set 1 level 1's)
+      if ((D < 3 ? k : (SLIM ? axis_of[k == 0 ? 2 : 1] : axis_of[k])) == c) kreg = k;
     u32 v[ITEMS];
-    if (c == D) {
+    if (c == D && !SLIM) {
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) v[i] = ids[i];
-    } else if (kreg >= 0) {
+      for (int i = 0; i < ITEMS; ++i) v[i] = ids[SLIM ? 0 : i];
+    } else if (kreg >= 0 && c < D) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         u32 x = 0;
@@ -4228,6 +4252,7 @@ Tuning Tuning::from_env() {
   t.g3_multi_below = std::max<i64>(1, ab_i("PKD_G3_MULTI_BELOW", t.g3_multi_below));
   t.g3_sample_blocks = std::max<i64>(1, ab_i("PKD_G3_SAMPLE_BLOCKS", t.g3_sample_blocks));
   t.g3_min_n = std::max<i64>(0, ab_i("PKD_G3_MIN_N", t.g3_min_n));
+  t.tail_slim12 = ab_i("PKD_TAIL_SLIM12", t.tail_slim12 ? 1 : 0) != 0;
   t.g3_max_dim = int(ab_i("PKD_G3_MAX_DIM", t.g3_max_dim));
   if (const char* z = ab_knob("PKD_G3_Z")) t.g3_z = float(std::atof(z));
   return t;
@@ -5058,9 +5083,17 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           };
           // one 1024-thread workgroup per CU (128 registers): the two-per-CU shape (64 registers)
           // spills and was slower (100M x 3D k_tail3 1.41 vs 1.32 ms, profiles/r3_tail.txt)
-          if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
-          else if (tail_items_ == 12) go(&k_tail3<D, 12, 4>);
-          else go(&k_tail3<D, 16, 4>);
+          // (16 items: two key sets and ids on demand, else the 128 registers spill)
+          if constexpr (D >= 3) {
+            if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
+            else if (tail_items_ == 12 && !tune_.tail_slim12) go(&k_tail3<D, 12, 4>);
+            else if (tail_items_ == 12) go(&k_tail3<D, 12, 4, true>);
+            else go(&k_tail3<D, 16, 4, true>);
+          } else {
+            if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
+            else if (tail_items_ == 12) go(&k_tail3<D, 12, 4>);
+            else go(&k_tail3<D, 16, 4>);
+          }
         }
       });
       PKD_LAUNCH_CHECK();

@@ -218,14 +218,34 @@ __device__ __forceinline__ u32 wave_find(const u32* h, int B, u32 rank, u32* bel
 
 // One workgroup per segment: the buckets of ranks m - 1 and m (every thread sums B / 256
 // consecutive buckets, one block scan, the owning threads walk their buckets).
-__global__ __launch_bounds__(kBlock) void k_ref_select(RefSeg* __restrict__ seg, int B, const u32* __restrict__ hist,
-                                                       u32* __restrict__ err) {
-  __shared__ u32 wsum[kBlock / 64];
-  const i64 s = blockIdx.x;
-  const RefSeg r = seg[s];
-  if (r.n < 3) return;  // (global segments always hold more than kFinCap rows)
+// The next level's descriptors of segment s's children (geometry, cleared cursors and ranges):
+// written for every segment of a level, so no separate initialisation launch is needed (the
+// children's key ranges are filled in by this level's refine).
+__device__ __forceinline__ void ref_children_init(RefSeg* __restrict__ nsg, i64 s, const RefSeg& r) {
+  if (nsg == nullptr || threadIdx.x != 0) return;
   const u32 m = r.n / 2;
-  const u32* h = hist + s * i64(B);
+  RefSeg c{};
+  c.kmin = 0xffffffffu;
+  c.kmax = 0u;
+  c.left_max = 0ull;
+  c.right_min = ~0ull;
+  c.lo = r.lo;
+  c.n = m;
+  nsg[2 * s] = c;
+  c.lo = r.lo + m + 1;
+  c.n = r.n > m ? r.n - m - 1 : 0u;
+  nsg[2 * s + 1] = c;
+}
+
+// The buckets of ranks m - 1 and m of segment s from its histogram h (global, or the LDS of the
+// histogram block itself): every thread sums B / 256 consecutive buckets, one block scan, the
+// owning threads walk their buckets. All threads of the block call it.
+__device__ __forceinline__ void ref_select_body(RefSeg* __restrict__ seg, i64 s, const RefSeg& r, int B, const u32* h,
+                                                u32* __restrict__ err) {
+  __shared__ u32 wsum[kBlock / 64];
+  __shared__ u32 res[4];  // b1, L, b2, rows up to the end of b2
+  if (r.n < 3) return;    // (uniform: every thread holds the same r)
+  const u32 m = r.n / 2;
   const int per = B >= kBlock ? B / kBlock : 1;
   const int t = threadIdx.x, b0 = t * per;
   u32 c = 0;
@@ -236,7 +256,6 @@ __global__ __launch_bounds__(kBlock) void k_ref_select(RefSeg* __restrict__ seg,
   __syncthreads();
   u32 ex = incl - c;
   for (int w = 0; w < t / 64; ++w) ex += wsum[w];
-  __shared__ u32 res[4];  // b1, L, b2, rows up to the end of b2
   if (t < 4) res[t] = 0xffffffffu;
   __syncthreads();
   for (int q = 0; q < 2; ++q) {
@@ -260,6 +279,16 @@ __global__ __launch_bounds__(kBlock) void k_ref_select(RefSeg* __restrict__ seg,
     seg[s].b2 = res[2];
     seg[s].M = res[3] - res[1];
   }
+}
+
+// One workgroup per segment: the buckets of ranks m - 1 and m (and, nsg != nullptr, the next
+// level's descriptors).
+__global__ __launch_bounds__(kBlock) void k_ref_select(RefSeg* __restrict__ seg, int B, const u32* __restrict__ hist,
+                                                       u32* __restrict__ err, RefSeg* __restrict__ nsg) {
+  const i64 s = blockIdx.x;
+  const RefSeg r = seg[s];
+  ref_children_init(nsg, s, r);
+  ref_select_body(seg, s, r, B, hist + s * i64(B), err);
 }
 
 // Every sortable row once: zone 0 (bucket < b1) -> [lo, lo + L), zone 1 -> [lo + L, lo + L + M)
@@ -715,8 +744,9 @@ __global__ __launch_bounds__(kBlock) void k_rr_prep(const float* __restrict__ pt
 // coalesced) -- straight into the segment's histogram when the segment has one block, else into
 // per-block partials that k_rr_hred sums. (Flushing with global atomics cost ~4 M atomics a level:
 // 256 blocks x 16 Ki bins; 30 us of a 10 M level's 36.)
-__global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const RefSeg* __restrict__ seg, int bps,
-                                                    int B, u32* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, RefSeg* __restrict__ seg, int bps,
+                                                    int B, u32* __restrict__ out, u32* __restrict__ err,
+                                                    RefSeg* __restrict__ nsg, int fuse_select) {
   extern __shared__ u32 h[];
   const i64 s = blockIdx.x / bps;
   const int part = blockIdx.x % bps;
@@ -742,6 +772,11 @@ __global__ __launch_bounds__(kBlock) void k_rr_hist(RowCols src, int axis, const
     }
   }
   __syncthreads();
+  if (fuse_select) {  // (bps == 1) the block holds its segment's whole histogram: select right here
+    ref_children_init(nsg, s, r);
+    ref_select_body(seg, s, r, B, h, err);
+    return;
+  }
   u32* o = out + i64(blockIdx.x) * B;  // (block = segment when bps == 1)
   for (int b = threadIdx.x; b < B; b += kBlock) o[b] = h[b];
 }
@@ -1381,22 +1416,23 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
       const int S = int(p.segs);
       RefSeg* sg = segs[l & 1];
       RefSeg* nsg = l + 1 < lfin_ ? segs[(l + 1) & 1] : nullptr;
-      // the next level's descriptors (its key ranges are filled by this level's moves); this
-      // level's histogram is stored whole below (no zeroing)
-      if (nsg) seg_init(nsg, plan_[size_t(l + 1)], l + 1, 0);
+      // this level's histogram (stored whole: no zeroing), the buckets of ranks m - 1 and m, and
+      // the next level's descriptors (their key ranges are filled in by this level's refine)
       ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_hist), p.bins * 4);
-      if (p.hbps == 1) {
-        k_rr_hist<<<S, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, 1, p.bins, hist);
+      if (p.hbps == 1) {  // one block per segment: the select runs in the histogram block
+        k_rr_hist<<<S, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, 1, p.bins, hist, words + 1, nsg, 1);
+        PKD_LAUNCH_CHECK();
       } else {
         u32* hpart = reinterpret_cast<u32*>(ws + off_hpart_);
-        k_rr_hist<<<S * p.hbps, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, p.hbps, p.bins, hpart);
+        k_rr_hist<<<S * p.hbps, kBlock, size_t(p.bins) * 4, stream>>>(cols[cur], axis, sg, p.hbps, p.bins, hpart,
+                                                                      words + 1, nsg, 0);
         PKD_LAUNCH_CHECK();
         const i64 tot = p.segs * p.bins;
         k_rr_hred<<<int((tot + kBlock - 1) / kBlock), kBlock, 0, stream>>>(hpart, p.hbps, p.bins, tot, hist);
+        PKD_LAUNCH_CHECK();
+        k_ref_select<<<S, kBlock, 0, stream>>>(sg, p.bins, hist, words + 1, nsg);
+        PKD_LAUNCH_CHECK();
       }
-      PKD_LAUNCH_CHECK();
-      k_ref_select<<<S, kBlock, 0, stream>>>(sg, p.bins, hist, words + 1);
-      PKD_LAUNCH_CHECK();
       switch (NC) {
 #define PKD_RR(N) \
   case N: k_rr_part<N><<<S * p.bps, kBlock, 0, stream>>>(cols[cur], cols[cur ^ 1], axis, naxis, sg, p.bps, p.bins, partials); break;
@@ -1442,7 +1478,7 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
     PKD_LAUNCH_CHECK();
     k_ref_hist<<<grid, kBlock, size_t(p.bins) * 4, stream>>>(keys, segs[0], p.bps, p.bins, hist);
     PKD_LAUNCH_CHECK();
-    k_ref_select<<<S, kBlock, 0, stream>>>(segs[0], p.bins, hist, words + 1);
+    k_ref_select<<<S, kBlock, 0, stream>>>(segs[0], p.bins, hist, words + 1, nullptr);
     PKD_LAUNCH_CHECK();
     k_ref_part<<<grid, kBlock, 0, stream>>>(keys, perm[cur], perm[cur ^ 1], midc, segs[0], p.bps, p.bins);
     PKD_LAUNCH_CHECK();

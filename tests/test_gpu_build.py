@@ -10,8 +10,8 @@ from parallel_kd_tree_amd import ops
 pytestmark = pytest.mark.gpu
 
 
-def check_same(x, dev, depth0=0, subtree_max=0):
-    b = ops.GpuTreeBuilder(x.shape[0], x.shape[1], depth0, subtree_max)
+def check_same(x, dev, depth0=0, subtree_max=0, allow_top=True):
+    b = ops.GpuTreeBuilder(x.shape[0], x.shape[1], depth0, subtree_max, allow_top=allow_top)
     tp, ti = b.build(x.to(dev))
     cp, ci = ops.build_cpu(x, None, "exact", depth0, 8)
     torch.cuda.synchronize()
@@ -79,14 +79,17 @@ def test_subtree_capacity_1536(gpu_device, n):
         check_same(pk.generate_problem(n % 89, 3, n), gpu_device, depth0=1)
 
 
+@pytest.mark.parametrize("slim12", ["0", "1"])
 @pytest.mark.parametrize("n,dim", [(40_000, 3), (70_000, 3), (100_000, 3), (200_000, 1), (150_000, 2), (120_000, 5),
                                    (60_000, 8)])
-def test_tail_levels(gpu_device, monkeypatch, n, dim):
+def test_tail_levels(gpu_device, monkeypatch, n, dim, slim12):
     """The last three global levels in one workgroup per segment (k_tail3: bucket bins, wave
     ranking of the median bin or the radix-select fallback for heavy duplicates, LDS-staged
-    leaf scatter): slot for slot the CPU exact tree."""
+    leaf scatter): slot for slot the CPU exact tree. 16-item shapes (100 k at 3-D) and, with
+    PKD_TAIL_SLIM12, the 12-item shapes run with two key register sets and ids read on demand."""
     monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TAIL", "1")
+    monkeypatch.setenv("PKD_TAIL_SLIM12", slim12)
     b = ops.GpuTreeBuilder(n, dim)
     assert "tail" in b.describe(), b.describe()
     check_same(pk.generate_problem(n % 101, dim, n), gpu_device)
@@ -171,7 +174,25 @@ def test_large_stage2_pairs_prefix_placement(gpu_device, monkeypatch, prefix):
     monkeypatch.setenv("PKD_PART_PREFIX", prefix)
     x = pk.generate_problem(6, 3, 18_000_000)
     x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
-    check_same(x, gpu_device)
+    check_same(x, gpu_device, allow_top=False)  # (the paired levels from level 0)
+    _check_sampled_or_rebuilt(x, gpu_device)
+
+
+def _check_sampled_or_rebuilt(x, dev):
+    """The default (sampled-top) build of duplicate-heavy data either succeeds exactly or reports
+    the band miss (a staging arena too large to stream); the checked entry point is exact."""
+    b = ops.GpuTreeBuilder(x.shape[0], x.shape[1], 0, 0)
+    tp, ti = b.build(x.to(dev))
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    torch.cuda.synchronize()
+    err = b.read_error()
+    if err == 0:
+        assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+    else:
+        assert b.sampled and err & ops.GpuTreeBuilder.TOP_BAND_MISS, (err, b.describe())
+    tp2, ti2, _ = ops.build_gpu_checked(x.to(dev), None, 0, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(ti2.cpu(), ci) and torch.equal(tp2.cpu(), cp)
 
 
 @pytest.mark.parametrize("n,dim,depth0", [(1, 3, 0), (1000, 3, 0), (200_000, 3, 0), (100_000, 5, 2), (30_000, 8, 0)])
@@ -272,7 +293,8 @@ def test_split_build_stage2_skewed(gpu_device, monkeypatch):
     monkeypatch.setenv("PKD_SPLIT_MIN_N", "0")
     x = pk.generate_problem(6, 3, 18_000_000)
     x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
-    check_same(x, gpu_device)
+    check_same(x, gpu_device, allow_top=False)
+    _check_sampled_or_rebuilt(x, gpu_device)
 
 
 def test_split_build_hipgraph(gpu_device, monkeypatch):
