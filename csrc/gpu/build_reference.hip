@@ -36,7 +36,9 @@
 // tree is then the (key, row)-ordered one, which may differ from the binary's, and callers fall
 // back to the CPU std::sort builder (kdtree_gpu / kdtree_dist --mode reference, KDTree.build).
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "device_utils.hpp"
 #include "pkdtree/gpu_reference.hpp"
@@ -1313,6 +1315,291 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim,
   }
 }
 
+// Row-path LDS finish by rank propagation (the default; k_rr_finish above moves rows instead):
+// rows never move. Every level ranks each live row among its sub-segment's sortable rows on
+// the level's axis, and the rank alone decides median / left / right, as in the exact builder's
+// subtree kernel (build_subtree.hip), with the reference's rules (kdtree_sequential.cpp:46-56):
+// a sub-segment's DESIGNATED row (the one in its last slot: the input's last row, or the left
+// maximum the parent put there) is not ranked and passes to the right child, which keeps it in
+// its last slot; the rank m - 1 row becomes the left child's designated row. A designated row
+// stays designated, so every row that is ranked again was ranked at the axis's previous use too.
+//   * first use of an axis in the finish: value-linear buckets over the segment's range on
+//     the axis, one block scan, bucket-ordered keys, exact (key, row) comparisons in a bucket;
+//   * later uses: every ranked row keeps its rank relative to the child it went to (cr, in
+//     registers); the ranks of a sub-segment's sortable rows are then distinct and ordered
+//     like their keys, so the rank is a popcount prefix over one bitmap per sub-segment
+//     (one atomicOr, a wave scan of word popcounts, one read) -- 3 barriers instead of 6.
+// Deciding ties: the rows of ranks m - 2 .. m + 1 leave their keys at their sorted slots; the
+// median row compares them after the level's closing barrier (the checks k_rr_finish makes).
+template <int D>
+__global__ __launch_bounds__(kFinThreads) void k_rr_finish_rank(RowCols src, int depth0, i64 n_total, int lf,
+                                                                int levels, const u32* __restrict__ ids, u32 id_base,
+                                                                float* __restrict__ out_pts, u32* __restrict__ out_ids,
+                                                                u32* __restrict__ words) {
+  constexpr int T = kFinThreads, I = kFinItems, CAP = kFinCap, NC = D + 1;
+  constexpr int kBm = 1024;  // bitmap words of a compressed level (S * Wt above: first-use path)
+  extern __shared__ float X[];  // [NC][CAP]
+  __shared__ u32 H[CAP + 1 + 64];
+  __shared__ u32 bm[2][kBm + 64];
+  __shared__ u32 tk[CAP + 64], K[CAP + 64];
+  __shared__ unsigned short tp[CAP + 64], fin[CAP + 64];
+  __shared__ u32 wsum[T / 64];
+  __shared__ u32 rng[D][2];
+  u32* ties = words;
+  i64 lo64 = 0, m64 = 0;
+  seg_geometry(n_total, lf, blockIdx.x, &lo64, &m64);
+  if (m64 <= 0) return;
+  const int M = int(m64);
+  const u32 glo = u32(lo64);
+  const int tid = threadIdx.x, ln = dev::lane();
+  const u32 dmy = u32(CAP) + u32(ln);  // per-lane dummy word of the H / tk / K / fin arrays
+  for (int c = 0; c < NC; ++c)
+    for (int p = tid; p < M; p += T) X[c * CAP + p] = src.at(c, glo + u32(p));
+  if (tid < D) {
+    rng[tid][0] = 0xffffffffu;
+    rng[tid][1] = 0u;
+  }
+  for (int w = tid; w < CAP + 1 + 64; w += T) H[w] = 0u;
+  for (int w = tid; w < 2 * (kBm + 64); w += T) (&bm[0][0])[w] = 0u;
+  __syncthreads();
+  {  // the segment's key range per axis: the first-use buckets' range
+    u32 mn[D], mx[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      mn[c] = 0xffffffffu;
+      mx[c] = 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int p = tid + i * T;
+      if (p < M)
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          const u32 k = orderable(X[c * CAP + p]);
+          mn[c] = min(mn[c], k);
+          mx[c] = max(mx[c], k);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const u32 a = dev::wave_min_u32(mn[c]), b = dev::wave_max_u32(mx[c]);
+      if (ln == 0 && a <= b) {
+        atomicMin(&rng[c][0], a);
+        atomicMax(&rng[c][1], b);
+      }
+    }
+  }
+  u32 lo[I], nn[I], sg[I], cr[I][D];
+  bool des[I], live[I], tchk[I];
+  u32 tlo[I], tn[I];
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const int p = tid + i * T;
+    live[i] = p < M;
+    des[i] = p == M - 1;
+    lo[i] = 0u;
+    nn[i] = u32(M);
+    sg[i] = 0u;
+    tchk[i] = false;
+    tlo[i] = tn[i] = 0u;
+#pragma unroll
+    for (int c = 0; c < D; ++c) cr[i][c] = 0u;
+  }
+  __syncthreads();
+  int cb = 0;
+  for (int l = lf; l < levels; ++l) {
+    const int t = l - lf, a = (depth0 + l) % D, S = 1 << t;
+    // the previous level's deciding-tie checks (its keys were written before its closing barrier)
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      if (!tchk[i]) continue;
+      tchk[i] = false;
+      const u32 m = tn[i] / 2;
+      const u32* kk = K + tlo[i];
+      bool tie = kk[m - 1] == kk[m];
+      if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
+      if (m + 1 <= tn[i] - 2 && kk[m] == kk[m + 1]) tie = true;
+      if (tie) atomicAdd(ties, 1u);
+    }
+    // rows of sub-segments of <= 2 rows are final (2: the designated row keeps the last slot)
+    bool srt[I];
+    u32 key[I], rank[I];
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int p = tid + i * T;
+      if (live[i] && nn[i] <= 2u) {
+        fin[lo[i] + ((nn[i] == 2u && des[i]) ? 1u : 0u)] = (unsigned short)p;
+        live[i] = false;
+      }
+      srt[i] = live[i] && !des[i];
+      key[i] = srt[i] ? orderable(X[a * CAP + (srt[i] ? p : 0)]) : 0u;
+      rank[i] = 0u;
+    }
+    int Wt = 0;
+    if (t >= D) {  // the axis was ranked at level t - D: child-relative ranks < M >> (t - D + 1)
+      const u32 bits = u32(M) >> (t - D + 1);
+      u32 w = (bits + 31u) / 32u;
+      w = w <= 1u ? 1u : 1u << (32 - __clz(w - 1u));
+      if (w <= 64u && u32(S) * w <= u32(kBm)) Wt = int(w);
+    }
+    if (Wt > 0) {
+      // ---- compressed: one bitmap of Wt words per sub-segment ----
+      u32* b = bm[cb];
+      u32 wi[I], c[I];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        u32 v = 0u;
+#pragma unroll
+        for (int q = 0; q < D; ++q) v = q == a ? cr[i][q] : v;
+        c[i] = v;
+        wi[i] = srt[i] ? sg[i] * u32(Wt) + (v >> 5) : u32(kBm) + u32(ln);
+        if (srt[i]) atomicOr(&b[wi[i]], 1u << (v & 31u));
+      }
+      __syncthreads();
+      for (int w = tid; w < kBm; w += T) bm[cb ^ 1][w] = 0u;  // the next compressed level's bitmaps
+      const int nw = S * Wt;
+      if (Wt > 1) {  // exclusive popcount prefix inside each group of Wt words (one wave holds a group)
+        const u32 g = u32(ln) & u32(Wt - 1);
+        for (int w0 = 0; w0 < nw; w0 += T) {
+          const int w = w0 + tid;
+          const bool in = w < nw;
+          const u32 v = in ? u32(__popc(b[w])) : 0u;
+          u32 incl = v;
+          for (int o = 1; o < Wt; o <<= 1) {
+            const u32 tt = __shfl_up(incl, o, 64);
+            incl += g >= u32(o) ? tt : 0u;
+          }
+          tk[in ? u32(w) : dmy] = incl - v;
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+        if (srt[i]) rank[i] = (Wt > 1 ? tk[wi[i]] : 0u) + u32(__popc(b[wi[i]] & ((1u << (c[i] & 31u)) - 1u)));
+      cb ^= 1;
+    } else {
+      // ---- first use: value-linear buckets over the segment's range ----
+      const int maxsz = M >> t;
+      const int B = maxsz > 16 ? max(1, min(int(1u << (32 - __clz(u32(maxsz) - 1u))), CAP >> t)) : 1;
+      const int nb = S * B;  // <= CAP; H[nb] = total after the scan
+      const RefBk sc = ref_scale(rng[a][0], rng[a][1], u32(B));
+      u32 bk[I], wi[I];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        bk[i] = srt[i] ? sg[i] * u32(B) + (B > 1 ? ref_bucket_s(key[i], sc, u32(B)) : 0u) : dmy + 1u;
+        wi[i] = atomicAdd(&H[bk[i]], 1u);
+      }
+      __syncthreads();
+      {  // exclusive scan of H[0, nb): thread t owns H[t * I, + I)
+        const int b0 = tid * I;
+        u32 x[I], sum = 0;
+#pragma unroll
+        for (int j = 0; j < I; ++j) {
+          x[j] = b0 + j < nb ? H[b0 + j] : 0u;
+          sum += x[j];
+        }
+        const u32 incl = dev::wave_incl_scan(sum);
+        if (ln == 63) wsum[tid / 64] = incl;
+        __syncthreads();
+        const u32 ws = wsum[ln & (T / 64 - 1)];
+        const u32 pin = dev::wave_incl_scan(ln < T / 64 ? ws : 0u);
+        const int wu = __builtin_amdgcn_readfirstlane(tid / 64);
+        const u32 pl = u32(__builtin_amdgcn_readlane(int(pin), wu > 0 ? wu - 1 : 0));
+        u32 run = (wu > 0 ? pl : 0u) + incl - sum;
+#pragma unroll
+        for (int j = 0; j < I; ++j) {
+          if (b0 + j < nb) H[b0 + j] = run;
+          run += x[j];
+        }
+        if (tid == T - 1) H[nb] = run;
+      }
+      __syncthreads();
+      u32 st[I], cnt[I];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int p = tid + i * T;
+        st[i] = cnt[i] = 0u;
+        if (srt[i]) {
+          st[i] = H[bk[i]];
+          cnt[i] = H[bk[i] + 1] - st[i];
+          rank[i] = st[i] - H[sg[i] * u32(B)];
+          tk[st[i] + wi[i]] = key[i];
+          tp[st[i] + wi[i]] = (unsigned short)p;
+        }
+      }
+      __syncthreads();
+      for (int w = tid; w <= nb; w += T) H[w] = 0u;  // (every read of H is behind the barrier)
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int p = tid + i * T;
+        for (u32 j = 0; j < cnt[i]; ++j) {
+          const u32 q = st[i] + j;
+          const u32 kq = tk[q];
+          rank[i] += (kq < key[i] || (kq == key[i] && int(tp[q]) < p)) ? 1u : 0u;
+        }
+      }
+      // tk is read above and rewritten only after the closing barrier (next level)
+    }
+    // ---- median / left / right ----
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      if (!live[i]) continue;
+      const int p = tid + i * T;
+      const u32 m = nn[i] / 2;
+      if (des[i]) {  // to the right child's last slot
+        lo[i] += m + 1;
+        nn[i] -= m + 1;
+        sg[i] = 2 * sg[i] + 1;
+        continue;
+      }
+      const u32 r = rank[i];
+      if (r + 2 >= m && r <= m + 1 && r + 2 <= nn[i]) K[lo[i] + r] = key[i];
+      if (r == m) {
+        fin[lo[i] + m] = (unsigned short)p;
+        live[i] = false;
+        tchk[i] = true;
+        tlo[i] = lo[i];
+        tn[i] = nn[i];
+      } else {
+        const bool right = r > m;
+        const u32 v = right ? r - m - 1 : r;
+#pragma unroll
+        for (int q = 0; q < D; ++q) cr[i][q] = q == a ? v : cr[i][q];
+        des[i] = r + 1 == m;
+        lo[i] += right ? m + 1 : 0u;
+        nn[i] = right ? nn[i] - m - 1 : m;
+        sg[i] = 2 * sg[i] + (right ? 1u : 0u);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const int p = tid + i * T;
+    if (tchk[i]) {
+      const u32 m = tn[i] / 2;
+      const u32* kk = K + tlo[i];
+      bool tie = kk[m - 1] == kk[m];
+      if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
+      if (m + 1 <= tn[i] - 2 && kk[m] == kk[m + 1]) tie = true;
+      if (tie) atomicAdd(ties, 1u);
+    }
+    if (live[i]) {
+      if (nn[i] <= 2u) fin[lo[i] + ((nn[i] == 2u && des[i]) ? 1u : 0u)] = (unsigned short)p;
+      else atomicOr(words + 1, 2u);  // (levels too few for the segment: never with the host's plan)
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < M * D; e += T) {  // rows out: consecutive threads, consecutive floats
+    const int p = e / D, c = e - p * D;
+    out_pts[i64(glo + u32(p)) * D + c] = X[c * CAP + fin[p]];
+  }
+  for (int p = tid; p < M; p += T) {
+    const u32 row = __float_as_uint(X[D * CAP + fin[p]]);
+    out_ids[glo + u32(p)] = ids ? ids[row] : id_base + row;
+  }
+}
+
 size_t align_up(size_t v) { return (v + 255) / 256 * 256; }
 int grid_for(i64 n) { return int(std::min<i64>(8192, std::max<i64>(1, (n + kBlock - 1) / kBlock))); }
 int pow2_floor(i64 v) {
@@ -1326,6 +1613,7 @@ int pow2_floor(i64 v) {
 ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim), depth0_(depth0) {
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
+  if (const char* e = std::getenv("PKD_REF_FIN")) fin_rank_ = std::string(e) != "0";  // A/B: 0 = k_rr_finish
   rows_ = dim <= 8;  // rows move as SoA columns; above, only a permutation (keys gathered per level)
   levels_ = 0;
   while ((n_ >> levels_) >= 2) ++levels_;  // the largest segment of level l has n >> l rows
@@ -1457,9 +1745,22 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
     }
     const i64 segs_f = i64(1) << lfin_;
     const size_t lds = size_t(NC) * kFinCap * 4;
-    ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_finish), int(lds));
-    k_rr_finish<<<int(segs_f), kFinThreads, lds, stream>>>(cols[cur], dim_, depth0_, n_, lfin_, levels_, ids, id_base,
-                                                           out_pts, out_ids, words);
+    if (fin_rank_) {
+      switch (NC) {
+#define PKD_RFR(N)                                                                                                    \
+  case N:                                                                                                             \
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_finish_rank<N - 1>), int(lds));                           \
+    k_rr_finish_rank<N - 1><<<int(segs_f), kFinThreads, lds, stream>>>(cols[cur], depth0_, n_, lfin_, levels_, ids,  \
+                                                                       id_base, out_pts, out_ids, words);            \
+    break;
+        PKD_RFR(2) PKD_RFR(3) PKD_RFR(4) PKD_RFR(5) PKD_RFR(6) PKD_RFR(7) PKD_RFR(8) default: PKD_RFR(9)
+#undef PKD_RFR
+      }
+    } else {
+      ensure_dynamic_lds(reinterpret_cast<const void*>(&k_rr_finish), int(lds));
+      k_rr_finish<<<int(segs_f), kFinThreads, lds, stream>>>(cols[cur], dim_, depth0_, n_, lfin_, levels_, ids,
+                                                             id_base, out_pts, out_ids, words);
+    }
     PKD_LAUNCH_CHECK();
     return;
   }

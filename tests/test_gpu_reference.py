@@ -52,6 +52,28 @@ def test_reference_selection_large_tie_free(gpu_device, n, dim):
     assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
 
 
+@pytest.mark.parametrize("n,dim", [(300_001, 3), (123_457, 2), (200_000, 5), (70_000, 8), (4_099, 1)])
+def test_reference_finish_rank_equals_moving_finish(gpu_device, monkeypatch, n, dim):
+    """The LDS finish by rank propagation (default) builds the tree the row-moving finish
+    (PKD_REF_FIN=0) builds, and the CPU reference's; on tie-heavy data both report ties."""
+    x = tie_free(n, dim, 3 * n + dim)
+    out = {}
+    for fin in ("0", "1"):
+        monkeypatch.setenv("PKD_REF_FIN", fin)
+        b = ops.ReferenceTreeBuilder(n, dim)
+        out[fin] = b.build(x.to(gpu_device), None, 1)
+        assert b.read_ties() == 0
+    cp, ci = ops.build_cpu(x, (torch.arange(n) + 1).to(torch.int32), "reference", 0, 1)
+    for tp, ti in out.values():
+        assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+    y = torch.randint(0, 300, (n, dim), generator=torch.Generator().manual_seed(n)).float()
+    for fin in ("0", "1"):
+        monkeypatch.setenv("PKD_REF_FIN", fin)
+        b = ops.ReferenceTreeBuilder(n, dim)
+        b.build(y.to(gpu_device), None, 1)
+        assert b.read_ties() > 0
+
+
 @pytest.mark.parametrize("n,vals", [(50_000, 7), (200_000, 1000), (3_001, 3)])
 def test_reference_ties_detected_and_rebuilt(gpu_device, n, vals):
     """Heavy duplicates: equal keys decide segments (where std::sort's order is its library's
