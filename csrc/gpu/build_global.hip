@@ -3763,7 +3763,8 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
 // starts) and no id registers (a row's id is read from its column only where a key equals the
 // pivot key or the row is a median-bin candidate): 32 fewer registers per 16 items, so the
 // 16-item shape of the 1 B build spills 120 instead of 212 bytes per lane (the 12-item one none).
-template <int D, int ITEMS, int WPE, bool SLIM = false>
+// IDS: ids in registers (default unless SLIM); SLIM with IDS keeps the two key sets and the ids.
+template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
@@ -3813,7 +3814,7 @@ void k_tail3(TailArgs a) {
 #pragma unroll
   for (int t = 0; t < 3; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
   float xs[KC][ITEMS];
-  u32 ids[SLIM ? 1 : ITEMS];
+  u32 ids[IDS ? ITEMS : 1];
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const auto r = col(a.src, D < 3 ? k : axis_of[k]);
@@ -3825,7 +3826,7 @@ void k_tail3(TailArgs a) {
     }
   }
   const auto rid = col(a.src, D);
-  if constexpr (!SLIM) {
+  if constexpr (IDS) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const auto v = ld4(rid, g);
@@ -3834,7 +3835,7 @@ void k_tail3(TailArgs a) {
     }
   }
   auto id_of = [&](int i) -> u32 {  // item i's id: a register, or (SLIM) one dword load
-    if constexpr (SLIM) return __builtin_amdgcn_raw_buffer_load_b32(rid, vo + u32(i % 4) * 4u, u32(i / 4 * T * 16), 0);
+    if constexpr (!IDS) return __builtin_amdgcn_raw_buffer_load_b32(rid, vo + u32(i % 4) * 4u, u32(i / 4 * T * 16), 0);
     else return ids[i];
   };
   if (tid < 15) {  // node k (heap order: 0 = h, 1-2 children, 3-6 grandchildren, 7-14 leaves)
@@ -4066,9 +4067,9 @@ void k_tail3(TailArgs a) {
     for (int k = 0; k < KC; ++k)  // (SLIM: set 0 holds level 2's keys by now, set 1 level 1's)
       if ((D < 3 ? k : (SLIM ? axis_of[k == 0 ? 2 : 1] : axis_of[k])) == c) kreg = k;
     u32 v[ITEMS];
-    if (c == D && !SLIM) {
+    if (c == D && IDS) {
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) v[i] = ids[SLIM ? 0 : i];
+      for (int i = 0; i < ITEMS; ++i) v[i] = ids[IDS ? i : 0];
     } else if (kreg >= 0 && c < D) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
@@ -4252,7 +4253,7 @@ Tuning Tuning::from_env() {
   t.g3_multi_below = std::max<i64>(1, ab_i("PKD_G3_MULTI_BELOW", t.g3_multi_below));
   t.g3_sample_blocks = std::max<i64>(1, ab_i("PKD_G3_SAMPLE_BLOCKS", t.g3_sample_blocks));
   t.g3_min_n = std::max<i64>(0, ab_i("PKD_G3_MIN_N", t.g3_min_n));
-  t.tail_slim12 = ab_i("PKD_TAIL_SLIM12", t.tail_slim12 ? 1 : 0) != 0;
+  t.tail_slim12 = ab_i("PKD_TAIL_SLIM12", t.tail_slim12);
   t.g3_max_dim = int(ab_i("PKD_G3_MAX_DIM", t.g3_max_dim));
   if (const char* z = ab_knob("PKD_G3_Z")) t.g3_z = float(std::atof(z));
   return t;
@@ -5086,8 +5087,9 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           // (16 items: two key sets and ids on demand, else the 128 registers spill)
           if constexpr (D >= 3) {
             if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
-            else if (tail_items_ == 12 && !tune_.tail_slim12) go(&k_tail3<D, 12, 4>);
-            else if (tail_items_ == 12) go(&k_tail3<D, 12, 4, true>);
+            else if (tail_items_ == 12 && tune_.tail_slim12 == 0) go(&k_tail3<D, 12, 4>);
+            else if (tail_items_ == 12 && tune_.tail_slim12 == 1) go(&k_tail3<D, 12, 4, true>);
+            else if (tail_items_ == 12) go(&k_tail3<D, 12, 4, true, true>);
             else go(&k_tail3<D, 16, 4, true>);
           } else {
             if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);

@@ -57,7 +57,7 @@ struct Tuning {
   int atomic_ranks3 = -1;     //   wave ballots (0); PKD_PART3_ATOMIC the same for triples; -1: by n
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool tail = true;           // PKD_TAIL=0: the last three global levels by pairs / triples instead of k_tail3
-  bool tail_slim12 = false;   // PKD_TAIL_SLIM12=1: the 12-item k_tail3 with the 16-item shape's register diet
+  int tail_slim12 = 0;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids, 1 two key sets (no ids), 2 two key sets + ids
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
   int colgroup = 0;           // PKD_COLGROUP: columns per load round of wide rows (0: by dim)

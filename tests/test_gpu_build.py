@@ -79,7 +79,7 @@ def test_subtree_capacity_1536(gpu_device, n):
         check_same(pk.generate_problem(n % 89, 3, n), gpu_device, depth0=1)
 
 
-@pytest.mark.parametrize("slim12", ["0", "1"])
+@pytest.mark.parametrize("slim12", ["0", "1", "2"])
 @pytest.mark.parametrize("n,dim", [(40_000, 3), (70_000, 3), (100_000, 3), (200_000, 1), (150_000, 2), (120_000, 5),
                                    (60_000, 8)])
 def test_tail_levels(gpu_device, monkeypatch, n, dim, slim12):
