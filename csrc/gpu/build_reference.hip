@@ -682,12 +682,30 @@ __global__ __launch_bounds__(kFinThreads) void k_ref_finish(const float* __restr
   for (int p = tid; p < M; p += kFinThreads) perm[lo + p] = P[cur][p];
 }
 
+// Rows out in slot order: one thread per output ELEMENT (slot p, coordinate c), so a wave reads
+// and writes runs of consecutive floats of a row (a thread per row strode a whole row between
+// lanes: 500 k x 128D 0.82 ms); 4 elements per thread in flight.
 __global__ __launch_bounds__(kBlock) void k_ref_gather(const float* __restrict__ pts, const u32* __restrict__ ids,
                                                        u32 id_base, int dim, const u32* __restrict__ perm, i64 n,
                                                        float* __restrict__ out_pts, u32* __restrict__ out_ids) {
-  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += i64(gridDim.x) * kBlock) {
+  const i64 total = n * dim, stride = i64(gridDim.x) * kBlock;
+  constexpr int U = 4;
+  for (i64 e0 = i64(blockIdx.x) * kBlock + threadIdx.x; e0 < total; e0 += U * stride) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + u * stride;
+      const i64 p = e / dim, c = e - p * dim;
+      v[u] = e < total ? pts[i64(perm[p]) * dim + c] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const i64 e = e0 + u * stride;
+      if (e < total) out_pts[e] = v[u];
+    }
+  }
+  for (i64 p = i64(blockIdx.x) * kBlock + threadIdx.x; p < n; p += stride) {
     const i64 r = perm[p];
-    for (int c = 0; c < dim; ++c) out_pts[p * dim + c] = pts[r * dim + c];
     out_ids[p] = ids ? ids[r] : id_base + u32(r);
   }
 }
@@ -1792,7 +1810,8 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
     k_ref_finish<<<int(segs_f), kFinThreads, 0, stream>>>(pts, dim_, depth0_, perm[cur], n_, lfin_, levels_, words);
     PKD_LAUNCH_CHECK();
   }
-  k_ref_gather<<<g, kBlock, 0, stream>>>(pts, ids, id_base, dim_, perm[cur], n_, out_pts, out_ids);
+  k_ref_gather<<<int(std::min<i64>(4096, std::max<i64>(1, (n_ * dim_ + 4 * kBlock - 1) / (4 * kBlock)))), kBlock, 0,
+                 stream>>>(pts, ids, id_base, dim_, perm[cur], n_, out_pts, out_ids);
   PKD_LAUNCH_CHECK();
 }
 

@@ -13,6 +13,6 @@ python3 - $OUT/kt_kernel_stats.csv > $OUT/summary.txt <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
-    if "k_ref" in r["Name"] or "k_rr" in r["Name"]:
+    if "k_ref" in r["Name"] or "k_rr" in r["Name"] or "pkdtree" in r["Name"]:
         print(f'{r["Name"][:60]:60s} calls={r["Calls"]:>6s} total_ms/build={float(r["TotalDurationNs"])/6e6:8.3f} avg_us={float(r["AverageNs"])/1e3:8.1f}')
 PY
