@@ -225,27 +225,55 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
   u32* sb = sbox;                                           // [2 * dim]
   float* tile = reinterpret_cast<float*>(sbox + 2 * dim);   // [dim][kPrepRows + 1]
   constexpr int TR = kPrepRows;
+  // dim dividing the block (16, 32, 64, 128, 256): every load of a thread is column tid % dim, so
+  // the box is kept in two registers and reduced once per block (a wave reduction per 64 elements
+  // of the transpose cost more than the copy: 500 k x 128D prep 0.20 ms for 256 MB)
+  const bool regbox = kBlock % dim == 0;
+  u32 bmn = 0xffffffffu, bmx = 0u;
   for (int c = threadIdx.x; c < 2 * dim; c += kBlock) sb[c] = (c < dim) ? 0xffffffffu : 0u;
   const int ln = dev::lane();
   for (i64 r0 = i64(blockIdx.x) * TR; r0 < n; r0 += i64(gridDim.x) * TR) {
     const int rows = int(min<i64>(TR, n - r0));
     __syncthreads();  // previous tile consumed (and sb initialised)
-    for (int k = threadIdx.x; k < rows * dim; k += kBlock) {
-      const int rr = k / dim, c = k - rr * dim;
-      tile[c * (TR + 1) + rr] = pts[(r0 + rr) * rs + c];
+    // the tile's loads in flight together (kU per thread) before their LDS stores
+    constexpr int kU = 16;
+    const int tot = rows * dim;
+    for (int k0 = threadIdx.x; k0 < tot; k0 += kBlock * kU) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int k = k0 + u * kBlock;
+        const int rr = k / dim, c = k - rr * dim;
+        v[u] = k < tot ? pts[(r0 + rr) * rs + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int k = k0 + u * kBlock;
+        const int rr = k / dim, c = k - rr * dim;
+        if (k < tot) {
+          tile[c * (TR + 1) + rr] = v[u];
+          if (regbox) {
+            bmn = min(bmn, orderable(v[u]));
+            bmx = max(bmx, orderable(v[u]));
+          }
+        }
+      }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < dim * TR; k += kBlock) {  // a wave = 64 rows of one column
       const int c = k / TR, rr = k - c * TR;
       const bool ok = rr < rows;
-      const float v = tile[c * (TR + 1) + rr];
       const int oc = out_col(c);
+      if (regbox && oc >= ncol_out) continue;  // (narrow: only the global levels' key columns)
+      const float v = tile[c * (TR + 1) + rr];
       if (ok && oc < ncol_out) cols[i64(oc) * ncol + r0 + rr] = v;
-      const u32 kv = ok ? orderable(v) : 0xffffffffu;
-      const u32 mn = dev::wave_min_u32(kv), mx = dev::wave_max_u32(ok ? orderable(v) : 0u);
-      if (ln == 0) {
-        atomicMin(&sb[c], mn);
-        atomicMax(&sb[dim + c], mx);
+      if (!regbox) {
+        const u32 kv = ok ? orderable(v) : 0xffffffffu;
+        const u32 mn = dev::wave_min_u32(kv), mx = dev::wave_max_u32(ok ? orderable(v) : 0u);
+        if (ln == 0) {
+          atomicMin(&sb[c], mn);
+          atomicMax(&sb[dim + c], mx);
+        }
       }
     }
     for (int rr = threadIdx.x; rr < rows; rr += kBlock) {
@@ -253,6 +281,11 @@ __global__ __launch_bounds__(kBlock) void k_prep_tiled(const float* __restrict__
       idcol[r] = ids_in_row ? __float_as_uint(pts[r * rs + dim]) : (ids ? ids[r] : id_base + u32(r));
       if (narrow) idcol[ncol + r] = u32(r);
     }
+  }
+  if (regbox && bmn <= bmx) {
+    const int c = int(threadIdx.x) % dim;
+    atomicMin(&sb[c], bmn);
+    atomicMax(&sb[dim + c], bmx);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * dim; c += kBlock) bbox[size_t(blockIdx.x) * 2 * dim + c] = sb[c];
@@ -544,6 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
   const u32* hs = a.hist + s * a.bins;
   const int per = (a.bins + kBlock - 1) / kBlock;
   const int b0 = min(a.bins, int(threadIdx.x) * per), b1 = min(a.bins, b0 + per);
+  if (threadIdx.x == 0) found[0] = 0xffffffffu;  // (the scan's barriers order it before the finder)
   u32 sum = 0;
   for (int b = b0; b < b1; ++b) sum += hs[b];
   u32 total;
@@ -563,6 +597,10 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (found[0] == 0xffffffffu) {  // the histogram does not hold the median rank: only after a
+      atomicOr(a.err, 2u);           // reported miss or overflow (rebuilt); empty zones keep the
+      found[0] = found[1] = found[2] = 0u;  // passes inside the segment
+    }
     SegState st;
     st.bstar = found[0];
     st.cnt_less = found[1];
@@ -650,6 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
   const u32 t = u32(n / 2) - st->cnt_less;  // rank inside the median bucket
   const u32* hs = a.hist2 + s * kBins2;
   constexpr int per = kBins2 / kBlock;
+  if (threadIdx.x == 0) found[0] = 0xffffffffu;
   u32 sum = 0;
   for (int b = 0; b < per; ++b) sum += hs[threadIdx.x * per + b];
   u32 total;
@@ -669,6 +708,10 @@ __global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (found[0] == 0xffffffffu) {  // (as in k_select)
+      atomicOr(a.err, 2u);
+      found[0] = found[1] = found[2] = 0u;
+    }
     const u32 cl = st->cnt_less + found[1];
     st->stage2 = 1;
     st->sbstar = found[0];
@@ -966,6 +1009,15 @@ __device__ __forceinline__ void add_next_hist(const LevelArgs& a, i64 s, i64 h, 
 
 // CAP: largest middle zone sorted in LDS (keys + indices in dynamic LDS); larger zones are
 // first narrowed by radix passes over the composite key.
+// A segment's zone counts as the previous pass left them, clamped to the segment: they exceed it
+// only after a reported miss or overflow (a tree that is rebuilt), and the refine / pivot passes
+// then still read and write inside the segment.
+__device__ __forceinline__ void zone_counts(const SegState& st, i64 n, i64* less, i64* mid) {
+  const i64 l = min(i64(st.cnt_less), n);
+  *less = l;
+  *mid = min(i64(st.cnt_mid), n - l);
+}
+
 template <int CAP>
 __device__ __forceinline__ void refine_body(LevelArgs a, i64 bid) {
   extern __shared__ __align__(16) u64 dynk[];
@@ -986,9 +1038,11 @@ __device__ __forceinline__ void refine_body(LevelArgs a, i64 bid) {
   float* __restrict__ alt = const_cast<float*>(a.src);  // dead input buffer: staging area
   const bool fuse = a.next_bins > 0;
   if (a.small_done && st.cnt_mid <= 64) return;
-  i64 zlo = lo + st.cnt_less;
-  i64 zc = st.cnt_mid;
-  i64 t = n / 2 - i64(st.cnt_less);
+  i64 cl = 0, cm = 0;
+  zone_counts(st, n, &cl, &cm);
+  i64 zlo = lo + cl;
+  i64 zc = cm;
+  i64 t = n / 2 - cl;
   auto ckey = [&](i64 p) -> u64 {
     const u32 id = reinterpret_cast<const u32*>(dst)[i64(a.idcol) * nc + p];
     return composite_key(dst[i64(a.kcol) * nc + p], id);
@@ -1045,6 +1099,7 @@ __device__ __forceinline__ void refine_body(LevelArgs a, i64 bid) {
       const int shift = hb >= kRadixBits - 1 ? hb - (kRadixBits - 1) : 0;
       const bool coop = zc <= CAP;  // destinations fit the LDS map: move rows column-major
       for (int b = threadIdx.x; b < kRadixBins; b += kBlock) rh[b] = 0;
+      if (threadIdx.x == 0) info[0] = 0xffffffffu;
       __syncthreads();
       for (i64 e = threadIdx.x; e < zc; e += kBlock)
         atomicAdd(&rh[u32(ckey(zlo + e) >> shift) & (kRadixBins - 1)], 1u);
@@ -1071,6 +1126,10 @@ __device__ __forceinline__ void refine_body(LevelArgs a, i64 bid) {
         __syncthreads();
       }
       const u32 bsel = info[0], cl = info[1], ce = info[2];
+      if (bsel == 0xffffffffu || i64(cl) + ce > zc) {  // rank t not in the zone (only after a reported
+        if (threadIdx.x == 0) atomicOr(a.err, 2u);    // miss): stop inside the segment
+        return;
+      }
       if (threadIdx.x == 0) {
         rh[0] = 0;       // reuse as cursors
         rh[1] = cl;
@@ -1216,9 +1275,11 @@ __device__ __forceinline__ void refine_small_body(LevelArgs a, i64 segs, i64 bid
   const SegState st = a.state[h];
   if (st.cnt_mid > 64) return;
   const i64 lo = a.seg_lo[h];
-  const int zc = int(st.cnt_mid);
-  const int t = int(n / 2 - i64(st.cnt_less));
-  const i64 zlo = lo + st.cnt_less;
+  i64 cl = 0, cm = 0;
+  zone_counts(st, n, &cl, &cm);
+  const int zc = int(cm);
+  const int t = int(n / 2 - cl);
+  const i64 zlo = lo + cl;
   const i64 nc = a.ncol;
   const int l = dev::lane();
   const bool valid = l < zc;
@@ -1476,9 +1537,11 @@ __device__ __forceinline__ void pivot_small_body(LevelArgs a, i64 segs, i64 bid)
   const SegState st = a.state[h];
   if (st.cnt_mid > 64) return;
   const i64 lo = a.seg_lo[h];
-  const int zc = int(st.cnt_mid);
-  const int t = int(n / 2 - i64(st.cnt_less));
-  const i64 zlo = lo + st.cnt_less;
+  i64 cl = 0, cm = 0;
+  zone_counts(st, n, &cl, &cm);
+  const int zc = int(cm);
+  const int t = int(n / 2 - cl);
+  const i64 zlo = lo + cl;
   const i64 nc = a.ncol;
   const int l = dev::lane();
   const bool valid = l < zc;
@@ -1516,8 +1579,10 @@ __device__ __forceinline__ void pivot_body(LevelArgs a, i64 bid) {
   const i64 lo = a.seg_lo[h];
   const i64 nc = a.ncol;
   const float* __restrict__ dst = a.dst;
-  const i64 zlo = lo + st.cnt_less, zc = st.cnt_mid;
-  u64 t = u64(n / 2 - i64(st.cnt_less));
+  i64 cl = 0, zc = 0;
+  zone_counts(st, n, &cl, &zc);
+  const i64 zlo = lo + cl;
+  u64 t = u64(n / 2 - cl);
   auto ckey = [&](i64 p) -> u64 {
     float key = dst[p];
 #pragma unroll
