@@ -1632,23 +1632,25 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
   if (dim <= 0) throw std::invalid_argument("pkdtree: dim must be > 0");
   if (n < 0 || n >= (i64(1) << 32)) throw std::invalid_argument("pkdtree: n must be in [0, 2^32)");
   if (const char* e = std::getenv("PKD_REF_FIN")) fin_rank_ = std::string(e) != "0";  // A/B: 0 = k_rr_finish
+  if (const char* e = std::getenv("PKD_REF_BLOCKS")) part_blocks_ = std::max(64, std::min(16384, std::atoi(e)));
   rows_ = dim <= 8;  // rows move as SoA columns; above, only a permutation (keys gathered per level)
   levels_ = 0;
   while ((n_ >> levels_) >= 2) ++levels_;  // the largest segment of level l has n >> l rows
   lfin_ = 0;  // global levels: while the largest segment exceeds the LDS finish
   while (lfin_ < levels_ && (n_ >> lfin_) > kFinCap) ++lfin_;
-  i64 max_segs = 1, max_hist = 1;
+  i64 max_segs = 1, max_hist = 1, max_parts = 1;
   for (int l = 0; l < lfin_; ++l) {
     RefLevel p;
     p.segs = i64(1) << l;
     // about 8 rows per bucket, so the middle zone (the buckets of ranks m - 1 and m) fits the
     // refine's LDS; the histogram pass runs on 1/8 of the partition's blocks (fewer flushes)
     p.bins = std::max(64, std::min(rows_ ? 16384 : 2048, pow2_floor(std::max<i64>(1, (n_ >> l) / 8))));
-    p.bps = int(std::max<i64>(1, std::min<i64>(2048 / p.segs, ((n_ >> l) + kChunk - 1) / kChunk)));
+    p.bps = int(std::max<i64>(1, std::min<i64>(part_blocks_ / p.segs, ((n_ >> l) + kChunk - 1) / kChunk)));
     p.hbps = int(std::max<i64>(1, std::min<i64>(p.bps, 256 / p.segs)));
     plan_.push_back(p);
     max_segs = std::max(max_segs, p.segs);
     max_hist = std::max(max_hist, p.segs * p.bins);
+    max_parts = std::max(max_parts, p.segs * p.bps);  // partition blocks: one PartPartial each
   }
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -1661,7 +1663,7 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
   if (rows_) {
     off_perm_[0] = take(size_t(dim + 1) * size_t(ncol_) * 4);  // SoA columns (ping)
     off_perm_[1] = take(size_t(dim + 1) * size_t(ncol_) * 4);  // (pong)
-    off_keys_ = take(size_t(std::max<i64>(2048, max_segs)) * sizeof(PartPartial));  // partition partials
+    off_keys_ = take(size_t(std::max<i64>(max_parts, max_segs)) * sizeof(PartPartial));  // partition partials
   } else {
     off_perm_[0] = take(nn * 4);
     off_perm_[1] = take(nn * 4);

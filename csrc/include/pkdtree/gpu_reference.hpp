@@ -35,6 +35,8 @@ class ReferenceBuilder {
   i64 n_, ncol_ = 0;
   int dim_, depth0_, levels_ = 0, lfin_ = 0;
   bool rows_ = false;  // dim <= 8: rows move as SoA columns (else a permutation, keys gathered)
+  int part_blocks_ = 16384;  // PKD_REF_BLOCKS: most blocks of a level's partition pass (one 2048-row chunk per block
+                             // up to 33 M rows: 10 M x 3D 2.76 -> 2.64 ms against 2048 blocks)
   bool fin_rank_ = true;  // row-path LDS finish by rank propagation (PKD_REF_FIN=0: k_rr_finish, rows move)
   std::vector<RefLevel> plan_;
   size_t off_perm_[2] = {0, 0}, off_keys_ = 0, off_midc_ = 0, off_hist_ = 0, off_segs_ = 0, off_words_ = 0,
