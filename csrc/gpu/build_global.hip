@@ -4249,9 +4249,11 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 //   scales with blocks. 100 M x 3D: 9.12-9.18 ms vs 9.24 on 2048 blocks; 12.5 M: 1.427 vs 1.44 on
 //   512 (profiles/r4_scan_grid_ab.txt). Round 2's reading at 100 M, on pairs:
 //   the sweep stays bandwidth-bound (100M x 3D k_scan 1.57 -> 1.51 ms).
-// * level_blocks: two rounds of 4 workgroups per CU for builds >= 64 M points, one round
-//   below: at 12.5 M points (a rank's share of 100 M on 8 GPUs) 1024 blocks build 7% faster
-//   than 2048, 1280 or 768 (profiles/r1_level_blocks_sweep.txt).
+// * level_blocks: four rounds of 4 workgroups per CU for builds >= 64 M points (round 5, with
+//   the sampled triples: 100 M x 3D 8.678 -> 8.641 ms against two rounds, 6144 and 8192 in
+//   between, 16384 slower: profiles/r5_level_blocks.txt), one round below: at 12.5 M points (a
+//   rank's share of 100 M on 8 GPUs) 1024 blocks build 7% faster than 2048, 1280 or 768
+//   (profiles/r1_level_blocks_sweep.txt).
 // * split: from level 2 (a pair boundary), 4 parts on 4 HIP streams for builds of >= 64 M
 //   points (50 M: time-neutral, 25 M: +3%, 12.5 M: +7%; profiles/r2_split_build.txt).
 const char* ab_knob(const char* name) {
@@ -4389,7 +4391,7 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   max_bins_ = 0;
   max_hist_ = 1;
   const i64 level_blocks =
-      tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? kLevelBlocks : kLevelBlocks / 2);
+      tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? 2 * kLevelBlocks : kLevelBlocks / 2);
   scan_div_ = tune_.scan_div > 0 ? tune_.scan_div : int(std::max<i64>(1, level_blocks / (kLevelBlocks / 2)));
   // The level plan: with the sampled top (levels 0..3 by top4::run, pairing from level 4) for the
   // AoS / caller-column entry points, and without it for the entry points that start at level 0
