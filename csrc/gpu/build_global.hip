@@ -4251,7 +4251,8 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 //   the sweep stays bandwidth-bound (100M x 3D k_scan 1.57 -> 1.51 ms).
 // * level_blocks: four rounds of 4 workgroups per CU for builds >= 64 M points (round 5, with
 //   the sampled triples: 100 M x 3D 8.678 -> 8.641 ms against two rounds, 6144 and 8192 in
-//   between, 16384 slower: profiles/r5_level_blocks.txt), one round below: at 12.5 M points (a
+//   between, 16384 slower; 100 M x 8D 20.11 -> 19.79 ms, 1 B neutral: profiles/r5_level_blocks.txt),
+//   one round below: at 12.5 M points (a
 //   rank's share of 100 M on 8 GPUs) 1024 blocks build 7% faster than 2048, 1280 or 768
 //   (profiles/r1_level_blocks_sweep.txt).
 // * split: from level 2 (a pair boundary), 4 parts on 4 HIP streams for builds of >= 64 M
