@@ -4249,7 +4249,8 @@ int global_bins(i64 nmax) { return std::max(32, std::min(kMaxBins, pow2_floor(st
 //   scales with blocks. 100 M x 3D: 9.12-9.18 ms vs 9.24 on 2048 blocks; 12.5 M: 1.427 vs 1.44 on
 //   512 (profiles/r4_scan_grid_ab.txt). Round 2's reading at 100 M, on pairs:
 //   the sweep stays bandwidth-bound (100M x 3D k_scan 1.57 -> 1.51 ms).
-// * level_blocks: four rounds of 4 workgroups per CU for builds >= 64 M points (round 5, with
+// * level_blocks: 4096 blocks from 40 M points, 2048 from 20 M, 1024 below (round 5, 50 M 4.85 ->
+//   4.78 ms, 25 M 2.535 -> 2.51 ms, 12.5 M best at 1024: profiles/r5_level_blocks.txt); before: four rounds of 4 workgroups per CU for builds >= 64 M points (round 5, with
 //   the sampled triples: 100 M x 3D 8.678 -> 8.641 ms against two rounds, 6144 and 8192 in
 //   between, 16384 slower; 100 M x 8D 20.11 -> 19.79 ms, 1 B neutral: profiles/r5_level_blocks.txt),
 //   one round below: at 12.5 M points (a
@@ -4392,7 +4393,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
   max_bins_ = 0;
   max_hist_ = 1;
   const i64 level_blocks =
-      tune_.level_blocks > 0 ? tune_.level_blocks : (n_ >= (i64(64) << 20) ? 2 * kLevelBlocks : kLevelBlocks / 2);
+      tune_.level_blocks > 0 ? tune_.level_blocks
+                             : (n_ >= 40000000 ? 2 * kLevelBlocks : (n_ >= 20000000 ? kLevelBlocks : kLevelBlocks / 2));
   scan_div_ = tune_.scan_div > 0 ? tune_.scan_div : int(std::max<i64>(1, level_blocks / (kLevelBlocks / 2)));
   // The level plan: with the sampled top (levels 0..3 by top4::run, pairing from level 4) for the
   // AoS / caller-column entry points, and without it for the entry points that start at level 0
