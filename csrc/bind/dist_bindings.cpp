@@ -242,8 +242,11 @@ plan_py(const std::vector<int64_t>& counts, int64_t n_total, int64_t P, int64_t 
 // (loopback communicator): rank r holds rows [first_r, first_r + local_r) of `x` (the reference's
 // MPI slicing), ids 1..N. Returns the assembled in-order tree (rank shares + boundary top rows)
 // on the host, the OR of the ranks' error words and the middle-bucket scale they ended at.
+// builds > 1: the same GlobalBuilder builds the input that many times (its leaf builders and their
+// shared workspace reused: a leaf whose sampled bands missed in one build is built again by the
+// same sampled builder in the next); the error words of all builds are OR-ed, the last tree returned.
 std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t, bool> global_loopback(const torch::Tensor& x, int64_t P,
-                                                                                 int64_t k) {
+                                                                                 int64_t k, int64_t builds) {
   TORCH_CHECK(!x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2,
               "x: contiguous float32 [N, dim] host tensor");
   const int64_t N = x.size(0);
@@ -269,9 +272,11 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t, int64_t, bool> global_loopback
         PKD_HIP_CHECK(hipMalloc(&d, size_t(std::max<int64_t>(local, 1)) * dim * 4));
         PKD_HIP_CHECK(hipMemcpy(d, x.data_ptr<float>() + first * dim, size_t(local) * dim * 4, hipMemcpyHostToDevice));
         GlobalBuilder gb(*comms[size_t(r)], N, dim, int(k));
-        gb.build(d, local, u32(first + 1), s);
-        gb.wait(s);
-        ew[size_t(r)] = gb.read_error(s);
+        for (int64_t it = 0; it < std::max<int64_t>(builds, 1); ++it) {
+          gb.build(d, local, u32(first + 1), s);
+          gb.wait(s);
+          ew[size_t(r)] |= gb.read_error(s);
+        }
         scales[size_t(r)] = gb.middle_scale();
         radix[size_t(r)] = gb.radix_mode() ? 1 : 0;
         PKD_HIP_CHECK(hipMemcpy(tp.data_ptr<float>() + gb.slot_lo() * dim, gb.tree_pts(), size_t(gb.n_leaf()) * dim * 4,
@@ -461,6 +466,7 @@ void bind_dist_ops(pybind11::module& m) {
   m.def("global_plan", &plan_py, pybind11::arg("counts"), pybind11::arg("n_total"), pybind11::arg("P"),
         pybind11::arg("k"), pybind11::arg("me"));
   m.def("global_loopback", &global_loopback, pybind11::arg("x"), pybind11::arg("P"), pybind11::arg("k") = -1,
+        pybind11::arg("builds") = 1,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("top_bbox", &bbox);
   m.def("fill_u64_multi", [](const std::vector<std::tuple<torch::Tensor, int64_t, uint64_t>>& segs) {

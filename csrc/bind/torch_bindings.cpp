@@ -192,8 +192,7 @@ std::vector<torch::Tensor> build_cpu(const torch::Tensor& pts, const c10::option
   if (mode == "exact") {
     pk::build_exact_cpu(pts.data_ptr<float>(), idp, n, dim, int(depth0), perm.data(), int(threads));
   } else if (mode == "reference") {
-    TORCH_CHECK(depth0 == 0, "reference mode builds whole trees only");
-    pk::build_reference_cpu(pts.data_ptr<float>(), n, dim, perm.data());
+    pk::build_reference_cpu(pts.data_ptr<float>(), n, dim, perm.data(), int(threads), int(depth0));
   } else {
     TORCH_CHECK(false, "mode must be 'exact' or 'reference'");
   }
@@ -352,6 +351,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(b.ws.defined(), "no build yet");
         return torch::from_blob(const_cast<pk::u32*>(b.b.error_word(b.ws.data_ptr())), {4},
                                 b.ws.options().dtype(torch::kInt32));
+      })
+      .def("accumulate_error", [](Builder& b, torch::Tensor acc) {  // acc: int32 [>= 3] on the build's device
+        TORCH_CHECK(b.ws.defined(), "no build yet");
+        TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == torch::kInt32 && acc.numel() >= 3 && acc.is_contiguous() &&
+                        acc.device() == b.ws.device(), "acc must be a contiguous int32 [>= 3] tensor on the build's device");
+        b.b.accumulate_error(b.ws.data_ptr(), reinterpret_cast<pk::u32*>(acc.data_ptr<int32_t>()),
+                             c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());
       })
       .def("read_error", [](Builder& b) {
         u32 d[3];

@@ -23,7 +23,7 @@ int main(int argc, char** argv) {
   std::vector<float> x = generate_problem(p.seed, p.dim, N + Q);
   std::vector<u32> perm(static_cast<size_t>(N));
   if (o.mode == "reference") {
-    build_reference_cpu(x.data(), N, p.dim, perm.data());
+    build_reference_cpu(x.data(), N, p.dim, perm.data(), o.threads > 0 ? o.threads : 1);
   } else {
     build_exact_cpu(x.data(), nullptr, N, p.dim, 0, perm.data(), o.threads > 0 ? o.threads : 1);
   }

@@ -36,7 +36,7 @@ inline u32 build_reference_checked(const ReferenceBuilder& rb, const float* d_pt
   std::vector<u32> perm(static_cast<size_t>(n)), ids(perm.size()), ti(perm.size());
   PKD_HIP_CHECK(hipMemcpy(h.data(), d_pts, h.size() * 4, hipMemcpyDeviceToHost));
   for (i64 r = 0; r < n; ++r) ids[size_t(r)] = id_base + u32(r);
-  build_reference_cpu(h.data(), n, dim, perm.data());
+  build_reference_cpu(h.data(), n, dim, perm.data(), default_cpu_threads());  // threaded: same tree
   gather_rows(h.data(), ids.data(), perm.data(), n, dim, tp.data(), ti.data());
   PKD_HIP_CHECK(hipMemcpy(d_tree, tp.data(), tp.size() * 4, hipMemcpyHostToDevice));
   PKD_HIP_CHECK(hipMemcpy(d_ids, ti.data(), ti.size() * 4, hipMemcpyHostToDevice));

@@ -41,16 +41,25 @@ void exact_rec(const ExactCtx& c, i64 lo, i64 n, int depth, int spawn_levels) {
   }
 }
 
-void reference_rec(const float* pts, int dim, u32* perm, i64 lo, i64 n, int depth) {
+void reference_rec(const float* pts, int dim, int depth0, u32* perm, i64 lo, i64 n, int depth, int spawn_levels) {
   // Mirrors build_tree_rec (kdtree_sequential.cpp:30-66) on an index array: the sort
-  // range deliberately excludes the last element of the segment.
+  // range deliberately excludes the last element of the segment. After a segment's sort its two
+  // children are disjoint ranges of perm, so they may run on two threads: std::sort is
+  // deterministic for a given input order, so the tree is the same for any thread count (the
+  // critical path drops from the whole O(N log^2 N) build to ~2 N log N: one sort per level).
   while (n > 1) {
-    const int axis = depth % dim;
+    const int axis = (depth0 + depth) % dim;
     std::sort(perm + lo, perm + lo + (n - 1), [&](u32 a, u32 b) {
       return pts[size_t(a) * size_t(dim) + size_t(axis)] < pts[size_t(b) * size_t(dim) + size_t(axis)];
     });
     const i64 nl = left_n(n), nr = right_n(n);
-    reference_rec(pts, dim, perm, lo, nl, depth + 1);
+    if (spawn_levels > 0 && n >= 4096) {
+      std::thread t([=] { reference_rec(pts, dim, depth0, perm, lo, nl, depth + 1, spawn_levels - 1); });
+      reference_rec(pts, dim, depth0, perm, lo + nl + 1, nr, depth + 1, spawn_levels - 1);
+      t.join();
+      return;
+    }
+    reference_rec(pts, dim, depth0, perm, lo, nl, depth + 1, 0);
     lo = lo + nl + 1;
     n = nr;
     ++depth;
@@ -138,9 +147,16 @@ void build_exact_cpu(const float* pts, const u32* ids, i64 n, int dim, int depth
   exact_rec(c, 0, n, 0, spawn);
 }
 
-void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm) {
+void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm, int threads, int depth0) {
   for (i64 i = 0; i < n; ++i) perm[i] = u32(i);
-  reference_rec(pts, dim, perm, 0, n, 0);
+  int spawn = 0;
+  while ((1 << spawn) < threads && spawn < 8) ++spawn;
+  reference_rec(pts, dim, depth0, perm, 0, n, 0, spawn);
+}
+
+int default_cpu_threads() {
+  const unsigned hw = std::thread::hardware_concurrency();
+  return int(std::max(1u, std::min(hw, 64u)));
 }
 
 void gather_rows(const float* pts, const u32* ids, const u32* perm, i64 n, int dim, float* tree_pts, u32* tree_ids) {

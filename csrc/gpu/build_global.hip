@@ -525,6 +525,7 @@ __device__ __forceinline__ void sweep_keys(const float* c0, const float* c1, i64
 // Histogram of a level's keys (used for the first global level only; later levels get
 // theirs from the fused partition pass).
 __global__ __launch_bounds__(kBlock) void k_hist(LevelArgs a, u32* __restrict__ hist) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   extern __shared__ __align__(16) u32 sh[];
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -562,6 +563,7 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* sh4, u32* total) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh4[4];
   __shared__ u32 found[3];
   const i64 s = blockIdx.x;
@@ -651,6 +653,7 @@ __global__ __launch_bounds__(kBlock) void k_select(LevelArgs a) {
 
 // Stage 2 (top levels): histogram of the median bucket's points over kBins2 sub-buckets.
 __global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh[kBins2];
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -678,6 +681,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2(LevelArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh4[4];
   __shared__ u32 found[3];
   const i64 s = blockIdx.x;
@@ -730,6 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_select2(LevelArgs a) {
 // serialise each load behind the previous store.
 template <int NCOL, int KI>
 __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins]
@@ -1351,6 +1356,7 @@ struct PairArgs {
 
 template <int NCOL>
 __global__ __launch_bounds__(kBlock) void k_scan(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   extern __shared__ __align__(16) u32 nh[];  // [2 * next_bins] + 64 per-lane dummy words
   constexpr int D = NCOL - 1;
   const i64 s = blockIdx.x / a.bps;
@@ -1648,6 +1654,7 @@ __device__ __forceinline__ void pivot_body(LevelArgs a, i64 bid) {
 
 template <int CAP>
 __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   refine_body<CAP>(a, blockIdx.x);
 }
 
@@ -1657,12 +1664,14 @@ __global__ __launch_bounds__(kBlock) void k_refine(LevelArgs a) {
 // launch and drain) per level, which adds up over the ~20 levels of a small build.
 template <int NCOL, int CAP>
 __global__ __launch_bounds__(kBlock) void k_refine_both(LevelArgs a, i64 segs, int gs) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   if (int(blockIdx.x) < gs) refine_small_body<NCOL>(a, segs, blockIdx.x);
   else refine_body<CAP>(a, i64(blockIdx.x) - gs);
 }
 
 template <int NCOL>
 __global__ __launch_bounds__(kBlock) void k_pivot_both(LevelArgs a, i64 segs, int gs) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   if (int(blockIdx.x) < gs) pivot_small_body<NCOL>(a, segs, blockIdx.x);
   else pivot_body<NCOL>(a, i64(blockIdx.x) - gs);
 }
@@ -1672,6 +1681,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_both(LevelArgs a, i64 segs, in
 // level l's median bucket); rows in the child's median bucket add to the child's sub-bucket
 // histogram (hist2 of level l+1, [2 * segs][kBins2]).
 __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh[2 * kBins2];
   const i64 s = blockIdx.x / a.bps;
   const int part = blockIdx.x % a.bps;
@@ -1736,6 +1746,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
 // the zone cursor then points past all certain rows, where the uncertain rows (the
 // child's median bucket, placed by the second stage) are appended with atomics.
 __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh4[4];
   const i64 s = blockIdx.x;
   const i64 h = a.heap0 + s;
@@ -1780,6 +1791,7 @@ __global__ __launch_bounds__(kBlock) void k_block_bases(LevelArgs a, PairArgs pa
 // form 6 more pseudo-zones placed with cursor atomics.
 template <int NCOL, int KI, bool PFX = false, bool ATOM = false>
 __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   constexpr int NZ = PFX ? 12 : 6;
@@ -2067,6 +2079,7 @@ struct TripleArgs {
 
 template <int NCOL>
 __global__ __launch_bounds__(kBlock) void k_scan2(LevelArgs a, TripleArgs ta) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   extern __shared__ __align__(16) u32 nh[];  // [4 * bins2] + 64 per-lane dummy words
   constexpr int D = NCOL - 1;
   const i64 s = blockIdx.x / a.bps;
@@ -2241,6 +2254,7 @@ __global__ __launch_bounds__(kBlock) void k_scan2(LevelArgs a, TripleArgs ta) {
 // Pass of a triple: a = level l (src -> dst); grandchildren (heap 4h + 3 + g) receive the rows.
 template <int NCOL, int KI, bool ATOM = true>
 __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs ta) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
   constexpr int NZ = 12;  // 4 grandchildren x (left of / inside / right of the level-(l+2) median bucket)
@@ -2594,6 +2608,7 @@ __device__ __forceinline__ BucketParams g3_node_params(const LevelArgs& a, const
 // Sample pass PASS (1: children, 2: grandchildren), grid segs x sblocks.
 template <int PASS>
 __global__ __launch_bounds__(kBlock) void k_g3_sample(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NN = PASS == 1 ? 2 : 4;
   __shared__ u32 hs[NN * kG3Bins];
   __shared__ BucketParams pn[NN];
@@ -2730,6 +2745,7 @@ __device__ __forceinline__ void g3_band(const u32* hb, BucketParams p, float z, 
 // great-grandchildren's bucketing and their zeroed level-(l+3) histograms.
 template <int PASS>
 __global__ __launch_bounds__(kBlock) void k_g3_band(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ BucketParams pn[4];
   __shared__ u32 sa1[2], sb1[2], sa2[4], sb2[4], sbs[6], stot[2];
   const i64 s = blockIdx.x, h = a.heap0 + s;
@@ -2827,6 +2843,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_band(LevelArgs a, G3Args g) {
 // k_partition3: LDS atomics (ATOM) or wave ballots.
 template <int NCOL, int KI, bool ATOM>
 __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
   constexpr int kCh = kBlock * KI;
   constexpr int NZ = 15;  // 0..7 great-grandchild, 8 + t staging tag t
@@ -3069,6 +3086,7 @@ __device__ u64 g3_block_select(Each each, u32 rank) {
 // its band rows). Grid: segments x nodes per segment.
 template <int NCOL, int LEVEL>
 __global__ __launch_bounds__(kG3Threads) void k_g3_res(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NT = kG3Threads;
   constexpr int D = NCOL - 1;
   constexpr int NODES = LEVEL == 0 ? 1 : (LEVEL == 1 ? 2 : 4);  // nodes of this level per segment
@@ -3417,6 +3435,7 @@ __device__ __forceinline__ BucketParams g3_res_params(const LevelArgs& a, const 
 
 template <int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_g3_mh(LevelArgs a, G3Args g, int K) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NODES = LEVEL == 1 ? 2 : 4;
   __shared__ u32 hres[kG3ResBins];
   __shared__ BucketParams bp;
@@ -3459,6 +3478,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_mh(LevelArgs a, G3Args g, int K) 
 
 template <int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_g3_ms(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NODES = LEVEL == 1 ? 2 : 4;
   __shared__ u32 ssum[kBlock / 64], sok, sm, st_, sbin, srank, scnt;
   const i64 s = blockIdx.x / NODES;
@@ -3518,6 +3538,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_ms(LevelArgs a, G3Args g) {
 
 template <int NCOL, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_g3_mc(LevelArgs a, G3Args g, int K) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NODES = LEVEL == 1 ? 2 : 4;
   constexpr int D = NCOL - 1;
   __shared__ BucketParams bp;
@@ -3563,6 +3584,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_mc(LevelArgs a, G3Args g, int K) 
 
 template <int NCOL, int LEVEL>
 __global__ __launch_bounds__(kG3Threads) void k_g3_mp(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NT = kG3Threads;
   constexpr int NODES = LEVEL == 1 ? 2 : 4;
   constexpr int D = NCOL - 1;
@@ -3614,6 +3636,7 @@ __global__ __launch_bounds__(kG3Threads) void k_g3_mp(LevelArgs a, G3Args g) {
 
 template <int NCOL, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_g3_mr(LevelArgs a, G3Args g, int K) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int NT = kBlock;
   constexpr int D = NCOL - 1;
   constexpr int NODES = LEVEL == 1 ? 2 : 4;
@@ -3743,6 +3766,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_mr(LevelArgs a, G3Args g, int K) 
 // One workgroup per great-grandchild after a multi-block resolve: every row placed, or (a failed
 // segment) its level-(l+3) histogram recounted from its slots.
 __global__ __launch_bounds__(kBlock) void k_g3_fin(LevelArgs a, G3Args g) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 h3[kTripleBins];
   __shared__ u32 incomplete;
   const i64 s = blockIdx.x / kG3Gg;
@@ -3832,6 +3856,7 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
 template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
   static_assert(!SLIM || D >= 3, "slim registers need three distinct level axes");
   // columns kept in registers: every column for D < 3, else the three levels' key columns (SLIM: two sets)
@@ -4593,6 +4618,23 @@ std::string GpuBuilder::describe() const {
        << (lp.pair ? " pair" : "") << (lp.triple ? " triple" : "") << (lp.tail ? " tail" : "")
        << (lp.sampled ? " sampled" : "") << (lp.g3 ? " g3" : "");
   return os.str();
+}
+
+namespace {
+// acc[0] |= err[0]; acc[1] += builds with any error bit; acc[2] += builds with the miss bit
+// (one thread: stream-ordered after the build, no host round trip).
+__global__ void k_accumulate_error(const u32* __restrict__ err, u32* __restrict__ acc) {
+  if (threadIdx.x != 0) return;
+  const u32 e = err[0];
+  acc[0] |= e;
+  acc[1] += e != 0u ? 1u : 0u;
+  acc[2] += (e & top4::kErrBit) ? 1u : 0u;
+}
+}  // namespace
+
+void GpuBuilder::accumulate_error(const void* workspace, u32* acc, hipStream_t stream) const {
+  k_accumulate_error<<<1, 64, 0, stream>>>(error_word(workspace), acc);
+  PKD_LAUNCH_CHECK();
 }
 
 u32 GpuBuilder::read_error(const void* workspace, hipStream_t stream, u32* detail) const {

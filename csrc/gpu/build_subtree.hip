@@ -520,6 +520,7 @@ template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0, int WPE = 0>
 __global__ __launch_bounds__(THREADS)
 __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (ITEMS * THREADS >= 4096 ? 1 : 2) * THREADS / 256)))
 void k_subtree_rank(SubArgs a) {
+  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   subtree_rank_body<ITEMS, THREADS, NARROW, DIMC>(a);
 }
 

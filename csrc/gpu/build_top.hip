@@ -753,6 +753,7 @@ struct ResArgs {
 // counts at level 0), summed over the wave and the block once at the end.
 template <int J>
 __global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   constexpr int NC = 3 << J, NO = J == 0 ? kNodes : 0;
   __shared__ u32 h[kResBins];
   __shared__ u32 cnt[8 * 3 + 16];  // [x][left / band / right], then the scatter's tags (j = 0)
@@ -854,6 +855,7 @@ __global__ __launch_bounds__(kHistThreads) void k_res_classify(ResArgs a) {
 // (rows certain left / right from the scatter, staged rows classified by k_res_classify),
 // then the bin holding it.
 __global__ __launch_bounds__(kBlock) void k_res_sel1(ResArgs a, Geom g) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   __shared__ __align__(16) u32 co[256];
   const int j = a.j, first = (1 << j) - 1, F = res_bins(j), gs = F / 256;
   const int X = first + blockIdx.x;
@@ -902,6 +904,7 @@ __global__ __launch_bounds__(kBlock) void k_res_sel1(ResArgs a, Geom g) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_res_collect(ResArgs a) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   __shared__ u32 sa[8], sb[8], ssel[8];
   __shared__ dev::BucketParams sbp[8];
   const int j = a.j, nodes = 1 << j, first = nodes - 1, F = res_bins(j);
@@ -1019,6 +1022,7 @@ __device__ u64 block_select(Each each, u32 rank) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_res_sel2(ResArgs a) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   __shared__ u64 buf[kSmallCap];
   const int j = a.j, first = (1 << j) - 1, F = res_bins(j);
   const int X = first + blockIdx.x, x = blockIdx.x;
@@ -1085,6 +1089,7 @@ struct InsArgs {
 // (after the scatter's certain rows), reordered through LDS per tile like the scatter.
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_res_insert(InsArgs a) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   constexpr int R = D <= 4 ? 16 : 8, NH = 2, HR = R / NH, HALF = kBlock * HR, NZ = kCells;
   constexpr int TILE = kBlock * R;
   __shared__ Reorder<NZ, NH> ro;
@@ -1184,6 +1189,7 @@ struct FinArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void k_finish(FinArgs a, Geom g) {
+  if (dev::build_failed(a.err)) return;  // an earlier kernel reported a miss: the build is redone
   __shared__ u32 box[16];
   __shared__ float split[kNodes];
   __shared__ u32 have[kNodes];

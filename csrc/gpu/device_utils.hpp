@@ -104,6 +104,24 @@ __device__ __forceinline__ u32 bucket_of(float x, BucketParams p, int nb) {
   return u32(t);
 }
 
+// Error-word gate of a build's kernels. Once a build has set its sticky error word (a sampled
+// band missed its median, a staging region overflowed, a consistency check failed) its tree is
+// invalid and is redone by the caller; every kernel after the first point where that can happen
+// returns here instead of running on a layout whose segments no longer hold what the geometry
+// says. (A missed top leaves the tail slots of under-filled level-4 segments holding whatever the
+// workspace held before: on a REUSED builder those are rows of its previous build, i.e. duplicate
+// (key, id) composites, which the exact-rank kernels below turn into colliding ranks and slot
+// indices past their segment -- the intermittent hipErrorIllegalAddress of round 5.)
+// Workgroup-uniform: thread 0 reads the word once and the block agrees on it through LDS, so a
+// word set concurrently (another workgroup of the same kernel, another stream of a split build)
+// can never split a workgroup at a later barrier. Every thread must call it (it holds a barrier).
+__device__ __forceinline__ bool build_failed(const u32* err) {
+  __shared__ u32 flag;
+  if (threadIdx.x == 0) flag = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return flag != 0u;
+}
+
 PKD_HD BucketParams make_params(float lo, float hi, int nb) {
   BucketParams p;
   p.lo = lo;

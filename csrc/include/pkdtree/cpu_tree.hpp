@@ -21,7 +21,11 @@ namespace pkdtree {
 // perm[k] = input row placed at in-order slot k. ids may be null (id = row index).
 void build_exact_cpu(const float* pts, const u32* ids, i64 n, int dim, int depth0, u32* perm,
                      int threads = 1);
-void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm);
+// threads > 1: a segment's two children are built on two threads once it is sorted (same tree
+// for any thread count); depth0 shifts the split axes like build_exact_cpu's.
+void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm, int threads = 1, int depth0 = 0);
+// Threads the CPU builders use when the caller does not say (hardware threads, at most 64).
+int default_cpu_threads();
 
 // Gather rows/ids through a permutation (tree_pts[k] = pts[perm[k]]).
 void gather_rows(const float* pts, const u32* ids, const u32* perm, i64 n, int dim, float* tree_pts,

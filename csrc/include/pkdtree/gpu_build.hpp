@@ -171,6 +171,10 @@ class GpuBuilder {
   // Sticky error word of the last build (0 = ok); synchronises the stream. Debug aid.
   // detail (optional, 3 words): first failure code, level, value.
   u32 read_error(const void* workspace, hipStream_t stream, u32* detail = nullptr) const;
+  // Folds the last build's error word into the device words acc[0..2] (OR of the words, builds
+  // with an error, builds with the miss bit), ordered after the build on `stream`: a benchmark
+  // checks EVERY timed build without a host round trip per build.
+  void accumulate_error(const void* workspace, u32* acc, hipStream_t stream) const;
   // Device address of that error word (valid until the workspace's next build).
   const u32* error_word(const void* workspace) const {
     return reinterpret_cast<const u32*>(static_cast<const char*>(workspace) + off_err_);

@@ -92,6 +92,11 @@ class GpuTreeBuilder:
         build's error words, ordered after it on the current stream: no host sync."""
         return self._b.error_words().clone()
 
+    def accumulate_error(self, acc: torch.Tensor) -> None:
+        """Fold the last build's error word into ``acc`` (int32 [>= 3] on the device): OR of the
+        words, builds with an error, builds with TOP_BAND_MISS. Stream-ordered, no host sync."""
+        self._b.accumulate_error(acc)
+
     def read_error_detail(self):
         """(error word, first failure code, level, value). Synchronises."""
         return tuple(int(v) for v in self._b.read_error())
@@ -160,29 +165,29 @@ def gpu_builder(n: int, dim: int, depth0: int = 0, subtree_max: int = 0, device=
 def build_gpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0, depth0: int = 0,
               subtree_max: int = 0):
     """Build the exact tree of ``points`` ([n, d] float32 on a GPU). Explicit ``ids`` must be
-    distinct: the exact order (coordinate, id) is only total for unique ids."""
+    distinct: the exact order (coordinate, id) is only total for unique ids. A build whose
+    sampled levels missed a median is redone unsampled (build_gpu_checked), so the result is
+    always the exact tree; GpuTreeBuilder.build is the asynchronous form that leaves that check
+    (read_error()) to the caller."""
     if not points.is_cuda:
         raise ValueError("build_gpu needs a GPU tensor")
-    points = points.contiguous()
-    b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
-    return b.build(points, ids, id_base)
+    tp, ti, _ = build_gpu_checked(points, ids, id_base, depth0, subtree_max)
+    return tp, ti
 
 
 def build_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
                       depth0: int = 0, subtree_max: int = 0):
-    """build_gpu, then -- for builds whose top levels were sampled -- a host check of the error
-    word: a band that missed its median (error bit TOP_BAND_MISS; ~1e-12 per node at the
-    default z, for any input order) is rebuilt without sampling. Returns (tree_pts, tree_ids,
-    builder). Synchronises only for sampled builds."""
+    """build_gpu, then -- for builds with sampled levels -- a host check of the error word: a
+    band that missed its median (error bit TOP_BAND_MISS) is rebuilt without sampling. Misses
+    are rare but not negligible: z = 6 for the top levels (~2e-9 per node), z = 5 for the
+    sampled triples (about one miss per 2000 builds of 100 M points), and duplicate-heavy data
+    whose median arenas are too large to stream always miss. A missed build stops at its first
+    failed check (every later kernel returns), so the builder stays reusable. Returns
+    (tree_pts, tree_ids, builder). Synchronises only for sampled builds."""
     points = points.contiguous()
     b = gpu_builder(points.shape[0], points.shape[1], depth0, subtree_max, points.device)
     tp, ti = b.build(points, ids, id_base)
     if b.sampled and (b.read_error() & GpuTreeBuilder.TOP_BAND_MISS):
-        # A builder whose build missed is not reused: on duplicate-heavy data the next build of
-        # such a builder faulted intermittently on MI355X (tests/test_gpu_build.py skewed stage-2
-        # cases, round 5; root cause open), so the next call constructs a fresh one.
-        _builders.pop((int(points.shape[0]), int(points.shape[1]), int(depth0), int(subtree_max), points.device),
-                      None)
         key = ("unsampled", points.shape[0], points.shape[1], depth0, subtree_max, points.device)
         fb = _builders.get(key)
         if fb is None:
@@ -218,9 +223,16 @@ def build_reference_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor
                       "reference's unstable std::sort picks the order; using the CPU std::sort builder",
                       RuntimeWarning, stacklevel=2)
         cids = ids if ids is not None else (torch.arange(points.shape[0], dtype=torch.int64) + id_base).to(torch.int32)
-        cp, ci = build_cpu(points.cpu(), cids.cpu(), "reference", depth0, 1)
+        cp, ci = build_cpu(points.cpu(), cids.cpu(), "reference", depth0, cpu_threads())
         tp, ti = cp.to(points.device), ci.to(points.device)
     return tp, ti, ties
+
+
+def cpu_threads() -> int:
+    """Threads of the host builders' fallbacks (the reference mode's std::sort builder gives the
+    same tree for any count)."""
+    import os
+    return max(1, min(64, os.cpu_count() or 1))
 
 
 def build_cpu(points: torch.Tensor, ids: Optional[torch.Tensor] = None, mode: str = "exact", depth0: int = 0,

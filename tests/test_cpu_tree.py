@@ -119,3 +119,31 @@ def test_ab_knobs_need_opt_in(monkeypatch, capfd):
     assert _ext().ab_knob("PKD_TOP_Z") == "0.5"
     monkeypatch.delenv("PKD_TOP_Z")
     assert _ext().ab_knob("PKD_TOP_Z") is None
+
+
+@pytest.mark.parametrize("n,dim", [(200_000, 3), (50_001, 2), (30_000, 128)])
+def test_reference_threaded_same_tree(n, dim):
+    """The threaded reference-mode builder (children of a sorted segment on two threads) gives
+    the single-threaded std::sort tree bit for bit: std::sort is deterministic for one input
+    order, and sibling segments are disjoint. The generator's data has ties (it holds ~22.5 M
+    distinct values per axis), so this also pins the unstable sort's tie order."""
+    x = pk.generate_problem(n + dim, dim, n)
+    ids = torch.arange(n, dtype=torch.int32)
+    p1, i1 = ops.build_cpu(x, ids, "reference", 0, 1)
+    for th in (2, 8, 64):
+        pt, it = ops.build_cpu(x, ids, "reference", 0, th)
+        assert torch.equal(it, i1) and torch.equal(pt, p1), th
+
+
+def test_reference_depth0():
+    """Reference mode with depth0 > 0 (a subtree of a deeper tree): axis (depth0 + depth) % dim,
+    the same as the single-threaded recursion started at that depth."""
+    x = pk.generate_problem(5, 3, 10_000)
+    ids = torch.arange(10_000, dtype=torch.int32)
+    p0, i0 = ops.build_cpu(x, ids, "reference", 0, 1)
+    # rotating the columns by depth0 and building at depth 0 is the same split sequence
+    p2, i2 = ops.build_cpu(x, ids, "reference", 2, 4)
+    xr = x[:, [2, 0, 1]].contiguous()
+    pr, ir = ops.build_cpu(xr, ids, "reference", 0, 1)
+    assert torch.equal(i2, ir)
+    assert not torch.equal(i2, i0)

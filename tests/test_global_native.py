@@ -125,8 +125,8 @@ def test_native_plan_errors(native):
             native.global_plan(flat, n, P, k, me)
 
 
-def _loopback_equal(native, x, P, k, with_radix=False):
-    tp, ti, err, scale, radix = native.global_loopback(x, P, k)
+def _loopback_equal(native, x, P, k, with_radix=False, builds=1):
+    tp, ti, err, scale, radix = native.global_loopback(x, P, k, builds)
     assert err == 0
     cp, ci = ops.build_cpu(x, None, "exact", 0, 16)
     assert torch.equal(ti, ci + 1), "native global tree differs from the exact tree"
@@ -191,3 +191,17 @@ def test_native_global_leaf_band_miss_rebuilt(gpu_device, native, monkeypatch, P
     monkeypatch.setenv("PKD_TOP_Z", "0.01")
     x = pk.generate_problem(31 + P, 3, 300_000 * P)
     _loopback_equal(native, x, P, k)
+
+
+@pytest.mark.gpu
+def test_native_global_leaf_builders_reused_after_misses(gpu_device, native, monkeypatch):
+    """Two builds by ONE global builder whose sampled leaves miss (z = 0.01): every leaf's sampled
+    builder (GlobalBuilder::leaf_builder) is reused after its miss, on the leaves' shared
+    workspace, and the second build is still exact with no error reported. (A missed build stops
+    at its failed check, so nothing of it runs on the stale layout the next build would inherit.)"""
+    monkeypatch.setenv("PKD_AB", "1")
+    monkeypatch.setenv("PKD_TOP_MIN_N", "0")
+    monkeypatch.setenv("PKD_TOP_Z", "0.01")
+    x = pk.generate_problem(41, 3, 1_200_000)
+    x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0  # duplicate-heavy axis, as the top-level miss tests
+    _loopback_equal(native, x, 4, 0, builds=3)

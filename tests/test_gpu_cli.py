@@ -69,3 +69,19 @@ def test_dist_cli_global_metrics_and_queries(bin_dir):
     lines = [l for l in r.stdout.splitlines() if not l.startswith("elapsed time")]
     assert lines == out(bin_dir / "kdtree_sequential", ["--queries", 300, 11, 4, 100000])
     assert len(lines) == 302 and '"decomp": "global"' in r.stderr
+
+
+def test_dist_cli_forest_slices_reuse_workspace_after_misses(bin_dir):
+    """kdtree_dist --ranks 4 on one process: four forest slices built one after another on ONE
+    shared workspace, every slice's sampled top forced to miss (z = 0.01 bands): each missed slice is redone unsampled and the next slice's sampled builder
+    starts on the workspace the miss and its rebuild left. Output equals the CPU executable.
+    (The reference stream's 3-D values are near-unique, so the z = 0.01 bands do the missing.)"""
+    import os
+    cfg = [17, 3, 1_600_000]
+    env = dict(os.environ, PKD_AB="1", PKD_TOP_MIN_N="0", PKD_TOP_Z="0.01")
+    r = subprocess.run([str(bin_dir / "kdtree_dist"), "--gpus", "1", "--ranks", "4", *map(str, cfg)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if not l.startswith("elapsed time")]
+    # the forest's MIN over the ranks' exact trees is the exact NN over all points
+    assert lines == out(bin_dir / "kdtree_sequential", cfg)

@@ -175,3 +175,56 @@ def test_top_heavy_duplicates_large_is_bounded(gpu_device):
     assert bool((seen == 1).all())
     assert dt < 2.0, dt
 
+
+
+def test_top_builder_reused_after_misses(gpu_device):
+    """One sampled builder reused on duplicate-heavy data whose builds miss (an axis with 9
+    distinct values: median arenas too large to stream). Every missed build must stay
+    memory-safe and report the miss, and must leave the builder usable: once the error word
+    is set the rest of the build returns at once (dev::build_failed), so no kernel runs on
+    level-4 segments whose unfilled tails still hold the previous build's rows. Then the SAME
+    builder builds data that does not miss, and its tree is the exact one."""
+    n = 18_000_000
+    x = pk.generate_problem(6, 3, n)
+    x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
+    xd = x.to(gpu_device)
+    b = ops.GpuTreeBuilder(n, 3, 0, 0)
+    assert b.sampled_top
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    misses = 0
+    for _ in range(4):
+        tp, ti = b.build(xd)
+        torch.cuda.synchronize()
+        err = b.read_error()
+        if err == 0:
+            assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+        else:
+            assert err & ops.GpuTreeBuilder.TOP_BAND_MISS, b.read_error_detail()
+            misses += 1
+    assert misses > 0, "this input is meant to miss (staged arena above the streaming cap)"
+    # the builder after its misses, on data that samples cleanly
+    y = pk.generate_problem(7, 3, n)
+    tp, ti = b.build(y.to(gpu_device))
+    torch.cuda.synchronize()
+    assert b.read_error_detail()[0] == 0, b.read_error_detail()
+    yp, yi = ops.build_cpu(y, None, "exact", 0, 8)
+    assert torch.equal(ti.cpu(), yi) and torch.equal(tp.cpu(), yp)
+
+
+def test_checked_build_reuses_builder_after_miss(gpu_device):
+    """build_gpu_checked keeps its cached sampled builder after a miss (no discard workaround):
+    miss, rebuild unsampled, then the next call on clean data reuses the same builder."""
+    n = 18_000_000
+    x = pk.generate_problem(6, 3, n)
+    x[:, 1] = torch.round(x[:, 1] / 25.0) * 25.0
+    tp, ti, b1 = ops.build_gpu_checked(x.to(gpu_device), None, 0, 0)
+    cp, ci = ops.build_cpu(x, None, "exact", 0, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(ti.cpu(), ci) and torch.equal(tp.cpu(), cp)
+    sampled = ops.gpu_builder(n, 3, 0, 0, x[:1].to(gpu_device).device)
+    y = pk.generate_problem(8, 3, n)
+    tp, ti, b2 = ops.build_gpu_checked(y.to(gpu_device), None, 0, 0)
+    torch.cuda.synchronize()
+    assert b2 is sampled, "the sampled builder is reused after a miss"
+    yp, yi = ops.build_cpu(y, None, "exact", 0, 8)
+    assert torch.equal(ti.cpu(), yi) and torch.equal(tp.cpu(), yp)
