@@ -3856,7 +3856,6 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
 template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
-  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
   static_assert(!SLIM || D >= 3, "slim registers need three distinct level axes");
   // columns kept in registers: every column for D < 3, else the three levels' key columns (SLIM: two sets)
@@ -3873,7 +3872,8 @@ void k_tail3(TailArgs a) {
   __shared__ BucketParams sprm[4];
   __shared__ i64 nlo[15];              // segment starts of the tail's 15 nodes (heap order below h)
   __shared__ u32 nn[15];
-  __shared__ u32 sbig;
+  __shared__ u32 sbig, failed;
+  dev::build_failed_issue(a.err, &failed);  // tested after the first barrier (level 0)
   const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
   const i64 h = a.heap0 + blockIdx.x;
   const i64 lo = a.seg_lo[h];
@@ -3969,7 +3969,10 @@ void k_tail3(TailArgs a) {
       sbst[tq] = 0xffffffffu;
       spiv[tq] = ~0ull;
     }
-    if (t == 0) __syncthreads();  // nn / scell
+    if (t == 0) {
+      __syncthreads();  // nn / scell
+      if (failed) return;  // the build already failed (a miss): it is redone
+    }
     if (tq < S) {
       const float* c = &scell[t & 1][tq][axis][0];
       sprm[tq] = make_params(c[0], c[1], B);

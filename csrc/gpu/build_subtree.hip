@@ -137,6 +137,8 @@ __device__ __forceinline__ void subtree_rank_body(const SubArgs& a) {
   if (n <= 0) return;
   const i64 glo = a.seg_lo[h];
   const int tid = threadIdx.x;
+  __shared__ u32 failed;  // the build's error word (tested after the load barrier below)
+  dev::build_failed_issue(a.err, &failed);
   const int lsub = rk::bitlen(u32(n));  // levels of the implicit subtree of n points
   const int kept_layout = rk::kept_axes(dim, NM);
   const bool keep = dim < lsub;
@@ -256,6 +258,7 @@ __device__ __forceinline__ void subtree_rank_body(const SubArgs& a) {
     nn[i] = kid(i) < n ? u32(n) : 0u;
   }
   __syncthreads();
+  if (failed) return;  // the build already failed (a miss): it is redone
   stamp(a, 1);
 
   int cb = 0;          // bitmap buffer of the next compressed level: 1 = bm1, 0 = work
@@ -520,7 +523,6 @@ template <int ITEMS, int THREADS, bool NARROW, int DIMC = 0, int WPE = 0>
 __global__ __launch_bounds__(THREADS)
 __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (ITEMS * THREADS >= 4096 ? 1 : 2) * THREADS / 256)))
 void k_subtree_rank(SubArgs a) {
-  if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   subtree_rank_body<ITEMS, THREADS, NARROW, DIMC>(a);
 }
 

@@ -115,9 +115,17 @@ __device__ __forceinline__ u32 bucket_of(float x, BucketParams p, int nb) {
 // Workgroup-uniform: thread 0 reads the word once and the block agrees on it through LDS, so a
 // word set concurrently (another workgroup of the same kernel, another stream of a split build)
 // can never split a workgroup at a later barrier. Every thread must call it (it holds a barrier).
+// Split form for the long kernels with an early barrier of their own (k_tail3, the subtree
+// kernel): thread 0 issues the load at the very start, into an LDS word, and the block tests it
+// after that barrier, so the load's latency hides behind the kernel's own first loads instead of
+// stalling every workgroup's start (the one-barrier form cost the 100 M build's 65 536 subtree
+// workgroups ~24 us).
+__device__ __forceinline__ void build_failed_issue(const u32* err, u32* flag) {
+  if (threadIdx.x == 0) *flag = *err;
+}
 __device__ __forceinline__ bool build_failed(const u32* err) {
   __shared__ u32 flag;
-  if (threadIdx.x == 0) flag = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) flag = *err;  // plain load: kernel boundaries order the earlier kernels' writes
   __syncthreads();
   return flag != 0u;
 }
