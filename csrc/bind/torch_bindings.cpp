@@ -5,6 +5,7 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <algorithm>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -151,6 +152,44 @@ struct RefBuilder {
     return {op, oi};
   }
 };
+
+// Hybrid reference mode (cpu_tree.hpp reference_repair): points [n, dim] (host), the GPU tree's
+// slot -> input row map [n] (int32, host), the tied segments' median slots. Returns (perm int32 [n]:
+// slot -> row of the reference tree, decided slots int64 [k]: the slots the host decided).
+std::vector<torch::Tensor> reference_repair(const torch::Tensor& pts, const torch::Tensor& gpu_rows,
+                                            const std::vector<int64_t>& tied, int64_t depth0, int64_t threads) {
+  check_points(pts, false);
+  const int64_t n = pts.size(0);
+  TORCH_CHECK(gpu_rows.scalar_type() == torch::kInt32 && !gpu_rows.is_cuda() && gpu_rows.is_contiguous() &&
+                  gpu_rows.numel() == n, "gpu_rows: int32 [n] host tensor");
+  std::vector<pk::u32> ts(tied.begin(), tied.end());
+  torch::Tensor perm = torch::empty({n}, torch::kInt32);
+  const auto ranges = pk::reference_repair(pts.data_ptr<float>(), n, int(pts.size(1)), int(depth0),
+                                           reinterpret_cast<const pk::u32*>(gpu_rows.data_ptr<int32_t>()), ts.data(),
+                                           ts.size(), reinterpret_cast<pk::u32*>(perm.data_ptr<int32_t>()),
+                                           int(threads));
+  int64_t k = 0;
+  for (const auto& r : ranges) k += r.second;
+  torch::Tensor slots = torch::empty({k}, torch::kInt64);
+  int64_t* sp = slots.data_ptr<int64_t>();
+  for (const auto& r : ranges)
+    for (int64_t j = 0; j < r.second; ++j) *sp++ = r.first + j;
+  return {perm, slots};
+}
+
+// The reference's std::sort of row indices by keys: libstdc++ itself (replica = false) or the
+// parallel replica (cpu_tree.hpp std_sort_replica) -- the test that they agree bit for bit.
+torch::Tensor sort_indices(const torch::Tensor& keys, bool replica, int64_t threads) {
+  TORCH_CHECK(keys.scalar_type() == torch::kFloat32 && !keys.is_cuda() && keys.is_contiguous() && keys.dim() == 1,
+              "keys: float32 host vector");
+  const int64_t n = keys.numel();
+  torch::Tensor idx = torch::arange(n, torch::kInt32);
+  auto* ip = reinterpret_cast<pk::u32*>(idx.data_ptr<int32_t>());
+  const float* k = keys.data_ptr<float>();
+  if (replica) pk::std_sort_replica(k, ip, n, int(threads));
+  else std::sort(ip, ip + n, [k](pk::u32 a, pk::u32 b) { return k[a] < k[b]; });
+  return idx;
+}
 
 torch::Tensor generate(int64_t seed, int64_t dim, int64_t rows, int64_t first, int64_t threads) {
   TORCH_CHECK(dim > 0 && rows >= 0 && first >= 0, "bad generator arguments");
@@ -371,6 +410,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(b.ws.defined(), "read_ties: no build yet");
         return int64_t(b.b.read_ties(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream()));
       })
+      .def("read_tie_slots", [](RefBuilder& b) {
+        TORCH_CHECK(b.ws.defined(), "read_tie_slots: no build yet");
+        const auto v = b.b.read_tie_slots(b.ws.data_ptr(), c10::hip::getCurrentHIPStream(b.ws.device().index()).stream());
+        return std::vector<int64_t>(v.begin(), v.end());
+      })
+      .def_property_readonly_static("tie_slots_cap", [](py::object) { return int64_t(pk::ReferenceBuilder::kTieSlots); })
       .def_property_readonly("sorted_levels", [](const RefBuilder& b) { return b.b.sorted_levels(); })
       .def_property_readonly("global_levels", [](const RefBuilder& b) { return b.b.global_levels(); })
       .def_property_readonly("workspace_bytes", [](const RefBuilder& b) { return int64_t(b.b.workspace_bytes()); });
@@ -383,6 +428,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const pk::DevGenPlan p = pk::devgen_plan(uint64_t(total));
     return std::vector<int64_t>{int64_t(p.S), int64_t(p.C), int64_t(p.R)};
   });
+  m.def("reference_repair", &reference_repair, py::arg("points"), py::arg("gpu_rows"), py::arg("tied"),
+        py::arg("depth0") = 0, py::arg("threads") = 1, py::call_guard<py::gil_scoped_release>());
+  m.def("sort_indices", &sort_indices, py::arg("keys"), py::arg("replica"), py::arg("threads") = 1,
+        py::call_guard<py::gil_scoped_release>());
   m.def("build_cpu", &build_cpu, py::arg("points"), py::arg("ids") = c10::nullopt, py::arg("mode") = "exact",
         py::arg("depth0") = 0, py::arg("threads") = 1);
   m.def("search_cpu", &search_cpu, py::arg("tree_pts"), py::arg("queries"), py::arg("depth0") = 0,

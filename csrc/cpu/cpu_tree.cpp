@@ -3,9 +3,106 @@
 
 #include <algorithm>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 namespace pkdtree {
+
+// ---------------------------------------------------------------------------------------------
+// A parallel replica of libstdc++'s std::sort (introsort: __introsort_loop with median-of-three
+// pivots and __unguarded_partition, a heapsort fallback at depth 2 floor(log2 n), ranges of at
+// most 16 left for __final_insertion_sort). The reference's tree IS std::sort's output order --
+// an unstable sort, so equal keys land wherever this exact algorithm puts them -- and the
+// permutation depends only on the comparisons it makes, so the replica reproduces it bit for
+// bit (tests/test_cpu_tree.py checks it against std::sort on duplicate-heavy inputs):
+//   * after a partition, [first, cut) <= pivot <= [cut, last): the two sides are independent, so
+//     they may run on two threads;
+//   * the final insertion pass can never move an element across such a boundary (it only moves
+//     an element left past STRICTLY greater ones), so it equals a stable insertion sort of each
+//     leaf range, done as soon as the leaf exists.
+// The critical path of one sort drops from n log n to ~2n comparisons (the top partitions).
+namespace refsort {
+
+constexpr std::ptrdiff_t kThreshold = 16;      // libstdc++ _S_threshold
+constexpr std::ptrdiff_t kSpawnMin = 1 << 15;  // smallest side worth its own thread
+
+template <class C>
+inline void move_median_to_first(u32* r, u32* a, u32* b, u32* c, const C& comp) {
+  if (comp(*a, *b)) {
+    if (comp(*b, *c)) std::iter_swap(r, b);
+    else if (comp(*a, *c)) std::iter_swap(r, c);
+    else std::iter_swap(r, a);
+  } else if (comp(*a, *c)) {
+    std::iter_swap(r, a);
+  } else if (comp(*b, *c)) {
+    std::iter_swap(r, c);
+  } else {
+    std::iter_swap(r, b);
+  }
+}
+
+template <class C>
+inline u32* unguarded_partition(u32* first, u32* last, u32* pivot, const C& comp) {
+  while (true) {
+    while (comp(*first, *pivot)) ++first;
+    --last;
+    while (comp(*pivot, *last)) --last;
+    if (!(first < last)) return first;
+    std::iter_swap(first, last);
+    ++first;
+  }
+}
+
+template <class C>
+inline void insertion(u32* first, u32* last, const C& comp) {  // stable: = the final pass on this leaf
+  for (u32* i = first + (first != last ? 1 : 0); i < last; ++i) {
+    const u32 v = *i;
+    u32* j = i;
+    while (j > first && comp(v, *(j - 1))) {
+      *j = *(j - 1);
+      --j;
+    }
+    *j = v;
+  }
+}
+
+template <class C>
+void loop(u32* first, u32* last, long depth, const C& comp, int spawn) {
+  while (last - first > kThreshold) {
+    if (depth == 0) {  // libstdc++: __partial_sort(first, last, last) -- heap select + sort_heap
+      std::partial_sort(first, last, last, comp);
+      return;
+    }
+    --depth;
+    u32* mid = first + (last - first) / 2;
+    move_median_to_first(first, first + 1, mid, last - 1, comp);
+    u32* cut = unguarded_partition(first + 1, last, first, comp);
+    if (spawn > 0 && last - cut >= kSpawnMin && cut - first >= kSpawnMin) {
+      std::thread t([=, &comp] { loop(cut, last, depth, comp, spawn - 1); });
+      loop(first, cut, depth, comp, spawn - 1);
+      t.join();
+      return;
+    }
+    loop(cut, last, depth, comp, 0);
+    last = cut;
+  }
+  insertion(first, last, comp);
+}
+
+template <class C>
+void sort(u32* first, u32* last, const C& comp, int spawn) {
+  if (last - first < 2) return;
+  const long n = long(last - first);
+  loop(first, last, 2L * long(63 - __builtin_clzl(static_cast<unsigned long>(n))), comp, spawn);
+}
+
+}  // namespace refsort
+
+void std_sort_replica(const float* keys, u32* idx, i64 n, int threads) {
+  int spawn = 0;
+  while ((1 << spawn) < threads && spawn < 8) ++spawn;
+  refsort::sort(idx, idx + n, [keys](u32 a, u32 b) { return keys[a] < keys[b]; }, spawn);
+}
 
 namespace {
 
@@ -49,9 +146,11 @@ void reference_rec(const float* pts, int dim, int depth0, u32* perm, i64 lo, i64
   // critical path drops from the whole O(N log^2 N) build to ~2 N log N: one sort per level).
   while (n > 1) {
     const int axis = (depth0 + depth) % dim;
-    std::sort(perm + lo, perm + lo + (n - 1), [&](u32 a, u32 b) {
+    // (the replica of std::sort: the same permutation; with threads to spare, the sort of a large
+    // segment splits its own partitions over threads too)
+    refsort::sort(perm + lo, perm + lo + (n - 1), [&](u32 a, u32 b) {
       return pts[size_t(a) * size_t(dim) + size_t(axis)] < pts[size_t(b) * size_t(dim) + size_t(axis)];
-    });
+    }, spawn_levels);
     const i64 nl = left_n(n), nr = right_n(n);
     if (spawn_levels > 0 && n >= 4096) {
       std::thread t([=] { reference_rec(pts, dim, depth0, perm, lo, nl, depth + 1, spawn_levels - 1); });
@@ -152,6 +251,94 @@ void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm, int thread
   int spawn = 0;
   while ((1 << spawn) < threads && spawn < 8) ++spawn;
   reference_rec(pts, dim, depth0, perm, 0, n, 0, spawn);
+}
+
+namespace {
+
+// Segment key of the implicit tree: (depth, start slot).
+inline u64 seg_key(int depth, i64 lo) { return (u64(u32(depth)) << 40) | u64(lo); }
+
+struct RepairCtx {
+  const float* pts;
+  int dim, depth0;
+  const u32* gpu;  // the GPU tree's slot -> row
+  u32* order;      // working input order of every CPU segment (the reference's array)
+  u32* out;        // result: slot -> row
+  const std::unordered_set<u64>* closure;
+  const std::unordered_set<u64>* tied;
+  std::vector<std::vector<std::pair<i64, i64>>>* cpu_ranges;  // per spawned task: slot ranges it decided
+};
+
+void repair_rec(const RepairCtx& c, i64 lo, i64 n, int depth, int spawn, int task) {
+  while (n > 0) {
+    const u64 key = seg_key(depth, lo);
+    const bool is_tied = c.tied->count(key) != 0;
+    if (!is_tied && c.closure->count(key) == 0) {  // no deciding tie at or below: the GPU's slots stand
+      std::copy(c.gpu + lo, c.gpu + lo + n, c.out + lo);
+      return;
+    }
+    if (is_tied) {  // std::sort decides here: the whole subtree from this segment's exact input order
+      reference_rec(c.pts, c.dim, c.depth0, c.order, lo, n, depth, spawn);
+      std::copy(c.order + lo, c.order + lo + n, c.out + lo);
+      (*c.cpu_ranges)[size_t(task)].push_back({lo, n});
+      return;
+    }
+    // an ancestor of a tied segment: its sort fixes the exact order its children start from
+    const int axis = (c.depth0 + depth) % c.dim;
+    refsort::sort(c.order + lo, c.order + lo + (n - 1), [&](u32 a, u32 b) {
+      return c.pts[size_t(a) * size_t(c.dim) + size_t(axis)] < c.pts[size_t(b) * size_t(c.dim) + size_t(axis)];
+    }, spawn);
+    const i64 nl = left_n(n), nr = right_n(n);
+    c.out[lo + nl] = c.order[lo + nl];
+    (*c.cpu_ranges)[size_t(task)].push_back({lo + nl, 1});
+    if (spawn > 0 && nl >= 4096) {
+      const int t2 = task + (1 << (spawn - 1));
+      std::thread t([&c, lo, nl, depth, spawn, t2] { repair_rec(c, lo, nl, depth + 1, spawn - 1, t2); });
+      repair_rec(c, lo + nl + 1, nr, depth + 1, spawn - 1, task);
+      t.join();
+      return;
+    }
+    repair_rec(c, lo, nl, depth + 1, 0, task);
+    lo = lo + nl + 1;
+    n = nr;
+    ++depth;
+  }
+}
+
+}  // namespace
+
+std::vector<std::pair<i64, i64>> reference_repair(const float* pts, i64 n, int dim, int depth0, const u32* gpu_perm,
+                                                  const u32* tied_slots, size_t ntied, u32* perm, int threads) {
+  std::unordered_set<u64> closure, tied;
+  for (size_t k = 0; k < ntied; ++k) {  // the path from the root to each tied segment (by its median slot)
+    const i64 s = i64(tied_slots[k]);
+    i64 lo = 0, m = n;
+    for (int d = 0; m > 0; ++d) {
+      const i64 nl = left_n(m);
+      if (s == lo + nl) {
+        tied.insert(seg_key(d, lo));
+        break;
+      }
+      closure.insert(seg_key(d, lo));
+      if (s < lo + nl) {
+        m = nl;
+      } else {
+        lo = lo + nl + 1;
+        m = right_n(m);
+      }
+    }
+  }
+  std::vector<u32> order(static_cast<size_t>(std::max<i64>(n, 1)));
+  for (i64 i = 0; i < n; ++i) order[size_t(i)] = u32(i);
+  int spawn = 0;
+  while ((1 << spawn) < threads && spawn < 8) ++spawn;
+  std::vector<std::vector<std::pair<i64, i64>>> ranges(size_t(1) << spawn);
+  RepairCtx c{pts, dim, depth0, gpu_perm, order.data(), perm, &closure, &tied, &ranges};
+  repair_rec(c, 0, n, 0, spawn, 0);
+  std::vector<std::pair<i64, i64>> all;
+  for (auto& r : ranges) all.insert(all.end(), r.begin(), r.end());
+  std::sort(all.begin(), all.end());
+  return all;
 }
 
 int default_cpu_threads() {

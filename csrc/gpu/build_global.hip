@@ -2393,14 +2393,27 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
     }
     __syncthreads();
     if constexpr (!ATOM) {
-      for (int z = w; z < NZ; z += W) {  // wave w scans zones w, w+4, w+8
-        const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
-        const u32 incl = dev::wave_incl_scan(v);
-        const u32 tot = __shfl(incl, 63, 64);
-        u32 base = 0;
-        if (ln == 0 && tot) base = atomicAdd(&a.state[g0 + z / 3].cur[z % 3], tot);
-        base = __shfl(base, 0, 64);
-        gcnt[z][ln] = base + incl - v;
+      // wave w scans zones w, w+4, w+8; lane k reserves the wave's k-th zone (all in flight at once)
+      constexpr int ZW = (NZ + W - 1) / W;
+      u32 v[ZW], incl[ZW], tot[ZW];
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) {
+        const int z = w + k * W;
+        v[k] = (z < NZ && ln < kItems * 4) ? gcnt[z < NZ ? z : 0][ln] : 0u;
+        incl[k] = dev::wave_incl_scan(v[k]);
+        tot[k] = __shfl(incl[k], 63, 64);
+      }
+      u32 mine = 0;
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) mine = ln == k ? tot[k] : mine;
+      const int zl = w + ln * W;
+      u32 base = 0;
+      if (ln < ZW && zl < NZ && mine) base = atomicAdd(&a.state[g0 + zl / 3].cur[zl % 3], mine);
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) {
+        const int z = w + k * W;
+        const u32 b = __shfl(base, k, 64);
+        if (z < NZ) gcnt[z][ln] = b + incl[k] - v[k];
       }
     } else if (threadIdx.x < NZ) {  // thread z: zone z's waves, scanned, reserved in the grandchild at once
       const int z = int(threadIdx.x);
@@ -2950,15 +2963,30 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
     }
     __syncthreads();
     if constexpr (!ATOM) {
-      for (int z = w; z < NZ; z += W) {  // wave w scans zones w, w + 4, ...
-        const int ln = dev::lane();
-        const u32 v = ln < kItems * 4 ? gcnt[z][ln] : 0u;
-        const u32 incl = dev::wave_incl_scan(v);
-        const u32 tot = __shfl(incl, 63, 64);
-        u32 base = 0;
-        if (ln == 0 && tot) base = atomicAdd(&gs->zc[z][0], tot);
-        base = __shfl(base, 0, 64);
-        gcnt[z][ln] = base + incl - v;
+      // wave w scans zones w, w + 4, ...; lane k then reserves the wave's k-th zone, so all of the
+      // wave's reservations are in flight together (one atomic round trip per chunk, not one per
+      // zone: the sequential form put ~4 global-atomic latencies on every chunk's critical path)
+      constexpr int ZW = (NZ + W - 1) / W;
+      const int ln = dev::lane();
+      u32 v[ZW], incl[ZW], tot[ZW];
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) {
+        const int z = w + k * W;
+        v[k] = (z < NZ && ln < kItems * 4) ? gcnt[z < NZ ? z : 0][ln] : 0u;
+        incl[k] = dev::wave_incl_scan(v[k]);
+        tot[k] = __shfl(incl[k], 63, 64);
+      }
+      u32 mine = 0;
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) mine = ln == k ? tot[k] : mine;
+      const int zl = w + ln * W;
+      u32 base = 0;
+      if (ln < ZW && zl < NZ && mine) base = atomicAdd(&gs->zc[zl][0], mine);
+#pragma unroll
+      for (int k = 0; k < ZW; ++k) {
+        const int z = w + k * W;
+        const u32 b = __shfl(base, k, 64);
+        if (z < NZ) gcnt[z][ln] = b + incl[k] - v[k];
       }
     } else if (threadIdx.x < NZ) {  // zone z's waves, scanned, reserved once per chunk
       const int z = int(threadIdx.x);

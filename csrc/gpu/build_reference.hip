@@ -56,6 +56,14 @@ constexpr int kFinItems = kFinCap / kFinThreads;
 constexpr int kItems = 8;         // rows per thread per partition chunk
 constexpr int kChunk = kBlock * kItems;
 constexpr int kRefineCap = 4096;  // middle rows selected in LDS (more: streamed from global)
+// Deciding ties: words[0] counts the tied segments; the median slots of the first kTieSlots of them
+// are listed from words[kTieOff] on, so the host can redo exactly those subtrees and their
+// ancestors' sorts (reference_repair, cpu_tree.hpp) instead of the whole tree.
+constexpr u32 kTieOff = 16;
+__device__ __forceinline__ void note_tie(u32* ties, u32 slot) {
+  const u32 k = atomicAdd(ties, 1u);
+  if (k < ReferenceBuilder::kTieSlots) ties[kTieOff + k] = slot;
+}
 
 struct RefSeg {
   u32 lo, n;              // slot range of the segment
@@ -489,7 +497,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_refine(const RefSeg* __restrict_
     bool tie = k1 == k2;
     if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;       // rank m - 2 vs the left's last
     if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;  // rank m + 1 vs the median
-    if (tie) atomicAdd(ties, 1u);
+    if (tie) note_tie(ties, r.lo + m);
   }
 }
 
@@ -656,7 +664,7 @@ __global__ __launch_bounds__(kFinThreads) void k_ref_finish(const float* __restr
         bool tie = kk[m - 1] == kk[m];
         if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
         if (m + 1 <= sn - 2 && kk[m] == kk[m + 1]) tie = true;
-        if (tie) atomicAdd(ties, 1u);
+        if (tie) note_tie(ties, lo + u32(sl) + u32(m));
       }
     }
     __syncthreads();
@@ -1012,7 +1020,7 @@ __device__ __forceinline__ void rr_refine_wave(const RefSeg& r, i64 s, RowCols d
     bool tie = k1 == k2;
     if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;
     if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;
-    if (tie) atomicAdd(ties, 1u);
+    if (tie) note_tie(ties, r.lo + m);
   }
 }
 
@@ -1158,7 +1166,7 @@ __global__ __launch_bounds__(kBlock) void k_rr_refine(RowCols src, RowCols dst, 
     bool tie = k1 == k2;
     if (m >= 2 && pred != 0ull && u32(pred >> 32) == k1) tie = true;
     if (m + 1 <= r.n - 2 && succ != ~0ull && u32(succ >> 32) == k2) tie = true;
-    if (tie) atomicAdd(ties, 1u);
+    if (tie) note_tie(ties, r.lo + m);
   }
 }
 
@@ -1298,7 +1306,7 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish(RowCols src, int dim,
         bool tie = kk[m - 1] == kk[m];
         if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
         if (m + 1 <= sn - 2 && kk[m] == kk[m + 1]) tie = true;
-        if (tie) atomicAdd(ties, 1u);
+        if (tie) note_tie(ties, lo + u32(sl) + u32(m));
       }
     }
     __syncthreads();
@@ -1437,7 +1445,7 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish_rank(RowCols src, int
       bool tie = kk[m - 1] == kk[m];
       if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
       if (m + 1 <= tn[i] - 2 && kk[m] == kk[m + 1]) tie = true;
-      if (tie) atomicAdd(ties, 1u);
+      if (tie) note_tie(ties, glo + tlo[i] + m);
     }
     // rows of sub-segments of <= 2 rows are final (2: the designated row keeps the last slot)
     bool srt[I];
@@ -1600,7 +1608,7 @@ __global__ __launch_bounds__(kFinThreads) void k_rr_finish_rank(RowCols src, int
       bool tie = kk[m - 1] == kk[m];
       if (m >= 2 && kk[m - 2] == kk[m - 1]) tie = true;
       if (m + 1 <= tn[i] - 2 && kk[m] == kk[m + 1]) tie = true;
-      if (tie) atomicAdd(ties, 1u);
+      if (tie) note_tie(ties, glo + tlo[i] + m);
     }
     if (live[i]) {
       if (nn[i] <= 2u) fin[lo[i] + ((nn[i] == 2u && des[i]) ? 1u : 0u)] = (unsigned short)p;
@@ -1679,8 +1687,19 @@ ReferenceBuilder::ReferenceBuilder(i64 n, int dim, int depth0) : n_(n), dim_(dim
     off_hpart_ = take(size_t(hp) * 4);
   }
   off_segs_ = take(2 * size_t(max_segs) * sizeof(RefSeg));
-  off_words_ = take(16);  // [0] ties, [1] error
+  off_words_ = take(size_t(kTieOff + kTieSlots) * 4);  // [0] ties, [1] error, [kTieOff..] tied median slots
   ws_bytes_ = off;
+}
+
+std::vector<u32> ReferenceBuilder::read_tie_slots(const void* workspace, hipStream_t stream) const {
+  const u32 t = read_ties(workspace, stream);
+  std::vector<u32> v(std::min<u32>(t, kTieSlots));
+  if (!v.empty()) {
+    PKD_HIP_CHECK(hipMemcpyAsync(v.data(), static_cast<const char*>(workspace) + off_words_ + kTieOff * 4,
+                                 v.size() * 4, hipMemcpyDeviceToHost, stream));
+    PKD_HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  return v;
 }
 
 u32 ReferenceBuilder::read_ties(const void* workspace, hipStream_t stream) const {
@@ -1814,6 +1833,50 @@ void ReferenceBuilder::build(const float* pts, const u32* ids, u32 id_base, floa
   }
   k_ref_gather<<<int(std::min<i64>(4096, std::max<i64>(1, (n_ * dim_ + 4 * kBlock - 1) / (4 * kBlock)))), kBlock, 0,
                  stream>>>(pts, ids, id_base, dim_, perm[cur], n_, out_pts, out_ids);
+  PKD_LAUNCH_CHECK();
+}
+
+namespace {
+// Host-decided slots of a repaired reference tree: slot slots[k] takes input row rows[k].
+__global__ __launch_bounds__(kBlock) void k_ref_patch(const float* __restrict__ pts, const u32* __restrict__ ids,
+                                                      u32 id_base, int dim, const u32* __restrict__ slots,
+                                                      const u32* __restrict__ rows, i64 count,
+                                                      float* __restrict__ out_pts, u32* __restrict__ out_ids) {
+  const i64 total = count * i64(dim);
+  for (i64 e = i64(blockIdx.x) * kBlock + threadIdx.x; e < total; e += i64(gridDim.x) * kBlock) {
+    const i64 k = e / dim;
+    const int c = int(e - k * dim);
+    const u32 r = rows[k], sl = slots[k];
+    out_pts[i64(sl) * dim + c] = pts[i64(r) * dim + c];
+    if (c == 0) out_ids[sl] = ids ? ids[r] : id_base + r;
+  }
+}
+}  // namespace
+
+void reference_patch(const float* pts, const u32* ids, u32 id_base, int dim, const u32* slots, const u32* rows,
+                     i64 count, float* out_pts, u32* out_ids, hipStream_t stream) {
+  if (count <= 0) return;
+  const int g = int(std::min<i64>(4096, (count * dim + kBlock - 1) / kBlock));
+  k_ref_patch<<<g, kBlock, 0, stream>>>(pts, ids, id_base, dim, slots, rows, count, out_pts, out_ids);
+  PKD_LAUNCH_CHECK();
+}
+
+namespace {
+__global__ __launch_bounds__(kBlock) void k_ref_keys_of_levels(const float* __restrict__ pts, i64 n, int dim,
+                                                               int depth0, int levels, float* __restrict__ out) {
+  const i64 total = n * i64(levels);
+  for (i64 e = i64(blockIdx.x) * kBlock + threadIdx.x; e < total; e += i64(gridDim.x) * kBlock) {
+    const i64 r = e / levels;
+    const int d = int(e - r * levels);
+    out[e] = pts[r * dim + (depth0 + d) % dim];
+  }
+}
+}  // namespace
+
+void reference_level_keys(const float* pts, i64 n, int dim, int depth0, int levels, float* out, hipStream_t stream) {
+  if (n <= 0 || levels <= 0) return;
+  const int g = int(std::min<i64>(8192, (n * levels + kBlock - 1) / kBlock));
+  k_ref_keys_of_levels<<<g, kBlock, 0, stream>>>(pts, n, dim, depth0, levels, out);
   PKD_LAUNCH_CHECK();
 }
 

@@ -974,13 +974,122 @@ void nn_traverse_sel(const float* tree_pts, const u32* tree_ids, i64 n, int dim,
   PKD_LAUNCH_CHECK();
 }
 
+namespace {
+// The reference's search on a high-dimensional tree visits every node: its far-side test
+// (axis distance^2 < best, kdtree_sequential.cpp:114-122) compares ONE coordinate's gap with a
+// squared distance over all of them. If every node's axis gap^2 is below m = min(incoming best,
+// min over the tree's points of d2) -- a bound the best never goes under -- then no far side is
+// ever skipped, the search visits all nodes, and its answer is the first-visited strict minimum:
+// the brute-force minimum when it is unique (or the incoming best when that is not beaten).
+// One thread per slot, the query tile in LDS: flag[q] |= "some gap^2 >= m"; ties[q] counts
+// the slots whose exact d2 equals the brute minimum.
+constexpr int kRefTile = 16;
+__global__ __launch_bounds__(kBlock) void k_ref_visit_all(const float* __restrict__ P, i64 n, int dim, int depth0,
+                                                          const float* __restrict__ queries, i64 nq,
+                                                          const u64* __restrict__ brute, const u64* __restrict__ incoming,
+                                                          u32* __restrict__ flag, u32* __restrict__ ties) {
+  extern __shared__ __align__(16) float qs[];  // [kRefTile][dim]
+  __shared__ float sm[kRefTile], sb[kRefTile];
+  __shared__ u32 sflag[kRefTile], sties[kRefTile];
+  const i64 q0 = i64(blockIdx.y) * kRefTile;
+  const int qt = int(min<i64>(kRefTile, nq - q0));
+  for (int f = threadIdx.x; f < kRefTile * dim; f += kBlock) qs[f] = f < qt * dim ? queries[q0 * dim + f] : 0.0f;
+  if (threadIdx.x < kRefTile) {
+    const int k = threadIdx.x;
+    const float b = k < qt ? packed_dist(brute[q0 + k]) : 0.0f;
+    const float in = k < qt ? packed_dist(incoming[q0 + k]) : 0.0f;
+    sb[k] = b;
+    sm[k] = fminf(b, in);
+    sflag[k] = 0u;
+    sties[k] = 0u;
+  }
+  __syncthreads();
+  for (i64 r = i64(blockIdx.x) * kBlock + threadIdx.x; r < n; r += i64(gridDim.x) * kBlock) {
+    int depth = 0;  // the slot's depth in the implicit tree: its split axis
+    for (i64 lo = 0, cnt = n; lo + cnt / 2 != r; ++depth) {
+      const i64 m = lo + cnt / 2;
+      if (r < m) {
+        cnt = cnt / 2;
+      } else {
+        lo = m + 1;
+        cnt = cnt - cnt / 2 - 1;
+      }
+    }
+    const int axis = (depth0 + depth) % dim;
+    const float* row = P + r * dim;
+    const float pa = row[axis];
+    for (int k = 0; k < qt; ++k) {
+      const float* q = qs + k * dim;
+      const float dax = q[axis] - pa;
+      if (!(dax * dax < sm[k])) atomicOr(&sflag[k], 1u);
+      const float d2 = sq_dist(row, q, dim);  // the reference's sequential no-FMA sum
+      if (d2 == sb[k]) atomicAdd(&sties[k], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < qt) {
+    if (sflag[threadIdx.x]) atomicOr(&flag[q0 + threadIdx.x], 1u);
+    if (sties[threadIdx.x]) atomicAdd(&ties[q0 + threadIdx.x], sties[threadIdx.x]);
+  }
+}
+
+// Per query: the answer when the search provably visits every node with a unique minimum, else
+// the query joins the list the stack walk takes.
+__global__ void k_ref_resolve(const u64* __restrict__ brute, const u32* __restrict__ flag, const u32* __restrict__ ties,
+                              i64 nq, u64* __restrict__ out, u32* __restrict__ sel, u32* __restrict__ sel_count) {
+  const i64 q = i64(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const float b = packed_dist(brute[q]), in = packed_dist(out[q]);
+  if (flag[q] == 0u && (!(b < in) || ties[q] == 1u)) {
+    if (b < in) out[q] = brute[q];
+  } else {
+    sel[atomicAdd(sel_count, 1u)] = u32(q);
+  }
+}
+}  // namespace
+
 void nn_traverse_reference(const float* tree_pts, const u32* tree_ids, i64 n, int dim, int depth0,
                            const float* queries, i64 nq, u64* out, hipStream_t stream) {
   if (nq <= 0 || n <= 0) return;
   TraceRange tr("pkd.nn_traverse_reference");
-  k_traverse<true><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries,
-                                                                          nq, out);
+  const bool visit_all = dim >= 16 && n < (i64(1) << 32) && size_t(kRefTile) * dim * 4 <= size_t(150) * 1024;
+  if (!visit_all) {  // low dims: the walk prunes, and one thread per query walks few nodes
+    k_traverse<true><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0,
+                                                                            queries, nq, out);
+    PKD_LAUNCH_CHECK();
+    return;
+  }
+  // high dims: one thread walking ~all n nodes per query is latency-bound (500 k x 128D: 14.7 s
+  // for 10 queries); the brute minimum and a parallel proof that the walk would visit every node
+  // answer instead, and only the queries without such a proof walk
+  char* w = nullptr;
+  const size_t words = size_t(nq) * 2 + size_t(nq) * 2 + size_t(nq) + 1;  // brute (u64) | flag | ties | sel | count
+  PKD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&w), words * 4 + 64, stream));
+  u64* brute = reinterpret_cast<u64*>(w);
+  u32* flag = reinterpret_cast<u32*>(brute + nq);
+  u32* ties = flag + nq;
+  u32* sel = ties + nq;
+  u32* cnt = sel + nq;
+  PKD_HIP_CHECK(hipMemsetAsync(flag, 0, size_t(2 * nq + nq + 1) * 4, stream));
+  nn_init(brute, nq, stream);
+  nn_brute(tree_pts, tree_ids, 0, n, dim, queries, nq, brute, stream);
+  const i64 tiles = (nq + kRefTile - 1) / kRefTile;
+  const int gx = int(std::min<i64>(std::max<i64>(1, 2048 / tiles), (n + kBlock - 1) / kBlock));
+  const size_t lds = size_t(kRefTile) * dim * 4;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&k_ref_visit_all), int(lds));
+  for (i64 t0 = 0; t0 < tiles; t0 += 65535) {
+    const i64 ty = std::min<i64>(65535, tiles - t0);
+    const i64 off = t0 * kRefTile;
+    k_ref_visit_all<<<dim3(unsigned(gx), unsigned(ty)), kBlock, lds, stream>>>(
+        tree_pts, n, dim, depth0, queries + off * dim, nq - off, brute + off, out + off, flag + off, ties + off);
+    PKD_LAUNCH_CHECK();
+  }
+  k_ref_resolve<<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(brute, flag, ties, nq, out, sel, cnt);
   PKD_LAUNCH_CHECK();
+  k_traverse<true><<<int((nq + kBlock - 1) / kBlock), kBlock, 0, stream>>>(tree_pts, tree_ids, n, dim, depth0, queries,
+                                                                          nq, out, sel, cnt);
+  PKD_LAUNCH_CHECK();
+  PKD_HIP_CHECK(hipFreeAsync(w, stream));
 }
 
 }  // namespace pkdtree

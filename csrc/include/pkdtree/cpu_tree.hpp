@@ -12,6 +12,7 @@
 #pragma once
 #include <cstdint>
 #include <ostream>
+#include <utility>
 #include <vector>
 
 #include "pkdtree/common.hpp"
@@ -26,6 +27,22 @@ void build_exact_cpu(const float* pts, const u32* ids, i64 n, int dim, int depth
 void build_reference_cpu(const float* pts, i64 n, int dim, u32* perm, int threads = 1, int depth0 = 0);
 // Threads the CPU builders use when the caller does not say (hardware threads, at most 64).
 int default_cpu_threads();
+
+// The reference's std::sort(idx, idx + n) by keys[idx] (a bit-exact parallel replica of libstdc++'s
+// introsort: the same permutation, ties included, for any thread count).
+void std_sort_replica(const float* keys, u32* idx, i64 n, int threads = 1);
+
+// Hybrid reference mode. gpu_perm: slot -> input row of a GPU reference-mode tree whose build
+// reported deciding ties (equal keys at ranks m-2..m+1 of a segment: there the reference's
+// unstable std::sort decides) at the segments whose median slots are tied_slots[0, ntied).
+// Only what std::sort's order decides is redone on the host, from the reference's own input
+// order: every ancestor of a tied segment is sorted (its order is what its children start from)
+// and every tied segment's whole subtree is built by build_reference_cpu's recursion; every other
+// subtree (no deciding tie at or below it) keeps the GPU's slots, which are exact there. Writes
+// the complete slot -> row map to perm and returns the slot ranges (start, count) the host decided
+// (the rows the caller must patch into the GPU tree).
+std::vector<std::pair<i64, i64>> reference_repair(const float* pts, i64 n, int dim, int depth0, const u32* gpu_perm,
+                                                  const u32* tied_slots, size_t ntied, u32* perm, int threads);
 
 // Gather rows/ids through a permutation (tree_pts[k] = pts[perm[k]]).
 void gather_rows(const float* pts, const u32* ids, const u32* perm, i64 n, int dim, float* tree_pts,

@@ -26,6 +26,10 @@ class ReferenceBuilder {
   // std::sort decides, so the tree may differ from the reference binary's; 0 = identical for
   // certain. Synchronises `stream`.
   u32 read_ties(const void* workspace, hipStream_t stream) const;
+  // Median slots of the tied segments (at most kTieSlots of them; read_ties() counts them all).
+  // Synchronises `stream`.
+  static constexpr u32 kTieSlots = 1u << 18;
+  std::vector<u32> read_tie_slots(const void* workspace, hipStream_t stream) const;
 
  private:
   struct RefLevel {
@@ -42,5 +46,15 @@ class ReferenceBuilder {
   size_t off_perm_[2] = {0, 0}, off_keys_ = 0, off_midc_ = 0, off_hist_ = 0, off_segs_ = 0, off_words_ = 0,
          off_hpart_ = 0, ws_bytes_ = 0;
 };
+
+// Writes input row rows[k] (coordinates from pts [*, dim], id ids[row] or id_base + row) to tree
+// slot slots[k] for k < count (device arrays): the host-decided slots of a repaired tree.
+void reference_patch(const float* pts, const u32* ids, u32 id_base, int dim, const u32* slots, const u32* rows,
+                     i64 count, float* out_pts, u32* out_ids, hipStream_t stream);
+
+// out [n][levels] (device) = the split key of every tree level: out[r][d] = pts[r][(depth0 + d) % dim].
+// For levels <= dim this is all a host reference build of the tree reads (its axis at depth d is
+// column d with depth0 0 and `levels` columns): high-dimensional inputs travel as ~20 columns, not dim.
+void reference_level_keys(const float* pts, i64 n, int dim, int depth0, int levels, float* out, hipStream_t stream);
 
 }  // namespace pkdtree

@@ -133,6 +133,14 @@ class ReferenceTreeBuilder:
         unstable std::sort decides: the tree may differ from the binary's). Synchronises."""
         return int(self._b.read_ties())
 
+    def read_tie_slots(self):
+        """Median slots of the last build's tied segments (at most ``tie_slots_cap`` of them)."""
+        return list(self._b.read_tie_slots())
+
+    @property
+    def tie_slots_cap(self) -> int:
+        return int(self._b.tie_slots_cap)
+
     @property
     def global_levels(self) -> int:
         return int(self._b.global_levels)
@@ -209,22 +217,51 @@ def check_unique_ids(ids: Optional[torch.Tensor]) -> None:
 
 def build_reference_gpu_checked(points: torch.Tensor, ids: Optional[torch.Tensor] = None, id_base: int = 0,
                                 depth0: int = 0):
-    """The reference tree on the GPU; if equal keys decided any segment (std::sort is unstable,
-    so there the reference binary's tree is its library's choice), the tree is rebuilt by the
-    CPU std::sort builder, which mirrors the binary, with a warning. Returns (tree_pts,
-    tree_ids, ties). Synchronises."""
+    """The reference tree on the GPU. Where equal keys decided a segment (std::sort is unstable,
+    so there the reference binary's tree is its library's introsort's choice, which depends on
+    the segment's exact input order), the tree is REPAIRED on the host: the sorts of the tied
+    segments' ancestors and the tied subtrees are replayed with a bit-exact replica of std::sort
+    (native reference_repair) and only those slots are patched; every other subtree keeps the
+    GPU's slots. A warning names the tie count. Returns (tree_pts, tree_ids, ties). Synchronises."""
     import warnings
     points = points.contiguous()
     b = reference_builder(points.shape[0], points.shape[1], depth0, points.device)
     tp, ti = b.build(points, ids, id_base)
     ties = b.read_ties()
     if ties:
+        n, dim = points.shape
+        cids = ids.to(torch.int64) if ids is not None else None
+        # the host sorts read one key per row and level: only the levels' columns travel when the
+        # rows are wider (500 k x 128D: 19 of 128 columns); their axis at depth d is then column d
+        levels = max(1, int(n).bit_length())
+        if levels < dim:
+            host = points[:, [(depth0 + d) % dim for d in range(levels)]].cpu()
+            hdepth0 = 0
+        else:
+            host, hdepth0 = points.cpu(), depth0
+        if ties <= b.tie_slots_cap:
+            # the GPU tree's slot -> input row (ids are distinct: invert them through a scatter)
+            if cids is None:
+                rows = (ti.to(torch.int64) - id_base).to(torch.int32).cpu()
+            else:
+                inv = torch.empty(int(cids.max()) - int(cids.min()) + 1, dtype=torch.int64, device=cids.device)
+                inv[cids - int(cids.min())] = torch.arange(n, device=cids.device)
+                rows = inv[ti.to(torch.int64) - int(cids.min())].to(torch.int32).cpu()
+            perm, slots = native().reference_repair(host, rows, b.read_tie_slots(), int(hdepth0), cpu_threads())
+            sl = slots.to(points.device)
+            rw = perm.to(points.device).to(torch.int64)[sl]
+            tp[sl] = points[rw]
+            ti[sl] = (rw + id_base).to(torch.int32) if ids is None else ids.to(points.device)[rw].to(torch.int32)
+            how = f"replayed their sorts on the host and patched {slots.numel()} of {n} slots"
+        else:
+            hids = (torch.arange(n, dtype=torch.int64) + id_base).to(torch.int32) if ids is None else ids.cpu()
+            _, perm = build_cpu(host, torch.arange(n, dtype=torch.int32), "reference", hdepth0, cpu_threads())
+            rw = perm.to(points.device).to(torch.int64)
+            tp = points[rw].contiguous()
+            ti = hids.to(points.device)[rw].contiguous()
+            how = "rebuilt the tree with the threaded host std::sort builder"
         warnings.warn(f"reference mode: {ties} segment(s) of this input are decided by equal keys, where the "
-                      "reference's unstable std::sort picks the order; using the CPU std::sort builder",
-                      RuntimeWarning, stacklevel=2)
-        cids = ids if ids is not None else (torch.arange(points.shape[0], dtype=torch.int64) + id_base).to(torch.int32)
-        cp, ci = build_cpu(points.cpu(), cids.cpu(), "reference", depth0, cpu_threads())
-        tp, ti = cp.to(points.device), ci.to(points.device)
+                      f"reference's unstable std::sort picks the order; {how}", RuntimeWarning, stacklevel=2)
     return tp, ti, ties
 
 

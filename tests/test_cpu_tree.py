@@ -147,3 +147,80 @@ def test_reference_depth0():
     pr, ir = ops.build_cpu(xr, ids, "reference", 0, 1)
     assert torch.equal(i2, ir)
     assert not torch.equal(i2, i0)
+
+
+@pytest.mark.parametrize("n,vals", [(0, 3), (1, 3), (17, 2), (100, 5), (5000, 3), (5000, 10_000), (200_000, 7),
+                                    (300_000, 1 << 30), (1_000_003, 1000)])
+def test_std_sort_replica_is_bit_exact(n, vals):
+    """The parallel replica of libstdc++'s std::sort (introsort) returns std::sort's permutation
+    itself -- the order it leaves equal keys in included -- for any thread count. Duplicate-heavy
+    keys exercise the unguarded partitions; 2 distinct values drive the heapsort fallback."""
+    g = torch.Generator().manual_seed(n + vals)
+    keys = torch.randint(0, vals, (n,), generator=g).float()
+    ref = ops.native().sort_indices(keys, False, 1)
+    for th in (1, 4, 32):
+        assert torch.equal(ops.native().sort_indices(keys, True, th), ref), th
+    s = keys[ref.long()]
+    assert bool((s[1:] >= s[:-1]).all())
+
+
+def test_std_sort_replica_adversarial_depth_limit():
+    """An organ-pipe input (median-of-three killer shape) and all-equal keys: the depth limit's
+    heapsort and the unguarded scans both run; still std::sort's exact permutation."""
+    n = 1 << 17
+    organ = torch.cat([torch.arange(n // 2), torch.arange(n // 2, 0, -1)]).float()
+    same = torch.zeros(n)
+    for keys in (organ, same, organ.flip(0)):
+        ref = ops.native().sort_indices(keys.contiguous(), False, 1)
+        assert torch.equal(ops.native().sort_indices(keys.contiguous(), True, 16), ref)
+
+
+def _tie_segments(x, depth0=0):
+    """Median slots of the segments of the reference tree of x whose deciding ranks tie (host
+    recursion over the reference's own order, for small inputs)."""
+    n, dim = x.shape
+    perm = list(range(n))
+    out = []
+
+    def rec(lo, m, d):
+        if m < 3:
+            return
+        ax = (depth0 + d) % dim
+        seg = sorted(perm[lo:lo + m - 1], key=lambda r: float(x[r, ax]))  # (stable: only the tie set matters)
+        k = [float(x[r, ax]) for r in seg]
+        h = m // 2
+        if k[h - 1] == k[h] or (h >= 2 and k[h - 2] == k[h - 1]) or (h + 1 <= m - 2 and k[h] == k[h + 1]):
+            out.append(lo + h)
+        perm[lo:lo + m - 1] = seg
+        rec(lo, h, d + 1)
+        rec(lo + h + 1, m - h - 1, d + 1)
+
+    rec(0, n, 0)
+    return out
+
+
+@pytest.mark.parametrize("n,vals,dim", [(3000, 40, 3), (5000, 9, 2), (2047, 300, 4), (20000, 20000, 3)])
+def test_reference_repair_restores_tied_subtrees(n, vals, dim):
+    """reference_repair (the hybrid reference mode's host half): given a tree that is right
+    everywhere except inside the subtrees of the tied segments (here: the true reference tree with
+    every tied subtree's slots scrambled), replaying the ancestors' sorts and the tied subtrees
+    with the std::sort replica restores the reference tree exactly, touching only those slots."""
+    g = torch.Generator().manual_seed(n * vals + dim)
+    x = torch.randint(0, vals, (n, dim), generator=g).float()
+    ids = torch.arange(n, dtype=torch.int32)
+    _, ref_rows = ops.build_cpu(x, ids, "reference", 0, 1)
+    tied = _tie_segments(x)
+    assert tied, "the input is meant to have deciding ties"
+    bad = ref_rows.clone()
+    from parallel_kd_tree_amd.parallel.geometry import segment
+    for s in tied:  # scramble the whole subtree of every tied segment (what an arbitrary tie order does)
+        h, lo, m = 0, 0, n
+        while lo + m // 2 != s:
+            h = 2 * h + (1 if s < lo + m // 2 else 2)
+            lo, m = segment(n, h)
+        bad[lo:lo + m] = bad[lo:lo + m].flip(0)
+    perm, slots = ops.native().reference_repair(x, bad, tied, 0, 8)
+    assert torch.equal(perm, ref_rows)
+    assert slots.numel() > 0
+    if n // 2 not in tied:  # (a tied root makes the whole tree the host's)
+        assert slots.numel() < n
