@@ -53,7 +53,18 @@ def test_bench_three_ranks():
     assert r.returncode == 0, r.stderr
     j = _one_json(r.stdout)
     assert j["n_gpus"] == 3 and j["config"]["parallelism"] == "global3" and j["config"]["tree_checked"]
-    assert j["metric"].endswith("(not the headline config)") and j["config"]["headline"] is False
+    assert "(not the headline config)" in j["metric"] and j["config"]["headline"] is False
+    # a host rehearsal is labelled as one, never as a GPU measurement
+    assert "rehearsal" in j["metric"] and j["config"]["shared_gpu"] is False
+
+
+def test_bench_headline_rehearsal_is_labelled():
+    """The headline config run as a host (gloo) rehearsal: same metric stem, but labelled and
+    headline false, so it can never pass for the 100 M x 3D measurement."""
+    r = _bench("--gpus", "2", "--device", "cpu", "--points", "20000", "--steps", "1", "--warmup", "0")
+    assert r.returncode == 0, r.stderr
+    j = _one_json(r.stdout)
+    assert j["config"]["headline"] is False and "rehearsal" in j["metric"]
 
 
 def test_bench_launcher_propagates_rank_failure():
