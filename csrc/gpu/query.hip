@@ -500,15 +500,25 @@ struct MfScratchKey {
   hipStream_t stream;
   bool operator<(const MfScratchKey& o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
 };
+// The cache is bounded (kMfScratchMax entries, least recently used evicted): a program that creates
+// and destroys streams (per-builder streams, loopback tests) does not grow it without limit. An
+// evicted buffer is released with hipFree, which waits for the device, so a batch still in
+// flight on a stream that is gone (or not) finishes first. Host threads that share one stream
+// handle (the null stream, hipStreamPerThread) share its buffer: their batches are ordered on it.
+constexpr size_t kMfScratchMax = 16;
 mf::Scratch* mf_scratch(hipStream_t stream, bool* transient) {
   static std::mutex mu;
-  static std::map<MfScratchKey, mf::Scratch*> cache;
+  static std::map<MfScratchKey, std::pair<mf::Scratch*, u64>> cache;  // buffer, last use
+  static u64 tick = 0;
   int dev = 0;
   PKD_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(MfScratchKey{dev, stream});
   *transient = false;
-  if (it != cache.end()) return it->second;
+  if (it != cache.end()) {
+    it->second.second = ++tick;
+    return it->second.first;
+  }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   PKD_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
   mf::Scratch* s = nullptr;
@@ -517,8 +527,18 @@ mf::Scratch* mf_scratch(hipStream_t stream, bool* transient) {
     *transient = true;
     return s;
   }
+  if (cache.size() >= kMfScratchMax) {
+    auto lru = cache.begin();
+    for (auto c = cache.begin(); c != cache.end(); ++c)
+      if (c->second.second < lru->second.second) lru = c;
+    int cur = dev;
+    PKD_HIP_CHECK(hipSetDevice(lru->first.dev));
+    PKD_HIP_CHECK(hipFree(lru->second.first));
+    PKD_HIP_CHECK(hipSetDevice(cur));
+    cache.erase(lru);
+  }
   PKD_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s), sizeof(mf::Scratch)));
-  cache[MfScratchKey{dev, stream}] = s;
+  cache[MfScratchKey{dev, stream}] = {s, ++tick};
   return s;
 }
 }  // namespace

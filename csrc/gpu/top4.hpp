@@ -20,10 +20,12 @@
 //             bin's rows are collected and radix-selected: the exact median. Staged rows are
 //             routed by it to the next level;
 //   insert    staged rows fill the remaining slots of their level-4 segments.
-// A band that misses its median (probability ~1e-12 per node at the default z for any input
-// order, since the sample positions are random) is DETECTED (counts do not bracket the median
-// rank) and reported in the error word (bit kErrBit); callers rebuild with PKD_TOP=0. Ties are
-// exact: bands are inclusive key ranges and the median is selected on the composite key.
+// A band that misses its median (~2e-9 per node at the default z = 6 for any input order, since
+// the sample positions are random; always on duplicate-heavy data whose median arenas are too
+// large to stream) is DETECTED (counts do not bracket the median rank) and reported in the error
+// word (bit kErrBit); every later kernel of the build then returns at once (dev::build_failed)
+// and callers rebuild unsampled. Ties are exact: bands are inclusive key ranges and the median is
+// selected on the composite key.
 // Replaces build_tree_rec's top four levels of std::sort (kdtree_sequential.cpp:30-66).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -70,7 +72,7 @@ struct IO {
 
 struct Tune {
   int sample_log2 = 0;  // sample rows = 2^sample_log2 (capped at n / 4); 0: by size (2^20 at 100 M)
-  float z = 9.0f;        // band half-width in sample-rank standard deviations (PKD_TOP_Z)
+  float z = 6.0f;        // band half-width in sample-rank standard deviations (the builder passes Tuning::top_z)
   int scatter_blocks = 0;  // 0: by size
   // Diagnostics (PKD_TOP_DIAG; timing only, the tree is NOT built): 1 stop after the scatter,
   // 2 the same with the scatter's reservation atomics replaced by in-range tile offsets, 3 also
