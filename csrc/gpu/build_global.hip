@@ -3881,11 +3881,18 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
 // pivot key or the row is a median-bin candidate): 32 fewer registers per 16 items, so the
 // 16-item shape of the 1 B build spills 120 instead of 212 bytes per lane (the 12-item one none).
 // IDS: ids in registers (default unless SLIM); SLIM with IDS keeps the two key sets and the ids.
-template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM>
+// LEV = 4 (8-D builds: 17 global levels leave 13 between the top and the tail, three triples
+// and a 4-level tail instead of two triples, two pairs and a 3-level tail): the same steps for
+// one more level (8 sub-segments at the last one, 16 leaves), SLIM: level t's keys in register
+// set t & 1, reloaded for levels 2 and 3.
+template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM, int LEV = 3>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
   constexpr int T = kTailThreads, W = T / 64, CAP = T * ITEMS, NB = kTailBins, G = ITEMS / 4;
   static_assert(!SLIM || D >= 3, "slim registers need three distinct level axes");
+  static_assert(LEV == 3 || LEV == 4, "3 or 4 tail levels");
+  static_assert(LEV == 3 || D < 3 || SLIM, "4 levels keep two key register sets");
+  constexpr int NS = 1 << (LEV - 1), NLEAF = 1 << LEV, NNODE = NLEAF - 1, NALL = 2 * NLEAF - 1;
   // columns kept in registers: every column for D < 3, else the three levels' key columns (SLIM: two sets)
   constexpr int KC = D < 3 ? D : (SLIM ? 2 : 3);
   constexpr u32 kDead = 0xffffffffu, kMed = 0x80000000u;  // absent row / median of tail node (low bits)
@@ -3893,13 +3900,13 @@ void k_tail3(TailArgs a) {
   static_assert(CAP >= NB, "the stage buffer holds the bins");
   extern __shared__ __align__(16) u32 stage[];  // CAP words: the output columns; bins / counters alias it
   u32* bins = stage;
-  __shared__ u32 ckey[4][kTailCand], cid[4][kTailCand];
-  __shared__ u32 ccnt[4], sbst[4], srank[4], wsum[W];
-  __shared__ unsigned long long spiv[4];
-  __shared__ float scell[2][8][D][2];  // cells of the level's sub-segments / of their children
-  __shared__ BucketParams sprm[4];
-  __shared__ i64 nlo[15];              // segment starts of the tail's 15 nodes (heap order below h)
-  __shared__ u32 nn[15];
+  __shared__ u32 ckey[NS][kTailCand], cid[NS][kTailCand];
+  __shared__ u32 ccnt[NS], sbst[NS], srank[NS], wsum[W];
+  __shared__ unsigned long long spiv[NS];
+  __shared__ float scell[2][NLEAF][D][2];  // cells of the level's sub-segments / of their children
+  __shared__ BucketParams sprm[NS];
+  __shared__ i64 nlo[NALL];                // segment starts of the tail's nodes and leaves (heap order below h)
+  __shared__ u32 nn[NALL];
   __shared__ u32 sbig, failed;
   dev::build_failed_issue(a.err, &failed);  // tested after the first barrier (level 0)
   const int tid = threadIdx.x, w = tid / 64, ln = dev::lane();
@@ -3928,9 +3935,9 @@ void k_tail3(TailArgs a) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, vo, u32(g * T * 16), 0);
   };
   // every row's level keys and id, loaded at once (the whole segment in flight)
-  int axis_of[3];
+  int axis_of[LEV];
 #pragma unroll
-  for (int t = 0; t < 3; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
+  for (int t = 0; t < LEV; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
   float xs[KC][ITEMS];
   u32 ids[IDS ? ITEMS : 1];
 #pragma unroll
@@ -3956,8 +3963,8 @@ void k_tail3(TailArgs a) {
     if constexpr (!IDS) return __builtin_amdgcn_raw_buffer_load_b32(rid, vo + u32(i % 4) * 4u, u32(i / 4 * T * 16), 0);
     else return ids[i];
   };
-  if (tid < 15) {  // node k (heap order: 0 = h, 1-2 children, 3-6 grandchildren, 7-14 leaves)
-    const int lev = tid >= 7 ? 3 : (tid >= 3 ? 2 : (tid >= 1 ? 1 : 0));
+  if (tid < NALL) {  // node k (heap order below h: 0 = h, 1-2 children, ..., NNODE.. the leaves)
+    const int lev = 31 - __builtin_clz(u32(tid) + 1u);
     const i64 hk = (h + 1) * (i64(1) << lev) - 1 + (tid - ((1 << lev) - 1));
     nlo[tid] = a.seg_lo[hk];
     nn[tid] = u32(a.seg_n[hk]);
@@ -3972,7 +3979,7 @@ void k_tail3(TailArgs a) {
     path[i] = (r >= 0 && r < n) ? 0u : kDead;
   }
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
+  for (int t = 0; t < LEV; ++t) {
     // the thread index, opaque per level: addresses derived from it (LDS and global, of the
     // few-thread steps) are recomputed per level instead of held in registers across levels
     int tq = tid;
@@ -3982,17 +3989,17 @@ void k_tail3(TailArgs a) {
     static_assert(NB == 4096, "lgB");
     const int axis = axis_of[t];
     const int kx = D < 3 ? axis : (SLIM ? (t & 1) : t);  // register set of this level's keys
-    if (SLIM && t == 2) {  // level 2's keys into level 0's (dead) registers
+    if (SLIM && t >= 2) {  // level t's keys into level t - 2's (dead) registers
       const auto r = col(a.src, axis);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const auto v = ld4(r, g);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xs[0][4 * g + j] = __uint_as_float(v[j]);
+        for (int j = 0; j < 4; ++j) xs[t & 1][4 * g + j] = __uint_as_float(v[j]);
       }
     }
     for (int b = tq; b < NB; b += T) bins[b] = 0;
-    if (tq < 4) {
+    if (tq < NS) {
       ccnt[tq] = 0;
       sbst[tq] = 0xffffffffu;
       spiv[tq] = ~0ull;
@@ -4006,7 +4013,7 @@ void k_tail3(TailArgs a) {
       sprm[tq] = make_params(c[0], c[1], B);
     }
     __syncthreads();
-    tail_stamp(a, 1 + 4 * t);
+    if (t < 3) tail_stamp(a, 1 + 4 * t);  // (level 3 of a 4-level tail: counted in move.rank)
     // ---- bins ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -4041,7 +4048,7 @@ void k_tail3(TailArgs a) {
       }
     }
     __syncthreads();
-    tail_stamp(a, 2 + 4 * t);
+    if (t < 3) tail_stamp(a, 2 + 4 * t);  // (level 3 of a 4-level tail: counted in move.rank)
     // ---- candidates of the median bins: (key, id) straight from registers ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -4073,12 +4080,12 @@ void k_tail3(TailArgs a) {
     if (sbig) {
       // radix select over the composite (key, id) of every sub-segment's median-bin rows,
       // 8 bits per pass from the top (ids are distinct, so 8 passes leave one row)
-      if (tq < 4) spiv[tq] = 0;
+      if (tq < NS) spiv[tq] = 0;
 #pragma unroll 1
       for (int pass = 0; pass < 8; ++pass) {
         const int sh = 56 - 8 * pass;
         const u64 known = pass == 0 ? 0ull : (~0ull << (sh + 8));  // digits fixed by earlier passes
-        for (int b = tq; b < 4 * 256; b += T) bins[b] = 0;
+        for (int b = tq; b < NS * 256; b += T) bins[b] = 0;
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
@@ -4116,7 +4123,7 @@ void k_tail3(TailArgs a) {
         __syncthreads();
       }
     }
-    tail_stamp(a, 3 + 4 * t);
+    if (t < 3) tail_stamp(a, 3 + 4 * t);  // (level 3 of a 4-level tail: counted in move.rank)
     // ---- classify: left / right of the pivot; the median row is marked (written with the columns) ----
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -4150,30 +4157,30 @@ void k_tail3(TailArgs a) {
       }
     }
     __syncthreads();
-    tail_stamp(a, 4 + 4 * t);
+    if (t < 3) tail_stamp(a, 4 + 4 * t);  // (level 3 of a 4-level tail: counted in move.rank)
   }
   // ---- move: position inside the leaf (one LDS counter per 16 lanes and leaf), then each
   // column staged through LDS in leaf order and written back coalesced ----
   constexpr int kGroups = W * 4;
-  static_assert(CAP >= kGroups * 8, "counters in the stage buffer");
-  __shared__ u32 gbase[kGroups][8];
+  static_assert(CAP >= kGroups * NLEAF, "counters in the stage buffer");
+  __shared__ u32 gbase[kGroups][NLEAF];
   u32* gcnt = stage;
   const int grp = tid / 16;
-  if (tid < kGroups * 8) gcnt[tid] = 0;
+  for (int k = tid; k < kGroups * NLEAF; k += T) gcnt[k] = 0;
   __syncthreads();
   // (leaf << 24) | rank among the 16-lane group's rows of that leaf, in place of the leaf index
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i)
-    if (path[i] < kMed) path[i] = (path[i] << 24) | atomicAdd(&gcnt[grp * 8 + path[i]], 1u);
+    if (path[i] < kMed) path[i] = (path[i] << 24) | atomicAdd(&gcnt[grp * NLEAF + path[i]], 1u);
   __syncthreads();
-  if (tid < 8) {
-    const u32 first = u32(nlo[7 + tid] - lo);
+  if (tid < NLEAF) {
+    const u32 first = u32(nlo[NNODE + tid] - lo);
     u32 off = first;
     for (int k = 0; k < kGroups; ++k) {
       gbase[k][tid] = off;
-      off += gcnt[k * 8 + tid];
+      off += gcnt[k * NLEAF + tid];
     }
-    if (off - first != nn[7 + tid]) atomicOr(a.err, 16u);
+    if (off - first != nn[NNODE + tid]) atomicOr(a.err, 16u);
   }
   __syncthreads();
 #pragma unroll
@@ -4185,8 +4192,8 @@ void k_tail3(TailArgs a) {
     // column c: from registers (a level's keys or the ids), else loaded
     int kreg = -1;
 #pragma unroll
-    for (int k = 0; k < KC; ++k)  // (SLIM: set 0 holds level 2's keys by now, set 1 level 1's)
-      if ((D < 3 ? k : (SLIM ? axis_of[k == 0 ? 2 : 1] : axis_of[k])) == c) kreg = k;
+    for (int k = 0; k < KC; ++k)  // (SLIM: set k holds the keys of the last level t with t & 1 == k)
+      if ((D < 3 ? k : (SLIM ? axis_of[((LEV - 1) & 1) == k ? LEV - 1 : LEV - 2] : axis_of[k])) == c) kreg = k;
     u32 v[ITEMS];
     if (c == D && IDS) {
 #pragma unroll
@@ -4353,6 +4360,7 @@ Tuning Tuning::from_env() {
   t.atomic_ranks3 = int(ab_i("PKD_PART3_ATOMIC", -1));
   t.prefix = ab_i("PKD_PART_PREFIX", 1) != 0;
   t.tail = ab_i("PKD_TAIL", 1) != 0;
+  t.tail4 = ab_i("PKD_TAIL4", 1) != 0;
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
   t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
@@ -4503,11 +4511,11 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     // registers (dim <= 8, full columns).
     // (A split build's parts start at split_level: the tail may not begin above it.)
     const bool may_split0 = tune_.split && opt.allow_split && n_ >= tune_.split_min(dim);
-    if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - 3 >= tune_.split_level)) {
-      const i64 nl = (n_ >> (lg_ - 3)) + 3;  // + the 16-B alignment shift of the segment start
+    if (tune_.tail && pairs && !narrow_ && lg_ >= 5 && (!may_split0 || lg_ - tail_lev_ >= tune_.split_level)) {
+      const i64 nl = (n_ >> (lg_ - tail_lev_)) + 3;  // + the 16-B alignment shift of the segment start
       tail_items_ = nl <= 8 * 1024 ? 8 : (nl <= 12 * 1024 ? 12 : (nl <= 16 * 1024 ? 16 : 0));
       if (tail_items_ > 0) {
-        tail_ = lg_ - 3;
+        tail_ = lg_ - tail_lev_;
         for (int l = tail_; l < lg_; ++l) lv[size_t(l)].tail = true;
       }
     }
@@ -4557,6 +4565,29 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     }
     return lv;
   };
+  // A 4-level tail where it leaves one row-moving pass fewer between the top and the tail (100 M x
+  // 8D: 17 levels = 4 sampled + 3 triples + 4, instead of 4 + 2 triples + 2 pairs + 3): both plans
+  // are laid out and their passes counted. Rows of 5..9 columns (the 4-level kernel keeps two key
+  // register sets), segments of <= 16 Ki rows at its first level.
+  auto passes = [&](const std::vector<LevelPlan>& lv) {
+    int c = 0;
+    const int lend = tail_ >= 0 ? tail_ : lg_;
+    for (int l = 0; l < lend; ++c) l += lv[size_t(l)].sampled ? top4::kLevels : (lv[size_t(l)].triple ? 3 : (lv[size_t(l)].pair ? 2 : 1));
+    return c;
+  };
+  if (tune_.tail4 && tune_.tail && dim >= 4 && dim <= 8 && !narrow_ && lg_ >= 9 && (n_ >> (lg_ - 4)) + 3 <= 16 * 1024) {
+    tail_lev_ = 3;
+    const int p3 = passes(make_plan(top_));
+    const bool had3 = tail_ >= 0;
+    tail_ = -1;
+    tail_lev_ = 4;
+    const int p4 = passes(make_plan(top_));
+    if (!(had3 && tail_ >= 0 && p4 < p3)) tail_lev_ = 3;
+    tail_ = -1;
+    tail_items_ = 0;
+    g3_ = false;
+    g3_segs = g3_multi_segs = 0;
+  }
   levels_ = make_plan(top_);
   if (top_) levels_nt_ = make_plan(false);
   for (const auto* plan : {&levels_, &levels_nt_})
@@ -5228,6 +5259,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           // one 1024-thread workgroup per CU (128 registers): the two-per-CU shape (64 registers)
           // spills and was slower (100M x 3D k_tail3 1.41 vs 1.32 ms, profiles/r3_tail.txt)
           // (16 items: two key sets and ids on demand, else the 128 registers spill)
+          if constexpr (D >= 4) {
+            if (tail_lev_ == 4) {  // (two key register sets: the SLIM shape, ids read where keys tie)
+              if (tail_items_ == 8) go(&k_tail3<D, 8, 4, true, false, 4>);
+              else if (tail_items_ == 12) go(&k_tail3<D, 12, 4, true, false, 4>);
+              else go(&k_tail3<D, 16, 4, true, false, 4>);
+              return;
+            }
+          }
           if constexpr (D >= 3) {
             if (tail_items_ == 8) go(&k_tail3<D, 8, 4>);
             else if (tail_items_ == 12 && tune_.tail_slim12 == 0) go(&k_tail3<D, 12, 4>);

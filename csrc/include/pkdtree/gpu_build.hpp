@@ -57,6 +57,7 @@ struct Tuning {
   int atomic_ranks3 = -1;     //   wave ballots (0); PKD_PART3_ATOMIC the same for triples; -1: by n
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool tail = true;           // PKD_TAIL=0: the last three global levels by pairs / triples instead of k_tail3
+  bool tail4 = true;          // PKD_TAIL4=0: never a 4-level tail (it replaces two pairs by a triple at 8-D)
   int tail_slim12 = 0;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids, 1 two key sets (no ids), 2 two key sets + ids
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
@@ -223,8 +224,9 @@ class GpuBuilder {
   i64 max_hist_ = 0;
   i64 max_hist2_ = 0;
   bool narrow_ = false;  // high-dim: narrow columns + key-slot subtree (capacity nsub_ sized for it)
-  int tail_ = -1;        // first of the last three global levels, built by k_tail3 (-1: none)
+  int tail_ = -1;        // first of the last tail_lev_ global levels, built by k_tail3 (-1: none)
   int tail_items_ = 0;   // rows per thread of its 1024-thread workgroups
+  int tail_lev_ = 3;     // levels of the tail: 4 where that leaves whole triples between the top and it (8-D)
   int scan_div_ = 1;     // the key sweeps run on 1 / scan_div_ of a level's partition blocks
   bool top_ = false;     // levels 0..3 by the sampled top pass (AoS input builds)
   mutable u32 top_salt_ = 0;  // per-build salt of the sample positions: a miss is never input-determined
