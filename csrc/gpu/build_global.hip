@@ -2252,8 +2252,8 @@ __global__ __launch_bounds__(kBlock) void k_scan2(LevelArgs a, TripleArgs ta) {
 }
 
 // Pass of a triple: a = level l (src -> dst); grandchildren (heap 4h + 3 + g) receive the rows.
-template <int NCOL, int KI, bool ATOM = true>
-__global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs ta) {
+template <int NCOL, int KI, bool ATOM = true, int NH = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NH > 0 ? 4 : 1))) void k_partition3(LevelArgs a, TripleArgs ta) {
   if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
   constexpr int kChunk = kBlock * KI;
@@ -2261,7 +2261,14 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
   constexpr int D = NCOL - 1;
   static_assert(kItems % 4 == 0, "16-B row loads take 4 rows per item group");
   constexpr int W = kBlock / 64;
-  extern __shared__ __align__(16) u32 nh[];  // [8 * bins3]
+  constexpr bool STG = !ATOM && NH > 0;  // stores through an LDS tile in zone order (as k_g3_part)
+  constexpr int NP = STG ? NH : 1;
+  constexpr int HI = KI / NP;
+  constexpr int HROWS = kBlock * HI;
+  static_assert(KI % NP == 0, "whole items per part");
+  constexpr int PK = STG ? 2 : 1;  // counts per histogram word (STG: 16-bit, blocks of < 64 Ki rows)
+  extern __shared__ __align__(16) u32 nh[];  // [8 * bins3], then (STG) the tile
+  __shared__ u32 zb_s[16], ztot_s[16], zpst[NP][16], zls[16];
   // Zone ranks: every row takes its rank inside (wave, zone) from one LDS atomic on the wave's
   // counter of its zone (16 counters per wave, the last one for rows that stay behind); after
   // a barrier the waves' counts are scanned per zone and reserved in the grandchild's zone.
@@ -2280,7 +2287,7 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
   const int nb3 = ta.bins3;
   const bool fuse = nb3 > 0;
   if (fuse)
-    for (int b = threadIdx.x; b < 8 * nb3; b += kBlock) nh[b] = 0;
+    for (int b = threadIdx.x; b < (8 * nb3 + PK - 1) / PK; b += kBlock) nh[b] = 0;
   const i64 g0 = 4 * h + 3;  // heap index of the first grandchild
   if (threadIdx.x < W * 16) (&wcnt[0][0])[threadIdx.x] = 0;
   if (threadIdx.x < 4) {
@@ -2383,7 +2390,8 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
       const u32 zz = q % 3;
       if (fuse && q < u32(NZ) && zz != 1) {
         const u32 gg = 2 * (q / 3) + (zz == 2 ? 1u : 0u);
-        atomicAdd(&nh[gg * u32(nb3) + bucket_of(k3, ggp[gg], nb3)], 1u);
+        const u32 hb = gg * u32(nb3) + bucket_of(k3, ggp[gg], nb3);
+        atomicAdd(&nh[hb / PK], STG ? 1u << ((hb & 1u) * 16) : 1u);
       }
       if (__ballot(q < u32(NZ) && zz == 1)) {  // level l+2 middle zones: track their composite key ranges
         const u64 ck = composite_key(k2, id);
@@ -2413,7 +2421,18 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
       for (int k = 0; k < ZW; ++k) {
         const int z = w + k * W;
         const u32 b = __shfl(base, k, 64);
-        if (z < NZ) gcnt[z][ln] = b + incl[k] - v[k];
+        if (z < NZ) gcnt[z][ln] = (STG ? 0u : b) + incl[k] - v[k];  // STG: offset inside the chunk's zone run
+        if constexpr (STG) {
+          u32 ps[NP];
+#pragma unroll
+          for (int hp = 0; hp < NP; ++hp) ps[hp] = hp == 0 ? 0u : u32(__shfl(int(incl[k]), hp * HI * W - 1, 64));
+          if (z < NZ && ln == 0) {
+            zb_s[z] = b;
+            ztot_s[z] = tot[k];
+#pragma unroll
+            for (int hp = 0; hp < NP; ++hp) zpst[hp][z] = ps[hp];
+          }
+        }
       }
     } else if (threadIdx.x < NZ) {  // thread z: zone z's waves, scanned, reserved in the grandchild at once
       const int z = int(threadIdx.x);
@@ -2433,26 +2452,65 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
     }
     if (ATOM && threadIdx.x >= NZ && threadIdx.x < NZ + W) wcnt[threadIdx.x - NZ][15] = 0;
     __syncthreads();
+    if constexpr (STG) {
+      float* tile = reinterpret_cast<float*>(nh + ((max(1, (8 * nb3 + 1) / 2) + 3) & ~3));
+      unsigned char* tz = reinterpret_cast<unsigned char*>(tile + NCOL * HROWS);
 #pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      const u32 zi = zone_pre[i] >> 16;
-      i64 dest = -1;
-      if (zi < u32(NZ)) {
-        const u32 gi = zi / 3;
-        const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
-        if (i64(off) >= gn[gi]) {
-          atomicOr(a.err, 1u);
-        } else {
-          dest = glo[gi] + off;
+      for (int hp = 0; hp < NP; ++hp) {
+        const u32 ch = ln < NZ ? (hp + 1 < NP ? zpst[hp + 1 < NP ? hp + 1 : 0][ln] : ztot_s[ln]) - zpst[hp][ln] : 0u;
+        const u32 inc = dev::wave_incl_scan(ch);
+        const u32 ex = inc - ch;
+        if (w == 0 && ln < NZ) zls[ln] = ex;
+        if (w == 0 && ln == NZ - 1) zls[NZ] = inc;
+#pragma unroll
+        for (int ii = 0; ii < HI; ++ii) {
+          const int i = hp * HI + ii;
+          const u32 zi = zone_pre[i] >> 16;
+          const u32 zs = zi < u32(NZ) ? zi : 0u;
+          const u32 exz = u32(__shfl(int(ex), int(zs), 64));
+          if (zi >= u32(NZ)) continue;
+          const u32 p = exz + gcnt[zs][i * 4 + w] - zpst[hp][zs] + (zone_pre[i] & 0xffffu);
+#pragma unroll
+          for (int c = 0; c < NCOL; ++c) tile[c * HROWS + p] = row[i][c];
+          tz[p] = (unsigned char)zi;
         }
-      }
+        __syncthreads();
+        const u32 T = zls[NZ];
+        for (u32 j = threadIdx.x; j < T; j += kBlock) {
+          const u32 zi = tz[j], gi = zi / 3;
+          const u32 off = zb_s[zi] + zpst[hp][zi] + (j - zls[zi]);
+          if (i64(off) >= gn[gi]) {
+            atomicOr(a.err, 1u);
+            continue;
+          }
+          const i64 dest = glo[gi] + off;
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c)
-        if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
+          for (int c = 0; c < NCOL; ++c) dst[i64(c) * nc + dest] = tile[c * HROWS + j];
+        }
+        __syncthreads();  // the tile, zls and (last part) gcnt are rewritten next
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kItems; ++i) {
+        const u32 zi = zone_pre[i] >> 16;
+        i64 dest = -1;
+        if (zi < u32(NZ)) {
+          const u32 gi = zi / 3;
+          const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
+          if (i64(off) >= gn[gi]) {
+            atomicOr(a.err, 1u);
+          } else {
+            dest = glo[gi] + off;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c)
+          if (dest >= 0) dst[i64(c) * nc + dest] = row[i][c];
+      }
+      // ATOM: the next chunk's atomics only touch the zeroed counters and its reads of wbase
+      // follow two more barriers; ballots: the next chunk rewrites gcnt
+      if (!ATOM) __syncthreads();
     }
-    // ATOM: the next chunk's atomics only touch the zeroed counters and its reads of wbase
-    // follow two more barriers; ballots: the next chunk rewrites gcnt
-    if (!ATOM) __syncthreads();
   }
   __syncthreads();
   if (threadIdx.x < 4 && bmin[threadIdx.x] != ~0ull) {
@@ -2463,7 +2521,7 @@ __global__ __launch_bounds__(kBlock) void k_partition3(LevelArgs a, TripleArgs t
   if (fuse) {
     u32* hn = ta.hist3 + (8 * s) * nb3;
     for (int b = threadIdx.x; b < 8 * nb3; b += kBlock) {
-      const u32 v = nh[b];
+      const u32 v = STG ? (nh[b >> 1] >> ((b & 1) * 16)) & 0xffffu : nh[b];
       if (v) atomicAdd(&hn[b], v);
     }
   }
@@ -2854,7 +2912,11 @@ __global__ __launch_bounds__(kBlock) void k_g3_band(LevelArgs a, G3Args g) {
 
 // The pass: every row once; 8 great-grandchild zones + the 7 staging regions. Zone ranks as in
 // k_partition3: LDS atomics (ATOM) or wave ballots.
-template <int NCOL, int KI, bool ATOM>
+// NH > 0 (ballot ranks only): the chunk's rows leave through LDS, in NH parts of KI / NH items:
+// each part's rows are written to an LDS tile in zone order, then stored by consecutive threads
+// at consecutive destinations, so every store instruction writes whole runs of one zone instead
+// of ~8 scattered 32-B pieces (one per zone a wave's 64 rows fall into).
+template <int NCOL, int KI, bool ATOM, int NH = 0>
 __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
   if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   constexpr int kItems = KI;
@@ -2862,8 +2924,18 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
   constexpr int NZ = 15;  // 0..7 great-grandchild, 8 + t staging tag t
   constexpr int D = NCOL - 1;
   constexpr int W = kBlock / 64;
+  constexpr bool STG = !ATOM && NH > 0;
+  constexpr int NP = STG ? NH : 1;          // parts of a chunk
+  constexpr int HI = KI / NP;               // items per part
+  constexpr int HROWS = kBlock * HI;        // rows per part (LDS tile)
   static_assert(kItems % 4 == 0, "16-B row loads take 4 rows per item group");
-  extern __shared__ __align__(16) u32 nh[];  // [8 * bins3]
+  static_assert(KI % NP == 0, "whole items per part");
+  // [8 * bins3] counts (STG: two 16-bit counts per word -- the host stages only blocks of < 64 Ki
+  // rows -- so the tile fits beside it at four workgroups per CU), then (STG) the tile: NCOL x HROWS
+  // floats + a zone byte per row
+  extern __shared__ __align__(16) u32 nh[];
+  constexpr int PK = STG ? 2 : 1;  // counts per histogram word
+  __shared__ u32 zb_s[16], ztot_s[16], zpst[NP][16], zls[16];
   __shared__ u32 wcnt[W][16];
   __shared__ u32 wbase[W][16];
   __shared__ u32 gcnt[ATOM ? 1 : NZ][64];
@@ -2880,7 +2952,7 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
   const bool fuse = nb3 > 0;
   G3Seg* gs = g.g3 + g.seg0 + s;
   if (fuse)
-    for (int b = threadIdx.x; b < kG3Gg * nb3; b += kBlock) nh[b] = 0;
+    for (int b = threadIdx.x; b < (kG3Gg * nb3 + PK - 1) / PK; b += kBlock) nh[b] = 0;
   const i64 gg0 = 8 * h + 7;
   if (threadIdx.x < W * 16) (&wcnt[0][0])[threadIdx.x] = 0;
   if (threadIdx.x < 8) {
@@ -2959,7 +3031,10 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
       } else {
         zone_pre[i] = (q << 16) | dev::wave_zone_rank<NZ>(q, &gcnt[0][i * 4 + w], 64);
       }
-      if (fuse && q < 8u) atomicAdd(&nh[q * u32(nb3) + bucket_of(k3, ggp[q], nb3)], 1u);
+      if (fuse && q < 8u) {
+        const u32 hb = q * u32(nb3) + bucket_of(k3, ggp[q], nb3);
+        atomicAdd(&nh[hb / PK], STG ? 1u << ((hb & 1u) * 16) : 1u);
+      }
     }
     __syncthreads();
     if constexpr (!ATOM) {
@@ -2986,7 +3061,18 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
       for (int k = 0; k < ZW; ++k) {
         const int z = w + k * W;
         const u32 b = __shfl(base, k, 64);
-        if (z < NZ) gcnt[z][ln] = b + incl[k] - v[k];
+        if (z < NZ) gcnt[z][ln] = (STG ? 0u : b) + incl[k] - v[k];  // STG: offset inside the chunk's zone run
+        if constexpr (STG) {
+          u32 ps[NP];  // part h's first row inside the zone run (groups are item-major: i * W + w)
+#pragma unroll
+          for (int hp = 0; hp < NP; ++hp) ps[hp] = hp == 0 ? 0u : u32(__shfl(int(incl[k]), hp * HI * W - 1, 64));
+          if (z < NZ && ln == 0) {
+            zb_s[z] = b;
+            ztot_s[z] = tot[k];
+#pragma unroll
+            for (int hp = 0; hp < NP; ++hp) zpst[hp][z] = ps[hp];
+          }
+        }
       }
     } else if (threadIdx.x < NZ) {  // zone z's waves, scanned, reserved once per chunk
       const int z = int(threadIdx.x);
@@ -3006,34 +3092,82 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
     }
     if (ATOM && threadIdx.x >= NZ && threadIdx.x < NZ + W) wcnt[threadIdx.x - NZ][15] = 0;
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kItems; ++i) {
-      const u32 zi = zone_pre[i] >> 16;
-      if (zi >= u32(NZ)) continue;
-      const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
-      i64 d = -1;
-      float* out = dst;
+    // destination of the row at offset `off` of zone zi's reservation (false: past its capacity)
+    auto dest = [&](u32 zi, u32 off, i64& d, float*& out) -> bool {
+      d = -1;
+      out = dst;
       if (zi < 8u) {
         if (i64(off) < gn[zi]) d = glo[zi] + off;
       } else if (off < rcap[zi - 8]) {
         d = lo + roff[zi - 8] + off;
         out = stg;
       }
-      if (d < 0) {
-        sbad = 1u;
-        continue;
-      }
+      return d >= 0;
+    };
+    if constexpr (STG) {
+      float* tile = reinterpret_cast<float*>(nh + ((max(1, (kG3Gg * nb3 + 1) / 2) + 3) & ~3));
+      unsigned char* tz = reinterpret_cast<unsigned char*>(tile + NCOL * HROWS);
+      const int ln = dev::lane();
 #pragma unroll
-      for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = row[i][c];
+      for (int hp = 0; hp < NP; ++hp) {
+        // part hp's tile: zones in order, each zone's rows in (item, wave, lane) order
+        const u32 ch = ln < NZ ? (hp + 1 < NP ? zpst[hp + 1 < NP ? hp + 1 : 0][ln] : ztot_s[ln]) - zpst[hp][ln] : 0u;
+        const u32 inc = dev::wave_incl_scan(ch);
+        const u32 ex = inc - ch;
+        if (w == 0 && ln < NZ) zls[ln] = ex;
+        if (w == 0 && ln == NZ - 1) zls[NZ] = inc;
+#pragma unroll
+        for (int ii = 0; ii < HI; ++ii) {
+          const int i = hp * HI + ii;
+          const u32 zi = zone_pre[i] >> 16;
+          const u32 zs = zi < u32(NZ) ? zi : 0u;
+          const u32 exz = u32(__shfl(int(ex), int(zs), 64));
+          if (zi >= u32(NZ)) continue;
+          const u32 p = exz + gcnt[zs][i * 4 + w] - zpst[hp][zs] + (zone_pre[i] & 0xffffu);
+#pragma unroll
+          for (int c = 0; c < NCOL; ++c) tile[c * HROWS + p] = row[i][c];
+          tz[p] = (unsigned char)zi;
+        }
+        __syncthreads();
+        const u32 T = zls[NZ];
+        for (u32 j = threadIdx.x; j < T; j += kBlock) {
+          const u32 zi = tz[j];
+          const u32 off = zb_s[zi] + zpst[hp][zi] + (j - zls[zi]);
+          i64 d;
+          float* out;
+          if (!dest(zi, off, d, out)) {
+            sbad = 1u;
+            continue;
+          }
+#pragma unroll
+          for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = tile[c * HROWS + j];
+        }
+        __syncthreads();  // the tile, zls and (last part) gcnt are rewritten next
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kItems; ++i) {
+        const u32 zi = zone_pre[i] >> 16;
+        if (zi >= u32(NZ)) continue;
+        const u32 off = (ATOM ? wbase[w][zi] : gcnt[ATOM ? 0 : zi][i * 4 + w]) + (zone_pre[i] & 0xffffu);
+        i64 d;
+        float* out;
+        if (!dest(zi, off, d, out)) {
+          sbad = 1u;
+          continue;
+        }
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) out[i64(c) * nc + d] = row[i][c];
+      }
+      if (!ATOM) __syncthreads();  // the next chunk rewrites gcnt
     }
-    if (!ATOM) __syncthreads();  // the next chunk rewrites gcnt
   }
   __syncthreads();
   if (threadIdx.x == 0 && sbad) g3_bad(a.err, gs);
   if (fuse) {
     u32* hn = g.hist3 + (kG3Gg * s) * nb3;
     for (int b = threadIdx.x; b < kG3Gg * nb3; b += kBlock) {
-      const u32 v = nh[b];
+      const u32 v = STG ? (nh[b >> 1] >> ((b & 1) * 16)) & 0xffffu : nh[b];
       if (v) atomicAdd(&hn[b], v);
     }
   }
@@ -4361,6 +4495,8 @@ Tuning Tuning::from_env() {
   t.prefix = ab_i("PKD_PART_PREFIX", 1) != 0;
   t.tail = ab_i("PKD_TAIL", 1) != 0;
   t.tail4 = ab_i("PKD_TAIL4", 1) != 0;
+  t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
+  t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
   t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
@@ -5089,7 +5225,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           if constexpr (NC >= 3) {
             constexpr int KI = NC <= 5 ? 8 : 4;
             const size_t lds3 = size_t(std::max(1, kG3Gg * ga.bins3)) * 4;
+            // staged tile of NH parts: NC x kBlock * KI / NH floats + a zone byte per row
+            auto lds_stg = [&](int nh) { return size_t((std::max(1, (kG3Gg * ga.bins3 + 1) / 2) + 3) & ~3) * 4 +
+                                                size_t(kBlock * KI / nh) * (4 * NC + 1); };
+            const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;  // 16-bit histogram counts suffice
             if (atomic_ranks(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
+            else if (!stg16) k_g3_part<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ga);
+            else if (tune_.g3_stage == 1) k_g3_part<NC, KI, false, 1><<<grid, kBlock, lds_stg(1), st>>>(a, ga);
+            else if (tune_.g3_stage == 2) k_g3_part<NC, KI, false, 2><<<grid, kBlock, lds_stg(2), st>>>(a, ga);
             else k_g3_part<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ga);
             PKD_LAUNCH_CHECK();
             k_g3_res<NC, 0><<<int(segs), kG3Threads, 0, st>>>(a, ga);
@@ -5154,7 +5297,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             PKD_LAUNCH_CHECK();
             constexpr int KI = NC <= 5 ? 8 : 4;
             const size_t lds3 = size_t(std::max(1, 8 * ta.bins3)) * 4;
+            // the ballot form's stores through an LDS tile (as k_g3_part): 16-bit histogram counts + the tile
+            const size_t lds_stg = size_t((std::max(1, (8 * ta.bins3 + 1) / 2) + 3) & ~3) * 4 +
+                                   size_t(kBlock * KI / 2) * (4 * NC + 1);
+            const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;
             if (atomic_ranks(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
+            else if (stg16 && tune_.part3_stage) k_partition3<NC, KI, false, 2><<<grid, kBlock, lds_stg, st>>>(a, ta);
             else k_partition3<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ta);
             PKD_LAUNCH_CHECK();
           }

@@ -676,7 +676,8 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     // ranking), so more waves per segment win: 100M x 8D 31.4 -> 28.1 ms with 1024 threads
     // instead of 256 (profiles/r1_subtree_config_sweep.txt). PKD_SUBTREE_CFG overrides.
     else if (nmax > 512 && (cfg == "4x256")) launch_rank_cfg<4, 256>(a, segs, stream);
-    else if (nmax > 512 && (cfg == "2x512" || (cfg.empty() && dim <= 5))) launch_rank_cfg<2, 512>(a, segs, stream);
+    // (2 x 512 up to 7-D: 100M x 6D 16.90 -> 16.79 ms, 7D 18.23 -> 18.18; 8D 18.42 -> 19.24 with it)
+    else if (nmax > 512 && (cfg == "2x512" || (cfg.empty() && dim <= 7))) launch_rank_cfg<2, 512>(a, segs, stream);
     else if (nmax > 512) launch_rank_cfg<1, 1024>(a, segs, stream);
     else if (nmax > 256 && cfg == "2x256") launch_rank_cfg<2, 256>(a, segs, stream);
     else if (nmax > 256) launch_rank_cfg<1, 512>(a, segs, stream);

@@ -58,6 +58,8 @@ struct Tuning {
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool tail = true;           // PKD_TAIL=0: the last three global levels by pairs / triples instead of k_tail3
   bool tail4 = true;          // PKD_TAIL4=0: never a 4-level tail (it replaces two pairs by a triple at 8-D)
+  int g3_stage = 2;           // k_g3_part stores through an LDS tile of 2 (1) parts; 0: from registers
+  bool part3_stage = true;    // PKD_PART3_STAGE=0: k_partition3 (ballot ranks) stores from registers
   int tail_slim12 = 0;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids, 1 two key sets (no ids), 2 two key sets + ids
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
@@ -94,8 +96,9 @@ struct Tuning {
   i64 g3_min_rows = 262144;   // PKD_G3_MIN_ROWS: smallest segment a sampled triple starts from
   i64 g3_min_n = i64(32) << 20;  // PKD_G3_MIN_N: smallest build that samples triples (12.5 M: 1.406 ms
                                  //   without, 1.434 with the 16-segment level-4 triple sampled)
-  int g3_max_dim = 3;         // PKD_G3_MAX_DIM: widest rows that sample triples (100M x 8D: 20.72 ms
-                              //   exact, 21.01 sampled: 36-B rows make the staging dearer)
+  int g3_max_dim = 8;         // PKD_G3_MAX_DIM: widest rows that sample triples (with k_g3_part's
+                              //   stores through LDS, 100M: 4D 11.76 -> 11.21 ms, 6D 17.17 -> 16.90,
+                              //   8D 18.89 -> 18.42; profiles/r6_stage_ab.txt)
   i64 g3_sample = 65536;      // PKD_G3_SAMPLE: sample rows per segment (64-row runs)
   int g3_div_min = 1;         // PKD_G3_DIV_MIN: the sample holds at most 1 / g3_div_min of a segment
   i64 g3_multi_below = 128;   // PKD_G3_MULTI_BELOW: triples of fewer segments resolve on several blocks per node

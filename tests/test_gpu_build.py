@@ -47,13 +47,15 @@ def test_duplicates(gpu_device):
     check_same(torch.randint(0, 2, (20_000, 3)).float(), gpu_device)
 
 
-@pytest.mark.parametrize("atomic", ["0", "1"])
+@pytest.mark.parametrize("atomic,stage", [("0", "1"), ("0", "0"), ("1", "1")])
 @pytest.mark.parametrize("triple_from", ["0", "3"])
-def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic):
+def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic, stage):
     """Three levels per scatter pass (k_scan2 + k_partition3, from level 0 or 3) with zone ranks
-    from wave ballots or LDS atomics (also in the pair scatters): slot for slot the CPU exact
-    tree on uniform, duplicate-heavy, 2-D, 8-D and odd-depth inputs."""
+    from wave ballots (stores through an LDS tile, or from registers) or LDS atomics (also in the
+    pair scatters): slot for slot the CPU exact tree on uniform, duplicate-heavy, 2-D, 8-D and
+    odd-depth inputs."""
     monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
+    monkeypatch.setenv("PKD_PART3_STAGE", stage)
     monkeypatch.setenv("PKD_TAIL", "0")  # the last three levels stay triples too
     monkeypatch.setenv("PKD_TRIPLE_FROM", triple_from)
     monkeypatch.setenv("PKD_PART_ATOMIC", atomic)
