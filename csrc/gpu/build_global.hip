@@ -3990,6 +3990,7 @@ struct TailArgs {
   u32* out_ids;
   u32* err;
   unsigned long long* stamps;  // diagnostic (PKD_TAIL_STAMPS=1): [block][kTailStampSlots] s_memtime, else null
+  int pipe;                    // move phase: next column's loads in flight, two stage buffers (2 x CAP words)
 };
 constexpr int kTailStampSlots = 24, kTailStampBlocks = 2048;
 __device__ __forceinline__ void tail_stamp(const TailArgs& a, int slot) {
@@ -4321,13 +4322,39 @@ void k_tail3(TailArgs a) {
   for (int i = 0; i < ITEMS; ++i)
     if (path[i] < kMed) path[i] = (path[i] & 0xffffffu) + gbase[grp][path[i] >> 24];
   tail_stamp(a, 13);
-#pragma unroll
-  for (int c = 0; c <= D; ++c) {
-    // column c: from registers (a level's keys or the ids), else loaded
+  // column c's register set (a level's keys), or -1: loaded
+  auto kreg_of = [&](int c) {
     int kreg = -1;
 #pragma unroll
     for (int k = 0; k < KC; ++k)  // (SLIM: set k holds the keys of the last level t with t & 1 == k)
       if ((D < 3 ? k : (SLIM ? axis_of[((LEV - 1) & 1) == k ? LEV - 1 : LEV - 2] : axis_of[k])) == c) kreg = k;
+    return kreg;
+  };
+  auto loaded = [&](int c) { return c == D ? !IDS : kreg_of(c) < 0; };
+  auto load_col = [&](int c, u32 (&v)[ITEMS]) {
+    const auto r = col(a.src, c);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto q = ld4(r, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * g + j] = q[j];
+    }
+  };
+  // pipe: the next loaded column's loads are issued before this column is staged and stored, and
+  // the columns alternate between two stage buffers (one barrier per column instead of two): the
+  // load latency and the barrier no longer serialise the D + 1 columns of the one workgroup per CU
+  const bool pipe = a.pipe != 0;
+  u32 pre[ITEMS];
+  if (pipe) {
+    int c0 = 0;
+    while (c0 <= D && !loaded(c0)) ++c0;
+    if (c0 <= D) load_col(c0, pre);
+  }
+#pragma unroll
+  for (int c = 0; c <= D; ++c) {
+    // column c: from registers (a level's keys or the ids), else loaded
+    const int kreg = kreg_of(c);
+    u32* sb = stage + (pipe ? (c & 1) * CAP : 0);
     u32 v[ITEMS];
     if (c == D && IDS) {
 #pragma unroll
@@ -4340,19 +4367,19 @@ void k_tail3(TailArgs a) {
         for (int k = 0; k < KC; ++k) x = k == kreg ? __float_as_uint(xs[k][i]) : x;
         v[i] = x;
       }
+    } else if (pipe) {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) v[i] = pre[i];
+      int cn = c + 1;
+      while (cn <= D && !loaded(cn)) ++cn;
+      if (cn <= D) load_col(cn, pre);
     } else {
-      const auto r = col(a.src, c);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const auto q = ld4(r, g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * g + j] = q[j];
-      }
+      load_col(c, v);
     }
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       if (path[i] < kMed) {
-        stage[path[i] + u32(shift)] = v[i];  // stage index = column row - alo: 16-B groups align
+        sb[path[i] + u32(shift)] = v[i];  // stage index = column row - alo: 16-B groups align
       } else if (path[i] != kDead) {  // a tail median: straight to its output slot
         const int k = int(path[i] & 15u);
         const i64 slot = nlo[k] + nn[k] / 2;
@@ -4371,22 +4398,26 @@ void k_tail3(TailArgs a) {
     for (int q = tid; q < ng; q += T) {
       const int j0 = 4 * q;
       if (j0 >= shift && j0 + 3 < n + shift) {
-        const u32x4 v4 = *reinterpret_cast<const u32x4*>(stage + j0);
+        const u32x4 v4 = *reinterpret_cast<const u32x4*>(sb + j0);
         __builtin_amdgcn_raw_buffer_store_b128(v4, dr, u32(j0) * 4u, 0, 0);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int j = j0 + e;
-          if (j >= shift && j < n + shift) __builtin_amdgcn_raw_buffer_store_b32(stage[j], dr, u32(j) * 4u, 0, 0);
+          if (j >= shift && j < n + shift) __builtin_amdgcn_raw_buffer_store_b32(sb[j], dr, u32(j) * 4u, 0, 0);
         }
       }
     }
-    __syncthreads();
+    // (pipe: the next column writes the other buffer; this one is rewritten two columns on,
+    // after the next column's barrier, which every thread reaches only once its reads here are done)
+    if (!pipe) __syncthreads();
     tail_stamp(a, 14 + c);
   }
 }
 
-size_t tail_lds_bytes(int items) { return size_t(items) * kTailThreads * 4; }  // k_tail3's dynamic LDS
+size_t tail_lds_bytes(int items, bool pipe) {  // k_tail3's dynamic LDS (pipe: two stage buffers)
+  return size_t(items) * kTailThreads * 4 * (pipe ? 2 : 1);
+}
 
 unsigned long long* tail_stamp_buffer() {  // PKD_TAIL_STAMPS=1 (diagnostic): allocated once, else null
   static unsigned long long* p = [] {
@@ -4495,6 +4526,7 @@ Tuning Tuning::from_env() {
   t.prefix = ab_i("PKD_PART_PREFIX", 1) != 0;
   t.tail = ab_i("PKD_TAIL", 1) != 0;
   t.tail4 = ab_i("PKD_TAIL4", 1) != 0;
+  t.tail_pipe = ab_i("PKD_TAIL_PIPE", 1) != 0;
   t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
   t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
@@ -5395,8 +5427,8 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       const LevelPlan& lp = levels[size_t(tail_)];
       const i64 segs = lp.segs / nparts;
       TailArgs ta{src, dst, ncol_, seg_lo, seg_n, cells, lp.segs - 1 + i64(part) * segs, tail_, opt_.depth0,
-                  out_pts, out_ids, err, tail_stamp_buffer()};
-      const size_t lds = tail_lds_bytes(tail_items_);
+                  out_pts, out_ids, err, tail_stamp_buffer(), tune_.tail_pipe ? 1 : 0};
+      const size_t lds = tail_lds_bytes(tail_items_, tune_.tail_pipe);
       with_ncol(dim_, [&](auto nc) {
         constexpr int D = decltype(nc)::value - 1;
         if constexpr (D >= 1) {

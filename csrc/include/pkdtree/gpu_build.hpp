@@ -58,9 +58,11 @@ struct Tuning {
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool tail = true;           // PKD_TAIL=0: the last three global levels by pairs / triples instead of k_tail3
   bool tail4 = true;          // PKD_TAIL4=0: never a 4-level tail (it replaces two pairs by a triple at 8-D)
+  bool tail_pipe = true;      // PKD_TAIL_PIPE=0: k_tail3 moves its columns one at a time (load, stage, store)
   int g3_stage = 2;           // k_g3_part stores through an LDS tile of 2 (1) parts; 0: from registers
   bool part3_stage = true;    // PKD_PART3_STAGE=0: k_partition3 (ballot ranks) stores from registers
-  int tail_slim12 = 0;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids, 1 two key sets (no ids), 2 two key sets + ids
+  int tail_slim12 = 2;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids (spills 52 B/lane at 3-D),
+                        //   1 two key sets (no ids), 2 two key sets + ids (no spill; 100M x 3D 8.46 ms either way)
   bool split = true;          // PKD_SPLIT=0: one-stream build
   bool split_trace = false;   // PKD_SPLIT_TRACE=1: part timeline on stderr (synchronises)
   int colgroup = 0;           // PKD_COLGROUP: columns per load round of wide rows (0: by dim)

@@ -81,17 +81,20 @@ def test_subtree_capacity_1536(gpu_device, n):
         check_same(pk.generate_problem(n % 89, 3, n), gpu_device, depth0=1)
 
 
-@pytest.mark.parametrize("slim12", ["0", "1", "2"])
+@pytest.mark.parametrize("slim12,pipe", [("0", "1"), ("1", "1"), ("2", "1"), ("2", "0")])
 @pytest.mark.parametrize("n,dim", [(40_000, 3), (70_000, 3), (100_000, 3), (200_000, 1), (150_000, 2), (120_000, 5),
                                    (60_000, 8)])
-def test_tail_levels(gpu_device, monkeypatch, n, dim, slim12):
+def test_tail_levels(gpu_device, monkeypatch, n, dim, slim12, pipe):
     """The last three global levels in one workgroup per segment (k_tail3: bucket bins, wave
     ranking of the median bin or the radix-select fallback for heavy duplicates, LDS-staged
     leaf scatter): slot for slot the CPU exact tree. 16-item shapes (100 k at 3-D) and, with
-    PKD_TAIL_SLIM12, the 12-item shapes run with two key register sets and ids read on demand."""
+    PKD_TAIL_SLIM12, the 12-item shapes run with all keys + ids (0), two key register sets and
+    ids read on demand (1) or two key sets + ids (2, the default); PKD_TAIL_PIPE=0 moves the
+    columns without the next column's loads in flight and with one stage buffer."""
     monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_TAIL", "1")
     monkeypatch.setenv("PKD_TAIL_SLIM12", slim12)
+    monkeypatch.setenv("PKD_TAIL_PIPE", pipe)
     b = ops.GpuTreeBuilder(n, dim)
     assert "tail" in b.describe(), b.describe()
     check_same(pk.generate_problem(n % 101, dim, n), gpu_device)
