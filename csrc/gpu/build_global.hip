@@ -4529,6 +4529,7 @@ Tuning Tuning::from_env() {
   t.tail_pipe = ab_i("PKD_TAIL_PIPE", 1) != 0;
   t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
   t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
+  t.wide_ki = int(ab_i("PKD_WIDE_KI", 4));
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
   t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
@@ -5261,7 +5262,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             auto lds_stg = [&](int nh) { return size_t((std::max(1, (kG3Gg * ga.bins3 + 1) / 2) + 3) & ~3) * 4 +
                                                 size_t(kBlock * KI / nh) * (4 * NC + 1); };
             const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;  // 16-bit histogram counts suffice
-            if (atomic_ranks(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
+            bool wide8 = false;  // rows of >= 6 columns: 8 rows per thread and chunk, stored in 4 parts
+            if constexpr (NC > 5) {
+              if (tune_.wide_ki == 8 && stg16 && !atomic_ranks(tune_.atomic_ranks3)) {
+                k_g3_part<NC, 8, false, 4><<<grid, kBlock, size_t((std::max(1, (kG3Gg * ga.bins3 + 1) / 2) + 3) & ~3) * 4 +
+                                                             size_t(kBlock * 2) * (4 * NC + 1), st>>>(a, ga);
+                wide8 = true;
+              }
+            }
+            if (wide8) {
+            } else if (atomic_ranks(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
             else if (!stg16) k_g3_part<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ga);
             else if (tune_.g3_stage == 1) k_g3_part<NC, KI, false, 1><<<grid, kBlock, lds_stg(1), st>>>(a, ga);
             else if (tune_.g3_stage == 2) k_g3_part<NC, KI, false, 2><<<grid, kBlock, lds_stg(2), st>>>(a, ga);
@@ -5333,7 +5343,16 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             const size_t lds_stg = size_t((std::max(1, (8 * ta.bins3 + 1) / 2) + 3) & ~3) * 4 +
                                    size_t(kBlock * KI / 2) * (4 * NC + 1);
             const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;
-            if (atomic_ranks(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
+            bool wide8 = false;  // rows of >= 6 columns: 8 rows per thread and chunk, stored in 4 parts
+            if constexpr (NC > 5) {
+              if (tune_.wide_ki == 8 && stg16 && tune_.part3_stage && !atomic_ranks(tune_.atomic_ranks3)) {
+                k_partition3<NC, 8, false, 4><<<grid, kBlock, size_t((std::max(1, (8 * ta.bins3 + 1) / 2) + 3) & ~3) * 4 +
+                                                                size_t(kBlock * 2) * (4 * NC + 1), st>>>(a, ta);
+                wide8 = true;
+              }
+            }
+            if (wide8) {
+            } else if (atomic_ranks(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
             else if (stg16 && tune_.part3_stage) k_partition3<NC, KI, false, 2><<<grid, kBlock, lds_stg, st>>>(a, ta);
             else k_partition3<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ta);
             PKD_LAUNCH_CHECK();

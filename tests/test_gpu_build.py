@@ -47,15 +47,16 @@ def test_duplicates(gpu_device):
     check_same(torch.randint(0, 2, (20_000, 3)).float(), gpu_device)
 
 
-@pytest.mark.parametrize("atomic,stage", [("0", "1"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("atomic,stage,wide", [("0", "1", "8"), ("0", "1", "4"), ("0", "0", "4"), ("1", "1", "8")])
 @pytest.mark.parametrize("triple_from", ["0", "3"])
-def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic, stage):
+def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic, stage, wide):
     """Three levels per scatter pass (k_scan2 + k_partition3, from level 0 or 3) with zone ranks
     from wave ballots (stores through an LDS tile, or from registers) or LDS atomics (also in the
     pair scatters): slot for slot the CPU exact tree on uniform, duplicate-heavy, 2-D, 8-D and
     odd-depth inputs."""
     monkeypatch.setenv("PKD_AB", "1")  # A/B knobs below
     monkeypatch.setenv("PKD_PART3_STAGE", stage)
+    monkeypatch.setenv("PKD_WIDE_KI", wide)
     monkeypatch.setenv("PKD_TAIL", "0")  # the last three levels stay triples too
     monkeypatch.setenv("PKD_TRIPLE_FROM", triple_from)
     monkeypatch.setenv("PKD_PART_ATOMIC", atomic)
@@ -66,6 +67,7 @@ def test_triple_levels(gpu_device, monkeypatch, triple_from, atomic, stage):
     check_same(torch.randint(0, 7, (600_000, 3)).float(), gpu_device)
     check_same(pk.generate_problem(12, 2, 700_001), gpu_device)
     check_same(pk.generate_problem(13, 8, 400_000), gpu_device)
+    check_same(pk.generate_problem(15, 6, 300_001), gpu_device, depth0=4)
     check_same(pk.generate_problem(14, 3, 900_000), gpu_device, depth0=2)
 
 

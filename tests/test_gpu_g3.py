@@ -58,13 +58,15 @@ def test_g3_equals_cpu_exact(gpu_device, g3_small, monkeypatch, n, dim, depth0, 
         assert sum(s[8:16]) + sum(s[16:24]) + 7 == s[0] or s[0] == 0, s
 
 
-@pytest.mark.parametrize("stage", ["0", "1", "2"])  # k_g3_part stores: from registers / LDS tile in 1 / 2 parts
-@pytest.mark.parametrize("n,dim,depth0", [(2_000_000, 3, 0), (1_000_003, 5, 1), (800_000, 8, 2)])
-def test_g3_ballot_ranks_staged_stores(gpu_device, g3_small, monkeypatch, n, dim, depth0, stage):
+# k_g3_part stores: from registers / LDS tile in 1 / 2 parts; rows of >= 6 columns: 4 or 8 per thread
+@pytest.mark.parametrize("stage,wide", [("0", "4"), ("1", "4"), ("2", "4"), ("2", "8")])
+@pytest.mark.parametrize("n,dim,depth0", [(2_000_000, 3, 0), (1_000_003, 5, 1), (900_001, 6, 0), (800_000, 8, 2)])
+def test_g3_ballot_ranks_staged_stores(gpu_device, g3_small, monkeypatch, n, dim, depth0, stage, wide):
     """The ballot-rank form of the pass (the default from 64 M points) with its stores staged
     through LDS in zone order: the same exact tree."""
     monkeypatch.setenv("PKD_PART3_ATOMIC", "0")
     monkeypatch.setenv("PKD_G3_STAGE", stage)
+    monkeypatch.setenv("PKD_WIDE_KI", wide)
     ids = torch.randperm(n, generator=torch.Generator().manual_seed(n)).to(torch.int32) + 3
     _same_as_cpu(pk.generate_problem(n + 11 * dim, dim, n), gpu_device, depth0, ids)
 
