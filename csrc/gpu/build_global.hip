@@ -4529,7 +4529,7 @@ Tuning Tuning::from_env() {
   t.tail_pipe = ab_i("PKD_TAIL_PIPE", 1) != 0;
   t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
   t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
-  t.wide_ki = int(ab_i("PKD_WIDE_KI", 4));
+  t.wide_ki = int(ab_i("PKD_WIDE_KI", t.wide_ki));
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
   t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
