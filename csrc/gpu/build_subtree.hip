@@ -563,7 +563,7 @@ void launch_rank_cfg(const SubArgs& a0, i64 segs, hipStream_t stream) {
       done = true;
     }
   }
-  if constexpr (ITEMS == 1 && THREADS == 1024) {  // d = 8 (BASELINE's high-dim config), capacity 1024
+  if constexpr ((ITEMS == 1 && THREADS == 1024) || ITEMS * THREADS == 768) {  // d = 8 (BASELINE's high-dim config)
     if (!done && a.dim == 8) {
       ensure_dynamic_lds(reinterpret_cast<const void*>(&k_subtree_rank<ITEMS, THREADS, false, 8>), int(kLdsMax));
       k_subtree_rank<ITEMS, THREADS, false, 8><<<dim3(unsigned(segs)), THREADS, lds, stream>>>(a);
@@ -661,24 +661,21 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
             std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
   {
-    static const bool wide = [] {
-      const char* e = ab_knob("PKD_SUBTREE_WIDE");
-      return !(e && std::string(e) == "0");
-    }();
-    static const std::string cfg = [] {
-      const char* e = ab_knob("PKD_SUBTREE_CFG");
-      return std::string(e ? e : "");
-    }();
-    static const bool c1536 = [] {
-      const char* e = ab_knob("PKD_SUBTREE_1536");
-      return !(e && std::string(e) == "0");
-    }();
+    // (read per launch, so tests can vary them within one process)
+    const char* ew = ab_knob("PKD_SUBTREE_WIDE");
+    const bool wide = !(ew && std::string(ew) == "0");
+    const char* ec = ab_knob("PKD_SUBTREE_CFG");
+    const std::string cfg = ec ? ec : "";
+    const char* e15 = ab_knob("PKD_SUBTREE_1536");
+    const bool c1536 = !(e15 && std::string(e15) == "0");
     if (nmax > 2048) launch_rank_cfg<4, 1024>(a, segs, stream);
     // 3-D segments of 1025..1536 points (100M / 2^16 and 12.5M / 2^13: 1525 points): capacity
     // 1536 = 3 items x 512 threads, 52 KiB of LDS, three workgroups (24 waves) per CU. Against
     // 2 x 1024 (4 idle waves of 16 at 1525 points, two workgroups per CU): 100M x 3D 11.64 ->
     // 11.14-11.43 ms, 12.5M 1.753 -> 1.680 ms; 2 x 768 (two workgroups of 12 waves) was in
     // between (profiles/r3_subtree_1536.txt)
+    else if (nmax > 1024 && nmax <= 1536 && cfg == "6x256" && a.ldim == 0) launch_rank_cfg<6, 256>(a, segs, stream);
+    else if (nmax > 1024 && nmax <= 1536 && cfg == "4x384" && a.ldim == 0) launch_rank_cfg<4, 384>(a, segs, stream);
     else if (nmax > 1024 && nmax <= 1536 && wide && c1536 && dim == 3 && a.ldim == 0)
       launch_rank_cfg<3, 512, 6>(a, segs, stream);
     else if (nmax > 1024 && wide) launch_rank_cfg<2, 1024>(a, segs, stream);
@@ -688,6 +685,22 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     // ranking), so more waves per segment win: 100M x 8D 31.4 -> 28.1 ms with 1024 threads
     // instead of 256 (profiles/r1_subtree_config_sweep.txt). PKD_SUBTREE_CFG overrides.
     else if (nmax > 512 && (cfg == "4x256")) launch_rank_cfg<4, 256>(a, segs, stream);
+    // Segments of 513..768 points (100M / 2^17 = 763 at dims 4..8): capacity 768 instead of 1024,
+    // fewer threads per workgroup, three workgroups per CU. 100M build, ms (profiles/r6_subtree_shapes.txt):
+    //            default (2x512 / 1x1024)  3x256   2x384
+    //   4-D      11.2                      10.24   11.14
+    //   5-D      12.46                     12.58   13.28
+    //   6-D      15.46                     12.97   13.71
+    //   7-D      17.53                     16.00   15.89
+    //   8-D      17.83                     16.97   16.78
+    else if (nmax > 512 && nmax <= 768 && cfg.empty() && a.ldim == 0 && (dim == 4 || dim == 6))
+      launch_rank_cfg<3, 256>(a, segs, stream);
+    else if (nmax > 512 && nmax <= 768 && cfg.empty() && a.ldim == 0 && (dim == 7 || dim == 8))
+      launch_rank_cfg<2, 384>(a, segs, stream);
+    else if (nmax > 512 && nmax <= 768 && cfg == "1x768") launch_rank_cfg<1, 768>(a, segs, stream);
+    else if (nmax > 512 && nmax <= 768 && cfg == "3x256") launch_rank_cfg<3, 256>(a, segs, stream);
+    else if (nmax > 512 && nmax <= 768 && cfg == "6x128") launch_rank_cfg<6, 128>(a, segs, stream);
+    else if (nmax > 512 && nmax <= 768 && cfg == "2x384") launch_rank_cfg<2, 384>(a, segs, stream);
     // (2 x 512 up to 7-D: 100M x 6D 16.90 -> 16.79 ms, 7D 18.23 -> 18.18; 8D 18.42 -> 19.24 with it)
     else if (nmax > 512 && (cfg == "2x512" || (cfg.empty() && dim <= 7))) launch_rank_cfg<2, 512>(a, segs, stream);
     else if (nmax > 512) launch_rank_cfg<1, 1024>(a, segs, stream);

@@ -40,6 +40,29 @@ def test_forced_small_subtree(gpu_device):
     check_same(pk.generate_problem(4, 3, 300_000), gpu_device, subtree_max=256)
 
 
+@pytest.mark.parametrize("cfg", ["1x768", "3x256", "6x128", "2x384", "2x512", "1x1024", "4x256"])
+@pytest.mark.parametrize("dim", [3, 5, 8])
+def test_subtree_launch_shapes(gpu_device, monkeypatch, cfg, dim):
+    """Segments of 513..768 points (100M x 8D: 763) under every LDS subtree launch shape for that
+    capacity: the same exact tree (uniform and duplicate-heavy rows)."""
+    monkeypatch.setenv("PKD_AB", "1")
+    monkeypatch.setenv("PKD_SUBTREE_CFG", cfg)
+    n = 763 * 512 + 17
+    check_same(pk.generate_problem(dim + 40, dim, n), gpu_device, subtree_max=1024)
+    check_same(torch.randint(0, 9, (n, dim)).float(), gpu_device, subtree_max=1024, depth0=dim - 1)
+
+
+@pytest.mark.parametrize("cfg", ["6x256", "4x384", ""])
+@pytest.mark.parametrize("dim", [2, 3, 4])
+def test_subtree_launch_shapes_1536(gpu_device, monkeypatch, cfg, dim):
+    """Segments of 1025..1536 points (100M x 3D: 1525) under the launch shapes of that capacity."""
+    monkeypatch.setenv("PKD_AB", "1")
+    monkeypatch.setenv("PKD_SUBTREE_CFG", cfg)
+    n = 1525 * 256 + 9
+    check_same(pk.generate_problem(dim + 50, dim, n), gpu_device, subtree_max=2048)
+    check_same(torch.randint(0, 9, (n, dim)).float(), gpu_device, subtree_max=2048, depth0=1)
+
+
 def test_duplicates(gpu_device):
     g = torch.randint(0, 5, (300_000, 3)).float()
     check_same(g, gpu_device)
