@@ -443,7 +443,28 @@ struct LevelArgs {
   i64 in_rs;
   int id_implicit;       // 1 (first level only): src has no id column, id of column row p = id_base0 + p
   u32 id_base0;
+  int xcd;               // 1: the row-moving passes keep a segment's blocks on one XCD (seg_part)
 };
+
+// Segment s and part of this block in a (segments x bps) grid, and its index s * bps + part in
+// (segment, part) order (per-block arrays are kept in that order). xcd (with a multiple of 8
+// segments): blocks are dealt round-robin over the 8 XCDs (block b shares one with b + 8), so
+// segment s is given the blocks b = s % 8 (mod 8): every block of a segment runs on one XCD, and
+// the cache lines its blocks' zone runs share at their reservation edges are merged in that XCD's
+// L2 instead of leaving it as partial writes from two or more L2s (100M x 8D k_g3_part wrote 4.37
+// GB per pass for 3.6 GB of rows).
+__device__ __forceinline__ void seg_part(int bps, int xcd, i64& s, int& part, i64& bidx) {
+  const u32 b = blockIdx.x, nseg = gridDim.x / u32(bps);
+  if (xcd && (nseg & 7u) == 0u) {
+    const u32 x = b & 7u, q = b >> 3;
+    s = i64(x) + 8 * i64(q / u32(bps));
+    part = int(q % u32(bps));
+  } else {
+    s = i64(b / u32(bps));
+    part = int(b % u32(bps));
+  }
+  bidx = s * bps + part;
+}
 
 // Id of src column row p (absolute), materialised or implicit (first level of a build whose
 // prep skipped the id column).
@@ -741,8 +762,9 @@ __global__ __launch_bounds__(kBlock) void k_partition(LevelArgs a) {
   __shared__ u32 gcnt[3][64];
   __shared__ unsigned long long bmin, bmax;  // block's middle-zone key range, flushed once
   const int dim = NCOL > 0 ? NCOL - 1 : a.dim;
-  const i64 s = blockIdx.x / a.bps;
-  const int part = blockIdx.x % a.bps;
+  i64 s, bidx;
+  int part;
+  seg_part(a.bps, a.xcd, s, part, bidx);
   const i64 h = a.heap0 + s;
   const i64 lo = a.seg_lo[h], n = a.seg_n[h];
   const bool fuse = a.next_bins > 0;
@@ -1683,8 +1705,9 @@ __global__ __launch_bounds__(kBlock) void k_pivot_both(LevelArgs a, i64 segs, in
 __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
   if (dev::build_failed(a.err)) return;  // the build already failed (a miss): it is redone
   __shared__ u32 sh[2 * kBins2];
-  const i64 s = blockIdx.x / a.bps;
-  const int part = blockIdx.x % a.bps;
+  i64 s, bidx;
+  int part;
+  seg_part(a.bps, a.xcd, s, part, bidx);
   const i64 h = a.heap0 + s;
   const i64 lo = a.seg_lo[h], n = a.seg_n[h];
   for (int b = threadIdx.x; b < 2 * kBins2; b += kBlock) sh[b] = 0;
@@ -1733,7 +1756,7 @@ __global__ __launch_bounds__(kBlock) void k_hist2p(LevelArgs a, PairArgs pa) {
     }
   }
   __syncthreads();
-  if (pa.bcnt && threadIdx.x < 4) pa.bcnt[i64(blockIdx.x) * 4 + threadIdx.x] = bc[threadIdx.x];
+  if (pa.bcnt && threadIdx.x < 4) pa.bcnt[bidx * 4 + threadIdx.x] = bc[threadIdx.x];
   u32* hs = a.hist2 + (2 * s) * kBins2;
   for (int b = threadIdx.x; b < 2 * kBins2; b += kBlock) {
     const u32 v = sh[b];
@@ -1809,8 +1832,9 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
     bmax[threadIdx.x] = 0ull;
   }
   constexpr int D = NCOL - 1;
-  const i64 s = blockIdx.x / a.bps;
-  const int part = blockIdx.x % a.bps;
+  i64 s, bidx;
+  int part;
+  seg_part(a.bps, a.xcd, s, part, bidx);
   const i64 h = a.heap0 + s;
   const i64 lo = a.seg_lo[h], n = a.seg_n[h];
   const int nb2 = pa.bins2;
@@ -1873,7 +1897,7 @@ __global__ __launch_bounds__(kBlock) void k_partition2(LevelArgs a, PairArgs pa)
   if (PFX) {
     if (threadIdx.x < 6) {
       const int t = int(threadIdx.x);
-      bcur[t] = (t == 1 || t == 4) ? 0u : pa.bbase[i64(blockIdx.x) * 4 + (t / 3) * 2 + (t % 3 == 2 ? 1 : 0)];
+      bcur[t] = (t == 1 || t == 4) ? 0u : pa.bbase[bidx * 4 + (t / 3) * 2 + (t % 3 == 2 ? 1 : 0)];
     }
   } else if (a.block_reserve) {
     u32 cnt[6] = {0, 0, 0, 0, 0, 0};
@@ -2280,8 +2304,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NH > 0 ?
   __shared__ BucketParams gpar[4], ggp[8];
   __shared__ u32 gbs[4];
   __shared__ i64 glo[4], gn[4];
-  const i64 s = blockIdx.x / a.bps;
-  const int part = blockIdx.x % a.bps;
+  i64 s, bidx;
+  int part;
+  seg_part(a.bps, a.xcd, s, part, bidx);
   const i64 h = a.heap0 + s;
   const i64 lo = a.seg_lo[h], n = a.seg_n[h];
   const int nb3 = ta.bins3;
@@ -2944,8 +2969,9 @@ __global__ __launch_bounds__(kBlock) void k_g3_part(LevelArgs a, G3Args g) {
   __shared__ u32 roff[8], rcap[8];
   __shared__ u32 ba1[2], bb1[2], ba2[4], bb2[4];
   __shared__ u32 sbad;
-  const i64 s = blockIdx.x / a.bps;
-  const int part = blockIdx.x % a.bps;
+  i64 s, bidx;
+  int part;
+  seg_part(a.bps, a.xcd, s, part, bidx);
   const i64 h = a.heap0 + s;
   const i64 lo = a.seg_lo[h], n = a.seg_n[h];
   const int nb3 = g.bins3;
@@ -4530,6 +4556,7 @@ Tuning Tuning::from_env() {
   t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
   t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
   t.wide_ki = int(ab_i("PKD_WIDE_KI", t.wide_ki));
+  t.xcd_map = ab_i("PKD_XCD_MAP", 1) != 0;
   t.colgroup = int(ab_i("PKD_COLGROUP", 0));
   t.hist_div = int(std::max<i64>(1, ab_i("PKD_HIST_DIV", 2)));
   t.scan_div = int(std::max<i64>(0, ab_i("PKD_SCAN_DIV", 0)));
@@ -5174,6 +5201,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
       a.small_done = 0;
       a.hist2 = hs.h2;
       a.id_implicit = (implicit_ids && l == 0) ? 1 : 0;
+      a.xcd = tune_.xcd_map ? 1 : 0;
       a.narrow = in_rows ? 1 : 0;
       a.kcol = a.narrow ? l : a.axis;
       a.nkcol = a.narrow ? std::min(l + 1, narrow_k) : a.next_axis;
