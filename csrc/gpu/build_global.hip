@@ -4552,6 +4552,7 @@ Tuning Tuning::from_env() {
   t.prefix = ab_i("PKD_PART_PREFIX", 1) != 0;
   t.tail = ab_i("PKD_TAIL", 1) != 0;
   t.tail4 = ab_i("PKD_TAIL4", 1) != 0;
+  t.tail4_min_dim = int(ab_i("PKD_TAIL4_MIN_DIM", t.tail4_min_dim));
   t.tail_pipe = ab_i("PKD_TAIL_PIPE", 1) != 0;
   t.g3_stage = int(ab_i("PKD_G3_STAGE", 2));
   t.part3_stage = ab_i("PKD_PART3_STAGE", 1) != 0;
@@ -4771,7 +4772,8 @@ GpuBuilder::GpuBuilder(i64 n, int dim, BuildOptions opt)
     for (int l = 0; l < lend; ++c) l += lv[size_t(l)].sampled ? top4::kLevels : (lv[size_t(l)].triple ? 3 : (lv[size_t(l)].pair ? 2 : 1));
     return c;
   };
-  if (tune_.tail4 && tune_.tail && dim >= 4 && dim <= 8 && !narrow_ && lg_ >= 9 && (n_ >> (lg_ - 4)) + 3 <= 16 * 1024) {
+  if (tune_.tail4 && tune_.tail && dim >= tune_.tail4_min_dim && dim >= 3 && dim <= 8 && !narrow_ && lg_ >= 9 &&
+      (n_ >> (lg_ - 4)) + 3 <= 16 * 1024) {
     tail_lev_ = 3;
     const int p3 = passes(make_plan(top_));
     const bool had3 = tail_ >= 0;
@@ -5158,6 +5160,12 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
   // Zone ranks of the scatter passes: LDS atomics below 64 M points, wave ballots above
   // (A/B in profiles/r3_partition_subtree_experiments.txt); knob -1 = by size.
   auto atomic_ranks = [&](int knob) { return knob >= 0 ? knob != 0 : n_ < (i64(64) << 20); };
+  // triples: wave ballots + LDS-staged stores from 10 M points at rows of <= 5 columns (3-D
+  // 12.5 M 1.415 -> 1.387 ms, 50 M 4.74 -> 4.41; 2 M - 8 M 1-2 % slower), else from 64 M (8-D
+  // 5 M - 30 M are 2-4 % slower with ballots); profiles/r6_ballot_sizes.txt
+  auto atomic_ranks3 = [&](int knob) {
+    return knob >= 0 ? knob != 0 : n_ < (dim_ <= 4 ? i64(10) << 20 : i64(64) << 20);
+  };
   auto run_range = [&](int base, int l0, int l1, int part, int nparts, hipStream_t st, const HistSet& hs,
                        float*& src, float*& dst) {
     auto hist_of = [&](int l) -> u32* {  // `base`: the level where the part's own arrays start
@@ -5292,14 +5300,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;  // 16-bit histogram counts suffice
             bool wide8 = false;  // rows of >= 6 columns: 8 rows per thread and chunk, stored in 4 parts
             if constexpr (NC > 5) {
-              if (tune_.wide_ki == 8 && stg16 && !atomic_ranks(tune_.atomic_ranks3)) {
+              if (tune_.wide_ki == 8 && stg16 && !atomic_ranks3(tune_.atomic_ranks3)) {
                 k_g3_part<NC, 8, false, 4><<<grid, kBlock, size_t((std::max(1, (kG3Gg * ga.bins3 + 1) / 2) + 3) & ~3) * 4 +
                                                              size_t(kBlock * 2) * (4 * NC + 1), st>>>(a, ga);
                 wide8 = true;
               }
             }
             if (wide8) {
-            } else if (atomic_ranks(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
+            } else if (atomic_ranks3(tune_.atomic_ranks3)) k_g3_part<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ga);
             else if (!stg16) k_g3_part<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ga);
             else if (tune_.g3_stage == 1) k_g3_part<NC, KI, false, 1><<<grid, kBlock, lds_stg(1), st>>>(a, ga);
             else if (tune_.g3_stage == 2) k_g3_part<NC, KI, false, 2><<<grid, kBlock, lds_stg(2), st>>>(a, ga);
@@ -5373,14 +5381,14 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
             const bool stg16 = (lp.nmax + a.bps - 1) / a.bps < 65536;
             bool wide8 = false;  // rows of >= 6 columns: 8 rows per thread and chunk, stored in 4 parts
             if constexpr (NC > 5) {
-              if (tune_.wide_ki == 8 && stg16 && tune_.part3_stage && !atomic_ranks(tune_.atomic_ranks3)) {
+              if (tune_.wide_ki == 8 && stg16 && tune_.part3_stage && !atomic_ranks3(tune_.atomic_ranks3)) {
                 k_partition3<NC, 8, false, 4><<<grid, kBlock, size_t((std::max(1, (8 * ta.bins3 + 1) / 2) + 3) & ~3) * 4 +
                                                                 size_t(kBlock * 2) * (4 * NC + 1), st>>>(a, ta);
                 wide8 = true;
               }
             }
             if (wide8) {
-            } else if (atomic_ranks(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
+            } else if (atomic_ranks3(tune_.atomic_ranks3)) k_partition3<NC, KI, true><<<grid, kBlock, lds3, st>>>(a, ta);
             else if (stg16 && tune_.part3_stage) k_partition3<NC, KI, false, 2><<<grid, kBlock, lds_stg, st>>>(a, ta);
             else k_partition3<NC, KI, false><<<grid, kBlock, lds3, st>>>(a, ta);
             PKD_LAUNCH_CHECK();
@@ -5486,7 +5494,7 @@ void GpuBuilder::run_levels(float* out_pts, u32* out_ids, char* ws, hipStream_t 
           // one 1024-thread workgroup per CU (128 registers): the two-per-CU shape (64 registers)
           // spills and was slower (100M x 3D k_tail3 1.41 vs 1.32 ms, profiles/r3_tail.txt)
           // (16 items: two key sets and ids on demand, else the 128 registers spill)
-          if constexpr (D >= 4) {
+          if constexpr (D >= 3) {
             if (tail_lev_ == 4) {  // (two key register sets: the SLIM shape, ids read where keys tie)
               if (tail_items_ == 8) go(&k_tail3<D, 8, 4, true, false, 4>);
               else if (tail_items_ == 12) go(&k_tail3<D, 12, 4, true, false, 4>);

@@ -58,6 +58,7 @@ struct Tuning {
   bool prefix = true;         // PKD_PART_PREFIX=0: counting pass instead of prefix placement
   bool tail = true;           // PKD_TAIL=0: the last three global levels by pairs / triples instead of k_tail3
   bool tail4 = true;          // PKD_TAIL4=0: never a 4-level tail (it replaces two pairs by a triple at 8-D)
+  int tail4_min_dim = 4;      // PKD_TAIL4_MIN_DIM: lowest dim a 4-level tail may be planned at (>= 3)
   bool tail_pipe = true;      // PKD_TAIL_PIPE=0: k_tail3 moves its columns one at a time (load, stage, store)
   int g3_stage = 2;           // k_g3_part stores through an LDS tile of 2 (1) parts; 0: from registers
   bool part3_stage = true;    // PKD_PART3_STAGE=0: k_partition3 (ballot ranks) stores from registers
