@@ -4099,6 +4099,29 @@ void k_tail3(TailArgs a) {
   int axis_of[LEV];
 #pragma unroll
   for (int t = 0; t < LEV; ++t) axis_of[t] = (a.depth0 + a.level + t) % D;
+  // the nodes' geometry and the root cell into LDS BEFORE the key loads are issued: their LDS
+  // stores wait for their own global loads, and the load counter is in order, so behind the keys'
+  // loads they made wave 0 (and with it the first barrier) wait for the whole segment's keys and
+  // ids; ahead of them, level 0 starts as soon as its own key column is in (the compiler barrier
+  // keeps the order)
+  {  // (all three loads in flight together, then the stores)
+    i64 vlo = 0;
+    u32 vn = 0;
+    float vc = 0.0f;
+    if (tid < NALL) {  // node k (heap order below h: 0 = h, 1-2 children, ..., NNODE.. the leaves)
+      const int lev = 31 - __builtin_clz(u32(tid) + 1u);
+      const i64 hk = (h + 1) * (i64(1) << lev) - 1 + (tid - ((1 << lev) - 1));
+      vlo = a.seg_lo[hk];
+      vn = u32(a.seg_n[hk]);
+    }
+    if (tid < 2 * D) vc = a.cells[h * 2 * D + tid];
+    if (tid < NALL) {
+      nlo[tid] = vlo;
+      nn[tid] = vn;
+    }
+    if (tid < 2 * D) (&scell[0][0][0][0])[tid] = vc;
+  }
+  asm volatile("" ::: "memory");
   float xs[KC][ITEMS];
   u32 ids[IDS ? ITEMS : 1];
 #pragma unroll
@@ -4124,13 +4147,6 @@ void k_tail3(TailArgs a) {
     if constexpr (!IDS) return __builtin_amdgcn_raw_buffer_load_b32(rid, vo + u32(i % 4) * 4u, u32(i / 4 * T * 16), 0);
     else return ids[i];
   };
-  if (tid < NALL) {  // node k (heap order below h: 0 = h, 1-2 children, ..., NNODE.. the leaves)
-    const int lev = 31 - __builtin_clz(u32(tid) + 1u);
-    const i64 hk = (h + 1) * (i64(1) << lev) - 1 + (tid - ((1 << lev) - 1));
-    nlo[tid] = a.seg_lo[hk];
-    nn[tid] = u32(a.seg_n[hk]);
-  }
-  if (tid < 2 * D) (&scell[0][0][0][0])[tid] = a.cells[h * 2 * D + tid];
   // path: the row's sub-segment at the current level (while a level bins, its bin: the
   // sub-segment is bin >> lgB); kDead for absent rows, kMed | node for the tail's medians
   u32 path[ITEMS];
