@@ -4045,7 +4045,7 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* wsum, u32* total,
 // LEV = 4 (8-D builds: 17 global levels leave 13 between the top and the tail, three triples
 // and a 4-level tail instead of two triples, two pairs and a 3-level tail): the same steps for
 // one more level (8 sub-segments at the last one, 16 leaves), SLIM: level t's keys in register
-// set t & 1, reloaded for levels 2 and 3.
+// set t & 1, reloaded for levels 2 and 3 (each issued when the level before it starts).
 template <int D, int ITEMS, int WPE, bool SLIM = false, bool IDS = !SLIM, int LEV = 3>
 __global__ __launch_bounds__(kTailThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_tail3(TailArgs a) {
@@ -4166,13 +4166,13 @@ void k_tail3(TailArgs a) {
     static_assert(NB == 4096, "lgB");
     const int axis = axis_of[t];
     const int kx = D < 3 ? axis : (SLIM ? (t & 1) : t);  // register set of this level's keys
-    if (SLIM && t >= 2) {  // level t's keys into level t - 2's (dead) registers
-      const auto r = col(a.src, axis);
+    if (SLIM && t + 1 >= 2 && t + 1 < LEV) {  // level t+1's keys into level t-1's (dead) registers, issued
+      const auto r = col(a.src, axis_of[t + 1]);  // a whole level ahead of their use
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const auto v = ld4(r, g);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xs[t & 1][4 * g + j] = __uint_as_float(v[j]);
+        for (int j = 0; j < 4; ++j) xs[(t + 1) & 1][4 * g + j] = __uint_as_float(v[j]);
       }
     }
     for (int b = tq; b < NB; b += T) bins[b] = 0;
