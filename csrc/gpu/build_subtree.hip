@@ -676,6 +676,7 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
     // between (profiles/r3_subtree_1536.txt)
     else if (nmax > 1024 && nmax <= 1536 && cfg == "6x256" && a.ldim == 0) launch_rank_cfg<6, 256>(a, segs, stream);
     else if (nmax > 1024 && nmax <= 1536 && cfg == "4x384" && a.ldim == 0) launch_rank_cfg<4, 384>(a, segs, stream);
+    else if (nmax > 1024 && nmax <= 1536 && cfg == "2x768" && a.ldim == 0) launch_rank_cfg<2, 768>(a, segs, stream);
     else if (nmax > 1024 && nmax <= 1536 && wide && c1536 && dim == 3 && a.ldim == 0)
       launch_rank_cfg<3, 512, 6>(a, segs, stream);
     else if (nmax > 1024 && wide) launch_rank_cfg<2, 1024>(a, segs, stream);

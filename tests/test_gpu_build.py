@@ -52,7 +52,7 @@ def test_subtree_launch_shapes(gpu_device, monkeypatch, cfg, dim):
     check_same(torch.randint(0, 9, (n, dim)).float(), gpu_device, subtree_max=1024, depth0=dim - 1)
 
 
-@pytest.mark.parametrize("cfg", ["6x256", "4x384", ""])
+@pytest.mark.parametrize("cfg", ["6x256", "4x384", "2x768", ""])
 @pytest.mark.parametrize("dim", [2, 3, 4])
 def test_subtree_launch_shapes_1536(gpu_device, monkeypatch, cfg, dim):
     """Segments of 1025..1536 points (100M x 3D: 1525) under the launch shapes of that capacity."""
