@@ -48,7 +48,9 @@ constexpr size_t kLdsMax = 160 * 1024 - 1024;  // minus static LDS
 // written then and streamed out at the end with coalesced stores.
 namespace rk {
 
-constexpr int kSmallSeg = 16;  // sub-segments up to this size rank by comparison in one bucket
+// sub-segments up to this size rank by comparison in one bucket, placed by slot range (PKD_SUBTREE_SMALL;
+// 100M 8D 16.62 -> 16.41 ms, 6D 13.37 -> 13.24 against 16; 32 is slower: profiles/r6_subtree_shapes.txt)
+constexpr int kSmallSeg = 8;
 
 __host__ __device__ inline int bitlen(u32 v) {
   int b = 0;
@@ -343,7 +345,7 @@ __device__ __forceinline__ void subtree_rank_body(const SubArgs& a) {
       // is a valid (wider) range. Any monotone bucketing gives exact ranks.
       // About one point per bucket (S * B <= NM): most buckets need no comparison at all.
       const int maxsize = n >> t;
-      const int B = maxsize > rk::kSmallSeg ? min(int(rk::pow2_ceil(u32(maxsize))), NM >> t) : 1;
+      const int B = maxsize > a.small_seg ? min(int(rk::pow2_ceil(u32(maxsize))), NM >> t) : 1;
       // B == 1 (sub-segments of <= kSmallSeg points): a sub-segment's points go to its own slot
       // range [lo, lo + nn) of the bucket order -- the layout the scan would give, up to gaps -- so
       // the level needs no scan (one barrier and a block scan fewer; 8-D's levels 6 and 7)
@@ -658,8 +660,9 @@ void launch_subtree(const float* cols, i64 ncol, int dim, const i64* seg_lo, con
   // columns only for dim >= the subtree's levels)
   const int ldim = narrow_idcol >= 0 ? rk::bitlen(u32(std::max(nmax, 1))) : 0;
   if (ldim > dim) throw std::runtime_error("pkdtree: narrow subtree needs dim >= its levels");
+  const char* ess = ab_knob("PKD_SUBTREE_SMALL");
   SubArgs a{cols, ncol, dim, seg_lo, seg_n, cells, heap0, depth_base, out_pts, out_ids, err, stamps,
-            std::max(narrow_idcol, 0), in_rows, in_rs, ldim};
+            std::max(narrow_idcol, 0), in_rows, in_rs, ldim, ess ? std::max(1, std::atoi(ess)) : rk::kSmallSeg};
   {
     // (read per launch, so tests can vary them within one process)
     const char* ew = ab_knob("PKD_SUBTREE_WIDE");

@@ -24,6 +24,7 @@ struct SubArgs {
   const float* in_rows;
   i64 in_rs;
   int ldim;                    // narrow: LDS key slots (slot t = key of subtree level t), 0 otherwise
+  int small_seg;               // first-use levels whose sub-segments hold <= this many points rank by comparison
 };
 
 // Orders this wave's LDS writes before its later LDS reads (different lanes): waits for the
