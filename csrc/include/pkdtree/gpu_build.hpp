@@ -62,8 +62,9 @@ struct Tuning {
   bool tail_pipe = true;      // PKD_TAIL_PIPE=0: k_tail3 moves its columns one at a time (load, stage, store)
   int g3_stage = 2;           // k_g3_part stores through an LDS tile of 2 (1) parts; 0: from registers
   bool part3_stage = true;    // PKD_PART3_STAGE=0: k_partition3 (ballot ranks) stores from registers
-  int wide_ki = 8;            // PKD_WIDE_KI: k_g3_part / k_partition3 rows per thread at >= 6 columns (8: staged
-                              //   in 4 parts; 100M 6D 16.59 -> 16.23 ms, 8D 18.36 -> 18.10 against 4)
+  int wide_ki = 4;            // PKD_WIDE_KI: k_g3_part / k_partition3 rows per thread at >= 6 columns (8: staged in
+                              //   4 parts; won before the XCD mapping (6D 16.59 -> 16.23 ms), loses after it: 100M
+                              //   5D 11.87 vs 12.18, 8D 16.45 vs 16.69 with 8; profiles/r6_wide_subtree_ab.txt)
   bool xcd_map = true;        // PKD_XCD_MAP=0: row-moving passes map block b to segment b / bps (not one XCD per segment)
   int tail_slim12 = 2;  // PKD_TAIL_SLIM12: 12-item k_tail3 registers: 0 all keys + ids (spills 52 B/lane at 3-D),
                         //   1 two key sets (no ids), 2 two key sets + ids (no spill; 100M x 3D 8.46 ms either way)
